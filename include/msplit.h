@@ -1,0 +1,181 @@
+/*
+ * msplit.h -- C ABI of the MI355X-native GMRES inner-solve path.
+ *
+ * The reference (craftman22/medane_tchakorom_ufc_thesis_repository) reaches
+ * this path through PETSc 3.22.1's object API.  Every entry point below names
+ * the reference call it replaces (file:line under the reference tree) and the
+ * PETSc operation behind it.  Plain pointers and sizes only: no PETSc, HIP or
+ * torch types cross this boundary.
+ *
+ * Conventions (mirroring PETSc's, src/utils/utils.c:12-17):
+ *   - every function returns int: 0 (= PETSC_SUCCESS) or a PETSc error number
+ *     (MSP_ERR_*); msp_get_last_error() gives the message of the calling
+ *     thread's last failure;
+ *   - objects are opaque handles; msp_xxx_destroy(&h) frees and NULLs h;
+ *   - work is stream-ordered on the context's HIP stream; functions returning
+ *     host scalars synchronise that stream;
+ *   - not thread-safe per context; one host thread (or process) per GPU.
+ *
+ * Arithmetic (see DESIGN.md "Parity"): IEEE binary64 with no FMA contraction.
+ * MatMult sums each row left to right over ascending columns (MatMult_SeqAIJ);
+ * VecMAXPY uses PETSc's 4-vector grouping (VecMAXPY_Seq); VecDot/VecNorm/
+ * VecMDot use the deterministic blocked reduction (DBR) order documented in
+ * oracle/oracle.h, so results are bitwise reproducible run to run and equal
+ * to the CPU oracle in its DBR mode.
+ */
+#ifndef MSPLIT_H
+#define MSPLIT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error numbers: the PETSc values (petscerror.h) for the same conditions. */
+#define MSP_SUCCESS 0
+#define MSP_ERR_MEM 55          /* PETSC_ERR_MEM */
+#define MSP_ERR_SUP 56          /* PETSC_ERR_SUP */
+#define MSP_ERR_ARG_SIZ 60      /* PETSC_ERR_ARG_SIZ: incompatible sizes */
+#define MSP_ERR_ARG_WRONG 62    /* PETSC_ERR_ARG_WRONG */
+#define MSP_ERR_ARG_OUTOFRANGE 63
+#define MSP_ERR_LIB 76          /* PETSC_ERR_LIB: HIP / RCCL runtime error */
+#define MSP_ERR_ARG_NULL 85     /* PETSC_ERR_ARG_NULL */
+
+/* KSPConvergedReason values (PETSc 3.22.1 include/petscksp.h). */
+#define MSP_CONVERGED_ITERATING 0
+#define MSP_CONVERGED_RTOL 2
+#define MSP_CONVERGED_ATOL 3
+#define MSP_DIVERGED_NULL (-2)
+#define MSP_DIVERGED_ITS (-3)
+#define MSP_DIVERGED_DTOL (-4)
+#define MSP_DIVERGED_BREAKDOWN (-5)
+#define MSP_DIVERGED_NANORINF (-9)
+
+/* Kernel classes for msp_ctx_get_kernel_stats(). */
+#define MSP_KERNEL_SPMV 0       /* MatMult / MatResidual (CSR) */
+#define MSP_KERNEL_MDOT 1       /* VecMDot (both DBR stages) */
+#define MSP_KERNEL_MAXPY 2      /* VecMAXPY (CGS update and BuildSoln) */
+#define MSP_KERNEL_NORM 3       /* VecNorm / VecDot (both DBR stages) */
+#define MSP_KERNEL_SCALE 4      /* VecScale (VecNormalize) */
+#define MSP_KERNEL_OTHER 5      /* copy/set/axpy/... */
+#define MSP_KERNEL_NCLASSES 6
+
+typedef struct msp_ctx msp_ctx;
+typedef struct msp_mat msp_mat;
+typedef struct msp_vec msp_vec;
+typedef struct msp_ksp msp_ksp;
+
+/* ---------------------------------------------------------------- context */
+/* One context per GPU: device id + the HIP stream all work is ordered on.
+ * stream == NULL creates a private non-blocking stream; otherwise the given
+ * hipStream_t (passed as void*) is used and not destroyed.  Replaces the
+ * per-rank PETSc/MPI setup: PetscInitialize + PetscSubcommCreate
+ * (synchronous-multisplitting.c:40, :66-73) -- npb = 1, one block per GPU. */
+int msp_ctx_create(int device, void *stream, msp_ctx **ctx);
+int msp_ctx_destroy(msp_ctx **ctx);
+int msp_ctx_synchronize(msp_ctx *ctx);
+int msp_get_device_count(int *count);
+const char *msp_get_last_error(void);
+/* Per-kernel-class HIP-event timing (used by bench.py; off by default). */
+int msp_ctx_set_timing(msp_ctx *ctx, int enable);
+int msp_ctx_reset_kernel_stats(msp_ctx *ctx);
+/* launches, summed kernel time (ms) and summed algorithmic bytes for one class;
+ * synchronises the stream. */
+int msp_ctx_get_kernel_stats(msp_ctx *ctx, int kernel_class, int64_t *launches, double *total_ms,
+                             double *total_bytes);
+
+/* -------------------------------------------------------------------- Mat */
+/* MATSEQAIJ from host CSR arrays (ascending columns per row), copied to HBM.
+ * Replaces create_matrix_sparse + MatSetValue(s) + MatAssemblyBegin/End
+ * (utils.c:139-155, :261-290) and MatCreateSubMatrix (utils.c:473). */
+int msp_mat_create_csr(msp_ctx *ctx, int32_t nrows, int32_t ncols, const int32_t *rowptr,
+                       const int32_t *col, const double *val, msp_mat **A);
+/* Row-compressed AIJ: only the nlisted rows row_ids[] (ascending) hold entries;
+ * every other row of the nrows x ncols matrix is empty.  This is how the
+ * coupling block A_ij (utils.c:473; one boundary plane of nonzeros) is stored. */
+int msp_mat_create_csr_rows(msp_ctx *ctx, int32_t nrows, int32_t ncols, int32_t nlisted,
+                            const int32_t *row_ids, const int32_t *rowptr, const int32_t *col,
+                            const double *val, msp_mat **A);
+/* Device-side assembly of the dim-D box Laplacian with Dirichlet boundaries:
+ * dim 3: nx*ny*nz 7-point (diag 6, off -1), row i + nx*j + nx*ny*k  (poisson3DMatrix,
+ *        utils.c:30-121, restricted to one z-slab's own columns);
+ * dim 2: nx = mesh columns (fastest), ny = mesh lines, 5-point (diag 4)
+ *        (poisson2DMatrix, utils.c:247-293, restricted to whole-line row blocks).
+ * Identical CSR to the host assembly, built in HBM (no host arrays). */
+int msp_mat_create_box_stencil(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, int32_t nz, msp_mat **A);
+int msp_mat_destroy(msp_mat **A);
+int msp_mat_get_info(const msp_mat *A, int32_t *nrows, int32_t *ncols, int64_t *nnz);
+/* Download the CSR (host buffers of nrows+1 / nnz entries); synchronising. */
+int msp_mat_get_csr(const msp_mat *A, int32_t *rowptr, int32_t *col, double *val);
+/* MatMult y = A x (utils.c:626; KSP_PCApplyBAorAB inside KSPGMRESCycle). */
+int msp_mat_mult(msp_mat *A, const msp_vec *x, msp_vec *y);
+/* MatResidual r = b - A x (utils.c:549, :565, :579, :946;
+ * synchronous-multisplitting.c:187). */
+int msp_mat_residual(msp_mat *A, const msp_vec *b, const msp_vec *x, msp_vec *r);
+
+/* -------------------------------------------------------------------- Vec */
+/* VecCreate/VecSetSizes/VecSetType (utils.c:157-168): zero-initialised, in HBM. */
+int msp_vec_create(msp_ctx *ctx, int64_t n, msp_vec **v);
+/* Wrap caller-owned device memory (VecCreateSeqWithArray analogue); not freed. */
+int msp_vec_create_with_array(msp_ctx *ctx, int64_t n, double *device_ptr, msp_vec **v);
+int msp_vec_destroy(msp_vec **v);
+int msp_vec_get_size(const msp_vec *v, int64_t *n);
+/* Device pointer of the storage (VecGetArray on the device). */
+int msp_vec_get_array(msp_vec *v, double **device_ptr);
+/* Host <-> device copies of [off, off+n) (VecSetValues / VecGetValues;
+ * the reference's VecGetArray + MPI buffers, comm.c:132-138). get synchronises. */
+int msp_vec_set_values(msp_vec *v, int64_t off, int64_t n, const double *host);
+int msp_vec_get_values(const msp_vec *v, int64_t off, int64_t n, double *host);
+/* dst[dst_off : dst_off+n] = src[src_off : src_off+n] on the device (halo packing). */
+int msp_vec_copy_range(const msp_vec *src, int64_t src_off, msp_vec *dst, int64_t dst_off, int64_t n);
+int msp_vec_set(msp_vec *v, double alpha);                                  /* VecSet */
+int msp_vec_copy(const msp_vec *x, msp_vec *y);                             /* VecCopy */
+int msp_vec_scale(msp_vec *x, double alpha);                                /* VecScale */
+int msp_vec_axpy(msp_vec *y, double alpha, const msp_vec *x);               /* VecAXPY */
+int msp_vec_aypx(msp_vec *y, double beta, const msp_vec *x);                /* VecAYPX */
+int msp_vec_waxpy(msp_vec *w, double alpha, const msp_vec *x, const msp_vec *y); /* VecWAXPY, utils.c:1054 */
+int msp_vec_dot(const msp_vec *x, const msp_vec *y, double *val);           /* VecDot */
+int msp_vec_norm(const msp_vec *x, double *val);                            /* VecNorm NORM_2, utils.c:550-604 */
+int msp_vec_normalize(msp_vec *x, double *val);                             /* VecNormalize */
+/* VecMDot: val[j] = x . y[j], j < nv (KSPGMRESClassicalGramSchmidtOrthogonalization). */
+int msp_vec_mdot(const msp_vec *x, int nv, const msp_vec *const *y, double *val);
+/* VecMAXPY: y += sum_j alpha[j] x[j] (PETSc 4-grouping order). */
+int msp_vec_maxpy(msp_vec *y, int nv, const double *alpha, const msp_vec *const *x);
+
+/* -------------------------------------------------------------------- KSP */
+/* KSPGMRES options -- the PETSc options database keys they stand for. */
+typedef struct msp_ksp_opts {
+  int32_t restart;       /* -ksp_gmres_restart           (30)    */
+  int32_t max_it;        /* -ksp_max_it                  (10000) */
+  double rtol;           /* -ksp_rtol                    (1e-5)  */
+  double abstol;         /* -ksp_atol                    (1e-50) */
+  double divtol;         /* -ksp_divtol                  (1e4)   */
+  double haptol;         /* -ksp_gmres_haptol            (1e-30) */
+  double breakdowntol;   /* -ksp_gmres_breakdown_tolerance (0.1) */
+  int32_t uirnorm;       /* KSPConvergedDefaultSetUIRNorm / -ksp_converged_use_initial_residual_norm */
+  int32_t guess_nonzero; /* KSPSetInitialGuessNonzero */
+} msp_ksp_opts;
+
+int msp_ksp_get_default_opts(msp_ksp_opts *o);
+/* KSPCreate + KSPSetType(KSPGMRES) + PCNONE, CGS with REFINE_NEVER
+ * (initializeKSP, utils.c:512-541; canonical options running_bulk_test_g5k:64-70). */
+int msp_ksp_create(msp_ctx *ctx, msp_ksp **ksp);
+int msp_ksp_destroy(msp_ksp **ksp);
+int msp_ksp_set_operators(msp_ksp *ksp, msp_mat *A);                 /* KSPSetOperators, utils.c:518 */
+int msp_ksp_set_opts(msp_ksp *ksp, const msp_ksp_opts *o);            /* KSPSetFromOptions, utils.c:530 */
+int msp_ksp_get_opts(const msp_ksp *ksp, msp_ksp_opts *o);
+int msp_ksp_set_up(msp_ksp *ksp);                                     /* KSPSetUp: Krylov basis in HBM */
+/* KSPSolve (utils.c:958, gmres_solution.c:70): x is the initial guess when
+ * guess_nonzero, and the solution on return. */
+int msp_ksp_solve(msp_ksp *ksp, const msp_vec *b, msp_vec *x);
+int msp_ksp_get_iteration_number(const msp_ksp *ksp, int32_t *its);  /* KSPGetIterationNumber, utils.c:960 */
+int msp_ksp_get_residual_norm(const msp_ksp *ksp, double *rnorm);     /* KSPGetResidualNorm */
+int msp_ksp_get_converged_reason(const msp_ksp *ksp, int32_t *reason);
+/* Residual history of the last solve (KSPGetResidualHistory): its+1 entries. */
+int msp_ksp_get_residual_history(const msp_ksp *ksp, const double **hist, int32_t *n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

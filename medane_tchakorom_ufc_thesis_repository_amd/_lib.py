@@ -1,0 +1,132 @@
+"""ctypes binding of libmsplit_hip.so (include/msplit.h).
+
+The product path has exactly one implementation: the HIP library.  Loading it
+fails loudly when the .so is missing, and every call raises MsplitError with
+the library's message when the C ABI returns a nonzero (PETSc-numbered) code.
+There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmsplit_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "msplit.h")
+
+KERNEL_CLASSES = {"spmv": 0, "mdot": 1, "maxpy": 2, "norm": 3, "scale": 4, "other": 5}
+
+REASONS = {
+    0: "CONVERGED_ITERATING", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
+    -2: "DIVERGED_NULL", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
+    -5: "DIVERGED_BREAKDOWN", -9: "DIVERGED_NANORINF",
+}
+
+
+class MsplitError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+class KspOpts(C.Structure):
+    _fields_ = [("restart", C.c_int32), ("max_it", C.c_int32), ("rtol", C.c_double),
+                ("abstol", C.c_double), ("divtol", C.c_double), ("haptol", C.c_double),
+                ("breakdowntol", C.c_double), ("uirnorm", C.c_int32), ("guess_nonzero", C.c_int32)]
+
+
+_lib = None
+
+_P = C.POINTER
+_vp = C.c_void_p
+_i32p = _P(C.c_int32)
+_dp = _P(C.c_double)
+
+# name -> argtypes (restype is int for all but msp_get_last_error)
+_SIGS = {
+    "msp_ctx_create": [C.c_int, _vp, _P(_vp)],
+    "msp_ctx_destroy": [_P(_vp)],
+    "msp_ctx_synchronize": [_vp],
+    "msp_get_device_count": [_P(C.c_int)],
+    "msp_ctx_set_timing": [_vp, C.c_int],
+    "msp_ctx_reset_kernel_stats": [_vp],
+    "msp_ctx_get_kernel_stats": [_vp, C.c_int, _P(C.c_int64), _dp, _dp],
+    "msp_mat_create_csr": [_vp, C.c_int32, C.c_int32, _i32p, _i32p, _dp, _P(_vp)],
+    "msp_mat_create_csr_rows": [_vp, C.c_int32, C.c_int32, C.c_int32, _i32p, _i32p, _i32p, _dp, _P(_vp)],
+    "msp_mat_create_box_stencil": [_vp, C.c_int, C.c_int32, C.c_int32, C.c_int32, _P(_vp)],
+    "msp_mat_destroy": [_P(_vp)],
+    "msp_mat_get_info": [_vp, _i32p, _i32p, _P(C.c_int64)],
+    "msp_mat_get_csr": [_vp, _i32p, _i32p, _dp],
+    "msp_mat_mult": [_vp, _vp, _vp],
+    "msp_mat_residual": [_vp, _vp, _vp, _vp],
+    "msp_vec_create": [_vp, C.c_int64, _P(_vp)],
+    "msp_vec_create_with_array": [_vp, C.c_int64, _vp, _P(_vp)],
+    "msp_vec_destroy": [_P(_vp)],
+    "msp_vec_get_size": [_vp, _P(C.c_int64)],
+    "msp_vec_get_array": [_vp, _P(_vp)],
+    "msp_vec_set_values": [_vp, C.c_int64, C.c_int64, _dp],
+    "msp_vec_get_values": [_vp, C.c_int64, C.c_int64, _dp],
+    "msp_vec_copy_range": [_vp, C.c_int64, _vp, C.c_int64, C.c_int64],
+    "msp_vec_set": [_vp, C.c_double],
+    "msp_vec_copy": [_vp, _vp],
+    "msp_vec_scale": [_vp, C.c_double],
+    "msp_vec_axpy": [_vp, C.c_double, _vp],
+    "msp_vec_aypx": [_vp, C.c_double, _vp],
+    "msp_vec_waxpy": [_vp, C.c_double, _vp, _vp],
+    "msp_vec_dot": [_vp, _vp, _dp],
+    "msp_vec_norm": [_vp, _dp],
+    "msp_vec_normalize": [_vp, _dp],
+    "msp_vec_mdot": [_vp, C.c_int, _P(_vp), _dp],
+    "msp_vec_maxpy": [_vp, C.c_int, _dp, _P(_vp)],
+    "msp_ksp_get_default_opts": [_P(KspOpts)],
+    "msp_ksp_create": [_vp, _P(_vp)],
+    "msp_ksp_destroy": [_P(_vp)],
+    "msp_ksp_set_operators": [_vp, _vp],
+    "msp_ksp_set_opts": [_vp, _P(KspOpts)],
+    "msp_ksp_get_opts": [_vp, _P(KspOpts)],
+    "msp_ksp_set_up": [_vp],
+    "msp_ksp_solve": [_vp, _vp, _vp],
+    "msp_ksp_get_iteration_number": [_vp, _i32p],
+    "msp_ksp_get_residual_norm": [_vp, _dp],
+    "msp_ksp_get_converged_reason": [_vp, _i32p],
+    "msp_ksp_get_residual_history": [_vp, _P(_dp), _i32p],
+}
+
+
+def header_symbols() -> list[str]:
+    """Every function declared in include/msplit.h."""
+    txt = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    return sorted(set(re.findall(r"\b(msp_[a-z0-9_]+)\s*\(", txt)))
+
+
+def load() -> C.CDLL:
+    """Load the HIP library.  Import torch first when it is used in the same
+    process, so that one HIP runtime (same soname) serves both."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C medane_tchakorom_ufc_thesis_repository_amd/csrc` (hipcc, gfx950). "
+            "There is no CPU fallback for the MI355X path.")
+    L = C.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    L.msp_get_last_error.argtypes = []
+    L.msp_get_last_error.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc:
+        msg = load().msp_get_last_error().decode(errors="replace")
+        raise MsplitError(rc, msg)
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args))

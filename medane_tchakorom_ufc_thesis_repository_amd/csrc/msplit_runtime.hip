@@ -1,0 +1,794 @@
+// msplit_runtime.hip -- context, Mat and Vec objects of the C ABI (include/msplit.h).
+//
+// One context per GPU owns one HIP stream; every Mat/Vec op is enqueued on it.
+// Host scalars (norms, dots) come back through a pinned staging buffer.
+// The KSP (GMRES) host logic lives in ksp_gmres.c and calls the mspi_* entry
+// points defined here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "msplit.h"
+#include "msplit_internal.h"
+#include "msplit_kernels.h"
+
+// ----------------------------------------------------------------- errors
+static thread_local char g_err[512] = "no error";
+
+extern "C" void mspi_set_error(int code, const char* fmt, ...) {
+  char buf[448];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  snprintf(g_err, sizeof(g_err), "[msplit error %d] %s", code, buf);
+}
+
+extern "C" const char* msp_get_last_error(void) { return g_err; }
+
+#define HIPCHK(call)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (call);                                                                       \
+    if (e_ != hipSuccess) {                                                                       \
+      mspi_set_error(MSP_ERR_LIB, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                     __LINE__);                                                                   \
+      return MSP_ERR_LIB;                                                                         \
+    }                                                                                             \
+  } while (0)
+
+#define KCHK(call)                                                                                  \
+  do {                                                                                              \
+    int e_ = (call);                                                                                \
+    if (e_) {                                                                                       \
+      mspi_set_error(MSP_ERR_LIB, "kernel launch %s failed: %s", #call,                             \
+                     hipGetErrorString((hipError_t)e_));                                            \
+      return MSP_ERR_LIB;                                                                           \
+    }                                                                                               \
+  } while (0)
+
+#define ARGCHK(cond, code, ...)        \
+  do {                                 \
+    if (!(cond)) {                     \
+      mspi_set_error(code, __VA_ARGS__); \
+      return code;                     \
+    }                                  \
+  } while (0)
+
+// ---------------------------------------------------------------- context
+struct TimedRec {
+  int cls;
+  int ev;  // index of the start event in the pool; stop = ev + 1
+  double bytes;
+};
+
+struct msp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  double* dscratch = nullptr;  // device scalars
+  double* hscratch = nullptr;  // pinned host scalars
+  double* partial = nullptr;   // DBR stage-1 partials
+  int64_t partial_cap = 0;     // doubles
+  bool timing = false;
+  std::vector<hipEvent_t> pool;
+  size_t pool_used = 0;
+  std::vector<TimedRec> recs;
+};
+
+static const int kScratch = 4 * MSPI_MAX_GROUP + 64;
+
+extern "C" int msp_get_device_count(int* count) {
+  ARGCHK(count, MSP_ERR_ARG_NULL, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = (e == hipSuccess) ? n : 0;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_create(int device, void* stream, msp_ctx** out) {
+  ARGCHK(out, MSP_ERR_ARG_NULL, "ctx out-pointer is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    mspi_set_error(MSP_ERR_LIB, "no HIP device visible (the MI355X path needs a GPU; there is no CPU fallback)");
+    return MSP_ERR_LIB;
+  }
+  ARGCHK(device >= 0 && device < ndev, MSP_ERR_ARG_OUTOFRANGE, "device %d out of range [0,%d)", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  msp_ctx* c = new msp_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      mspi_set_error(MSP_ERR_LIB, "hipStreamCreate failed");
+      return MSP_ERR_LIB;
+    }
+    c->own_stream = true;
+  }
+  if (hipMalloc((void**)&c->dscratch, kScratch * sizeof(double)) != hipSuccess ||
+      hipHostMalloc((void**)&c->hscratch, kScratch * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+    mspi_set_error(MSP_ERR_MEM, "scratch allocation failed");
+    msp_ctx_destroy(&c);
+    return MSP_ERR_MEM;
+  }
+  *out = c;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_destroy(msp_ctx** pc) {
+  if (!pc || !*pc) return MSP_SUCCESS;
+  msp_ctx* c = *pc;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto e : c->pool) (void)hipEventDestroy(e);
+  if (c->partial) (void)hipFree(c->partial);
+  if (c->dscratch) (void)hipFree(c->dscratch);
+  if (c->hscratch) (void)hipHostFree(c->hscratch);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  *pc = nullptr;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_synchronize(msp_ctx* c) {
+  ARGCHK(c, MSP_ERR_ARG_NULL, "ctx is NULL");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_set_timing(msp_ctx* c, int enable) {
+  ARGCHK(c, MSP_ERR_ARG_NULL, "ctx is NULL");
+  c->timing = enable != 0;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_reset_kernel_stats(msp_ctx* c) {
+  ARGCHK(c, MSP_ERR_ARG_NULL, "ctx is NULL");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->recs.clear();
+  c->pool_used = 0;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_get_kernel_stats(msp_ctx* c, int cls, int64_t* launches, double* total_ms, double* total_bytes) {
+  ARGCHK(c, MSP_ERR_ARG_NULL, "ctx is NULL");
+  ARGCHK(cls >= 0 && cls < MSP_KERNEL_NCLASSES, MSP_ERR_ARG_OUTOFRANGE, "kernel class %d", cls);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int64_t n = 0;
+  double ms = 0.0, by = 0.0;
+  for (const auto& r : c->recs) {
+    if (r.cls != cls) continue;
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, c->pool[r.ev], c->pool[r.ev + 1]));
+    ++n;
+    ms += t;
+    by += r.bytes;
+  }
+  if (launches) *launches = n;
+  if (total_ms) *total_ms = ms;
+  if (total_bytes) *total_bytes = by;
+  return MSP_SUCCESS;
+}
+
+// Brackets one logical kernel (possibly two launches) with a pair of events.
+struct KTimer {
+  msp_ctx* c;
+  int ev = -1;
+  KTimer(msp_ctx* ctx, int cls, double bytes) : c(ctx) {
+    if (!c->timing) return;
+    if (c->pool_used + 2 > c->pool.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->pool.push_back(e);
+      }
+    }
+    ev = (int)c->pool_used;
+    c->pool_used += 2;
+    (void)hipEventRecord(c->pool[ev], c->stream);
+    c->recs.push_back({cls, ev, bytes});
+  }
+  ~KTimer() {
+    if (ev >= 0) (void)hipEventRecord(c->pool[ev + 1], c->stream);
+  }
+};
+
+extern "C" double* mspi_dev_scratch(msp_ctx* c) { return c->dscratch; }
+extern "C" double* mspi_host_scratch(msp_ctx* c) { return c->hscratch; }
+
+extern "C" int mspi_malloc(msp_ctx* c, void** p, size_t bytes) {
+  (void)c;
+  if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) {
+    *p = nullptr;
+    mspi_set_error(MSP_ERR_MEM, "hipMalloc(%zu bytes) failed", bytes);
+    return MSP_ERR_MEM;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_free(msp_ctx* c, void* p) {
+  (void)c;
+  if (p) HIPCHK(hipFree(p));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_host_malloc(void** p, size_t bytes) {
+  if (hipHostMalloc(p, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) {
+    *p = nullptr;
+    mspi_set_error(MSP_ERR_MEM, "hipHostMalloc(%zu bytes) failed", bytes);
+    return MSP_ERR_MEM;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_host_free(void* p) {
+  if (p) HIPCHK(hipHostFree(p));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_set_device(msp_ctx* c) {
+  HIPCHK(hipSetDevice(c->device));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_d2h_sync(msp_ctx* c, void* host, const void* dev, size_t bytes) {
+  HIPCHK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MSP_SUCCESS;
+}
+
+static int ensure_partial(msp_ctx* c, int64_t need) {
+  if (need <= c->partial_cap) return MSP_SUCCESS;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->partial) HIPCHK(hipFree(c->partial));
+  c->partial = nullptr;
+  c->partial_cap = 0;
+  HIPCHK(hipMalloc((void**)&c->partial, (size_t)need * sizeof(double)));
+  c->partial_cap = need;
+  return MSP_SUCCESS;
+}
+
+static inline int64_t nchunks_of(int64_t n) { return (n + MSK_DBR_CHUNK - 1) / MSK_DBR_CHUNK; }
+
+// --------------------------------------------------------------- internal ops
+extern "C" int mspi_mdot(msp_ctx* c, const double* w, int nv, const double* const* V, int64_t n, double* out_dev) {
+  if (nv <= 0) return MSP_SUCCESS;
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0) {  // empty vectors: every dot is +0
+    HIPCHK(hipMemsetAsync(out_dev, 0, (size_t)nv * sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
+  if (rc) return rc;
+  KTimer kt(c, MSP_KERNEL_MDOT, 8.0 * (double)n * (nv + 1));
+  for (int g0 = 0; g0 < nv; g0 += MSPI_MAX_GROUP) {
+    const int g = std::min(MSPI_MAX_GROUP, nv - g0);
+    VecGroup vg;
+    for (int j = 0; j < g; ++j) vg.p[j] = V[g0 + j];
+    KCHK(msk_dot_stage1(w, &vg, g, n, c->partial, nch, 0, c->stream));
+    KCHK(msk_dot_stage2(c->partial, nch, g, out_dev + g0, c->stream));
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_norm2sq(msp_ctx* c, const double* x, int64_t n, double* out_dev) {
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0) {
+    HIPCHK(hipMemsetAsync(out_dev, 0, sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
+  if (rc) return rc;
+  KTimer kt(c, MSP_KERNEL_NORM, 8.0 * (double)n);
+  VecGroup vg;
+  vg.p[0] = x;
+  KCHK(msk_dot_stage1(x, &vg, 1, n, c->partial, nch, 1, c->stream));
+  KCHK(msk_dot_stage2(c->partial, nch, 1, out_dev, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_maxpy(msp_ctx* c, double* w, int nv, const double* const* V, int64_t n, const double* alpha_host,
+                          const double* alpha_dev, int negate, int accumulate) {
+  if (nv <= 0 || n <= 0) return MSP_SUCCESS;
+  if (accumulate && nv > MSPI_MAX_GROUP) {
+    mspi_set_error(MSP_ERR_SUP, "accumulating MAXPY over more than %d vectors", MSPI_MAX_GROUP);
+    return MSP_ERR_SUP;
+  }
+  KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n * (nv + 2));
+  // Launches of up to 32 vectors compose exactly into PETSc's order (the
+  // nv & 3 leading vectors, then groups of four) when the FIRST launch takes
+  // nv mod 32 vectors: its own leading group is then nv & 3 and every later
+  // launch is a whole number of 4-groups.
+  int g = nv % MSPI_MAX_GROUP ? nv % MSPI_MAX_GROUP : MSPI_MAX_GROUP;
+  for (int g0 = 0; g0 < nv; g0 += g, g = MSPI_MAX_GROUP) {
+    VecGroup vg;
+    Coefs cf;
+    for (int j = 0; j < g; ++j) {
+      vg.p[j] = V[g0 + j];
+      cf.a[j] = alpha_host ? alpha_host[g0 + j] : 0.0;
+    }
+    KCHK(msk_maxpy(w, &vg, g, &cf, alpha_dev ? alpha_dev + g0 : nullptr, negate, n, accumulate, c->stream));
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_scale(msp_ctx* c, double* x, int64_t n, double alpha) {
+  KTimer kt(c, MSP_KERNEL_SCALE, 16.0 * (double)n);
+  KCHK(msk_blas1(MSK_SCALE, x, nullptr, nullptr, alpha, n, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_copy(msp_ctx* c, double* dst, const double* src, int64_t n) {
+  if (n <= 0 || dst == src) return MSP_SUCCESS;
+  KTimer kt(c, MSP_KERNEL_OTHER, 16.0 * (double)n);
+  HIPCHK(hipMemcpyAsync(dst, src, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_set(msp_ctx* c, double* x, int64_t n, double alpha) {
+  if (n <= 0) return MSP_SUCCESS;
+  KTimer kt(c, MSP_KERNEL_OTHER, 8.0 * (double)n);
+  KCHK(msk_blas1(MSK_SET, x, nullptr, nullptr, alpha, n, c->stream));
+  return MSP_SUCCESS;
+}
+
+// -------------------------------------------------------------------- Mat
+struct msp_mat {
+  msp_ctx* ctx = nullptr;
+  int32_t nrows = 0, ncols = 0;
+  int64_t nnz = 0;
+  int32_t* rowptr = nullptr;  // nrows+1 (or nlisted+1 when compressed)
+  int32_t* col = nullptr;     // nnz (+4 pad)
+  double* val = nullptr;      // nnz (+2 pad)
+  int32_t lds_cap = 0;        // LDS entries per 256-row block (0: direct kernel)
+  bool compressed = false;
+  int32_t nlisted = 0;
+  int32_t* row_ids = nullptr;
+};
+
+extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
+  *nr = A->nrows;
+  *nc = A->ncols;
+  return MSP_SUCCESS;
+}
+extern "C" msp_ctx* mspi_mat_ctx(const msp_mat* A) { return A->ctx; }
+
+static const int32_t kMaxLdsCap = 4096;  // 48 KiB of col+val per 256-row block
+
+static int32_t lds_cap_for(int64_t max_block_nnz) {
+  if (max_block_nnz + 8 > kMaxLdsCap) return 0;
+  return (int32_t)((max_block_nnz + 8 + 3) & ~(int64_t)3);
+}
+
+static int mat_alloc(msp_ctx* c, msp_mat* A, int64_t nptr, int64_t nnz) {
+  HIPCHK(hipMalloc((void**)&A->rowptr, (size_t)nptr * sizeof(int32_t)));
+  HIPCHK(hipMalloc((void**)&A->col, (size_t)(nnz + 4) * sizeof(int32_t)));
+  HIPCHK(hipMalloc((void**)&A->val, (size_t)(nnz + 2) * sizeof(double)));
+  HIPCHK(hipMemsetAsync(A->col + nnz, 0, 4 * sizeof(int32_t), c->stream));
+  HIPCHK(hipMemsetAsync(A->val + nnz, 0, 2 * sizeof(double), c->stream));
+  return MSP_SUCCESS;
+}
+
+static int check_csr(int32_t nrows, int32_t ncols, const int32_t* rowptr, const int32_t* col, int64_t* nnz_out,
+                     int64_t* max_block) {
+  ARGCHK(rowptr[0] == 0, MSP_ERR_ARG_WRONG, "rowptr[0] = %d, expected 0", rowptr[0]);
+  int64_t mb = 0;
+  for (int32_t r = 0; r < nrows; ++r) {
+    ARGCHK(rowptr[r + 1] >= rowptr[r], MSP_ERR_ARG_WRONG, "rowptr not monotone at row %d", r);
+    for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+      ARGCHK(col[k] >= 0 && col[k] < ncols, MSP_ERR_ARG_OUTOFRANGE, "column %d out of range [0,%d) in row %d",
+             col[k], ncols, r);
+      ARGCHK(k == rowptr[r] || col[k] > col[k - 1], MSP_ERR_ARG_WRONG,
+             "columns of row %d not strictly ascending (PETSc AIJ order)", r);
+    }
+    if ((r & 255) == 0) {
+      const int32_t r1 = std::min(r + 256, nrows);
+      mb = std::max<int64_t>(mb, (int64_t)rowptr[r1] - rowptr[r]);
+    }
+  }
+  *nnz_out = rowptr[nrows];
+  *max_block = mb;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_create_csr(msp_ctx* c, int32_t nrows, int32_t ncols, const int32_t* rowptr, const int32_t* col,
+                                  const double* val, msp_mat** out) {
+  ARGCHK(c && out && rowptr, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(nrows >= 0 && ncols >= 0, MSP_ERR_ARG_SIZ, "negative size %d x %d", nrows, ncols);
+  int64_t nnz = 0, mb = 0;
+  int rc = check_csr(nrows, ncols, rowptr, col, &nnz, &mb);
+  if (rc) return rc;
+  ARGCHK(nnz == 0 || (col && val), MSP_ERR_ARG_NULL, "col/val NULL with nnz=%lld", (long long)nnz);
+  msp_mat* A = new msp_mat();
+  A->ctx = c;
+  A->nrows = nrows;
+  A->ncols = ncols;
+  A->nnz = nnz;
+  A->lds_cap = lds_cap_for(mb);
+  if ((rc = mat_alloc(c, A, (int64_t)nrows + 1, nnz))) {
+    msp_mat_destroy(&A);
+    return rc;
+  }
+  HIPCHK(hipMemcpyAsync(A->rowptr, rowptr, ((size_t)nrows + 1) * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  if (nnz) {
+    HIPCHK(hipMemcpyAsync(A->col, col, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(A->val, val, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));  // host arrays stay the caller's
+  *out = A;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_create_csr_rows(msp_ctx* c, int32_t nrows, int32_t ncols, int32_t nlisted,
+                                       const int32_t* row_ids, const int32_t* rowptr, const int32_t* col,
+                                       const double* val, msp_mat** out) {
+  ARGCHK(c && out && (nlisted == 0 || (row_ids && rowptr)), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(nrows >= 0 && ncols >= 0 && nlisted >= 0 && nlisted <= nrows, MSP_ERR_ARG_SIZ, "bad sizes");
+  for (int32_t k = 0; k < nlisted; ++k) {
+    ARGCHK(row_ids[k] >= 0 && row_ids[k] < nrows, MSP_ERR_ARG_OUTOFRANGE, "row id %d out of range", row_ids[k]);
+    ARGCHK(k == 0 || row_ids[k] > row_ids[k - 1], MSP_ERR_ARG_WRONG, "row ids not strictly ascending");
+  }
+  int64_t nnz = 0, mb = 0;
+  int32_t zero = 0;
+  int rc = check_csr(nlisted, ncols, nlisted ? rowptr : &zero, col, &nnz, &mb);
+  if (rc) return rc;
+  msp_mat* A = new msp_mat();
+  A->ctx = c;
+  A->nrows = nrows;
+  A->ncols = ncols;
+  A->nnz = nnz;
+  A->compressed = true;
+  A->nlisted = nlisted;
+  if ((rc = mat_alloc(c, A, (int64_t)nlisted + 1, nnz))) {
+    msp_mat_destroy(&A);
+    return rc;
+  }
+  HIPCHK(hipMalloc((void**)&A->row_ids, (size_t)(nlisted + 1) * sizeof(int32_t)));
+  if (nlisted) {
+    HIPCHK(hipMemcpyAsync(A->row_ids, row_ids, (size_t)nlisted * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(A->rowptr, rowptr, ((size_t)nlisted + 1) * sizeof(int32_t), hipMemcpyHostToDevice,
+                          c->stream));
+  } else {
+    HIPCHK(hipMemsetAsync(A->rowptr, 0, sizeof(int32_t), c->stream));
+  }
+  if (nnz) {
+    HIPCHK(hipMemcpyAsync(A->col, col, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(A->val, val, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *out = A;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_create_box_stencil(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, msp_mat** out) {
+  ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(dim == 2 || dim == 3, MSP_ERR_ARG_WRONG, "dim must be 2 or 3, got %d", dim);
+  if (dim == 2) nz = 1;
+  ARGCHK(nx > 0 && ny > 0 && nz > 0, MSP_ERR_ARG_SIZ, "box %d x %d x %d", nx, ny, nz);
+  const int64_t nrows = (int64_t)nx * ny * nz;
+  const int64_t deg = dim == 3 ? 7 : 5;
+  ARGCHK(nrows <= INT32_MAX && deg * nrows <= INT32_MAX, MSP_ERR_ARG_OUTOFRANGE,
+         "box of %lld rows exceeds 32-bit PetscInt indexing", (long long)nrows);
+  msp_mat* A = new msp_mat();
+  A->ctx = c;
+  A->nrows = (int32_t)nrows;
+  A->ncols = (int32_t)nrows;
+  // exact nnz: deg*N minus missing neighbours on each face
+  int64_t nnz = deg * nrows - 2 * (nrows / nx) - 2 * (nrows / ny);
+  if (dim == 3) nnz -= 2 * (nrows / nz);
+  A->nnz = nnz;
+  A->lds_cap = lds_cap_for(deg * 256);
+  int rc = mat_alloc(c, A, nrows + 1, nnz);
+  if (rc) {
+    msp_mat_destroy(&A);
+    return rc;
+  }
+  KCHK(msk_box_stencil(dim, nx, ny, nz, nrows, A->rowptr, A->col, A->val, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *out = A;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_destroy(msp_mat** pA) {
+  if (!pA || !*pA) return MSP_SUCCESS;
+  msp_mat* A = *pA;
+  if (A->ctx && A->ctx->stream) (void)hipStreamSynchronize(A->ctx->stream);
+  if (A->rowptr) (void)hipFree(A->rowptr);
+  if (A->col) (void)hipFree(A->col);
+  if (A->val) (void)hipFree(A->val);
+  if (A->row_ids) (void)hipFree(A->row_ids);
+  delete A;
+  *pA = nullptr;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_get_info(const msp_mat* A, int32_t* nrows, int32_t* ncols, int64_t* nnz) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
+  if (nrows) *nrows = A->nrows;
+  if (ncols) *ncols = A->ncols;
+  if (nnz) *nnz = A->nnz;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_get_csr(const msp_mat* A, int32_t* rowptr, int32_t* col, double* val) {
+  ARGCHK(A && rowptr, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(!A->compressed, MSP_ERR_SUP, "msp_mat_get_csr on a row-compressed matrix");
+  hipStream_t s = A->ctx->stream;
+  HIPCHK(hipMemcpyAsync(rowptr, A->rowptr, ((size_t)A->nrows + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (A->nnz) {
+    ARGCHK(col && val, MSP_ERR_ARG_NULL, "col/val NULL");
+    HIPCHK(hipMemcpyAsync(col, A->col, (size_t)A->nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(val, A->val, (size_t)A->nnz * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  return MSP_SUCCESS;
+}
+
+static double spmv_bytes(const msp_mat* A, bool resid) {
+  const double rows = A->compressed ? (double)A->nlisted : (double)A->nrows;
+  const double xs = A->compressed ? (double)A->nnz : (double)A->ncols;
+  return 12.0 * (double)A->nnz + 4.0 * (rows + 1) + 8.0 * xs + 8.0 * rows + (resid ? 8.0 * rows : 0.0);
+}
+
+static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bool resid) {
+  msp_ctx* c = A->ctx;
+  KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, resid));
+  if (A->compressed) {
+    // rows that hold no entries: y = 0 (MatMult) or r = b - 0 = b (MatResidual)
+    if (resid) {
+      if (y != b) HIPCHK(hipMemcpyAsync(y, b, (size_t)A->nrows * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    } else {
+      KCHK(msk_blas1(MSK_SET, y, nullptr, nullptr, 0.0, A->nrows, c->stream));
+    }
+    KCHK(msk_spmv_rows(A->nlisted, A->row_ids, A->rowptr, A->col, A->val, x, b, y, resid ? 1 : 0, c->stream));
+    return MSP_SUCCESS;
+  }
+  KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, b, y, A->lds_cap, resid ? 1 : 0, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_spmv(msp_mat* A, const double* x, double* y) { return spmv_impl(A, nullptr, x, y, false); }
+extern "C" int mspi_residual(msp_mat* A, const double* b, const double* x, double* r) {
+  return spmv_impl(A, b, x, r, true);
+}
+
+static int vec_ok(const msp_vec* v, const char* name) {
+  if (!v) {
+    mspi_set_error(MSP_ERR_ARG_NULL, "%s is NULL", name);
+    return MSP_ERR_ARG_NULL;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_mult(msp_mat* A, const msp_vec* x, msp_vec* y) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
+  int rc;
+  if ((rc = vec_ok(x, "x")) || (rc = vec_ok(y, "y"))) return rc;
+  ARGCHK(x->n == A->ncols && y->n == A->nrows, MSP_ERR_ARG_SIZ,
+         "MatMult sizes: A %d x %d, x %lld, y %lld", A->nrows, A->ncols, (long long)x->n, (long long)y->n);
+  ARGCHK(x->d != y->d, MSP_ERR_ARG_WRONG, "x and y must be different vectors");
+  return mspi_spmv(A, x->d, y->d);
+}
+
+extern "C" int msp_mat_residual(msp_mat* A, const msp_vec* b, const msp_vec* x, msp_vec* r) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
+  int rc;
+  if ((rc = vec_ok(b, "b")) || (rc = vec_ok(x, "x")) || (rc = vec_ok(r, "r"))) return rc;
+  ARGCHK(x->n == A->ncols && b->n == A->nrows && r->n == A->nrows, MSP_ERR_ARG_SIZ,
+         "MatResidual sizes: A %d x %d, b %lld, x %lld, r %lld", A->nrows, A->ncols, (long long)b->n,
+         (long long)x->n, (long long)r->n);
+  ARGCHK(x->d != r->d, MSP_ERR_ARG_WRONG, "x and r must be different vectors");
+  return mspi_residual(A, b->d, x->d, r->d);
+}
+
+// -------------------------------------------------------------------- Vec
+extern "C" int msp_vec_create(msp_ctx* c, int64_t n, msp_vec** out) {
+  ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(n >= 0, MSP_ERR_ARG_SIZ, "negative vector size %lld", (long long)n);
+  msp_vec* v = new msp_vec();
+  v->ctx = c;
+  v->n = n;
+  v->owned = 1;
+  // pad to 512 doubles so every vector is 4 KiB aligned and double2 loads stay in bounds
+  const size_t bytes = (size_t)((n + 511) / 512 * 512 + 512) * sizeof(double);
+  if (hipMalloc((void**)&v->d, bytes) != hipSuccess) {
+    delete v;
+    mspi_set_error(MSP_ERR_MEM, "hipMalloc of a %lld-entry vector failed", (long long)n);
+    return MSP_ERR_MEM;
+  }
+  HIPCHK(hipMemsetAsync(v->d, 0, bytes, c->stream));
+  *out = v;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_create_with_array(msp_ctx* c, int64_t n, double* dptr, msp_vec** out) {
+  ARGCHK(c && out && (dptr || n == 0), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(n >= 0, MSP_ERR_ARG_SIZ, "negative vector size");
+  ARGCHK(((uintptr_t)dptr & 15) == 0, MSP_ERR_ARG_WRONG, "device array must be 16-byte aligned");
+  msp_vec* v = new msp_vec();
+  v->ctx = c;
+  v->n = n;
+  v->d = dptr;
+  v->owned = 0;
+  *out = v;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_destroy(msp_vec** pv) {
+  if (!pv || !*pv) return MSP_SUCCESS;
+  msp_vec* v = *pv;
+  if (v->owned && v->d) {
+    (void)hipStreamSynchronize(v->ctx->stream);
+    (void)hipFree(v->d);
+  }
+  delete v;
+  *pv = nullptr;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_get_size(const msp_vec* v, int64_t* n) {
+  ARGCHK(v && n, MSP_ERR_ARG_NULL, "NULL argument");
+  *n = v->n;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_get_array(msp_vec* v, double** p) {
+  ARGCHK(v && p, MSP_ERR_ARG_NULL, "NULL argument");
+  *p = v->d;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_set_values(msp_vec* v, int64_t off, int64_t n, const double* host) {
+  ARGCHK(v && (host || n == 0), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(off >= 0 && n >= 0 && off + n <= v->n, MSP_ERR_ARG_OUTOFRANGE, "range [%lld,%lld) outside [0,%lld)",
+         (long long)off, (long long)(off + n), (long long)v->n);
+  if (n == 0) return MSP_SUCCESS;
+  HIPCHK(hipMemcpyAsync(v->d + off, host, (size_t)n * sizeof(double), hipMemcpyHostToDevice, v->ctx->stream));
+  HIPCHK(hipStreamSynchronize(v->ctx->stream));  // the host buffer stays the caller's
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_get_values(const msp_vec* v, int64_t off, int64_t n, double* host) {
+  ARGCHK(v && (host || n == 0), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(off >= 0 && n >= 0 && off + n <= v->n, MSP_ERR_ARG_OUTOFRANGE, "range [%lld,%lld) outside [0,%lld)",
+         (long long)off, (long long)(off + n), (long long)v->n);
+  if (n == 0) return MSP_SUCCESS;
+  HIPCHK(hipMemcpyAsync(host, v->d + off, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, v->ctx->stream));
+  HIPCHK(hipStreamSynchronize(v->ctx->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_copy_range(const msp_vec* src, int64_t so, msp_vec* dst, int64_t dof, int64_t n) {
+  ARGCHK(src && dst, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(n >= 0 && so >= 0 && dof >= 0 && so + n <= src->n && dof + n <= dst->n, MSP_ERR_ARG_OUTOFRANGE,
+         "copy_range out of bounds");
+  if (n == 0) return MSP_SUCCESS;
+  return mspi_copy(dst->ctx, dst->d + dof, src->d + so, n);
+}
+
+extern "C" int msp_vec_set(msp_vec* v, double a) {
+  int rc = vec_ok(v, "v");
+  if (rc) return rc;
+  return mspi_set(v->ctx, v->d, v->n, a);
+}
+
+extern "C" int msp_vec_copy(const msp_vec* x, msp_vec* y) {
+  int rc;
+  if ((rc = vec_ok(x, "x")) || (rc = vec_ok(y, "y"))) return rc;
+  ARGCHK(x->n == y->n, MSP_ERR_ARG_SIZ, "VecCopy sizes %lld vs %lld", (long long)x->n, (long long)y->n);
+  return mspi_copy(y->ctx, y->d, x->d, x->n);
+}
+
+extern "C" int msp_vec_scale(msp_vec* x, double a) {
+  int rc = vec_ok(x, "x");
+  if (rc) return rc;
+  if (a == 1.0) return MSP_SUCCESS;  // VecScale returns early for alpha == 1
+  return mspi_scale(x->ctx, x->d, x->n, a);
+}
+
+static int blas1(msp_ctx* c, int op, double* y, const double* x, const double* z, double a, int64_t n, double bytes) {
+  KTimer kt(c, MSP_KERNEL_OTHER, bytes);
+  KCHK(msk_blas1(op, y, x, z, a, n, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_axpy(msp_vec* y, double a, const msp_vec* x) {
+  int rc;
+  if ((rc = vec_ok(x, "x")) || (rc = vec_ok(y, "y"))) return rc;
+  ARGCHK(x->n == y->n, MSP_ERR_ARG_SIZ, "VecAXPY sizes");
+  if (a == 0.0) return MSP_SUCCESS;  // daxpy returns for da == 0
+  return blas1(y->ctx, MSK_AXPY, y->d, x->d, nullptr, a, y->n, 24.0 * y->n);
+}
+
+extern "C" int msp_vec_aypx(msp_vec* y, double b, const msp_vec* x) {
+  int rc;
+  if ((rc = vec_ok(x, "x")) || (rc = vec_ok(y, "y"))) return rc;
+  ARGCHK(x->n == y->n, MSP_ERR_ARG_SIZ, "VecAYPX sizes");
+  return blas1(y->ctx, MSK_AYPX, y->d, x->d, nullptr, b, y->n, 24.0 * y->n);
+}
+
+extern "C" int msp_vec_waxpy(msp_vec* w, double a, const msp_vec* x, const msp_vec* y) {
+  int rc;
+  if ((rc = vec_ok(w, "w")) || (rc = vec_ok(x, "x")) || (rc = vec_ok(y, "y"))) return rc;
+  ARGCHK(x->n == y->n && w->n == x->n, MSP_ERR_ARG_SIZ, "VecWAXPY sizes");
+  int op = a == 1.0 ? MSK_WAXPY_P1 : (a == -1.0 ? MSK_WAXPY_M1 : MSK_WAXPY);
+  if (a == 0.0) return mspi_copy(w->ctx, w->d, y->d, w->n);
+  return blas1(w->ctx, op, w->d, x->d, y->d, a, w->n, 24.0 * w->n);
+}
+
+extern "C" int msp_vec_dot(const msp_vec* x, const msp_vec* y, double* val) {
+  int rc;
+  if ((rc = vec_ok(x, "x")) || (rc = vec_ok(y, "y"))) return rc;
+  ARGCHK(val, MSP_ERR_ARG_NULL, "val is NULL");
+  ARGCHK(x->n == y->n, MSP_ERR_ARG_SIZ, "VecDot sizes");
+  msp_ctx* c = x->ctx;
+  const double* V[1] = {y->d};
+  if ((rc = mspi_mdot(c, x->d, 1, V, x->n, c->dscratch))) return rc;
+  if ((rc = mspi_d2h_sync(c, c->hscratch, c->dscratch, sizeof(double)))) return rc;
+  *val = c->hscratch[0];
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_norm(const msp_vec* x, double* val) {
+  int rc = vec_ok(x, "x");
+  if (rc) return rc;
+  ARGCHK(val, MSP_ERR_ARG_NULL, "val is NULL");
+  msp_ctx* c = x->ctx;
+  if ((rc = mspi_norm2sq(c, x->d, x->n, c->dscratch))) return rc;
+  if ((rc = mspi_d2h_sync(c, c->hscratch, c->dscratch, sizeof(double)))) return rc;
+  *val = sqrt(c->hscratch[0]);
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_normalize(msp_vec* x, double* val) {
+  double t = 0.0;
+  int rc = msp_vec_norm(x, &t);
+  if (rc) return rc;
+  if (t != 0.0 && !std::isnan(t) && !std::isinf(t)) {
+    const double s = 1.0 / t;
+    if ((rc = mspi_scale(x->ctx, x->d, x->n, s))) return rc;
+  }
+  if (val) *val = t;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_mdot(const msp_vec* x, int nv, const msp_vec* const* y, double* val) {
+  int rc = vec_ok(x, "x");
+  if (rc) return rc;
+  ARGCHK(nv >= 0 && (nv == 0 || (y && val)), MSP_ERR_ARG_NULL, "NULL argument");
+  std::vector<const double*> V(nv);
+  for (int j = 0; j < nv; ++j) {
+    if ((rc = vec_ok(y[j], "y[j]"))) return rc;
+    ARGCHK(y[j]->n == x->n, MSP_ERR_ARG_SIZ, "VecMDot sizes");
+    V[j] = y[j]->d;
+  }
+  msp_ctx* c = x->ctx;
+  const int step = kScratch - 8;
+  for (int g0 = 0; g0 < nv; g0 += step) {
+    const int g = std::min(step, nv - g0);
+    if ((rc = mspi_mdot(c, x->d, g, V.data() + g0, x->n, c->dscratch))) return rc;
+    if ((rc = mspi_d2h_sync(c, c->hscratch, c->dscratch, (size_t)g * sizeof(double)))) return rc;
+    memcpy(val + g0, c->hscratch, (size_t)g * sizeof(double));
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_vec_maxpy(msp_vec* y, int nv, const double* alpha, const msp_vec* const* x) {
+  int rc = vec_ok(y, "y");
+  if (rc) return rc;
+  ARGCHK(nv >= 0 && (nv == 0 || (x && alpha)), MSP_ERR_ARG_NULL, "NULL argument");
+  std::vector<const double*> V(nv);
+  for (int j = 0; j < nv; ++j) {
+    if ((rc = vec_ok(x[j], "x[j]"))) return rc;
+    ARGCHK(x[j]->n == y->n, MSP_ERR_ARG_SIZ, "VecMAXPY sizes");
+    ARGCHK(((uintptr_t)x[j]->d & 15) == 0, MSP_ERR_ARG_WRONG, "unaligned vector");
+    V[j] = x[j]->d;
+  }
+  return mspi_maxpy(y->ctx, y->d, nv, V.data(), y->n, alpha, nullptr, 0, 0);
+}

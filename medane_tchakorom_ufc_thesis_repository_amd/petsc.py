@@ -1,0 +1,436 @@
+"""PETSc-style host objects over the HIP C ABI (include/msplit.h).
+
+This mirrors the slice of PETSc 3.22.1's Mat/Vec/KSP/options API that the
+reference's drivers and glue use on the inner-solve path
+(src/utils/utils.c:139-168, :512-541, :943-970; drivers' PetscOptionsGet*):
+same object roles, same option keys and prefixes, same error behaviour
+(nonzero PETSc error numbers raise).  Every numeric operation runs in
+libmsplit_hip.so on the GPU; nothing here computes on vector data.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import shlex
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import KspOpts, MsplitError, call
+
+PETSC_ERR_SUP = 56
+PETSC_ERR_ARG_WRONG = 62
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+# --------------------------------------------------------------------- options
+class Options:
+    """The PETSc options database (PetscOptionsGetInt/Real/String/Bool)."""
+
+    def __init__(self, args: Iterable[str] | str | None = None):
+        self._db: dict[str, str | None] = {}
+        if args is None:
+            return
+        toks = shlex.split(args) if isinstance(args, str) else list(args)
+        i = 0
+        while i < len(toks):
+            t = toks[i]
+            if not t.startswith("-") or _is_number(t):
+                raise MsplitError(PETSC_ERR_ARG_WRONG, f"stray option value {t!r}")
+            key = t.lstrip("-")
+            if i + 1 < len(toks) and (not toks[i + 1].startswith("-") or _is_number(toks[i + 1])):
+                self._db[key] = toks[i + 1]
+                i += 2
+            else:
+                self._db[key] = None
+                i += 1
+
+    def set(self, key: str, value=None):
+        self._db[key.lstrip("-")] = None if value is None else str(value)
+
+    def has(self, key: str, prefix: str | None = None) -> bool:
+        return ((prefix or "") + key) in self._db
+
+    def get_string(self, key, default=None, prefix=None):
+        k = (prefix or "") + key
+        if k not in self._db:
+            return default
+        v = self._db[k]
+        return default if v is None else v
+
+    def get_int(self, key, default=None, prefix=None):
+        v = self.get_string(key, None, prefix)
+        return default if v is None else int(float(v)) if "e" in v.lower() else int(v)
+
+    def get_real(self, key, default=None, prefix=None):
+        v = self.get_string(key, None, prefix)
+        return default if v is None else float(v)
+
+    def get_bool(self, key, default=False, prefix=None):
+        k = (prefix or "") + key
+        if k not in self._db:
+            return default
+        v = self._db[k]
+        if v is None:
+            return True
+        return v.lower() in ("1", "true", "yes", "on")
+
+    def keys(self):
+        return list(self._db)
+
+
+def _is_number(s: str) -> bool:
+    try:
+        float(s)
+        return True
+    except ValueError:
+        return False
+
+
+# --------------------------------------------------------------------- context
+class Context:
+    """One GPU: device id + the HIP stream every object's work is ordered on."""
+
+    def __init__(self, device: int = 0, stream: int | None = None, timing: bool = False):
+        L = _lib.load()
+        h = C.c_void_p()
+        call("msp_ctx_create", device, C.c_void_p(stream) if stream else None, C.byref(h))
+        self.h = h
+        self.device = device
+        self._L = L
+        if timing:
+            self.set_timing(True)
+
+    def synchronize(self):
+        call("msp_ctx_synchronize", self.h)
+
+    def set_timing(self, on: bool):
+        call("msp_ctx_set_timing", self.h, 1 if on else 0)
+
+    def reset_kernel_stats(self):
+        call("msp_ctx_reset_kernel_stats", self.h)
+
+    def kernel_stats(self) -> dict:
+        out = {}
+        for name, cls in _lib.KERNEL_CLASSES.items():
+            n = C.c_int64()
+            ms = C.c_double()
+            by = C.c_double()
+            call("msp_ctx_get_kernel_stats", self.h, cls, C.byref(n), C.byref(ms), C.byref(by))
+            out[name] = {"launches": n.value, "ms": ms.value, "bytes": by.value}
+        return out
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_ctx_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    n = C.c_int()
+    call("msp_get_device_count", C.byref(n))
+    return n.value
+
+
+# ------------------------------------------------------------------------- Vec
+class Vec:
+    """A device vector (VecCreate + VecSetSizes, utils.c:157-168)."""
+
+    def __init__(self, ctx: Context, n: int, device_ptr: int | None = None):
+        self.ctx = ctx
+        h = C.c_void_p()
+        if device_ptr is None:
+            call("msp_vec_create", ctx.h, int(n), C.byref(h))
+        else:
+            call("msp_vec_create_with_array", ctx.h, int(n), C.c_void_p(device_ptr), C.byref(h))
+        self.h = h
+        self.n = int(n)
+
+    @classmethod
+    def from_array(cls, ctx: Context, a) -> "Vec":
+        a = np.ascontiguousarray(a, np.float64)
+        v = cls(ctx, a.size)
+        v.set_values(a)
+        return v
+
+    def duplicate(self) -> "Vec":                                  # VecDuplicate
+        return Vec(self.ctx, self.n)
+
+    def get_size(self) -> int:
+        return self.n
+
+    def device_ptr(self) -> int:
+        p = C.c_void_p()
+        call("msp_vec_get_array", self.h, C.byref(p))
+        return p.value or 0
+
+    def set_values(self, a, offset: int = 0):                      # VecSetValues (contiguous)
+        a = np.ascontiguousarray(a, np.float64)
+        call("msp_vec_set_values", self.h, int(offset), a.size, _dp(a))
+
+    def get_array(self, offset: int = 0, n: int | None = None) -> np.ndarray:  # VecGetArrayRead (copy)
+        n = self.n - offset if n is None else n
+        out = np.empty(n)
+        call("msp_vec_get_values", self.h, int(offset), int(n), _dp(out))
+        return out
+
+    def copy_range_to(self, src_off: int, dst: "Vec", dst_off: int, n: int):
+        call("msp_vec_copy_range", self.h, int(src_off), dst.h, int(dst_off), int(n))
+
+    def set(self, alpha: float):                                   # VecSet
+        call("msp_vec_set", self.h, float(alpha))
+
+    def copy(self, y: "Vec"):                                      # VecCopy(self, y)
+        call("msp_vec_copy", self.h, y.h)
+
+    def scale(self, alpha: float):                                 # VecScale
+        call("msp_vec_scale", self.h, float(alpha))
+
+    def axpy(self, alpha: float, x: "Vec"):                        # VecAXPY(self, alpha, x)
+        call("msp_vec_axpy", self.h, float(alpha), x.h)
+
+    def aypx(self, beta: float, x: "Vec"):                         # VecAYPX(self, beta, x)
+        call("msp_vec_aypx", self.h, float(beta), x.h)
+
+    def waxpy(self, alpha: float, x: "Vec", y: "Vec"):             # VecWAXPY(self, alpha, x, y)
+        call("msp_vec_waxpy", self.h, float(alpha), x.h, y.h)
+
+    def dot(self, y: "Vec") -> float:                              # VecDot
+        v = C.c_double()
+        call("msp_vec_dot", self.h, y.h, C.byref(v))
+        return v.value
+
+    def norm(self) -> float:                                       # VecNorm(NORM_2)
+        v = C.c_double()
+        call("msp_vec_norm", self.h, C.byref(v))
+        return v.value
+
+    def normalize(self) -> float:                                  # VecNormalize
+        v = C.c_double()
+        call("msp_vec_normalize", self.h, C.byref(v))
+        return v.value
+
+    def mdot(self, ys: Sequence["Vec"]) -> np.ndarray:             # VecMDot
+        out = np.zeros(len(ys))
+        arr = (C.c_void_p * max(len(ys), 1))(*[y.h.value for y in ys])
+        call("msp_vec_mdot", self.h, len(ys), arr, _dp(out))
+        return out
+
+    def maxpy(self, alpha, xs: Sequence["Vec"]):                   # VecMAXPY
+        a = np.ascontiguousarray(alpha, np.float64)
+        if a.size != len(xs):
+            raise MsplitError(60, "VecMAXPY: len(alpha) != len(x)")
+        arr = (C.c_void_p * max(len(xs), 1))(*[x.h.value for x in xs])
+        call("msp_vec_maxpy", self.h, len(xs), _dp(a), arr)
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_vec_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------- Mat
+class Mat:
+    """A device AIJ (CSR) matrix."""
+
+    def __init__(self, ctx: Context, h: C.c_void_p, keep=None):
+        self.ctx = ctx
+        self.h = h
+        self._keep = keep
+        nr, nc, nnz = C.c_int32(), C.c_int32(), C.c_int64()
+        call("msp_mat_get_info", h, C.byref(nr), C.byref(nc), C.byref(nnz))
+        self.shape = (nr.value, nc.value)
+        self.nnz = nnz.value
+
+    @classmethod
+    def from_csr(cls, ctx: Context, nrows: int, ncols: int, rowptr, col, val) -> "Mat":
+        rp = np.ascontiguousarray(rowptr, np.int32)
+        cl = np.ascontiguousarray(col, np.int32)
+        vl = np.ascontiguousarray(val, np.float64)
+        if rp.size != nrows + 1:
+            raise MsplitError(60, f"rowptr has {rp.size} entries, expected {nrows + 1}")
+        h = C.c_void_p()
+        call("msp_mat_create_csr", ctx.h, int(nrows), int(ncols), _ip(rp), _ip(cl), _dp(vl), C.byref(h))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_csr_rows(cls, ctx: Context, nrows: int, ncols: int, row_ids, rowptr, col, val) -> "Mat":
+        ri = np.ascontiguousarray(row_ids, np.int32)
+        rp = np.ascontiguousarray(rowptr, np.int32) if len(row_ids) else np.zeros(1, np.int32)
+        cl = np.ascontiguousarray(col, np.int32) if len(col) else np.zeros(1, np.int32)
+        vl = np.ascontiguousarray(val, np.float64) if len(val) else np.zeros(1)
+        h = C.c_void_p()
+        call("msp_mat_create_csr_rows", ctx.h, int(nrows), int(ncols), int(ri.size), _ip(ri), _ip(rp), _ip(cl),
+             _dp(vl), C.byref(h))
+        return cls(ctx, h)
+
+    @classmethod
+    def box_stencil(cls, ctx: Context, dim: int, nx: int, ny: int, nz: int = 1) -> "Mat":
+        h = C.c_void_p()
+        call("msp_mat_create_box_stencil", ctx.h, int(dim), int(nx), int(ny), int(nz), C.byref(h))
+        return cls(ctx, h)
+
+    def get_csr(self):
+        rp = np.empty(self.shape[0] + 1, np.int32)
+        cl = np.empty(max(self.nnz, 1), np.int32)
+        vl = np.empty(max(self.nnz, 1))
+        call("msp_mat_get_csr", self.h, _ip(rp), _ip(cl), _dp(vl))
+        return rp, cl[: self.nnz], vl[: self.nnz]
+
+    def create_vecs(self):                                          # MatCreateVecs
+        return Vec(self.ctx, self.shape[1]), Vec(self.ctx, self.shape[0])
+
+    def mult(self, x: Vec, y: Vec):                                 # MatMult
+        call("msp_mat_mult", self.h, x.h, y.h)
+
+    def residual(self, b: Vec, x: Vec, r: Vec):                     # MatResidual
+        call("msp_mat_residual", self.h, b.h, x.h, r.h)
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_mat_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------- KSP
+class KSP:
+    """KSPGMRES with PCNONE (the reference's canonical inner solver,
+    running_bulk_test_g5k:64-70; initializeKSP, utils.c:512-541)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        call("msp_ksp_create", ctx.h, C.byref(h))
+        self.h = h
+        self.prefix = ""
+        self.A: Mat | None = None
+
+    # -- configuration
+    def get_opts(self) -> KspOpts:
+        o = KspOpts()
+        call("msp_ksp_get_opts", self.h, C.byref(o))
+        return o
+
+    def _set(self, **kw):
+        o = self.get_opts()
+        for k, v in kw.items():
+            setattr(o, k, v)
+        call("msp_ksp_set_opts", self.h, C.byref(o))
+
+    def set_operators(self, A: Mat):                                # KSPSetOperators
+        self.A = A
+        call("msp_ksp_set_operators", self.h, A.h)
+
+    def set_options_prefix(self, prefix: str | None):                # KSPSetOptionsPrefix
+        self.prefix = prefix or ""
+
+    def set_initial_guess_nonzero(self, flag: bool):                # KSPSetInitialGuessNonzero
+        self._set(guess_nonzero=1 if flag else 0)
+
+    def converged_default_set_uirnorm(self):                        # KSPConvergedDefaultSetUIRNorm
+        self._set(uirnorm=1)
+
+    def set_tolerances(self, rtol=None, abstol=None, divtol=None, max_it=None):   # KSPSetTolerances
+        kw = {}
+        if rtol is not None:
+            kw["rtol"] = float(rtol)
+        if abstol is not None:
+            kw["abstol"] = float(abstol)
+        if divtol is not None:
+            kw["divtol"] = float(divtol)
+        if max_it is not None:
+            kw["max_it"] = int(max_it)
+        self._set(**kw)
+
+    def gmres_set_restart(self, m: int):                            # KSPGMRESSetRestart
+        self._set(restart=int(m))
+
+    def set_from_options(self, opts: Options):                      # KSPSetFromOptions
+        p = self.prefix
+        kt = opts.get_string("ksp_type", "gmres", p)
+        if kt.lower() != "gmres":
+            raise MsplitError(PETSC_ERR_SUP, f"-{p}ksp_type {kt}: only gmres is implemented on the MI355X path")
+        pt = opts.get_string("pc_type", "none", p)
+        if pt.lower() != "none":
+            raise MsplitError(PETSC_ERR_SUP, f"-{p}pc_type {pt}: only none is implemented on the MI355X path")
+        if opts.has("ksp_gmres_modifiedgramschmidt", p):
+            raise MsplitError(PETSC_ERR_SUP, "modified Gram-Schmidt is not implemented (CGS only)")
+        rt = opts.get_string("ksp_gmres_cgs_refinement_type", "refine_never", p)
+        if rt.lower() != "refine_never":
+            raise MsplitError(PETSC_ERR_SUP, f"CGS refinement {rt} not implemented (REFINE_NEVER only)")
+        nt = opts.get_string("ksp_norm_type", "preconditioned", p).lower()
+        if nt not in ("preconditioned", "unpreconditioned"):
+            raise MsplitError(PETSC_ERR_SUP, f"-{p}ksp_norm_type {nt} not supported by GMRES")
+        o = self.get_opts()
+        o.restart = opts.get_int("ksp_gmres_restart", o.restart, p)
+        o.max_it = opts.get_int("ksp_max_it", o.max_it, p)
+        o.rtol = opts.get_real("ksp_rtol", o.rtol, p)
+        o.abstol = opts.get_real("ksp_atol", o.abstol, p)
+        o.divtol = opts.get_real("ksp_divtol", o.divtol, p)
+        o.haptol = opts.get_real("ksp_gmres_haptol", o.haptol, p)
+        o.breakdowntol = opts.get_real("ksp_gmres_breakdown_tolerance", o.breakdowntol, p)
+        if opts.get_bool("ksp_converged_use_initial_residual_norm", False, p):
+            o.uirnorm = 1
+        if opts.has("ksp_initial_guess_nonzero", p):
+            o.guess_nonzero = 1 if opts.get_bool("ksp_initial_guess_nonzero", False, p) else 0
+        call("msp_ksp_set_opts", self.h, C.byref(o))
+
+    def set_up(self):
+        call("msp_ksp_set_up", self.h)
+
+    # -- solve
+    def solve(self, b: Vec, x: Vec):                                # KSPSolve
+        call("msp_ksp_solve", self.h, b.h, x.h)
+
+    def get_iteration_number(self) -> int:
+        v = C.c_int32()
+        call("msp_ksp_get_iteration_number", self.h, C.byref(v))
+        return v.value
+
+    def get_residual_norm(self) -> float:
+        v = C.c_double()
+        call("msp_ksp_get_residual_norm", self.h, C.byref(v))
+        return v.value
+
+    def get_converged_reason(self) -> int:
+        v = C.c_int32()
+        call("msp_ksp_get_converged_reason", self.h, C.byref(v))
+        return v.value
+
+    def get_residual_history(self) -> np.ndarray:
+        p = C.POINTER(C.c_double)()
+        n = C.c_int32()
+        call("msp_ksp_get_residual_history", self.h, C.byref(p), C.byref(n))
+        return np.ctypeslib.as_array(p, shape=(n.value,)).copy() if n.value else np.zeros(0)
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_ksp_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass

@@ -1,0 +1,653 @@
+/*
+ * oracle.c -- CPU restatement of the reference's GMRES inner-solve path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Compiled with -ffp-contract=off so
+ * that every a*b+c is two roundings, as in PETSc's Seq kernels built without
+ * FMA contraction.
+ *
+ * PETSc 3.22.1 is an external, un-vendored dependency of the reference
+ * (README.md:31, makefile:36); its KSPGMRES behaviour is restated here from
+ * that release's published semantics.  Functions carry the reference call site
+ * they stand in for.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PMAX(a, b) ((a) < (b) ? (b) : (a)) /* PetscMax */
+#define ORC_OK 0
+#define ORC_ERR_MEM 55
+#define ORC_ERR_ARG 62
+
+void orc_csr_free(orc_csr *A) {
+  if (!A) return;
+  free(A->rowptr);
+  free(A->col);
+  free(A->val);
+  memset(A, 0, sizeof(*A));
+}
+
+static int csr_alloc(orc_csr *A, int64_t nrows, int64_t ncols, int64_t nnz_cap) {
+  memset(A, 0, sizeof(*A));
+  if (nrows < 0 || nrows > INT32_MAX || ncols < 0 || ncols > INT32_MAX) return ORC_ERR_ARG;
+  A->nrows = (int32_t)nrows;
+  A->ncols = (int32_t)ncols;
+  A->rowptr = (int32_t *)calloc((size_t)nrows + 1, sizeof(int32_t));
+  A->col = (int32_t *)malloc((size_t)(nnz_cap > 0 ? nnz_cap : 1) * sizeof(int32_t));
+  A->val = (double *)malloc((size_t)(nnz_cap > 0 ? nnz_cap : 1) * sizeof(double));
+  if (!A->rowptr || !A->col || !A->val) {
+    orc_csr_free(A);
+    return ORC_ERR_MEM;
+  }
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Assembly                                                                  */
+/* ------------------------------------------------------------------------ */
+
+/* poisson3DMatrix, src/utils/utils.c:30-121.  The reference inserts
+ * (row, row-1, row+1, row-nx, row+nx, row-nxny, row+nxny) and PETSc AIJ keeps
+ * each row's columns ascending, which is the order written here.  The
+ * reference splits z at n_grid_columns/2 for its 2 blocks (utils.c:45,51);
+ * this takes the plane range explicitly so nb blocks are z-slabs. */
+int orc_poisson3d_rows(int nx, int ny, int nz, int z0, int z1, orc_csr *A) {
+  if (nx <= 0 || ny <= 0 || nz <= 0 || z0 < 0 || z1 > nz || z0 > z1) return ORC_ERR_ARG;
+  const int64_t nxny = (int64_t)nx * ny;
+  const int64_t N = nxny * nz;
+  if (N > INT32_MAX) return ORC_ERR_ARG;
+  const int64_t nrows = nxny * (z1 - z0);
+  int rc = csr_alloc(A, nrows, N, 7 * nrows);
+  if (rc) return rc;
+  int64_t p = 0, lr = 0;
+  for (int k = z0; k < z1; ++k)
+    for (int j = 0; j < ny; ++j)
+      for (int i = 0; i < nx; ++i, ++lr) {
+        const int64_t row = i + (int64_t)j * nx + (int64_t)k * nxny;
+        A->rowptr[lr] = (int32_t)p;
+        if (k > 0) { A->col[p] = (int32_t)(row - nxny); A->val[p++] = -1.0; }
+        if (j > 0) { A->col[p] = (int32_t)(row - nx); A->val[p++] = -1.0; }
+        if (i > 0) { A->col[p] = (int32_t)(row - 1); A->val[p++] = -1.0; }
+        A->col[p] = (int32_t)row; A->val[p++] = 6.0;
+        if (i < nx - 1) { A->col[p] = (int32_t)(row + 1); A->val[p++] = -1.0; }
+        if (j < ny - 1) { A->col[p] = (int32_t)(row + nx); A->val[p++] = -1.0; }
+        if (k < nz - 1) { A->col[p] = (int32_t)(row + nxny); A->val[p++] = -1.0; }
+      }
+  A->rowptr[nrows] = (int32_t)p;
+  A->nnz = p;
+  return ORC_OK;
+}
+
+/* poisson2DMatrix, src/utils/utils.c:247-293: global row Ii of an m x n grid,
+ * i = Ii / n (n = n_grid_columns), j = Ii - i*n; neighbours Ii-+n (i), Ii-+1 (j);
+ * diagonal 4.  Rows [row0,row1) of the block, local row = Ii - row0. */
+int orc_poisson2d_rows(int m, int n, int64_t row0, int64_t row1, orc_csr *A) {
+  if (m <= 0 || n <= 0) return ORC_ERR_ARG;
+  const int64_t N = (int64_t)m * n;
+  if (N > INT32_MAX || row0 < 0 || row1 > N || row0 > row1) return ORC_ERR_ARG;
+  const int64_t nrows = row1 - row0;
+  int rc = csr_alloc(A, nrows, N, 5 * nrows);
+  if (rc) return rc;
+  int64_t p = 0;
+  for (int64_t Ii = row0; Ii < row1; ++Ii) {
+    const int64_t i = Ii / n, j = Ii - i * n;
+    A->rowptr[Ii - row0] = (int32_t)p;
+    if (i > 0) { A->col[p] = (int32_t)(Ii - n); A->val[p++] = -1.0; }
+    if (j > 0) { A->col[p] = (int32_t)(Ii - 1); A->val[p++] = -1.0; }
+    A->col[p] = (int32_t)Ii; A->val[p++] = 4.0;
+    if (j < n - 1) { A->col[p] = (int32_t)(Ii + 1); A->val[p++] = -1.0; }
+    if (i < m - 1) { A->col[p] = (int32_t)(Ii + n); A->val[p++] = -1.0; }
+  }
+  A->rowptr[nrows] = (int32_t)p;
+  A->nnz = p;
+  return ORC_OK;
+}
+
+/* poisson2DMatrix_complete, src/utils/utils.c:383-445: Ii = i*N + j with
+ * N = n_mesh_lines (the reference assumes a square mesh, utils.c:390). */
+int orc_poisson2d_complete(int m, int n, orc_csr *A) {
+  if (m <= 0 || n <= 0 || m != n) return ORC_ERR_ARG; /* square meshes only, as the reference */
+  const int64_t Ntot = (int64_t)m * n, Nl = m;
+  if (Ntot > INT32_MAX) return ORC_ERR_ARG;
+  int rc = csr_alloc(A, Ntot, Ntot, 5 * Ntot);
+  if (rc) return rc;
+  /* rows are produced in Ii order only when n == m; build per-row lists */
+  int64_t p = 0;
+  for (int64_t Ii = 0; Ii < Ntot; ++Ii) {
+    A->rowptr[Ii] = (int32_t)p;
+    const int64_t i = Ii / Nl, j = Ii - i * Nl;
+    if (i >= m || j >= n) continue; /* unreachable for square meshes */
+    if (i > 0) { A->col[p] = (int32_t)(Ii - Nl); A->val[p++] = -1.0; }
+    if (j > 0) { A->col[p] = (int32_t)(Ii - 1); A->val[p++] = -1.0; }
+    A->col[p] = (int32_t)Ii; A->val[p++] = 4.0;
+    if (j < Nl - 1) { A->col[p] = (int32_t)(Ii + 1); A->val[p++] = -1.0; }
+    if (i < Nl - 1) { A->col[p] = (int32_t)(Ii + Nl); A->val[p++] = -1.0; }
+  }
+  A->rowptr[Ntot] = (int32_t)p;
+  A->nnz = p;
+  return ORC_OK;
+}
+
+/* divideSubDomainIntoBlockMatrices, src/utils/utils.c:450-478: A_sub[i] =
+ * MatCreateSubMatrix(A_block, own rows, cols of block i).  Here the diagonal
+ * block gets local columns and every off-block column goes to one coupling
+ * matrix (global ids), which for 2 blocks is exactly the reference's A_ij. */
+int orc_split(const orc_csr *Ab, int64_t c0, int64_t c1, orc_csr *Aii, orc_csr *Aoff) {
+  int64_t nin = 0, nout = 0;
+  for (int64_t k = 0; k < Ab->nnz; ++k) {
+    if (Ab->col[k] >= c0 && Ab->col[k] < c1) ++nin; else ++nout;
+  }
+  int rc = csr_alloc(Aii, Ab->nrows, c1 - c0, nin);
+  if (rc) return rc;
+  rc = csr_alloc(Aoff, Ab->nrows, Ab->ncols, nout);
+  if (rc) { orc_csr_free(Aii); return rc; }
+  int64_t pi = 0, po = 0;
+  for (int32_t r = 0; r < Ab->nrows; ++r) {
+    Aii->rowptr[r] = (int32_t)pi;
+    Aoff->rowptr[r] = (int32_t)po;
+    for (int32_t k = Ab->rowptr[r]; k < Ab->rowptr[r + 1]; ++k) {
+      const int32_t c = Ab->col[k];
+      if (c >= c0 && c < c1) { Aii->col[pi] = (int32_t)(c - c0); Aii->val[pi++] = Ab->val[k]; }
+      else { Aoff->col[po] = c; Aoff->val[po++] = Ab->val[k]; }
+    }
+  }
+  Aii->rowptr[Ab->nrows] = (int32_t)pi;
+  Aoff->rowptr[Ab->nrows] = (int32_t)po;
+  Aii->nnz = pi;
+  Aoff->nnz = po;
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Mat / Vec kernels                                                         */
+/* ------------------------------------------------------------------------ */
+
+/* MatMult_SeqAIJ [PETSc-ext]: sum = 0; sum += aa[k]*x[aj[k]] left to right. */
+void orc_spmv(const orc_csr *A, const double *x, double *y) {
+  for (int32_t r = 0; r < A->nrows; ++r) {
+    double s = 0.0;
+    for (int32_t k = A->rowptr[r]; k < A->rowptr[r + 1]; ++k) s += A->val[k] * x[A->col[k]];
+    y[r] = s;
+  }
+}
+
+/* MatResidual default [PETSc-ext]: MatMult(A,x,r); VecAYPX(r,-1,b) -> r = b - A x. */
+void orc_residual(const orc_csr *A, const double *b, const double *x, double *r) {
+  for (int32_t row = 0; row < A->nrows; ++row) {
+    double s = 0.0;
+    for (int32_t k = A->rowptr[row]; k < A->rowptr[row + 1]; ++k) s += A->val[k] * x[A->col[k]];
+    r[row] = b[row] - s;
+  }
+}
+
+/* Butterfly over one wave of 64 lane values: v[l] <- v[l] + v[l ^ off],
+ * off = 32,16,...,1.  Lane 0 holds the result (all lanes agree). */
+static double dbr_wave(const double *lanes) {
+  double v[64], t[64];
+  memcpy(v, lanes, sizeof(v));
+  for (int off = 32; off >= 1; off >>= 1) {
+    for (int l = 0; l < 64; ++l) t[l] = v[l] + v[l ^ off];
+    memcpy(v, t, sizeof(v));
+  }
+  return v[0];
+}
+
+/* One 256-thread workgroup: 4 wave butterflies, then (w0 + w1) + (w2 + w3). */
+static double dbr_group(const double *lanes) {
+  const double w0 = dbr_wave(lanes), w1 = dbr_wave(lanes + 64);
+  const double w2 = dbr_wave(lanes + 128), w3 = dbr_wave(lanes + 192);
+  return (w0 + w1) + (w2 + w3);
+}
+
+/* Deterministic blocked reduction of sum_i x[i]*y[i] (the device order). */
+static double dbr_dot(int64_t n, const double *x, const double *y) {
+  const int64_t nchunks = (n + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
+  double *part = (double *)malloc((size_t)(nchunks > 0 ? nchunks : 1) * sizeof(double));
+  double lanes[ORC_DBR_THREADS];
+  for (int64_t c = 0; c < nchunks; ++c) {
+    const int64_t base = c * ORC_DBR_CHUNK;
+    for (int t = 0; t < ORC_DBR_THREADS; ++t) {
+      double acc = 0.0;
+      for (int j = 0; j < ORC_DBR_ITERS; ++j) {
+        const int64_t e = base + (int64_t)j * (ORC_DBR_THREADS * ORC_DBR_VW) + ORC_DBR_VW * t;
+        for (int v = 0; v < ORC_DBR_VW; ++v)
+          if (e + v < n) acc += x[e + v] * y[e + v];
+      }
+      lanes[t] = acc;
+    }
+    part[c] = dbr_group(lanes);
+  }
+  for (int t = 0; t < ORC_DBR_THREADS; ++t) {
+    double acc = 0.0;
+    for (int64_t i = t; i < nchunks; i += ORC_DBR_THREADS) acc += part[i];
+    lanes[t] = acc;
+  }
+  free(part);
+  return dbr_group(lanes);
+}
+
+/* VecDot / BLAS ddot order: sequential (reference ddot's unroll-by-5 is
+ * evaluated left to right, i.e. still sequential). */
+static double seq_dot(int64_t n, const double *x, const double *y) {
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s += x[i] * y[i];
+  return s;
+}
+
+double orc_dot(int mode, int64_t n, const double *x, const double *y) {
+  return mode == ORC_REDUCE_DBR ? dbr_dot(n, x, y) : seq_dot(n, x, y);
+}
+
+/* VecNorm(NORM_2) [PETSc-ext]: sqrt(ddot(x,x)). */
+double orc_norm2(int mode, int64_t n, const double *x) { return sqrt(orc_dot(mode, n, x, x)); }
+
+/* VecMDot_Seq [PETSc-ext]: out[j] = sum_i w[i]*V_j[i], sequential per vector. */
+void orc_mdot(int mode, int64_t n, int k, const double *w, const double *const *V, double *out) {
+  for (int j = 0; j < k; ++j) out[j] = orc_dot(mode, n, w, V[j]);
+}
+
+/* VecMAXPY_Seq [PETSc-ext]: the nv & 3 leading vectors first (PetscKernelAXPY3/2/1),
+ * then groups of four (PetscKernelAXPY4): U += a0*p0 + a1*p1 + a2*p2 + a3*p3,
+ * evaluated left to right and then added to U. */
+void orc_maxpy(int64_t n, int k, const double *a, const double *const *V, double *w) {
+  const int jrem = k & 3;
+  for (int64_t i = 0; i < n; ++i) {
+    double u = w[i];
+    if (jrem == 3) u = u + ((a[0] * V[0][i] + a[1] * V[1][i]) + a[2] * V[2][i]);
+    else if (jrem == 2) u = u + (a[0] * V[0][i] + a[1] * V[1][i]);
+    else if (jrem == 1) u = a[0] * V[0][i] + u;
+    for (int j = jrem; j < k; j += 4)
+      u = u + (((a[j] * V[j][i] + a[j + 1] * V[j + 1][i]) + a[j + 2] * V[j + 2][i]) + a[j + 3] * V[j + 3][i]);
+    w[i] = u;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* KSPGMRES [PETSc-ext]                                                      */
+/* ------------------------------------------------------------------------ */
+
+void orc_gmres_default_opts(orc_gmres_opts *o) {
+  o->restart = 30;
+  o->max_it = 10000;
+  o->rtol = 1e-5;
+  o->abstol = 1e-50;
+  o->divtol = 1e4;
+  o->haptol = 1e-30;
+  o->breakdowntol = 0.1;
+  o->uirnorm = 0;
+  o->guess_nonzero = 0;
+  o->reduce_mode = ORC_REDUCE_SEQ;
+}
+
+typedef struct {
+  const orc_csr *A;
+  const double *b;
+  double *x;
+  const orc_gmres_opts *o;
+  int64_t n;
+  int m;
+  double **VV;     /* VEC_VV(0..m) */
+  double *tmp;     /* VEC_TEMP */
+  double *hh;      /* HH(a,b) = hh[b*(m+2)+a] */
+  double *cc, *ss, *grs, *lhh;
+  /* KSP state */
+  int its, reason, guess_zero;
+  double rnorm;    /* ksp->rnorm */
+  double rnorm0;   /* ksp->rnorm0 (convergence test) */
+  double ttol;
+  double gm_rnorm0;/* gmres->rnorm0 */
+  double *hist;
+  int hist_cap, nhist;
+} gm_t;
+
+#define HH(g, a, b) ((g)->hh[(int64_t)(b) * ((g)->m + 2) + (a)])
+
+static int is_bad(double v) { return isnan(v) || isinf(v); }
+
+static void gm_log(gm_t *g, double r) {
+  if (g->hist && g->nhist < g->hist_cap) g->hist[g->nhist] = r;
+  g->nhist++;
+}
+
+/* KSPConvergedDefault [PETSc-ext] */
+static void gm_converged(gm_t *g, int n, double rnorm) {
+  g->reason = ORC_CONVERGED_ITERATING;
+  if (n == 0) {
+    if (!g->guess_zero && !g->o->uirnorm) {
+      double snorm = orc_norm2(g->o->reduce_mode, g->n, g->b);
+      if (snorm == 0.0) snorm = rnorm;
+      g->rnorm0 = snorm;
+    } else {
+      g->rnorm0 = rnorm;
+    }
+    g->ttol = PMAX(g->o->rtol * g->rnorm0, g->o->abstol);
+  }
+  if (is_bad(rnorm)) {
+    g->reason = ORC_DIVERGED_NANORINF;
+  } else if (rnorm <= g->ttol) {
+    g->reason = (rnorm < g->o->abstol) ? ORC_CONVERGED_ATOL : ORC_CONVERGED_RTOL;
+  } else if (rnorm >= g->o->divtol * g->rnorm0) {
+    g->reason = ORC_DIVERGED_DTOL;
+  }
+}
+
+/* VecNormalize [PETSc-ext]: t = ||v||; v *= 1/t unless t is 0 or not finite. */
+static double gm_normalize(gm_t *g, double *v) {
+  const double t = orc_norm2(g->o->reduce_mode, g->n, v);
+  if (t != 0.0 && !is_bad(t)) {
+    const double s = 1.0 / t;
+    for (int64_t i = 0; i < g->n; ++i) v[i] = v[i] * s;
+  }
+  return t;
+}
+
+/* KSPGMRESUpdateHessenberg [PETSc-ext] */
+static void gm_update_hessenberg(gm_t *g, int it, int hapend, double *res) {
+  double *hh = &HH(g, 0, it);
+  for (int j = 1; j <= it; ++j) {
+    const double tt = hh[j - 1];
+    hh[j - 1] = g->cc[j - 1] * tt + g->ss[j - 1] * hh[j];
+    hh[j] = g->cc[j - 1] * hh[j] - (g->ss[j - 1] * tt);
+  }
+  if (!hapend) {
+    const double tt = sqrt(hh[it] * hh[it] + hh[it + 1] * hh[it + 1]);
+    if (tt == 0.0) {
+      g->reason = ORC_DIVERGED_NULL;
+      return;
+    }
+    g->cc[it] = hh[it] / tt;
+    g->ss[it] = hh[it + 1] / tt;
+    g->grs[it + 1] = -(g->ss[it] * g->grs[it]);
+    g->grs[it] = g->cc[it] * g->grs[it];
+    hh[it] = g->cc[it] * hh[it] + g->ss[it] * hh[it + 1];
+    *res = fabs(g->grs[it + 1]);
+  } else {
+    *res = 0.0;
+  }
+}
+
+/* KSPGMRESBuildSoln(GRS(0), x, x, ksp, it) [PETSc-ext]; nrs aliases GRS. */
+static void gm_build_soln(gm_t *g, int it) {
+  if (it < 0) return;
+  double *nrs = g->grs;
+  if (HH(g, it, it) != 0.0) {
+    nrs[it] = g->grs[it] / HH(g, it, it);
+  } else {
+    g->reason = ORC_DIVERGED_BREAKDOWN;
+    return;
+  }
+  for (int ii = 1; ii <= it; ++ii) {
+    const int k = it - ii;
+    double tt = g->grs[k];
+    for (int j = k + 1; j <= it; ++j) tt = tt - HH(g, k, j) * nrs[j];
+    if (HH(g, k, k) == 0.0) {
+      g->reason = ORC_DIVERGED_BREAKDOWN;
+      return;
+    }
+    nrs[k] = tt / HH(g, k, k);
+  }
+  /* VecSet(TEMP,0); VecMAXPY(TEMP,it+1,nrs,VV); KSPUnwindPreconditioner (PCNONE: identity);
+   * VecAXPY(x, 1.0, TEMP) */
+  for (int64_t i = 0; i < g->n; ++i) g->tmp[i] = 0.0;
+  orc_maxpy(g->n, it + 1, nrs, (const double *const *)g->VV, g->tmp);
+  for (int64_t i = 0; i < g->n; ++i) g->x[i] = g->x[i] + 1.0 * g->tmp[i];
+}
+
+/* KSPGMRESClassicalGramSchmidtOrthogonalization, REFINE_NEVER [PETSc-ext] */
+static void gm_cgs(gm_t *g, int it) {
+  double *hh = &HH(g, 0, it);
+  for (int j = 0; j <= it; ++j) hh[j] = 0.0;
+  orc_mdot(g->o->reduce_mode, g->n, it + 1, g->VV[it + 1], (const double *const *)g->VV, g->lhh);
+  for (int j = 0; j <= it; ++j) {
+    if (is_bad(g->lhh[j])) {
+      g->reason = ORC_DIVERGED_NANORINF;
+      return;
+    }
+    g->lhh[j] = -g->lhh[j];
+  }
+  orc_maxpy(g->n, it + 1, g->lhh, (const double *const *)g->VV, g->VV[it + 1]);
+  for (int j = 0; j <= it; ++j) hh[j] -= g->lhh[j];
+}
+
+/* KSPGMRESCycle [PETSc-ext] */
+static void gm_cycle(gm_t *g, int *itcount) {
+  int it = 0, hapend = 0;
+  double res;
+  *itcount = 0;
+  res = gm_normalize(g, g->VV[0]);
+  if (is_bad(res)) { /* KSPCheckNorm */
+    g->reason = ORC_DIVERGED_NANORINF;
+    return;
+  }
+  if (g->rnorm > 0.0 && fabs(res - g->rnorm) > g->o->breakdowntol * g->gm_rnorm0) {
+    g->reason = ORC_DIVERGED_BREAKDOWN;
+    return;
+  }
+  g->grs[0] = g->gm_rnorm0 = res;
+  g->rnorm = res;
+  gm_log(g, res);
+  if (res == 0.0) {
+    g->reason = ORC_CONVERGED_ATOL;
+    return;
+  }
+  gm_converged(g, g->its, res);
+  while (!g->reason && it < g->m && g->its < g->o->max_it) {
+    if (it) gm_log(g, res);
+    /* KSP_PCApplyBAorAB, PCNONE: VV(it+1) = A * VV(it) */
+    orc_spmv(g->A, g->VV[it], g->VV[it + 1]);
+    gm_cgs(g, it);
+    if (g->reason) break;
+    const double tt = gm_normalize(g, g->VV[it + 1]);
+    if (is_bad(tt)) {
+      g->reason = ORC_DIVERGED_NANORINF;
+      return;
+    }
+    HH(g, it + 1, it) = tt;
+    double hapbnd = fabs(tt / g->grs[it]);
+    if (hapbnd > g->o->haptol) hapbnd = g->o->haptol;
+    if (tt < hapbnd) hapend = 1;
+    gm_update_hessenberg(g, it, hapend, &res);
+    it++;
+    g->its++;
+    g->rnorm = res;
+    if (g->reason) break;
+    gm_converged(g, g->its, res);
+    if (hapend) {
+      if (!g->reason) {
+        g->reason = ORC_DIVERGED_BREAKDOWN;
+        break;
+      }
+    }
+  }
+  if (it && (g->reason || g->its >= g->o->max_it)) gm_log(g, res);
+  *itcount = it;
+  gm_build_soln(g, it - 1);
+}
+
+/* KSPSolve -> KSPSolve_GMRES [PETSc-ext] */
+int orc_gmres_solve(const orc_csr *A, const double *b, double *x, const orc_gmres_opts *o,
+                    orc_gmres_result *res, double *hist, int hist_cap) {
+  if (!A || !o || o->restart < 1 || A->nrows != A->ncols) return ORC_ERR_ARG;
+  gm_t g;
+  memset(&g, 0, sizeof(g));
+  g.A = A;
+  g.b = b;
+  g.x = x;
+  g.o = o;
+  g.n = A->nrows;
+  g.m = o->restart;
+  g.hist = hist;
+  g.hist_cap = hist_cap;
+  const int64_t n = g.n, m = g.m;
+  g.VV = (double **)malloc((size_t)(m + 1) * sizeof(double *));
+  double *vv = (double *)calloc((size_t)((m + 1) * n + n + 1), sizeof(double));
+  g.hh = (double *)calloc((size_t)((m + 2) * (m + 1)), sizeof(double));
+  g.cc = (double *)calloc((size_t)(m + 2), sizeof(double));
+  g.ss = (double *)calloc((size_t)(m + 2), sizeof(double));
+  g.grs = (double *)calloc((size_t)(m + 2), sizeof(double));
+  g.lhh = (double *)calloc((size_t)(m + 2), sizeof(double));
+  if (!g.VV || !vv || !g.hh || !g.cc || !g.ss || !g.grs || !g.lhh) {
+    free(g.VV); free(vv); free(g.hh); free(g.cc); free(g.ss); free(g.grs); free(g.lhh);
+    return ORC_ERR_MEM;
+  }
+  for (int64_t j = 0; j <= m; ++j) g.VV[j] = vv + j * n;
+  g.tmp = vv + (m + 1) * n;
+
+  g.guess_zero = !o->guess_nonzero;
+  if (g.guess_zero)
+    for (int64_t i = 0; i < n; ++i) x[i] = 0.0; /* KSPSolve zeroes x for a zero guess */
+  g.its = 0;
+  g.reason = 0;
+  g.rnorm = -1.0; /* special marker for KSPGMRESCycle() */
+  int itcount = 0;
+  while (!g.reason) {
+    /* KSPInitialResidual: r = b - A x (VecCopy + VecAXPY(-1)), or r = b for a zero guess */
+    if (!g.guess_zero) {
+      orc_spmv(A, x, g.tmp);
+      for (int64_t i = 0; i < n; ++i) g.VV[0][i] = b[i] + (-1.0) * g.tmp[i];
+    } else {
+      memcpy(g.VV[0], b, (size_t)n * sizeof(double));
+    }
+    int its = 0;
+    gm_cycle(&g, &its);
+    itcount += its;
+    if (itcount >= o->max_it) {
+      if (!g.reason) g.reason = ORC_DIVERGED_ITS;
+      break;
+    }
+    g.guess_zero = 0;
+  }
+  if (res) {
+    res->its = g.its;
+    res->reason = g.reason;
+    res->rnorm = g.rnorm;
+    res->nhist = g.nhist;
+  }
+  free(g.VV); free(vv); free(g.hh); free(g.cc); free(g.ss); free(g.grs); free(g.lhh);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reference glue                                                            */
+/* ------------------------------------------------------------------------ */
+
+/* computeFinalResidualNorm_new, src/utils/utils.c:597-620 (and the block-root
+ * variant computeFinalResidualNorm, :575-595): VecNorm of each block's
+ * residual, squared, summed over blocks (block order), square root. */
+double orc_final_residual_norm(int mode, int nb, const orc_csr *const *Ab, const double *x,
+                               const double *const *bb) {
+  double total = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    double *r = (double *)malloc((size_t)(Ab[b]->nrows > 0 ? Ab[b]->nrows : 1) * sizeof(double));
+    orc_residual(Ab[b], bb[b], x, r);
+    const double ln = orc_norm2(mode, Ab[b]->nrows, r);
+    total += ln * ln;
+    free(r);
+  }
+  return sqrt(total);
+}
+
+static int build_block(const orc_sm_problem *p, int b, orc_csr *Ablock, int64_t *r0, int64_t *r1) {
+  if (p->dim == 3) {
+    const int ppb = p->nz / p->nb;
+    const int64_t nxny = (int64_t)p->nx * p->ny;
+    *r0 = (int64_t)b * ppb * nxny;
+    *r1 = (int64_t)(b + 1) * ppb * nxny;
+    return orc_poisson3d_rows(p->nx, p->ny, p->nz, b * ppb, (b + 1) * ppb, Ablock);
+  }
+  const int64_t N = (int64_t)p->nx * p->ny, rbs = N / p->nb;
+  *r0 = b * rbs;
+  *r1 = (b + 1) * rbs;
+  return orc_poisson2d_rows(p->nx, p->ny, *r0, *r1, Ablock);
+}
+
+/* Synchronous multisplitting, src/synchronous-multisplitting/synchronous-multisplitting.c:
+ * setup :101-164, loop :170-206; nb blocks simulated in block order.  For nb = 2
+ * this is the reference loop; the block exchange (comm.c:126) is the copy of
+ * every block's x_i into the global x before the RHS updates. */
+int orc_sm_solve(const orc_sm_problem *p, const orc_gmres_opts *inner, orc_sm_result *res,
+                 double *outer_hist, int outer_cap, int *inner_its, double *x_out) {
+  const int nb = p->nb;
+  if (nb < 1 || (p->dim != 2 && p->dim != 3)) return ORC_ERR_ARG;
+  if (p->dim == 3 && p->nz % nb) return ORC_ERR_ARG;
+  if (p->dim == 2 && ((int64_t)p->nx * p->ny) % nb) return ORC_ERR_ARG;
+  const int64_t N = (int64_t)p->nx * p->ny * (p->dim == 3 ? p->nz : 1);
+  const int mode = inner->reduce_mode;
+  orc_csr *Ab = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
+  orc_csr *Aii = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
+  orc_csr *Aoff = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
+  int64_t *r0 = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
+  int64_t *r1 = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
+  double *x = (double *)calloc((size_t)N, sizeof(double));
+  double *u = (double *)malloc((size_t)N * sizeof(double));
+  double *bvec = (double *)calloc((size_t)N, sizeof(double));
+  double *rhs = (double *)calloc((size_t)N, sizeof(double));
+  double *r = (double *)calloc((size_t)N, sizeof(double));
+  double *y = (double *)calloc((size_t)N, sizeof(double));
+  const orc_csr **Abp = (const orc_csr **)calloc((size_t)nb, sizeof(orc_csr *));
+  const double **bbp = (const double **)calloc((size_t)nb, sizeof(double *));
+  int rc = ORC_OK;
+  if (!Ab || !Aii || !Aoff || !r0 || !r1 || !x || !u || !bvec || !rhs || !r || !y || !Abp || !bbp) {
+    rc = ORC_ERR_MEM;
+    goto done;
+  }
+  for (int64_t i = 0; i < N; ++i) u[i] = 1.0;
+  for (int b = 0; b < nb; ++b) {
+    if ((rc = build_block(p, b, &Ab[b], &r0[b], &r1[b]))) goto done;
+    if ((rc = orc_split(&Ab[b], r0[b], r1[b], &Aii[b], &Aoff[b]))) goto done;
+    /* computeTheRightHandSideWithInitialGuess (utils.c:623-650): b_i = A_block u */
+    orc_spmv(&Ab[b], u, bvec + r0[b]);
+    Abp[b] = &Ab[b];
+    bbp[b] = bvec + r0[b];
+  }
+  /* computeFinalResidualNorm at x = 0 (synchronous-multisplitting.c:162) */
+  const double norm0 = orc_final_residual_norm(mode, nb, Abp, x, bbp);
+  /* updateLocalRHS before the loop (:164) */
+  for (int b = 0; b < nb; ++b) orc_residual(&Aoff[b], bvec + r0[b], x, rhs + r0[b]);
+
+  orc_gmres_opts io = *inner;
+  io.guess_nonzero = 1; /* inner_solver, utils.c:956-957 */
+  io.uirnorm = 1;
+  int outer = 0;
+  double norm = 0.0;
+  int64_t total_inner = 0;
+  for (;;) {
+    for (int b = 0; b < nb; ++b) {
+      orc_gmres_result gr;
+      if ((rc = orc_gmres_solve(&Aii[b], rhs + r0[b], x + r0[b], &io, &gr, NULL, 0))) goto done;
+      if (inner_its && outer < outer_cap) inner_its[(int64_t)outer * nb + b] = gr.its;
+      total_inner += gr.its;
+    }
+    /* comm_sync_send_and_receive: every block now sees every x_j (x is shared here) */
+    double sum = 0.0;
+    for (int b = 0; b < nb; ++b) {
+      const int64_t nbk = r1[b] - r0[b];
+      orc_residual(&Aoff[b], bvec + r0[b], x, rhs + r0[b]);     /* updateLocalRHS */
+      orc_residual(&Aii[b], rhs + r0[b], x + r0[b], r + r0[b]);  /* MatResidual(A_ii,...) */
+      const double ln = orc_norm2(mode, nbk, r + r0[b]);
+      sum += ln * ln;                                            /* Allreduce(SUM) of squares */
+    }
+    norm = sqrt(sum);
+    if (outer_hist && outer < outer_cap) outer_hist[outer] = norm;
+    outer++;
+    if (norm <= PMAX(p->atol, p->rtol * norm0)) break;
+    if (p->max_outer > 0 && outer >= p->max_outer) break;
+  }
+  if (res) {
+    res->outer_its = outer;
+    res->norm0 = norm0;
+    res->final_norm = orc_final_residual_norm(mode, nb, Abp, x, bbp);
+    for (int64_t i = 0; i < N; ++i) y[i] = -1.0 * u[i] + x[i]; /* VecWAXPY(diff,-1,u,x) */
+    res->error = orc_norm2(mode, N, y);
+    res->total_inner_its = total_inner;
+  }
+  if (x_out) memcpy(x_out, x, (size_t)N * sizeof(double));
+done:
+  if (Ab)
+    for (int b = 0; b < nb; ++b) { orc_csr_free(&Ab[b]); orc_csr_free(&Aii[b]); orc_csr_free(&Aoff[b]); }
+  free(Ab); free(Aii); free(Aoff); free(r0); free(r1); free(x); free(u); free(bvec);
+  free(rhs); free(r); free(y); free(Abp); free(bbp);
+  return rc;
+}

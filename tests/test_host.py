@@ -1,0 +1,109 @@
+"""CPU tests of the boundary and the host logic (no compute calls)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from medane_tchakorom_ufc_thesis_repository_amd import _lib, utils
+from medane_tchakorom_ufc_thesis_repository_amd.petsc import Options
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    L = _lib.load()
+    syms = _lib.header_symbols()
+    assert len(syms) > 40
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    # the dynamic symbol table of the .so, independently of ctypes
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(syms) <= exported, sorted(set(syms) - exported)
+    # every header symbol has a binding signature
+    assert set(syms) == set(_lib._SIGS) | {"msp_get_last_error"}
+
+
+def test_library_is_gfx950_code():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", _lib.LIB_PATH], capture_output=True,
+                         text=True)
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_no_gpu_means_loud_failure():
+    """Without a GPU the product path raises; there is no CPU fallback."""
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, device_count
+    if device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(_lib.MsplitError):
+        Context(0)
+
+
+def test_options_database_prefixes():
+    o = Options("-m 256 -n 128 -rtol 1e-3 -inner1_ksp_max_it 20 -inner1_ksp_rtol 1e-20 -inner2_pc_type none "
+                "-ksp_converged_use_initial_residual_norm -x -1.5")
+    assert o.get_int("m") == 256 and o.get_int("n") == 128
+    assert o.get_real("rtol") == 1e-3
+    assert o.get_int("ksp_max_it", prefix="inner1_") == 20
+    assert o.get_real("ksp_rtol", prefix="inner1_") == 1e-20
+    assert o.get_int("ksp_max_it", 10000, prefix="inner2_") == 10000
+    assert o.get_string("pc_type", prefix="inner2_") == "none"
+    assert o.get_bool("ksp_converged_use_initial_residual_norm")
+    assert o.get_real("x") == -1.5
+
+
+def _dense_block(L, A_rows):
+    rp, c, v, nc = A_rows
+    D = np.zeros((rp.size - 1, nc))
+    for r in range(rp.size - 1):
+        D[r, c[rp[r]:rp[r + 1]]] = v[rp[r]:rp[r + 1]]
+    return D
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,nb", [(3, 5, 4, 6, 3), (3, 4, 3, 4, 4), (3, 3, 3, 2, 1),
+                                             (2, 8, 6, 1, 4), (2, 6, 5, 1, 2)])
+def test_block_layout_reproduces_the_split(dim, nx, ny, nz, nb):
+    """A_ii (box stencil) + coupling rows in halo numbering == the host split of
+    the reference's block rows (divideSubDomainIntoBlockMatrices)."""
+    for b in range(nb):
+        L = utils.block_layout(dim, nx, ny, nz, nb, b)
+        if dim == 3:
+            rows = utils.poisson3DMatrix_rows(nx, ny, nz, b * nz // nb, (b + 1) * nz // nb)
+        else:
+            rows = utils.poisson2DMatrix_rows(nx, ny, L.r0, L.r1)
+        (rpi, ci, vi), (rpo, co, vo) = utils.split_columns(*rows[:3], L.r0, L.r1)
+        bd, bx, by, bz = L.box
+        if bd == 3:
+            box = utils.poisson3DMatrix_rows(bx, by, bz, 0, bz)
+        else:
+            box = utils.poisson2DMatrix_rows(by, bx, 0, bx * by)
+        assert np.array_equal(box[0], rpi) and np.array_equal(box[1], ci) and np.array_equal(box[2], vi)
+        # coupling: map halo index back to the global column it stands for
+        halo_global = np.zeros(L.halo_size, np.int64)
+        for nbr, hoff, cnt, nbr_off in L.recv:
+            nbr_r0 = utils.block_layout(dim, nx, ny, nz, nb, nbr).r0
+            halo_global[hoff:hoff + cnt] = nbr_r0 + nbr_off + np.arange(cnt)
+        row_ids, crp, cc, cv = L.coupling
+        full_rp = np.zeros(L.nrows + 1, np.int64)
+        full_rp[row_ids + 1] = np.diff(crp)
+        full_rp = np.cumsum(full_rp)
+        assert np.array_equal(full_rp, rpo)
+        assert np.array_equal(halo_global[cc], co) and np.array_equal(cv, vo)
+        # what I send is exactly what my neighbours' halos expect
+        for nbr, off, cnt in L.send:
+            Ln = utils.block_layout(dim, nx, ny, nz, nb, nbr)
+            (match,) = [r for r in Ln.recv if r[0] == b]
+            assert match[2] == cnt and match[3] == off
+
+
+def test_oracle_is_not_imported_by_the_product():
+    """The product package never references the oracle."""
+    pkg = os.path.join(ROOT, "medane_tchakorom_ufc_thesis_repository_amd")
+    for dp, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".c", ".hip", ".h", ".cpp")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "pyoracle" not in txt and "liborc" not in txt and "oracle.h" not in txt, f
