@@ -1,0 +1,211 @@
+"""Benchmark: DOF-updates/s of the GMRES inner solve on the 3D 7-point Poisson
+operator (BASELINE.json metric), one process per GPU.
+
+N = 1 : configs[1] -- 3D 7-pt Poisson 256^3, single-block GMRES(30), pc none,
+        one step = one KSPSolve from x0 = 0 with the canonical options
+        (running_bulk_test_g5k:64-70: rtol 1e-4, unpreconditioned norm) and a
+        fixed max_it = 300 (10 restart cycles).
+N > 1 : synchronous multisplitting, weak scaling: one 256^3 z-slab block per
+        GPU (global 256 x 256 x 256N); one step = one outer iteration
+        (inner GMRES(30) max_it 300 on every block, RCCL boundary-plane
+        exchange, right-hand-side update, residual norm all-gather).
+value = sum over blocks of (rows x GMRES iterations) / max-over-ranks time.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]   (N > 1 under
+torch.distributed.run, one rank per GPU, RCCL = backend "nccl").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "DOF-updates/s on 3D 7-pt Poisson GMRES; achieved HBM GB/s vs peak, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+KERNEL_NAMES = {"spmv": "k_spmv_lds (CSR MatMult/MatResidual)", "mdot": "k_dot_stage1+2 (VecMDot, DBR)",
+                "maxpy": "k_maxpy (VecMAXPY, CGS update + BuildSoln)", "norm": "k_dot_stage1<1,self>+stage2 (VecNorm)",
+                "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy"}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--n", type=int, default=256, help="mesh edge per block (256 -> configs[1])")
+    p.add_argument("--max-it", type=int, default=300)
+    p.add_argument("--restart", type=int, default=30)
+    p.add_argument("--rtol", type=float, default=1e-4)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-its", type=int, default=30)
+    p.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
+    return p.parse_args()
+
+
+def cpu_baseline(n: int, restart: int, its: int, rtol: float):
+    """The CPU restatement (oracle/, sequential PETSc order, 1 thread) on a
+    bounded sample of the same workload: the same 256^3 operator, `its`
+    GMRES iterations."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import pyoracle as po
+    A = po.poisson3d_rows(n, n, n, 0, n)
+    b = A.mult(np.ones(A.shape[0]))
+    t0 = time.perf_counter()
+    _, r = po.gmres(A, b, restart=restart, max_it=its, rtol=rtol, reduce_mode=po.REDUCE_SEQ)
+    dt = time.perf_counter() - t0
+    return {"value": A.shape[0] * r["its"] / dt, "unit": "DOF-updates/s", "cores": 1, "kind": "port",
+            "sample": f"3D 7-pt Poisson {n}^3, GMRES({restart}) pc none, {r['its']} iterations from x0=0, "
+                      f"oracle/oracle.c (PETSc Seq order, no FMA), 1 thread, {dt:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes of this benchmark), or None."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p))
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import GpuBlock
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Context, Mat, Options, Vec
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
+
+    n = args.n
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx = Context(local_rank, stream=stream)
+    kspopts = (f"-ksp_type gmres -ksp_gmres_restart {args.restart} -pc_type none -ksp_norm_type unpreconditioned "
+               f"-ksp_rtol {args.rtol} -ksp_max_it {args.max_it}")
+    rows = n * n * n
+
+    if world == 1:
+        # configs[1]: single-block GMRES(30) on 256^3 (gmres_solution.c:50-70 in 3D)
+        A = Mat.box_stencil(ctx, 3, n, n, n)
+        ones = Vec(ctx, rows)
+        ones.set(1.0)
+        b = Vec(ctx, rows)
+        A.mult(ones, b)
+        x = Vec(ctx, rows)
+        ksp = KSP(ctx)
+        ksp.set_operators(A)
+        ksp.set_from_options(Options(kspopts))
+        ksp.set_initial_guess_nonzero(False)
+        ksp.set_up()
+
+        def step():
+            ksp.solve(b, x)                     # zero initial guess: x is reset by KSPSolve
+            return ksp.get_iteration_number()
+        workload = f"3D 7-pt Poisson {n}^3, single-block GMRES({args.restart}) on 1 MI355X (configs[1])"
+    else:
+        comm = TorchComm(device=torch.device("cuda", local_rank))
+        L = block_layout(3, n, n, n * world, world, rank)
+        o = Options(kspopts)
+        blk = GpuBlock(ctx, L, None, comm, prefix="")
+        blk.ksp.set_from_options(o)
+        blk.halo.set(0.0)
+        blk.update_rhs()
+
+        def step():
+            its = blk.solve()                   # inner_solver (warm start, UIRNorm)
+            comm.exchange([blk])
+            blk.update_rhs()
+            sq = blk.local_residual_sq()
+            comm.ordered_sum([blk], [sq])
+            return its
+        workload = (f"3D 7-pt Poisson {n}x{n}x{n * world} synchronous multisplitting, {world} z-slab blocks of "
+                    f"{n}^3 (one per MI355X), inner GMRES({args.restart}) max_it {args.max_it}, RCCL halo exchange")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    timing = not args.no_timing
+    ctx.set_timing(timing)
+    ctx.reset_kernel_stats()
+    barrier()
+    t0 = time.perf_counter()
+    its_total = 0
+    for _ in range(args.steps):
+        its_total += step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    stats = ctx.kernel_stats() if timing else {}
+
+    my_updates = float(rows) * its_total
+    if world > 1:
+        t = torch.tensor([elapsed, my_updates], dtype=torch.float64, device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed_max, updates = float(tmax[0]), float(t[1])
+    else:
+        elapsed_max, updates = elapsed, my_updates
+
+    if rank == 0:
+        value = updates / elapsed_max
+        out = {"metric": METRIC, "value": value, "unit": "DOF-updates/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": 1e3 * elapsed_max / args.steps, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic: b = A*1 (exact solution u = 1), x0 = 0; device-assembled operator",
+               "config": {"workload": workload, "mesh_per_gpu": [n, n, n], "blocks": world,
+                          "ksp": kspopts, "gmres_iterations_per_step_per_block": its_total / args.steps,
+                          "parallelism": f"{world} z-slab block(s), one per GPU"}}
+        if stats:
+            total_ms = sum(s["ms"] for s in stats.values())
+            dom = max(stats, key=lambda k: stats[k]["ms"])
+            s = stats[dom]
+            achieved = (s["bytes"] / s["launches"]) / (s["ms"] / s["launches"] * 1e-3) / 1e9 if s["launches"] else 0
+            tr = load_traffic()
+            traffic = None
+            if tr and tr.get("kernel_class") == dom and tr.get("n") == n:
+                traffic = tr.get("hbm_bytes_per_launch")
+            out["roofline"] = {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": achieved,
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                               "traffic": traffic,
+                               "bytes_per_launch": s["bytes"] / max(s["launches"], 1),
+                               "avg_launch_ms": s["ms"] / max(s["launches"], 1)}
+            out["kernels"] = {k: {"launches": v["launches"], "ms_total": v["ms"],
+                                  "GBps": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] else None,
+                                  "share": v["ms"] / total_ms if total_ms else None} for k, v in stats.items()}
+            alg_bytes = sum(v["bytes"] for v in stats.values())
+            out["hbm_alg_GBps_whole_step"] = alg_bytes / (elapsed / 1) / 1e9
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n, args.restart, args.cpu_sample_its, args.rtol)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
