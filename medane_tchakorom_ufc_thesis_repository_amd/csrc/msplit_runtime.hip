@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -100,6 +101,13 @@ extern "C" int msp_ctx_create(int device, void* stream, msp_ctx** out) {
   }
   ARGCHK(device >= 0 && device < ndev, MSP_ERR_ARG_OUTOFRANGE, "device %d out of range [0,%d)", device, ndev);
   HIPCHK(hipSetDevice(device));
+  {
+    static const char* names[MSK_NVAR] = {"MSPLIT_VARIANT_SPMV", "MSPLIT_VARIANT_MDOT", "MSPLIT_VARIANT_MAXPY"};
+    for (int i = 0; i < MSK_NVAR; ++i) {
+      const char* e = getenv(names[i]);
+      if (e) msk_set_variant(i, atoi(e));
+    }
+  }
   msp_ctx* c = new msp_ctx();
   c->device = device;
   if (stream) {
