@@ -7,8 +7,7 @@
  * inner_solver() (src/utils/utils.c:950-970) and gmres_solution.c:70.
  *
  * Data layout: the m+1 basis vectors VV(0..m) are one HBM allocation,
- * (m+1) x stride doubles, stride = n rounded up to 512 plus a 16640-double
- * skew (4 KiB aligned, never a power of two apart).
+ * (m+1) x stride doubles, stride = n rounded up to 512 (4 KiB aligned).
  * Per Arnoldi step the device runs SpMV, the fused MDot (DBR), MAXPY with the
  * MDot results read straight from HBM, and the squared norm; ONE synchronising
  * copy brings h(0..it) and ||w||^2 to the host, which updates the 31x30
@@ -161,9 +160,12 @@ int msp_ksp_set_up(msp_ksp *k) {
   }
   if (k->setup) return MSP_SUCCESS;
   const int m = k->o.restart;
-  /* vectors exactly 2^k bytes apart alias HBM channels when MAXPY/MDot stream
-   * 30 of them at the same offset; a 130 KiB skew is worth ~8% on MAXPY(30) */
-  k->stride = (k->n + 511) / 512 * 512 + 16640;
+  /* an extra skew between basis vectors measured no gain in the solve
+   * (same-box A/B, profiles/r01/README.md); kept as a tuning knob */
+  int64_t skew = 0;
+  const char *env = getenv("MSPLIT_BASIS_SKEW"); /* tuning knob, doubles, rounded to 512 */
+  if (env) skew = (atoll(env) + 511) / 512 * 512;
+  k->stride = (k->n + 511) / 512 * 512 + skew;
   int rc = mspi_malloc(k->ctx, (void **)&k->basis, (size_t)(m + 1) * (size_t)k->stride * sizeof(double) + 4096);
   if (!rc) rc = mspi_malloc(k->ctx, (void **)&k->dh, (size_t)(m + 2) * sizeof(double));
   if (!rc) rc = mspi_host_malloc((void **)&k->hbuf, (size_t)(m + 2) * sizeof(double));
@@ -333,8 +335,8 @@ static int cycle(msp_ksp *k, int *itcount) {
     if ((rc = mspi_spmv(k->A, k->VV[it], w))) return rc;
     /* CGS: h = VecMDot(w, VV(0..it)); VecMAXPY(w, -h, VV); then ||w||^2 -- one sync */
     if ((rc = mspi_mdot(k->ctx, w, it + 1, (const double *const *)k->VV, k->n, k->dh))) return rc;
-    if ((rc = mspi_maxpy(k->ctx, w, it + 1, (const double *const *)k->VV, k->n, NULL, k->dh, 1, 0))) return rc;
-    if ((rc = mspi_norm2sq(k->ctx, w, k->n, k->dh + it + 1))) return rc;
+    if ((rc = mspi_maxpy_norm(k->ctx, w, it + 1, (const double *const *)k->VV, k->n, k->dh, 1, k->dh + it + 1)))
+      return rc;
     if ((rc = mspi_d2h_sync(k->ctx, k->hbuf, k->dh, (size_t)(it + 2) * sizeof(double)))) return rc;
     double *hh = &HH(k, 0, it);
     int bad = 0;

@@ -56,6 +56,10 @@ int mspi_norm2sq(msp_ctx *ctx, const double *x, int64_t n, double *out_dev);
  * VecMAXPY(T); VecAXPY(x,1,T) in one pass). */
 int mspi_maxpy(msp_ctx *ctx, double *w, int nv, const double *const *V, int64_t n, const double *alpha_host,
                const double *alpha_dev, int negate, int accumulate_into_x);
+/* CGS update fused with VecNorm: w += sum_j (-h_j) V[j] (h on the device),
+ * then out_dev[0] = ||w||^2 in DBR order, in one pass over the vectors. */
+int mspi_maxpy_norm(msp_ctx *ctx, double *w, int nv, const double *const *V, int64_t n, const double *alpha_dev,
+                    int negate, double *out_dev);
 int mspi_scale(msp_ctx *ctx, double *x, int64_t n, double alpha);
 int mspi_copy(msp_ctx *ctx, double *dst, const double *src, int64_t n);
 int mspi_set(msp_ctx *ctx, double *x, int64_t n, double alpha);

@@ -27,6 +27,8 @@ int msk_dot_stage1(const double* w, const VecGroup* V, int nv, int64_t n, double
 int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, hipStream_t s);
 int msk_maxpy(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate, int64_t n, int accum,
               hipStream_t s);
+int msk_maxpy_norm(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate, int64_t n,
+                   int accum, double* partial, hipStream_t s);
 int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
              const double* b, double* y, int32_t lds_cap, int resid, hipStream_t s);
 int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int32_t* rowptr, const int32_t* col,

@@ -118,9 +118,9 @@ __global__ __launch_bounds__(kT) void k_dot_stage2(const double* __restrict__ pa
 template <int NV>
 __device__ __forceinline__ double maxpy_elem(double u, const double (&a)[NV], const double (&p)[NV]) {
   constexpr int jrem = NV & 3;
-  if (jrem == 3) u = u + ((a[0] * p[0] + a[1] * p[1]) + a[2] * p[2]);
-  else if (jrem == 2) u = u + (a[0] * p[0] + a[1] * p[1]);
-  else if (jrem == 1) u = a[0] * p[0] + u;
+  if constexpr (jrem == 3) u = u + ((a[0] * p[0] + a[1] * p[1]) + a[2] * p[2]);
+  else if constexpr (jrem == 2) u = u + (a[0] * p[0] + a[1] * p[1]);
+  else if constexpr (jrem == 1) u = a[0] * p[0] + u;
 #pragma unroll
   for (int j = jrem; j < NV; j += 4) u = u + (((a[j] * p[j] + a[j + 1] * p[j + 1]) + a[j + 2] * p[j + 2]) + a[j + 3] * p[j + 3]);
   return u;
@@ -161,6 +161,139 @@ __global__ __launch_bounds__(kT, MINW) void k_maxpy(double* __restrict__ w, VecG
     for (int j = 0; j < NV; ++j) p[j] = V.p[j][e];
     const double u = maxpy_elem<NV>(ACCUM ? 0.0 : w[e], a, p);
     w[e] = ACCUM ? w[e] + u : u;
+  }
+}
+
+// Vector-major MAXPY in the DBR chunk layout: workgroup c owns elements
+// [4096c, 4096c+4096); lane t owns base + j*512 + 2t, +1 (j = 0..7) and keeps
+// their 16 running values in registers while the vectors stream past group by
+// group (each group = up to 4 vectors x 32 KiB contiguous per workgroup).
+// Per element the arithmetic is exactly PETSc's grouping (as maxpy_elem).
+// NORM: also the DBR partial of ||w_new||^2 for this chunk (VecNorm fused).
+template <int G>
+__device__ __forceinline__ double group_sum(const double (&a)[G], const double (&p)[G]) {
+  if constexpr (G == 1) {
+    return a[0] * p[0];
+  } else {
+  double s = a[0] * p[0] + a[1] * p[1];
+  if constexpr (G > 2) s = s + a[2] * p[2];
+  if constexpr (G > 3) s = s + a[3] * p[3];
+  return s;
+  }
+}
+
+template <int G, bool FULL>
+__device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const VecGroup& V, const Coefs& A,
+                                            const double* __restrict__ adev, int negate, int g, int64_t base,
+                                            int64_t n) {
+  double a[G];
+  const double* vp[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q) {  // wave-uniform: scalar loads from the kernel arguments / adev
+    const double aq = adev ? adev[g + q] : A.a[g + q];
+    a[q] = negate ? -aq : aq;
+    vp[q] = V.p[g + q];
+  }
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    const int64_t e = base + j * (2 * kT);
+    double p0[G], p1[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      if (FULL) {
+        const double2 v = *reinterpret_cast<const double2*>(vp[q] + e);
+        p0[q] = v.x;
+        p1[q] = v.y;
+      } else {
+        p0[q] = e < n ? vp[q][e] : 0.0;
+        p1[q] = e + 1 < n ? vp[q][e + 1] : 0.0;
+      }
+    }
+    const double s0 = group_sum<G>(a, p0), s1 = group_sum<G>(a, p1);
+    if constexpr (G == 1) {  // PetscKernelAXPY: s = a*p; s += U
+      u[2 * j] = s0 + u[2 * j];
+      u[2 * j + 1] = s1 + u[2 * j + 1];
+    } else {
+      u[2 * j] = u[2 * j] + s0;
+      u[2 * j + 1] = u[2 * j + 1] + s1;
+    }
+  }
+}
+
+template <bool ACCUM, bool NORM, bool FULL>
+__device__ __forceinline__ void maxpy_chunk_body(double* __restrict__ w, const VecGroup& V, const Coefs& A,
+                                                 const double* __restrict__ adev, int negate, int nv, int64_t base,
+                                                 int64_t n, double& sq) {
+  double u[2 * kIters];
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    const int64_t e = base + j * (2 * kT);
+    if (ACCUM) {
+      u[2 * j] = 0.0;
+      u[2 * j + 1] = 0.0;
+    } else if (FULL) {
+      const double2 q = *reinterpret_cast<const double2*>(w + e);
+      u[2 * j] = q.x;
+      u[2 * j + 1] = q.y;
+    } else {
+      u[2 * j] = e < n ? w[e] : 0.0;
+      u[2 * j + 1] = e + 1 < n ? w[e + 1] : 0.0;
+    }
+  }
+  const int jrem = nv & 3;
+  if (jrem == 3) chunk_group<3, FULL>(u, V, A, adev, negate, 0, base, n);
+  else if (jrem == 2) chunk_group<2, FULL>(u, V, A, adev, negate, 0, base, n);
+  else if (jrem == 1) chunk_group<1, FULL>(u, V, A, adev, negate, 0, base, n);
+#pragma unroll 1
+  for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL>(u, V, A, adev, negate, g, base, n);
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    const int64_t e = base + j * (2 * kT);
+    double r0 = u[2 * j], r1 = u[2 * j + 1];
+    if (FULL) {
+      if (ACCUM) {
+        const double2 q = *reinterpret_cast<const double2*>(w + e);
+        r0 = q.x + r0;
+        r1 = q.y + r1;
+      }
+      *reinterpret_cast<double2*>(w + e) = make_double2(r0, r1);
+      if (NORM) {
+        acc = acc + r0 * r0;
+        acc = acc + r1 * r1;
+      }
+    } else {
+      if (e < n) {
+        if (ACCUM) r0 = w[e] + r0;
+        w[e] = r0;
+        if (NORM) acc = acc + r0 * r0;
+      }
+      if (e + 1 < n) {
+        if (ACCUM) r1 = w[e + 1] + r1;
+        w[e + 1] = r1;
+        if (NORM) acc = acc + r1 * r1;
+      }
+    }
+  }
+  sq = acc;
+}
+
+template <bool ACCUM, bool NORM>
+__global__ __launch_bounds__(kT) void k_maxpy_chunk(double* __restrict__ w, VecGroup V, Coefs A,
+                                                    const double* __restrict__ adev, int negate, int nv, int64_t n,
+                                                    double* __restrict__ partial) {
+  const int t = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const int64_t base = c * kChunk + 2 * t;
+  double sq = 0.0;
+  if ((c + 1) * kChunk <= n) maxpy_chunk_body<ACCUM, NORM, true>(w, V, A, adev, negate, nv, base, n, sq);
+  else maxpy_chunk_body<ACCUM, NORM, false>(w, V, A, adev, negate, nv, base, n, sq);
+  if (NORM) {
+    __shared__ double red[4];
+    sq = wave_butterfly(sq);
+    if ((t & 63) == 0) red[t >> 6] = sq;
+    __syncthreads();
+    if (t == 0) partial[c] = (red[0] + red[1]) + (red[2] + red[3]);
   }
 }
 
@@ -389,12 +522,22 @@ extern "C" int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, do
   return (int)hipGetLastError();
 }
 
+extern "C" int msk_maxpy_norm(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate,
+                              int64_t n, int accum, double* partial, hipStream_t s) {
+  if (n <= 0 || nv <= 0) return 0;
+  const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
+  if (partial) k_maxpy_chunk<false, true><<<dim3(g), dim3(kT), 0, s>>>(w, *V, *A, adev, negate, nv, n, partial);
+  else if (accum) k_maxpy_chunk<true, false><<<dim3(g), dim3(kT), 0, s>>>(w, *V, *A, adev, negate, nv, n, partial);
+  else k_maxpy_chunk<false, false><<<dim3(g), dim3(kT), 0, s>>>(w, *V, *A, adev, negate, nv, n, partial);
+  return (int)hipGetLastError();
+}
+
 template <int NV>
 static void maxpy_dispatch(int nv, double* w, const VecGroup& V, const Coefs& A, const double* adev, int negate,
                            int64_t n, int accum, hipStream_t s) {
   if (nv == NV) {
     const int g = grid_for((n + 1) / 2, 4096);
-    if (g_variant[MSK_VAR_MAXPY] == 1) {
+    if (g_variant[MSK_VAR_MAXPY] == 2) {
       if (accum) k_maxpy<NV, true, 4><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
       else k_maxpy<NV, false, 4><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
     } else {
@@ -409,6 +552,7 @@ static void maxpy_dispatch(int nv, double* w, const VecGroup& V, const Coefs& A,
 extern "C" int msk_maxpy(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate,
                          int64_t n, int accum, hipStream_t s) {
   if (n <= 0 || nv <= 0) return 0;
+  if (g_variant[MSK_VAR_MAXPY] == 0) return msk_maxpy_norm(w, V, nv, A, adev, negate, n, accum, nullptr, s);
   maxpy_dispatch<1>(nv, w, *V, *A, adev, negate, n, accum, s);
   return (int)hipGetLastError();
 }

@@ -326,6 +326,27 @@ extern "C" int mspi_maxpy(msp_ctx* c, double* w, int nv, const double* const* V,
   return MSP_SUCCESS;
 }
 
+extern "C" int mspi_maxpy_norm(msp_ctx* c, double* w, int nv, const double* const* V, int64_t n,
+                               const double* alpha_dev, int negate, double* out_dev) {
+  if (nv > MSPI_MAX_GROUP || n <= 0) {
+    int rc = mspi_maxpy(c, w, nv, V, n, nullptr, alpha_dev, negate, 0);
+    return rc ? rc : mspi_norm2sq(c, w, n, out_dev);
+  }
+  const int64_t nch = nchunks_of(n);
+  int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
+  if (rc) return rc;
+  KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n * (nv + 2));
+  VecGroup vg;
+  Coefs cf;
+  for (int j = 0; j < nv; ++j) {
+    vg.p[j] = V[j];
+    cf.a[j] = 0.0;
+  }
+  KCHK(msk_maxpy_norm(w, &vg, nv, &cf, alpha_dev, negate, n, 0, c->partial, c->stream));
+  KCHK(msk_dot_stage2(c->partial, nch, 1, out_dev, c->stream));
+  return MSP_SUCCESS;
+}
+
 extern "C" int mspi_scale(msp_ctx* c, double* x, int64_t n, double alpha) {
   KTimer kt(c, MSP_KERNEL_SCALE, 16.0 * (double)n);
   KCHK(msk_blas1(MSK_SCALE, x, nullptr, nullptr, alpha, n, c->stream));

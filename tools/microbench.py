@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="spmv:0,1;maxpy:0,1;mdot:0")
+    ap.add_argument("--variants", default="spmv:0;maxpy:0,1;mdot:0")
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401
