@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-its", type=int, default=30)
     p.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="N>1 exchange backend: nccl (= RCCL, the product) or gloo (single-GPU rehearsal)")
     return p.parse_args()
 
 
@@ -88,9 +90,14 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
-    torch.cuda.set_device(local_rank)
+    ndev = max(1, torch.cuda.device_count())
+    dev = local_rank % ndev                  # identity on a full node; rehearsals may share a GPU
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
     from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
     from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import GpuBlock
     from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Context, Mat, Options, Vec
@@ -98,7 +105,7 @@ def main():
 
     n = args.n
     stream = torch.cuda.current_stream().cuda_stream
-    ctx = Context(local_rank, stream=stream)
+    ctx = Context(dev, stream=stream)
     kspopts = (f"-ksp_type gmres -ksp_gmres_restart {args.restart} -pc_type none -ksp_norm_type unpreconditioned "
                f"-ksp_rtol {args.rtol} -ksp_max_it {args.max_it}")
     rows = n * n * n
@@ -122,12 +129,12 @@ def main():
             return ksp.get_iteration_number()
         workload = f"3D 7-pt Poisson {n}^3, single-block GMRES({args.restart}) on 1 MI355X (configs[1])"
     else:
-        comm = TorchComm(device=torch.device("cuda", local_rank))
+        comm = TorchComm(device=torch.device("cuda", dev) if args.backend == "nccl" else torch.device("cpu"))
         L = block_layout(3, n, n, n * world, world, rank)
         o = Options(kspopts)
         blk = GpuBlock(ctx, L, None, comm, prefix="")
         blk.ksp.set_from_options(o)
-        blk.halo.set(0.0)
+        blk.reset_halo()
         blk.update_rhs()
 
         def step():
@@ -138,7 +145,8 @@ def main():
             comm.ordered_sum([blk], [sq])
             return its
         workload = (f"3D 7-pt Poisson {n}x{n}x{n * world} synchronous multisplitting, {world} z-slab blocks of "
-                    f"{n}^3 (one per MI355X), inner GMRES({args.restart}) max_it {args.max_it}, RCCL halo exchange")
+                    f"{n}^3 (one per MI355X), inner GMRES({args.restart}) max_it {args.max_it}, "
+                    f"{'RCCL' if args.backend == 'nccl' else 'gloo (rehearsal)'} halo exchange")
 
     def barrier():
         if world > 1:
@@ -162,7 +170,8 @@ def main():
 
     my_updates = float(rows) * its_total
     if world > 1:
-        t = torch.tensor([elapsed, my_updates], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, my_updates], dtype=torch.float64,
+                         device="cuda" if args.backend == "nccl" else "cpu")
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)

@@ -7,26 +7,29 @@ roots (synchronous-multisplitting.c:189-196, utils.c:584-592):
 * boundary exchange: each block sends only the plane(s) its neighbours'
   coupling rows read (the reference swaps whole block vectors, comm.c:135;
   A_ij is zero outside that plane, so the result is identical), over RCCL
-  (torch.distributed backend "nccl") with grouped send/recv, or gloo on CPU;
+  (torch.distributed backend "nccl", grouped send/recv GPU to GPU over xGMI),
+  or gloo (host tensors; CPU tests and single-GPU rehearsals);
 * the sum of per-block squared norms is an all-gather followed by a sum in
   block order, so the result does not depend on the collective's reduction
   order (for 2 blocks this is the reference's a + b).
 
-Two implementations share one interface:
-  LocalComm  -- every block in this process (one GPU, or tests): device copies;
+A block object provides: layout (utils.BlockLayout), pack_send(nbr) -> tensor
+with the plane(s) for neighbour nbr, recv_buffer(nbr) -> tensor to receive
+into, unpack_recv(), and, for LocalComm, copy_halo_from(block).
+
+  LocalComm  -- every block in this process (one GPU or tests): direct copies;
   TorchComm  -- one block per rank (one rank per GPU), torch.distributed.
 """
 from __future__ import annotations
-
-import math
 
 
 class LocalComm:
     """All blocks live in this process; the exchange is a device-to-device copy
     of each neighbour's boundary plane into the block's halo."""
 
-    def __init__(self):
-        self.world = 1
+    world = 1
+    rank = 0
+    backend = "local"
 
     def alloc(self, ctx, n):
         from .petsc import Vec
@@ -35,9 +38,7 @@ class LocalComm:
     def exchange(self, blocks):
         by_id = {blk.layout.b: blk for blk in blocks}
         for blk in blocks:
-            for nbr, halo_off, cnt, nbr_off in blk.layout.recv:
-                src = by_id[nbr]
-                src.x.copy_range_to(nbr_off, blk.halo, halo_off, cnt)
+            blk.copy_halo_from(by_id)
 
     def ordered_sum(self, blocks, values):
         """values[i] belongs to blocks[i]; sum in global block order."""
@@ -51,10 +52,10 @@ class LocalComm:
 
 
 class TorchComm:
-    """One block per rank over a torch.distributed process group.  With the
-    "nccl" backend (= RCCL on ROCm) the halo planes move GPU to GPU over xGMI
-    inside one ncclGroupStart/End (batch_isend_irecv); with "gloo" (CPU tests)
-    the same pattern runs on host tensors."""
+    """One block per rank over a torch.distributed process group (block id =
+    rank).  With "nccl" (= RCCL on ROCm) the halo planes move GPU to GPU inside
+    one ncclGroupStart/End (batch_isend_irecv); with "gloo" the same pattern
+    runs on host tensors (device planes are staged through the host)."""
 
     def __init__(self, group=None, device=None):
         import torch
@@ -65,24 +66,29 @@ class TorchComm:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.backend = dist.get_backend(group)
-        self.device = device if device is not None else (
-            torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu"))
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        self.device = device
+
+    @property
+    def device_buffers(self) -> bool:
+        """Halo buffers live in HBM (nccl) or on the host (gloo)."""
+        return self.backend == "nccl"
 
     def alloc(self, ctx, n):
-        """A device buffer visible both to torch (for the collective) and to the
-        HIP library (wrapped as a Vec over the same memory)."""
+        """A buffer visible to torch (for the collective) and, for nccl, to the
+        HIP library (a Vec over the same device memory)."""
         from .petsc import Vec
-        t = self.torch.zeros(max(int(n), 2), dtype=self.torch.float64, device=self.device)
-        return Vec(ctx, n, device_ptr=t.data_ptr()), t
+        if self.device_buffers:
+            t = self.torch.zeros(max(int(n), 2), dtype=self.torch.float64, device=self.device)
+            return Vec(ctx, n, device_ptr=t.data_ptr()), t
+        return Vec(ctx, n), self.torch.zeros(max(int(n), 2), dtype=self.torch.float64)
 
     def exchange_tensors(self, send: dict, recv: dict):
         """send/recv: {neighbour rank: tensor}.  Grouped point-to-point."""
         dist = self.dist
-        ops = []
-        for nbr, t in recv.items():
-            ops.append(dist.P2POp(dist.irecv, t, nbr, self.group))
-        for nbr, t in send.items():
-            ops.append(dist.P2POp(dist.isend, t, nbr, self.group))
+        ops = [dist.P2POp(dist.irecv, t, nbr, self.group) for nbr, t in recv.items()]
+        ops += [dist.P2POp(dist.isend, t, nbr, self.group) for nbr, t in send.items()]
         if not ops:
             return
         if self.backend == "nccl":
@@ -95,34 +101,31 @@ class TorchComm:
 
     def exchange(self, blocks):
         (blk,) = blocks
-        ctx = blk.ctx
-        # pack my boundary planes (device copies on the block's stream)
-        for nbr, off, cnt in blk.layout.send:
-            blk.x.copy_range_to(off, blk.send_bufs[nbr][0], 0, cnt)
-        ctx.synchronize()
-        send = {nbr: blk.send_bufs[nbr][1][:cnt] for nbr, _, cnt in blk.layout.send}
-        recv = {nbr: blk.halo_t[halo_off:halo_off + cnt] for nbr, halo_off, cnt, _ in blk.layout.recv}
+        send = {nbr: blk.pack_send(nbr) for nbr, _, _ in blk.layout.send}
+        recv = {nbr: blk.recv_buffer(nbr) for nbr, _, _, _ in blk.layout.recv}
         self.exchange_tensors(send, recv)
         if self.backend == "nccl":
-            self.torch.cuda.synchronize(self.device)
+            self.torch.cuda.current_stream(self.device).synchronize()
+        blk.unpack_recv()
 
     def allgather_scalar(self, v: float):
         torch = self.torch
-        t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
-        out = torch.zeros(self.world, dtype=torch.float64, device=self.device)
-        self.dist.all_gather_into_tensor(out, t, group=self.group)
-        return out.cpu().tolist()
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+        if self.backend == "nccl":
+            out = torch.zeros(self.world, dtype=torch.float64, device=dev)
+            self.dist.all_gather_into_tensor(out, t, group=self.group)
+            return out.cpu().tolist()
+        outs = [torch.zeros(1, dtype=torch.float64) for _ in range(self.world)]
+        self.dist.all_gather(outs, t, group=self.group)
+        return [float(o[0]) for o in outs]
 
     def ordered_sum(self, blocks, values):
         (v,) = values
         tot = 0.0
-        for x in self.allgather_scalar(v):
+        for x in self.allgather_scalar(v):       # rank order = block order
             tot += x
         return tot
 
     def barrier(self):
         self.dist.barrier(group=self.group)
-
-
-def sqrt(x):
-    return math.sqrt(x)

@@ -37,6 +37,9 @@ class GpuBlock:
         self.A_off = Mat.from_csr_rows(ctx, n, layout.halo_size, row_ids, rowptr, col, val)
         self.halo, self.halo_t = comm.alloc(ctx, layout.halo_size)
         self.send_bufs = {nbr: comm.alloc(ctx, cnt) for nbr, _, cnt in layout.send}
+        self._send_spec = {nbr: (off, cnt) for nbr, off, cnt in layout.send}
+        self._recv_spec = {nbr: (hoff, cnt) for nbr, hoff, cnt, _ in layout.recv}
+        self._device_bufs = getattr(comm, "device_buffers", True)
         self.b = Vec(ctx, n)
         self.x = Vec(ctx, n)
         self.rhs = Vec(ctx, n)
@@ -55,7 +58,37 @@ class GpuBlock:
         self.ksp = initializeKSP(ctx, self.A, False, self.prefix, opts)
         self.last_its = 0
 
+    # -- exchange hooks (comm.py)
+    def pack_send(self, nbr):
+        """The plane(s) neighbour nbr's coupling rows read, as a torch tensor."""
+        off, cnt = self._send_spec[nbr]
+        vec, t = self.send_bufs[nbr]
+        if self._device_bufs:                       # HBM buffer shared with torch (RCCL)
+            self.x.copy_range_to(off, vec, 0, cnt)
+            self.ctx.synchronize()
+            return t[:cnt]
+        import torch
+        t[:cnt] = torch.from_numpy(self.x.get_array(off, cnt))
+        return t[:cnt]
+
+    def recv_buffer(self, nbr):
+        hoff, cnt = self._recv_spec[nbr]
+        return self.halo_t[hoff:hoff + cnt]
+
+    def unpack_recv(self):
+        if not self._device_bufs and self.layout.halo_size:
+            self.halo.set_values(self.halo_t[:self.layout.halo_size].numpy())
+
+    def copy_halo_from(self, by_id):
+        """LocalComm: neighbour blocks in this process, device-to-device."""
+        for nbr, hoff, cnt, nbr_off in self.layout.recv:
+            by_id[nbr].x.copy_range_to(nbr_off, self.halo, hoff, cnt)
+
     # -- block operations used by the driver
+    def reset_halo(self):
+        """x_j = 0 before the first exchange (vectors are zero-initialised)."""
+        self.halo.set(0.0)
+
     def norm0_sq(self) -> float:
         """computeFinalResidualNorm at x = 0 (utils.c:575-595): ||b_i - A 0||^2 = ||b_i||^2."""
         ln = self.b.norm()
@@ -101,7 +134,7 @@ def sm_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_outer: int = 1
     # global_norm_0 (:162): sqrt of the block-ordered sum of squared local norms
     res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
     for blk in blocks:                                      # updateLocalRHS before the loop (:164)
-        blk.halo.set(0.0)
+        blk.reset_halo()
         blk.update_rhs()
     comm.barrier()
     t0 = time.perf_counter()
