@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--n", type=int, default=256, help="mesh edge per block (256 -> configs[1])")
+    p.add_argument("--mesh", type=int, default=256, help="mesh edge per block (256 -> configs[1])")
     p.add_argument("--max-it", type=int, default=300)
     p.add_argument("--restart", type=int, default=30)
     p.add_argument("--rtol", type=float, default=1e-4)
@@ -103,7 +103,7 @@ def main():
     from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Context, Mat, Options, Vec
     from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
 
-    n = args.n
+    n = args.mesh
     stream = torch.cuda.current_stream().cuda_stream
     ctx = Context(dev, stream=stream)
     kspopts = (f"-ksp_type gmres -ksp_gmres_restart {args.restart} -pc_type none -ksp_norm_type unpreconditioned "
