@@ -1,0 +1,218 @@
+// msplit_gmres.hip -- the scalar recurrence of KSPGMRES on the device.
+//
+// PETSc's KSPGMRESCycle alternates vector work with a few scalar steps (the
+// Givens update of one Hessenberg column, the happy-breakdown and convergence
+// tests, the residual history).  Doing those on the host costs a device->host
+// round trip per Arnoldi step.  Here they run in one-lane kernels reading and
+// writing a device-resident state (mspi_gmres_state), so the host enqueues a
+// whole restart cycle and synchronises once per cycle.  Each one-lane kernel is
+// a literal restatement of the corresponding PETSc 3.22.1 code (the same
+// statements as oracle/oracle.c); with IEEE division and square root correctly
+// rounded on gfx950 and no FMA contraction, the recurrence is bitwise the
+// host's.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "msplit.h"
+#include "msplit_internal.h"
+
+namespace {
+
+#define HHD(a, b) (g.hh[(int64_t)(b) * (st->m + 2) + (a)])
+
+__device__ inline bool bad(double v) { return isnan(v) || isinf(v); }
+
+__device__ inline void log_res(const mspi_gmres_dev& g, double r) {
+  mspi_gmres_state* st = g.st;
+  if (st->nhist < st->hist_cap) g.hist[st->nhist] = r;
+  st->nhist++;
+}
+
+// KSPConvergedDefault
+__device__ inline void converged(const mspi_gmres_dev& g, int n, double rnorm) {
+  mspi_gmres_state* st = g.st;
+  st->reason = MSP_CONVERGED_ITERATING;
+  if (n == 0) {
+    if (!st->guess_zero && !st->uirnorm) {
+      double snorm = st->bnorm;
+      if (snorm == 0.0) snorm = rnorm;
+      st->rnorm0 = snorm;
+    } else {
+      st->rnorm0 = rnorm;
+    }
+    const double t = st->rtol * st->rnorm0;
+    st->ttol = t < st->abstol ? st->abstol : t;  // PetscMax
+  }
+  if (bad(rnorm)) st->reason = MSP_DIVERGED_NANORINF;
+  else if (rnorm <= st->ttol) st->reason = (rnorm < st->abstol) ? MSP_CONVERGED_ATOL : MSP_CONVERGED_RTOL;
+  else if (rnorm >= st->divtol * st->rnorm0) st->reason = MSP_DIVERGED_DTOL;
+}
+
+// Start of KSPGMRESCycle, after VecNorm(VV(0)) (the scale is applied by the first SpMV).
+__global__ void k_cycle_start(mspi_gmres_dev g, const double* __restrict__ sumsq) {
+  mspi_gmres_state* st = g.st;
+  st->it = 0;
+  st->stop = 0;
+  st->skip_build = 0;
+  const double res = sqrt(*sumsq);
+  st->scale = (res != 0.0 && !bad(res)) ? 1.0 / res : 1.0;
+  if (bad(res)) {  // KSPCheckNorm: return
+    st->reason = MSP_DIVERGED_NANORINF;
+    st->stop = st->skip_build = 1;
+    return;
+  }
+  if (st->rnorm > 0.0 && fabs(res - st->rnorm) > st->breakdowntol * st->gm_rnorm0) {
+    st->reason = MSP_DIVERGED_BREAKDOWN;
+    st->stop = st->skip_build = 1;
+    return;
+  }
+  g.grs[0] = st->gm_rnorm0 = res;
+  st->rnorm = res;
+  st->res = res;
+  log_res(g, res);
+  if (res == 0.0) {
+    st->reason = MSP_CONVERGED_ATOL;
+    st->stop = st->skip_build = 1;
+    return;
+  }
+  converged(g, st->its, res);
+  if (st->reason || !(st->its < st->max_it) || st->m < 1) st->stop = 1;  // the while loop does not run
+}
+
+// KSPGMRESUpdateHessenberg
+__device__ inline void update_hessenberg(const mspi_gmres_dev& g, int it, int hapend, double* res) {
+  mspi_gmres_state* st = g.st;
+  double* hh = &HHD(0, it);
+  for (int j = 1; j <= it; ++j) {
+    const double tt = hh[j - 1];
+    hh[j - 1] = g.cc[j - 1] * tt + g.ss[j - 1] * hh[j];
+    hh[j] = g.cc[j - 1] * hh[j] - (g.ss[j - 1] * tt);
+  }
+  if (!hapend) {
+    const double tt = sqrt(hh[it] * hh[it] + hh[it + 1] * hh[it + 1]);
+    if (tt == 0.0) {
+      st->reason = MSP_DIVERGED_NULL;
+      return;
+    }
+    g.cc[it] = hh[it] / tt;
+    g.ss[it] = hh[it + 1] / tt;
+    g.grs[it + 1] = -(g.ss[it] * g.grs[it]);
+    g.grs[it] = g.cc[it] * g.grs[it];
+    hh[it] = g.cc[it] * hh[it] + g.ss[it] * hh[it + 1];
+    *res = fabs(g.grs[it + 1]);
+  } else {
+    *res = 0.0;
+  }
+}
+
+// The rest of one KSPGMRESCycle iteration once h(0..it) = VecMDot and
+// h(it+1) = ||w||^2 (after the CGS VecMAXPY) are in HBM.
+__global__ void k_iter_update(mspi_gmres_dev g) {
+  mspi_gmres_state* st = g.st;
+  if (st->stop) return;
+  const int it = st->it;
+  double* hh = &HHD(0, it);
+  bool nan_dot = false;
+  for (int j = 0; j <= it; ++j) {
+    hh[j] = 0.0;
+    if (bad(g.h[j])) nan_dot = true;
+  }
+  double res = st->res;
+  int hapend = 0;
+  if (nan_dot) {  // KSPCheckDot in the orthogonalisation -> break
+    st->reason = MSP_DIVERGED_NANORINF;
+  } else {
+    for (int j = 0; j <= it; ++j) hh[j] -= -g.h[j];  // lhh = -lhh; hh -= lhh
+    const double tt = sqrt(g.h[it + 1]);
+    if (bad(tt)) {  // KSPCheckNorm: return without BuildSoln
+      st->reason = MSP_DIVERGED_NANORINF;
+      st->stop = st->skip_build = 1;
+      return;
+    }
+    st->scale = (tt != 0.0) ? 1.0 / tt : 1.0;  // VecNormalize of VV(it+1), applied by the next SpMV
+    HHD(it + 1, it) = tt;
+    double hapbnd = fabs(tt / g.grs[it]);
+    if (hapbnd > st->haptol) hapbnd = st->haptol;
+    if (tt < hapbnd) hapend = 1;
+    update_hessenberg(g, it, hapend, &res);
+    st->it = it + 1;
+    st->its++;
+    st->rnorm = res;
+    st->res = res;
+    if (!st->reason) {
+      converged(g, st->its, res);
+      if (hapend && !st->reason) st->reason = MSP_DIVERGED_BREAKDOWN;
+    }
+  }
+  const int itn = st->it;
+  if (!st->reason && itn < st->m && st->its < st->max_it) {
+    log_res(g, res);  // "if (it) log" at the top of the next iteration
+    return;
+  }
+  st->stop = 1;  // loop exit
+  if (itn && (st->reason || st->its >= st->max_it)) log_res(g, res);
+}
+
+// KSPGMRESBuildSoln(GRS(0), x, x, ksp, it - 1): back-solve in place (nrs
+// aliases GRS); the x update is the accumulate-MAXPY that follows.
+__global__ void k_build(mspi_gmres_dev g) {
+  mspi_gmres_state* st = g.st;
+  st->nbuild = 0;
+  if (st->skip_build) return;
+  const int it = st->it - 1;
+  if (it < 0) return;
+  double* nrs = g.grs;
+  if (HHD(it, it) != 0.0) {
+    nrs[it] = g.grs[it] / HHD(it, it);
+  } else {
+    st->reason = MSP_DIVERGED_BREAKDOWN;
+    return;
+  }
+  for (int ii = 1; ii <= it; ++ii) {
+    const int k = it - ii;
+    double tt = g.grs[k];
+    for (int j = k + 1; j <= it; ++j) tt = tt - HHD(k, j) * nrs[j];
+    if (HHD(k, k) == 0.0) {
+      st->reason = MSP_DIVERGED_BREAKDOWN;
+      return;
+    }
+    nrs[k] = tt / HHD(k, k);
+  }
+  st->nbuild = it + 1;
+}
+
+}  // namespace
+
+// ctx stream accessor lives in msplit_runtime.hip
+extern "C" hipStream_t mspi_stream(msp_ctx* ctx);
+
+extern "C" int mspi_gm_cycle_start(msp_ctx* ctx, mspi_gmres_dev g, const double* sumsq_dev) {
+  k_cycle_start<<<1, 1, 0, mspi_stream(ctx)>>>(g, sumsq_dev);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    mspi_set_error(MSP_ERR_LIB, "k_cycle_start: %s", hipGetErrorString(e));
+    return MSP_ERR_LIB;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_gm_iter_update(msp_ctx* ctx, mspi_gmres_dev g) {
+  k_iter_update<<<1, 1, 0, mspi_stream(ctx)>>>(g);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    mspi_set_error(MSP_ERR_LIB, "k_iter_update: %s", hipGetErrorString(e));
+    return MSP_ERR_LIB;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_gm_build(msp_ctx* ctx, mspi_gmres_dev g) {
+  k_build<<<1, 1, 0, mspi_stream(ctx)>>>(g);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    mspi_set_error(MSP_ERR_LIB, "k_build: %s", hipGetErrorString(e));
+    return MSP_ERR_LIB;
+  }
+  return MSP_SUCCESS;
+}

@@ -56,13 +56,48 @@ int mspi_norm2sq(msp_ctx *ctx, const double *x, int64_t n, double *out_dev);
  * VecMAXPY(T); VecAXPY(x,1,T) in one pass). */
 int mspi_maxpy(msp_ctx *ctx, double *w, int nv, const double *const *V, int64_t n, const double *alpha_host,
                const double *alpha_dev, int negate, int accumulate_into_x);
-/* CGS update fused with VecNorm: w += sum_j (-h_j) V[j] (h on the device),
- * then out_dev[0] = ||w||^2 in DBR order, in one pass over the vectors. */
-int mspi_maxpy_norm(msp_ctx *ctx, double *w, int nv, const double *const *V, int64_t n, const double *alpha_dev,
-                    int negate, double *out_dev);
 int mspi_scale(msp_ctx *ctx, double *x, int64_t n, double alpha);
 int mspi_copy(msp_ctx *ctx, double *dst, const double *src, int64_t n);
 int mspi_set(msp_ctx *ctx, double *x, int64_t n, double alpha);
+
+/* ---- device-resident KSPGMRES state (msplit_gmres.hip) ---- */
+typedef struct {
+  int32_t stop;        /* cycle over: later kernels of this cycle return at once */
+  int32_t skip_build;  /* cycle returned before BuildSoln (PETSc's early PetscFunctionReturn) */
+  int32_t it;          /* iterations done in this cycle */
+  int32_t its;         /* ksp->its */
+  int32_t reason;      /* KSPConvergedReason */
+  int32_t nhist;       /* residual history entries written */
+  int32_t nbuild;      /* vectors BuildSoln combines (it of BuildSoln + 1, or 0) */
+  int32_t guess_zero;  /* the solve's original zero-guess flag (KSPConvergedDefault n == 0) */
+  int32_t m, max_it, uirnorm, hist_cap;
+  double res, rnorm, rnorm0, ttol, gm_rnorm0;
+  double scale;        /* VecNormalize factor still to apply to the newest vector (fused into SpMV) */
+  double bnorm;        /* ||b|| for the n == 0 test with a nonzero guess and no UIRNorm */
+  double rtol, abstol, divtol, haptol, breakdowntol;
+} mspi_gmres_state;
+
+typedef struct {
+  mspi_gmres_state *st; /* device */
+  double *hh;           /* (m+2) x (m+1), HH(a,b) = hh[b*(m+2)+a] */
+  double *cc, *ss, *grs; /* m+2 each */
+  double *h;            /* m+2: MDot results h(0..it), then ||w||^2 at h(it+1) */
+  double *hist;         /* hist_cap */
+} mspi_gmres_dev;
+
+/* one-lane kernels of the GMRES recurrence */
+int mspi_gm_cycle_start(msp_ctx *ctx, mspi_gmres_dev g, const double *sumsq_dev);
+int mspi_gm_iter_update(msp_ctx *ctx, mspi_gmres_dev g);
+int mspi_gm_build(msp_ctx *ctx, mspi_gmres_dev g);
+/* data-path pieces with a stop flag; basis = VV(j) at base + j*stride */
+int mspi_spmv_scaled(msp_mat *A, const double *x, const double *sdev, double *vout, double *y, const int *stop);
+int mspi_mdot_basis(msp_ctx *ctx, const double *w, int nv, const double *base, int64_t stride, int64_t n,
+                    double *out_dev, const int *stop);
+int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv, const double *base, int64_t stride,
+                          int64_t n, const double *alpha_dev, double *sumsq_dev, const int *stop);
+int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const double *base, int64_t stride, int64_t n,
+                           const double *coef_dev, int nv_expected);
+int mspi_h2d_async(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,4 @@
-// msplit_kernels.h -- launcher declarations shared by msplit_kernels.hip and
-// msplit_runtime.hip (C++/HIP side only).
+// msplit_kernels.h -- launcher declarations shared by the .hip files (C++/HIP side only).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -11,26 +10,39 @@
 
 enum { MSK_SET = 0, MSK_COPY, MSK_SCALE, MSK_AXPY, MSK_AYPX, MSK_WAXPY_P1, MSK_WAXPY_M1, MSK_WAXPY };
 
-struct VecGroup {
+// A set of vectors: an explicit table (up to 32), or a strided basis
+// V_j = base + j*stride (any count) when base != nullptr.
+struct Vecs {
   const double* p[MSK_MAX_GROUP];
+  const double* base;
+  int64_t stride;
 };
 struct Coefs {
   double a[MSK_MAX_GROUP];
 };
 
-enum { MSK_VAR_SPMV = 0, MSK_VAR_MDOT, MSK_VAR_MAXPY, MSK_NVAR };
+// SpMV modes
+enum { MSK_SPMV_MULT = 0, MSK_SPMV_RESID = 1, MSK_SPMV_SCALED = 2 };
+
+// tuning flags
+enum { MSK_TUNE_MDOT_REV = 1, MSK_TUNE_SPMV_NT = 2 };
 
 extern "C" {
-void msk_set_variant(int which, int v);
-int msk_dot_stage1(const double* w, const VecGroup* V, int nv, int64_t n, double* partial, int64_t nchunks, int self,
-                   hipStream_t s);
-int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, hipStream_t s);
-int msk_maxpy(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate, int64_t n, int accum,
-              hipStream_t s);
-int msk_maxpy_norm(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate, int64_t n,
-                   int accum, double* partial, hipStream_t s);
+void msk_set_tuning(int flags);
+int msk_get_tuning(void);
+// DBR stage 1 over nv <= 32 vectors (self: ||w||^2).  stop: device flag, skip when set (may be null).
+int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks, int self,
+                   const int* stop, hipStream_t s);
+int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, const int* stop, hipStream_t s);
+// wout = win + sum_j a_j V_j (PETSc grouping), a_j = (negate ? -1 : 1) * (adev ? adev[j] : A->a[j]);
+// nv = *nvdev when nvdev != null; accum: wout = win + (0 + sum); partial != null: DBR partial of ||wout||^2.
+int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, const int* nvdev, const Coefs* A,
+                    const double* adev, int negate, int64_t n, int accum, double* partial, const int* stop,
+                    hipStream_t s);
+// mode MULT: y = A x; RESID: y = b - A x; SCALED: sc = *sdev, vout = sc*x (own rows), y = A (sc*x).
 int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
-             const double* b, double* y, int32_t lds_cap, int resid, hipStream_t s);
+             const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
+             const int* stop, hipStream_t s);
 int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int32_t* rowptr, const int32_t* col,
                   const double* val, const double* x, const double* b, double* y, int resid, hipStream_t s);
 int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int32_t* rowptr, int32_t* col,

@@ -7,6 +7,10 @@
 // bit.  Reductions use the deterministic blocked reduction (DBR) whose exact
 // order is restated in oracle/oracle.c (dbr_dot): results never depend on the
 // launch geometry, the XCD a workgroup lands on, or timing.
+//
+// Kernels that run inside a GMRES cycle take a device `stop` flag: once the
+// device-side convergence logic (msplit_gmres.hip) ends the cycle, the rest of
+// the speculatively enqueued iterations return at once.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -15,11 +19,28 @@
 
 namespace msk {
 
-constexpr int kT = 256;          // threads per workgroup (4 wave64)
-constexpr int kIters = 8;        // double2 slices per thread per DBR chunk
+constexpr int kT = 256;                  // threads per workgroup (4 wave64)
+constexpr int kIters = 8;                // double2 slices per thread per DBR chunk
 constexpr int kChunk = kT * 2 * kIters;  // 4096 elements per DBR chunk
 
 static_assert(kChunk == MSK_DBR_CHUNK, "DBR chunk must match the oracle");
+
+__device__ __forceinline__ bool stopped(const int* stop) { return stop && *stop; }
+
+typedef double dx2 __attribute__((ext_vector_type(2)));
+typedef int ix4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double2 ld_nt(const double2* p) {
+  const dx2 v = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(p));
+  return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ int4 ld_nt(const int4* p) {
+  const ix4 v = __builtin_nontemporal_load(reinterpret_cast<const ix4*>(p));
+  return make_int4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ const double* vec_at(const Vecs& V, int j) {
+  return V.base ? V.base + (int64_t)j * V.stride : V.p[j];
+}
 
 __device__ __forceinline__ double wave_butterfly(double v) {
   // v[l] <- v[l] + v[l ^ off], off = 32..1: every lane ends with the same sum.
@@ -31,10 +52,13 @@ __device__ __forceinline__ double wave_butterfly(double v) {
 // ---------------------------------------------------------------- DBR dots
 // Stage 1: workgroup c reduces chunk c of every vector: lane t accumulates its
 // elements base + j*512 + 2t, +1 (j = 0..7) in order, wave butterfly, then
-// (w0 + w1) + (w2 + w3).  partial[v * nchunks + c].
+// (w0 + w1) + (w2 + w3).  partial[v * nchunks + c].  w stays in registers and
+// each vector streams 32 KiB contiguous per workgroup.
 template <int NV, bool SELF>
-__global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w, VecGroup V, int64_t n,
-                                                   double* __restrict__ partial, int64_t nchunks) {
+__global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w, Vecs V, int64_t n,
+                                                   double* __restrict__ partial, int64_t nchunks,
+                                                   const int* __restrict__ stop, int rev) {
+  if (stopped(stop)) return;
   __shared__ double red[NV][4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t c = blockIdx.x;
@@ -57,7 +81,10 @@ __global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w,
     }
   }
 #pragma unroll
-  for (int v = 0; v < NV; ++v) {
+  for (int vi = 0; vi < NV; ++vi) {
+    // load order only (each dot is independent): newest vector first when rev,
+    // so the CGS MAXPY that follows finds the oldest ones still in the MALL
+    const int v = rev ? NV - 1 - vi : vi;
     double acc = 0.0;
     if (SELF) {
       if (full) {
@@ -72,7 +99,7 @@ __global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w,
         }
       }
     } else {
-      const double* __restrict__ y = V.p[v];
+      const double* __restrict__ y = vec_at(V, v);
       if (full) {
         double2 q[kIters];
 #pragma unroll
@@ -100,7 +127,8 @@ __global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w,
 
 // Stage 2: workgroup v folds the nchunks partials of vector v the same way.
 __global__ __launch_bounds__(kT) void k_dot_stage2(const double* __restrict__ partial, int64_t nchunks,
-                                                   double* __restrict__ out) {
+                                                   double* __restrict__ out, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
   __shared__ double red[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const double* p = partial + blockIdx.x * nchunks;
@@ -113,77 +141,28 @@ __global__ __launch_bounds__(kT) void k_dot_stage2(const double* __restrict__ pa
 }
 
 // ------------------------------------------------------------------ MAXPY
-// u = w (or 0 when ACCUM); PETSc VecMAXPY_Seq grouping: the nv&3 leading
-// vectors (AXPY3/AXPY2/AXPY), then groups of four; w = u (or x + u when ACCUM).
-template <int NV>
-__device__ __forceinline__ double maxpy_elem(double u, const double (&a)[NV], const double (&p)[NV]) {
-  constexpr int jrem = NV & 3;
-  if constexpr (jrem == 3) u = u + ((a[0] * p[0] + a[1] * p[1]) + a[2] * p[2]);
-  else if constexpr (jrem == 2) u = u + (a[0] * p[0] + a[1] * p[1]);
-  else if constexpr (jrem == 1) u = a[0] * p[0] + u;
-#pragma unroll
-  for (int j = jrem; j < NV; j += 4) u = u + (((a[j] * p[j] + a[j + 1] * p[j + 1]) + a[j + 2] * p[j + 2]) + a[j + 3] * p[j + 3]);
-  return u;
-}
-
-template <int NV, bool ACCUM, int MINW>
-__global__ __launch_bounds__(kT, MINW) void k_maxpy(double* __restrict__ w, VecGroup V, Coefs A, const double* __restrict__ adev,
-                                              int negate, int64_t n) {
-  double a[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const double aj = adev ? adev[j] : A.a[j];
-    a[j] = negate ? -aj : aj;
-  }
-  const int64_t npair = n >> 1;
-  const int64_t stride = (int64_t)gridDim.x * kT;
-  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < npair; i += stride) {
-    const double2 wv = *reinterpret_cast<const double2*>(w + 2 * i);
-    double p0[NV], p1[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const double2 q = *reinterpret_cast<const double2*>(V.p[j] + 2 * i);
-      p0[j] = q.x;
-      p1[j] = q.y;
-    }
-    double u0 = maxpy_elem<NV>(ACCUM ? 0.0 : wv.x, a, p0);
-    double u1 = maxpy_elem<NV>(ACCUM ? 0.0 : wv.y, a, p1);
-    if (ACCUM) {
-      u0 = wv.x + u0;
-      u1 = wv.y + u1;
-    }
-    *reinterpret_cast<double2*>(w + 2 * i) = make_double2(u0, u1);
-  }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    const int64_t e = n - 1;
-    double p[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) p[j] = V.p[j][e];
-    const double u = maxpy_elem<NV>(ACCUM ? 0.0 : w[e], a, p);
-    w[e] = ACCUM ? w[e] + u : u;
-  }
-}
-
 // Vector-major MAXPY in the DBR chunk layout: workgroup c owns elements
 // [4096c, 4096c+4096); lane t owns base + j*512 + 2t, +1 (j = 0..7) and keeps
 // their 16 running values in registers while the vectors stream past group by
 // group (each group = up to 4 vectors x 32 KiB contiguous per workgroup).
-// Per element the arithmetic is exactly PETSc's grouping (as maxpy_elem).
+// Per element the arithmetic is PETSc VecMAXPY_Seq's: the nv&3 leading vectors
+// (PetscKernelAXPY3/2/1), then groups of four (PetscKernelAXPY4),
+// U += a0*p0 + a1*p1 + a2*p2 + a3*p3 evaluated left to right.
 // NORM: also the DBR partial of ||w_new||^2 for this chunk (VecNorm fused).
 template <int G>
 __device__ __forceinline__ double group_sum(const double (&a)[G], const double (&p)[G]) {
   if constexpr (G == 1) {
     return a[0] * p[0];
   } else {
-  double s = a[0] * p[0] + a[1] * p[1];
-  if constexpr (G > 2) s = s + a[2] * p[2];
-  if constexpr (G > 3) s = s + a[3] * p[3];
-  return s;
+    double s = a[0] * p[0] + a[1] * p[1];
+    if constexpr (G > 2) s = s + a[2] * p[2];
+    if constexpr (G > 3) s = s + a[3] * p[3];
+    return s;
   }
 }
 
 template <int G, bool FULL>
-__device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const VecGroup& V, const Coefs& A,
+__device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs& V, const Coefs& A,
                                             const double* __restrict__ adev, int negate, int g, int64_t base,
                                             int64_t n) {
   double a[G];
@@ -192,7 +171,7 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const VecGr
   for (int q = 0; q < G; ++q) {  // wave-uniform: scalar loads from the kernel arguments / adev
     const double aq = adev ? adev[g + q] : A.a[g + q];
     a[q] = negate ? -aq : aq;
-    vp[q] = V.p[g + q];
+    vp[q] = vec_at(V, g + q);
   }
 #pragma unroll
   for (int j = 0; j < kIters; ++j) {
@@ -221,9 +200,9 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const VecGr
 }
 
 template <bool ACCUM, bool NORM, bool FULL>
-__device__ __forceinline__ void maxpy_chunk_body(double* __restrict__ w, const VecGroup& V, const Coefs& A,
-                                                 const double* __restrict__ adev, int negate, int nv, int64_t base,
-                                                 int64_t n, double& sq) {
+__device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win, double* __restrict__ wout,
+                                                 const Vecs& V, const Coefs& A, const double* __restrict__ adev,
+                                                 int negate, int nv, int64_t base, int64_t n, double& sq) {
   double u[2 * kIters];
 #pragma unroll
   for (int j = 0; j < kIters; ++j) {
@@ -232,12 +211,12 @@ __device__ __forceinline__ void maxpy_chunk_body(double* __restrict__ w, const V
       u[2 * j] = 0.0;
       u[2 * j + 1] = 0.0;
     } else if (FULL) {
-      const double2 q = *reinterpret_cast<const double2*>(w + e);
+      const double2 q = *reinterpret_cast<const double2*>(win + e);
       u[2 * j] = q.x;
       u[2 * j + 1] = q.y;
     } else {
-      u[2 * j] = e < n ? w[e] : 0.0;
-      u[2 * j + 1] = e + 1 < n ? w[e + 1] : 0.0;
+      u[2 * j] = e < n ? win[e] : 0.0;
+      u[2 * j + 1] = e + 1 < n ? win[e + 1] : 0.0;
     }
   }
   const int jrem = nv & 3;
@@ -252,25 +231,25 @@ __device__ __forceinline__ void maxpy_chunk_body(double* __restrict__ w, const V
     const int64_t e = base + j * (2 * kT);
     double r0 = u[2 * j], r1 = u[2 * j + 1];
     if (FULL) {
-      if (ACCUM) {
-        const double2 q = *reinterpret_cast<const double2*>(w + e);
+      if (ACCUM) {  // VecAXPY(x, 1.0, T): x + T
+        const double2 q = *reinterpret_cast<const double2*>(win + e);
         r0 = q.x + r0;
         r1 = q.y + r1;
       }
-      *reinterpret_cast<double2*>(w + e) = make_double2(r0, r1);
+      *reinterpret_cast<double2*>(wout + e) = make_double2(r0, r1);
       if (NORM) {
         acc = acc + r0 * r0;
         acc = acc + r1 * r1;
       }
     } else {
       if (e < n) {
-        if (ACCUM) r0 = w[e] + r0;
-        w[e] = r0;
+        if (ACCUM) r0 = win[e] + r0;
+        wout[e] = r0;
         if (NORM) acc = acc + r0 * r0;
       }
       if (e + 1 < n) {
-        if (ACCUM) r1 = w[e + 1] + r1;
-        w[e + 1] = r1;
+        if (ACCUM) r1 = win[e + 1] + r1;
+        wout[e + 1] = r1;
         if (NORM) acc = acc + r1 * r1;
       }
     }
@@ -279,15 +258,19 @@ __device__ __forceinline__ void maxpy_chunk_body(double* __restrict__ w, const V
 }
 
 template <bool ACCUM, bool NORM>
-__global__ __launch_bounds__(kT) void k_maxpy_chunk(double* __restrict__ w, VecGroup V, Coefs A,
-                                                    const double* __restrict__ adev, int negate, int nv, int64_t n,
-                                                    double* __restrict__ partial) {
+__global__ __launch_bounds__(kT) void k_maxpy_chunk(const double* win, double* wout, Vecs V, Coefs A,
+                                                    const double* __restrict__ adev, int negate, int nv,
+                                                    const int* __restrict__ nvdev, int64_t n,
+                                                    double* __restrict__ partial, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  if (nvdev) nv = *nvdev;
+  if (nv <= 0) return;
   const int t = threadIdx.x;
   const int64_t c = blockIdx.x;
   const int64_t base = c * kChunk + 2 * t;
   double sq = 0.0;
-  if ((c + 1) * kChunk <= n) maxpy_chunk_body<ACCUM, NORM, true>(w, V, A, adev, negate, nv, base, n, sq);
-  else maxpy_chunk_body<ACCUM, NORM, false>(w, V, A, adev, negate, nv, base, n, sq);
+  if ((c + 1) * kChunk <= n) maxpy_chunk_body<ACCUM, NORM, true>(win, wout, V, A, adev, negate, nv, base, n, sq);
+  else maxpy_chunk_body<ACCUM, NORM, false>(win, wout, V, A, adev, negate, nv, base, n, sq);
   if (NORM) {
     __shared__ double red[4];
     sq = wave_butterfly(sq);
@@ -299,46 +282,23 @@ __global__ __launch_bounds__(kT) void k_maxpy_chunk(double* __restrict__ w, VecG
 
 // ------------------------------------------------------------------- SpMV
 // Row-blocked CSR: workgroup b owns rows [256b, 256b+256).  Its contiguous
-// slice of col/val is staged into LDS with 16-byte coalesced loads, then lane
-// t sums row 256b+t left to right over its columns (MatMult_SeqAIJ order),
-// gathering x from L2/MALL.  RESID: r = b - sum.
-template <bool RESID>
-__global__ __launch_bounds__(kT) void k_spmv_lds(int32_t nrows, const int32_t* __restrict__ rowptr,
-                                                 const int32_t* __restrict__ col, const double* __restrict__ val,
-                                                 const double* __restrict__ x, const double* __restrict__ b,
-                                                 double* __restrict__ y, int32_t lds_cap) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* sval = reinterpret_cast<double*>(smem);
-  int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
-  const int t = threadIdx.x;
-  const int32_t r0 = blockIdx.x * kT;
-  const int32_t r1 = min(r0 + kT, nrows);
-  const int32_t start = rowptr[r0], end = rowptr[r1];
-  const int32_t s2 = start & ~1, s4 = start & ~3;
-  const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
-  const double2* v2 = reinterpret_cast<const double2*>(val + s2);
-  const int4* c4 = reinterpret_cast<const int4*>(col + s4);
-  for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = v2[i];
-  for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = c4[i];
-  __syncthreads();
-  const int32_t r = r0 + t;
-  if (r < r1) {
-    const int32_t k0 = rowptr[r], k1 = rowptr[r + 1];
-    double s = 0.0;
-    for (int32_t k = k0; k < k1; ++k) s = s + sval[k - s2] * x[scol[k - s4]];
-    y[r] = RESID ? b[r] - s : s;
-  }
-}
-
-// Same staging; the row is consumed in chunks of 8 entries whose 8 LDS reads
-// and 8 x-gathers are all issued before the first product (indices clamped
-// to the row, never branched around), so each lane keeps 8 gathers in flight.
-// The sum is still left to right over the row.
-template <bool RESID>
+// slice of col/val is staged into LDS with 16-byte coalesced loads; lane t then
+// sums row 256b+t left to right over its columns (MatMult_SeqAIJ order), in
+// chunks of 8 entries whose 8 LDS reads and 8 x-gathers are all issued before
+// the first product (indices clamped to the row, never branched around), so
+// each lane keeps 8 gathers in flight.
+//   MULT: y = A x    RESID: y = b - A x
+//   SCALED (VecNormalize fused into the next MatMult): sc = *sdev,
+//     vout[r] = x[r]*sc and y = A (sc*x), each product val*(x*sc) rounded
+//     exactly as VecScale followed by MatMult.
+template <int MODE, bool NT>
 __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col, const double* __restrict__ val,
                                                   const double* __restrict__ x, const double* __restrict__ b,
-                                                  double* __restrict__ y, int32_t lds_cap) {
+                                                  double* __restrict__ y, int32_t lds_cap,
+                                                  const double* __restrict__ sdev, double* __restrict__ vout,
+                                                  const int* __restrict__ stop) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sval = reinterpret_cast<double*>(smem);
   int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
@@ -351,15 +311,17 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
   const double2* v2 = reinterpret_cast<const double2*>(val + s2);
   const int4* c4 = reinterpret_cast<const int4*>(col + s4);
   const int32_t r = r0 + t;
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   int32_t k0 = 0, k1 = 0;
   double bb = 0.0;
   if (r < r1) {
     k0 = rowptr[r];
     k1 = rowptr[r + 1];
-    if (RESID) bb = b[r];
+    if (MODE == MSK_SPMV_RESID) bb = b[r];
+    if (MODE == MSK_SPMV_SCALED) vout[r] = x[r] * sc;
   }
-  for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = v2[i];
-  for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = c4[i];
+  for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = NT ? ld_nt(v2 + i) : v2[i];
+  for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = NT ? ld_nt(c4 + i) : c4[i];
   __syncthreads();
   if (r < r1) {
     double s = 0.0;
@@ -372,24 +334,34 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
         xv[q] = x[scol[k - s4]];
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int q = 0; q < 8; ++q) {
+        if (MODE == MSK_SPMV_SCALED) xv[q] = xv[q] * sc;
         if (kb + q < k1) s = s + av[q] * xv[q];
+      }
     }
-    y[r] = RESID ? bb - s : s;
+    y[r] = MODE == MSK_SPMV_RESID ? bb - s : s;
   }
 }
 
 // Rows too long for the LDS stage: one lane per row, direct loads (same order).
-template <bool RESID>
+template <int MODE>
 __global__ __launch_bounds__(kT) void k_spmv_direct(int32_t nrows, const int32_t* __restrict__ rowptr,
                                                     const int32_t* __restrict__ col, const double* __restrict__ val,
                                                     const double* __restrict__ x, const double* __restrict__ b,
-                                                    double* __restrict__ y) {
+                                                    double* __restrict__ y, const double* __restrict__ sdev,
+                                                    double* __restrict__ vout, const int* __restrict__ stop) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   const int32_t r = blockIdx.x * kT + threadIdx.x;
   if (r >= nrows) return;
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   double s = 0.0;
-  for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) s = s + val[k] * x[col[k]];
-  y[r] = RESID ? b[r] - s : s;
+  for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+    double xv = x[col[k]];
+    if (MODE == MSK_SPMV_SCALED) xv = xv * sc;
+    s = s + val[k] * xv;
+  }
+  if (MODE == MSK_SPMV_SCALED) vout[r] = x[r] * sc;
+  y[r] = MODE == MSK_SPMV_RESID ? b[r] - s : s;
 }
 
 // Row-compressed matrix: only rows row_ids[0..nlisted) hold entries.
@@ -478,12 +450,10 @@ __global__ __launch_bounds__(kT) void k_blas1(double* __restrict__ y, const doub
 // ===================================================================== launchers
 using namespace msk;
 
-// Kernel variants (A/B tuning; MSPLIT_VARIANT_<KERNEL>=<n> at context creation).
-static int g_variant[MSK_NVAR] = {0};
-
-extern "C" void msk_set_variant(int which, int v) {
-  if (which >= 0 && which < MSK_NVAR) g_variant[which] = v;
-}
+// Tuning flags (A/B experiments; MSPLIT_TUNING at context creation).
+static int g_tuning = 0;
+extern "C" void msk_set_tuning(int flags) { g_tuning = flags; }
+extern "C" int msk_get_tuning(void) { return g_tuning; }
 
 static inline int grid_for(int64_t work, int cap) {
   int64_t g = (work + kT - 1) / kT;
@@ -493,85 +463,68 @@ static inline int grid_for(int64_t work, int cap) {
 }
 
 template <int NV>
-static void launch_dot1(const double* w, const VecGroup& V, int64_t n, double* partial, int64_t nchunks, bool self,
-                        hipStream_t s) {
-  if (self) k_dot_stage1<1, true><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, V, n, partial, nchunks);
-  else k_dot_stage1<NV, false><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, V, n, partial, nchunks);
-}
-
-template <int... Is>
-struct Seq {};
-
-template <int NV>
-static void dot1_dispatch(int nv, const double* w, const VecGroup& V, int64_t n, double* partial, int64_t nchunks,
-                          hipStream_t s) {
-  if (nv == NV) launch_dot1<NV>(w, V, n, partial, nchunks, false, s);
-  else if constexpr (NV < MSK_MAX_GROUP) dot1_dispatch<NV + 1>(nv, w, V, n, partial, nchunks, s);
-}
-
-extern "C" int msk_dot_stage1(const double* w, const VecGroup* V, int nv, int64_t n, double* partial,
-                              int64_t nchunks, int self, hipStream_t s) {
-  if (nchunks <= 0) return 0;
-  if (self) launch_dot1<1>(w, *V, n, partial, nchunks, true, s);
-  else dot1_dispatch<1>(nv, w, *V, n, partial, nchunks, s);
-  return (int)hipGetLastError();
-}
-
-extern "C" int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, hipStream_t s) {
-  k_dot_stage2<<<dim3(nv), dim3(kT), 0, s>>>(partial, nchunks, out);
-  return (int)hipGetLastError();
-}
-
-extern "C" int msk_maxpy_norm(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate,
-                              int64_t n, int accum, double* partial, hipStream_t s) {
-  if (n <= 0 || nv <= 0) return 0;
-  const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
-  if (partial) k_maxpy_chunk<false, true><<<dim3(g), dim3(kT), 0, s>>>(w, *V, *A, adev, negate, nv, n, partial);
-  else if (accum) k_maxpy_chunk<true, false><<<dim3(g), dim3(kT), 0, s>>>(w, *V, *A, adev, negate, nv, n, partial);
-  else k_maxpy_chunk<false, false><<<dim3(g), dim3(kT), 0, s>>>(w, *V, *A, adev, negate, nv, n, partial);
-  return (int)hipGetLastError();
-}
-
-template <int NV>
-static void maxpy_dispatch(int nv, double* w, const VecGroup& V, const Coefs& A, const double* adev, int negate,
-                           int64_t n, int accum, hipStream_t s) {
+static void dot1_dispatch(int nv, const double* w, const Vecs& V, int64_t n, double* partial, int64_t nchunks,
+                          const int* stop, hipStream_t s) {
   if (nv == NV) {
-    const int g = grid_for((n + 1) / 2, 4096);
-    if (g_variant[MSK_VAR_MAXPY] == 2) {
-      if (accum) k_maxpy<NV, true, 4><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
-      else k_maxpy<NV, false, 4><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
-    } else {
-      if (accum) k_maxpy<NV, true, 1><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
-      else k_maxpy<NV, false, 1><<<dim3(g), dim3(kT), 0, s>>>(w, V, A, adev, negate, n);
-    }
+    k_dot_stage1<NV, false><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, V, n, partial, nchunks, stop,
+                                                                          (g_tuning & MSK_TUNE_MDOT_REV) ? 1 : 0);
   } else if constexpr (NV < MSK_MAX_GROUP) {
-    maxpy_dispatch<NV + 1>(nv, w, V, A, adev, negate, n, accum, s);
+    dot1_dispatch<NV + 1>(nv, w, V, n, partial, nchunks, stop, s);
   }
 }
 
-extern "C" int msk_maxpy(double* w, const VecGroup* V, int nv, const Coefs* A, const double* adev, int negate,
-                         int64_t n, int accum, hipStream_t s) {
-  if (n <= 0 || nv <= 0) return 0;
-  if (g_variant[MSK_VAR_MAXPY] == 0) return msk_maxpy_norm(w, V, nv, A, adev, negate, n, accum, nullptr, s);
-  maxpy_dispatch<1>(nv, w, *V, *A, adev, negate, n, accum, s);
+extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
+                              int self, const int* stop, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  if (self) k_dot_stage1<1, true><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, *V, n, partial, nchunks, stop, 0);
+  else dot1_dispatch<1>(nv, w, *V, n, partial, nchunks, stop, s);
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, const int* stop,
+                              hipStream_t s) {
+  k_dot_stage2<<<dim3(nv), dim3(kT), 0, s>>>(partial, nchunks, out, stop);
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, const int* nvdev,
+                               const Coefs* A, const double* adev, int negate, int64_t n, int accum, double* partial,
+                               const int* stop, hipStream_t s) {
+  if (n <= 0 || (nv <= 0 && !nvdev)) return 0;
+  const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
+  if (partial)
+    k_maxpy_chunk<false, true><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n, partial,
+                                                            stop);
+  else if (accum)
+    k_maxpy_chunk<true, false><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n, partial,
+                                                            stop);
+  else
+    k_maxpy_chunk<false, false><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n, partial,
+                                                             stop);
   return (int)hipGetLastError();
 }
 
 extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
-                        const double* b, double* y, int32_t lds_cap, int resid, hipStream_t s) {
+                        const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
+                        const int* stop, hipStream_t s) {
   if (nrows <= 0) return 0;
   const unsigned g = (unsigned)((nrows + kT - 1) / kT);
-  if (lds_cap > 0 && g_variant[MSK_VAR_SPMV] == 0) {
-    const size_t lds = (size_t)lds_cap * 12;
-    if (resid) k_spmv_lds8<true><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);
-    else k_spmv_lds8<false><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);
-  } else if (lds_cap > 0) {
-    const size_t lds = (size_t)lds_cap * 12;
-    if (resid) k_spmv_lds<true><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);
-    else k_spmv_lds<false><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap);
+  const size_t lds = (size_t)lds_cap * 12;
+  if (lds_cap > 0) {
+    const bool nt = (g_tuning & MSK_TUNE_SPMV_NT) != 0;
+#define LAUNCH_LDS8(M, NTF) \
+  k_spmv_lds8<M, NTF><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev, vout, stop)
+    if (mode == MSK_SPMV_RESID) { if (nt) LAUNCH_LDS8(MSK_SPMV_RESID, true); else LAUNCH_LDS8(MSK_SPMV_RESID, false); }
+    else if (mode == MSK_SPMV_SCALED) { if (nt) LAUNCH_LDS8(MSK_SPMV_SCALED, true); else LAUNCH_LDS8(MSK_SPMV_SCALED, false); }
+    else { if (nt) LAUNCH_LDS8(MSK_SPMV_MULT, true); else LAUNCH_LDS8(MSK_SPMV_MULT, false); }
+#undef LAUNCH_LDS8
   } else {
-    if (resid) k_spmv_direct<true><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y);
-    else k_spmv_direct<false><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y);
+    if (mode == MSK_SPMV_RESID)
+      k_spmv_direct<MSK_SPMV_RESID><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y, sdev, vout, stop);
+    else if (mode == MSK_SPMV_SCALED)
+      k_spmv_direct<MSK_SPMV_SCALED><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y, sdev, vout, stop);
+    else
+      k_spmv_direct<MSK_SPMV_MULT><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y, sdev, vout, stop);
   }
   return (int)hipGetLastError();
 }

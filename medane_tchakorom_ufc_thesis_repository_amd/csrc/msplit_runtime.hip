@@ -101,13 +101,7 @@ extern "C" int msp_ctx_create(int device, void* stream, msp_ctx** out) {
   }
   ARGCHK(device >= 0 && device < ndev, MSP_ERR_ARG_OUTOFRANGE, "device %d out of range [0,%d)", device, ndev);
   HIPCHK(hipSetDevice(device));
-  {
-    static const char* names[MSK_NVAR] = {"MSPLIT_VARIANT_SPMV", "MSPLIT_VARIANT_MDOT", "MSPLIT_VARIANT_MAXPY"};
-    for (int i = 0; i < MSK_NVAR; ++i) {
-      const char* e = getenv(names[i]);
-      if (e) msk_set_variant(i, atoi(e));
-    }
-  }
+  if (const char* e = getenv("MSPLIT_TUNING")) msk_set_tuning(atoi(e));
   msp_ctx* c = new msp_ctx();
   c->device = device;
   if (stream) {
@@ -277,10 +271,10 @@ extern "C" int mspi_mdot(msp_ctx* c, const double* w, int nv, const double* cons
   KTimer kt(c, MSP_KERNEL_MDOT, 8.0 * (double)n * (nv + 1));
   for (int g0 = 0; g0 < nv; g0 += MSPI_MAX_GROUP) {
     const int g = std::min(MSPI_MAX_GROUP, nv - g0);
-    VecGroup vg;
+    Vecs vg = {};
     for (int j = 0; j < g; ++j) vg.p[j] = V[g0 + j];
-    KCHK(msk_dot_stage1(w, &vg, g, n, c->partial, nch, 0, c->stream));
-    KCHK(msk_dot_stage2(c->partial, nch, g, out_dev + g0, c->stream));
+    KCHK(msk_dot_stage1(w, &vg, g, n, c->partial, nch, 0, nullptr, c->stream));
+    KCHK(msk_dot_stage2(c->partial, nch, g, out_dev + g0, nullptr, c->stream));
   }
   return MSP_SUCCESS;
 }
@@ -294,10 +288,10 @@ extern "C" int mspi_norm2sq(msp_ctx* c, const double* x, int64_t n, double* out_
   int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
   if (rc) return rc;
   KTimer kt(c, MSP_KERNEL_NORM, 8.0 * (double)n);
-  VecGroup vg;
+  Vecs vg = {};
   vg.p[0] = x;
-  KCHK(msk_dot_stage1(x, &vg, 1, n, c->partial, nch, 1, c->stream));
-  KCHK(msk_dot_stage2(c->partial, nch, 1, out_dev, c->stream));
+  KCHK(msk_dot_stage1(x, &vg, 1, n, c->partial, nch, 1, nullptr, c->stream));
+  KCHK(msk_dot_stage2(c->partial, nch, 1, out_dev, nullptr, c->stream));
   return MSP_SUCCESS;
 }
 
@@ -315,37 +309,76 @@ extern "C" int mspi_maxpy(msp_ctx* c, double* w, int nv, const double* const* V,
   // launch is a whole number of 4-groups.
   int g = nv % MSPI_MAX_GROUP ? nv % MSPI_MAX_GROUP : MSPI_MAX_GROUP;
   for (int g0 = 0; g0 < nv; g0 += g, g = MSPI_MAX_GROUP) {
-    VecGroup vg;
+    Vecs vg = {};
     Coefs cf;
     for (int j = 0; j < g; ++j) {
       vg.p[j] = V[g0 + j];
       cf.a[j] = alpha_host ? alpha_host[g0 + j] : 0.0;
     }
-    KCHK(msk_maxpy(w, &vg, g, &cf, alpha_dev ? alpha_dev + g0 : nullptr, negate, n, accumulate, c->stream));
+    KCHK(msk_maxpy_chunk(w, w, &vg, g, nullptr, &cf, alpha_dev ? alpha_dev + g0 : nullptr, negate, n, accumulate,
+                         nullptr, nullptr, c->stream));
   }
   return MSP_SUCCESS;
 }
 
-extern "C" int mspi_maxpy_norm(msp_ctx* c, double* w, int nv, const double* const* V, int64_t n,
-                               const double* alpha_dev, int negate, double* out_dev) {
-  if (nv > MSPI_MAX_GROUP || n <= 0) {
-    int rc = mspi_maxpy(c, w, nv, V, n, nullptr, alpha_dev, negate, 0);
-    return rc ? rc : mspi_norm2sq(c, w, n, out_dev);
-  }
-  const int64_t nch = nchunks_of(n);
-  int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
-  if (rc) return rc;
-  KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n * (nv + 2));
-  VecGroup vg;
-  Coefs cf;
-  for (int j = 0; j < nv; ++j) {
-    vg.p[j] = V[j];
-    cf.a[j] = 0.0;
-  }
-  KCHK(msk_maxpy_norm(w, &vg, nv, &cf, alpha_dev, negate, n, 0, c->partial, c->stream));
-  KCHK(msk_dot_stage2(c->partial, nch, 1, out_dev, c->stream));
+extern "C" hipStream_t mspi_stream(msp_ctx* c) { return c->stream; }
+
+extern "C" int mspi_h2d_async(msp_ctx* c, void* dev, const void* host, size_t bytes) {
+  HIPCHK(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->stream));
   return MSP_SUCCESS;
 }
+
+extern "C" int mspi_mdot_basis(msp_ctx* c, const double* w, int nv, const double* base, int64_t stride, int64_t n,
+                               double* out_dev, const int* stop) {
+  if (nv <= 0) return MSP_SUCCESS;
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0) {
+    HIPCHK(hipMemsetAsync(out_dev, 0, (size_t)nv * sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  KTimer kt(c, MSP_KERNEL_MDOT, 8.0 * (double)n * (nv + 1));
+  for (int g0 = 0; g0 < nv; g0 += MSPI_MAX_GROUP) {
+    const int g = std::min(MSPI_MAX_GROUP, nv - g0);
+    Vecs vg = {};
+    vg.base = base + (int64_t)g0 * stride;
+    vg.stride = stride;
+    KCHK(msk_dot_stage1(w, &vg, g, n, c->partial, nch, 0, stop, c->stream));
+    KCHK(msk_dot_stage2(c->partial, nch, g, out_dev + g0, stop, c->stream));
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_maxpy_norm_basis(msp_ctx* c, const double* win, double* wout, int nv, const double* base,
+                                     int64_t stride, int64_t n, const double* alpha_dev, double* sumsq_dev,
+                                     const int* stop) {
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0 || nv <= 0) {
+    mspi_set_error(MSP_ERR_ARG_SIZ, "maxpy_norm on an empty basis");
+    return MSP_ERR_ARG_SIZ;
+  }
+  KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n * (nv + 2));
+  Vecs vg = {};
+  vg.base = base;
+  vg.stride = stride;
+  Coefs cf = {};
+  KCHK(msk_maxpy_chunk(win, wout, &vg, nv, nullptr, &cf, alpha_dev, 1, n, 0, c->partial, stop, c->stream));
+  KCHK(msk_dot_stage2(c->partial, nch, 1, sumsq_dev, stop, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_maxpy_accum_basis(msp_ctx* c, double* x, const int* nvdev, const double* base, int64_t stride,
+                                      int64_t n, const double* coef_dev, int nv_expected) {
+  if (n <= 0) return MSP_SUCCESS;
+  // BuildSoln: the vector count lives on the device; bytes use the host's expectation
+  KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n * (nv_expected + 2));
+  Vecs vg = {};
+  vg.base = base;
+  vg.stride = stride;
+  Coefs cf = {};
+  KCHK(msk_maxpy_chunk(x, x, &vg, 0, nvdev, &cf, coef_dev, 0, n, 1, nullptr, nullptr, c->stream));
+  return MSP_SUCCESS;
+}
+
 
 extern "C" int mspi_scale(msp_ctx* c, double* x, int64_t n, double alpha) {
   KTimer kt(c, MSP_KERNEL_SCALE, 16.0 * (double)n);
@@ -578,13 +611,27 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
     KCHK(msk_spmv_rows(A->nlisted, A->row_ids, A->rowptr, A->col, A->val, x, b, y, resid ? 1 : 0, c->stream));
     return MSP_SUCCESS;
   }
-  KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, b, y, A->lds_cap, resid ? 1 : 0, c->stream));
+  KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, b, y, A->lds_cap, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT,
+                nullptr, nullptr, nullptr, c->stream));
   return MSP_SUCCESS;
 }
 
 extern "C" int mspi_spmv(msp_mat* A, const double* x, double* y) { return spmv_impl(A, nullptr, x, y, false); }
 extern "C" int mspi_residual(msp_mat* A, const double* b, const double* x, double* r) {
   return spmv_impl(A, b, x, r, true);
+}
+
+extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev, double* vout, double* y,
+                                const int* stop) {
+  msp_ctx* c = A->ctx;
+  if (A->compressed || A->nrows != A->ncols) {
+    mspi_set_error(MSP_ERR_SUP, "scaled MatMult needs a square, uncompressed operator");
+    return MSP_ERR_SUP;
+  }
+  KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, false) + 8.0 * (double)A->nrows);
+  KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, nullptr, y, A->lds_cap, MSK_SPMV_SCALED, sdev, vout, stop,
+                c->stream));
+  return MSP_SUCCESS;
 }
 
 static int vec_ok(const msp_vec* v, const char* name) {
