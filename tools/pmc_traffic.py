@@ -57,6 +57,7 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--out", default="profiles/traffic.json")
+    ap.add_argument("--bench", default=None, help="bench JSON of the same build: algorithmic bytes per launch")
     a = ap.parse_args()
     N = a.n ** 3
     fetch = load(a.fetch_dir, "FETCH_SIZE")
@@ -88,6 +89,12 @@ def main():
                                "hbm_bytes_per_launch": rd + wr, "alg_bytes_per_launch": alg,
                                "hbm_over_alg": (rd + wr) / alg if alg else None}
     dom = "maxpy"
+    if a.bench and os.path.exists(a.bench):
+        b = json.load(open(a.bench))
+        alg = b.get("roofline", {}).get("bytes_per_launch")
+        if alg and dom in out["classes"]:
+            out["classes"][dom]["alg_bytes_per_launch"] = alg
+            out["classes"][dom]["hbm_over_alg"] = out["classes"][dom]["hbm_bytes_per_launch"] / alg
     if dom in out["classes"]:
         out["kernel_class"] = dom
         out["hbm_bytes_per_launch"] = out["classes"][dom]["hbm_bytes_per_launch"]
