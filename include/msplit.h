@@ -44,8 +44,11 @@ extern "C" {
 
 /* KSPConvergedReason values (PETSc 3.22.1 include/petscksp.h). */
 #define MSP_CONVERGED_ITERATING 0
+#define MSP_CONVERGED_RTOL_NORMAL 1
 #define MSP_CONVERGED_RTOL 2
 #define MSP_CONVERGED_ATOL 3
+#define MSP_CONVERGED_ITS 4
+#define MSP_CONVERGED_ATOL_NORMAL 9
 #define MSP_DIVERGED_NULL (-2)
 #define MSP_DIVERGED_ITS (-3)
 #define MSP_DIVERGED_DTOL (-4)
@@ -59,12 +62,18 @@ extern "C" {
 #define MSP_KERNEL_NORM 3       /* VecNorm / VecDot (both DBR stages) */
 #define MSP_KERNEL_SCALE 4      /* VecScale (VecNormalize) */
 #define MSP_KERNEL_OTHER 5      /* copy/set/axpy/... */
-#define MSP_KERNEL_NCLASSES 6
+#define MSP_KERNEL_SPMM 6       /* MatMatMult(AIJ, DENSE): R = A S */
+#define MSP_KERNEL_DGEMV 7      /* dense MatMult (LSQR's R v - alpha u, and x = S alpha) */
+#define MSP_KERNEL_DGEMVT 8     /* dense MatMultTranspose (LSQR's R^T u), both DBR stages */
+#define MSP_KERNEL_NCLASSES 9
 
 typedef struct msp_ctx msp_ctx;
 typedef struct msp_mat msp_mat;
 typedef struct msp_vec msp_vec;
 typedef struct msp_ksp msp_ksp;
+typedef struct msp_dense msp_dense;
+typedef struct msp_lsqr msp_lsqr;
+typedef struct msp_comm msp_comm;
 
 /* ---------------------------------------------------------------- context */
 /* One context per GPU: device id + the HIP stream all work is ordered on.
@@ -104,6 +113,15 @@ int msp_mat_create_csr_rows(msp_ctx *ctx, int32_t nrows, int32_t ncols, int32_t 
  *        (poisson2DMatrix, utils.c:247-293, restricted to whole-line row blocks).
  * Identical CSR to the host assembly, built in HBM (no host arrays). */
 int msp_mat_create_box_stencil(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, int32_t nz, msp_mat **A);
+/* The same block rows with their coupling to the neighbour plane below (lo)
+ * and/or above (hi) kept as extra columns: ncols = nrows + (lo+hi)*plane, the
+ * column space being [plane below | own rows | plane above] (ascending global
+ * order, so each row's sum order is MatMult_SeqAIJ's on the reference's
+ * A_block_jacobi / A_block_jacobi_resdistributed rows, utils.c:30-121,
+ * :247-293, :891-921).  plane = nx*ny (dim 3) or nx (dim 2).  This is the
+ * operator of R = A S in the minimization variants (SMSM-global.c:326). */
+int msp_mat_create_box_stencil_ext(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
+                                   int32_t hi, msp_mat **A);
 int msp_mat_destroy(msp_mat **A);
 int msp_mat_get_info(const msp_mat *A, int32_t *nrows, int32_t *ncols, int64_t *nnz);
 /* Download the CSR (host buffers of nrows+1 / nnz entries); synchronising. */
@@ -174,6 +192,99 @@ int msp_ksp_get_residual_norm(const msp_ksp *ksp, double *rnorm);     /* KSPGetR
 int msp_ksp_get_converged_reason(const msp_ksp *ksp, int32_t *reason);
 /* Residual history of the last solve (KSPGetResidualHistory): its+1 entries. */
 int msp_ksp_get_residual_history(const msp_ksp *ksp, const double **hist, int32_t *n);
+
+/* ------------------------------------------------------------------ dense */
+/* A block of rows of a MATDENSE / MATMPIDENSE matrix, column-major in HBM with
+ * leading dimension lda >= nrows (create_matrix_dense, utils.c:123-137:
+ * MatCreateDense + MatZeroEntries).  The minimization variants hold S (the s
+ * most recent multisplitting iterates, one per column) and R = A S this way;
+ * each GPU keeps only its own rows (plus, for S, the neighbour planes R needs). */
+int msp_dense_create(msp_ctx *ctx, int64_t nrows, int32_t ncols, msp_dense **A);   /* zero entries */
+int msp_dense_destroy(msp_dense **A);
+int msp_dense_get_info(const msp_dense *A, int64_t *nrows, int32_t *ncols, int64_t *lda);
+int msp_dense_get_array(msp_dense *A, double **device_ptr);                        /* MatDenseGetArray */
+int msp_dense_zero_entries(msp_dense *A);                                          /* MatZeroEntries */
+/* Host <-> device copies of the whole block (host column-major, leading dim ld). */
+int msp_dense_set_values(msp_dense *A, const double *host, int64_t ld);
+int msp_dense_get_values(const msp_dense *A, double *host, int64_t ld);
+/* A[row0 : row0+n, j] = x[xoff : xoff+n] -- MatSetValuesLocal(S, n, rows, 1, &j, x)
+ * (SMSM-global.c:314-316), device to device. */
+int msp_dense_set_column(msp_dense *A, int32_t j, int64_t row0, const msp_vec *x, int64_t xoff, int64_t n);
+/* y[yoff : yoff+n] = A[row0 : row0+n, :] alpha -- MatMult(S, alpha, x_minimized)
+ * (outer_solver_norm_equation, utils.c:1076).  Per row, columns in order, from 0
+ * (reference dgemv 'N').  alpha has ncols entries. */
+int msp_dense_mult(msp_dense *A, const msp_vec *alpha, int64_t row0, int64_t n, msp_vec *y, int64_t yoff);
+/* out[j] = column_j . u over this block's rows (DBR order) -- the local part of
+ * MatMultTranspose (KSPSolve_LSQR); out has ncols entries. */
+int msp_dense_mult_transpose(msp_dense *A, const msp_vec *u, msp_vec *out);
+/* R = A S -- MatMatMult(A_block_jacobi_resdistributed, S, MAT_REUSE_MATRIX, R)
+ * (SMSM-global.c:325-327): A is nrows(R) x nrows(S), R and S have the same
+ * column count.  Per row of A and column of S: ascending columns, from 0. */
+int msp_mat_matmult_dense(msp_mat *A, const msp_dense *S, msp_dense *R);
+
+/* ------------------------------------------------------------------- comm */
+/* Cross-process reductions of the distributed minimization (one rank per GPU).
+ * The reference runs the whole least-squares solve redundantly on every block
+ * after swapping halves of R (comm_sync_send_and_receive_minimization,
+ * comm.c:252-286: (N/2)*s doubles per block per outer iteration); here R stays
+ * row-distributed and only s+1 partial sums per block cross the link per LSQR
+ * step, all-gathered so that every rank adds them in block order (bitwise
+ * identical on every rank and independent of the collective's algorithm).
+ *   rccl: an RCCL communicator over xGMI (ncclCommInitRank with an id from
+ *         msp_comm_get_unique_id, distributed by the host, e.g. MPI_Bcast);
+ *   host: a host callback all-gathers pinned host buffers (MPI_Allgather,
+ *         gloo, ...); the device buffers are staged through it. */
+#define MSP_COMM_ID_BYTES 128
+typedef int (*msp_allgather_fn)(void *user, const double *send, double *recv, int64_t count);
+int msp_comm_get_unique_id(uint8_t id[MSP_COMM_ID_BYTES]);
+int msp_comm_create_rccl(msp_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[MSP_COMM_ID_BYTES],
+                         msp_comm **comm);
+int msp_comm_create_host(msp_ctx *ctx, int32_t nranks, int32_t rank, msp_allgather_fn fn, void *user,
+                         msp_comm **comm);
+int msp_comm_destroy(msp_comm **comm);
+int msp_comm_get_size(const msp_comm *comm, int32_t *nranks, int32_t *rank);
+/* recv[r*count + i] = rank r's send[i]; recv has nranks*count entries. */
+int msp_comm_allgather(msp_comm *comm, const msp_vec *send, msp_vec *recv, int64_t count);
+
+/* ------------------------------------------------------------------- LSQR */
+/* KSPLSQR options (the outer solver of the minimization variants,
+ * running_bulk_test_g5k:247-248). */
+#define MSP_LSQR_CONV_DEFAULT 0 /* -ksp_convergence_test default: KSPConvergedDefault */
+#define MSP_LSQR_CONV_LSQR 1    /* KSPLSQRConvergedDefault (KSPCreate_LSQR's choice)  */
+#define MSP_LSQR_CONV_SKIP 2    /* -ksp_convergence_test skip                         */
+typedef struct msp_lsqr_opts {
+  int32_t max_it;       /* -ksp_max_it             (10000) */
+  double rtol;          /* -ksp_rtol               (1e-5)  */
+  double abstol;        /* -ksp_atol               (1e-50) */
+  double divtol;        /* -ksp_divtol             (1e4)   */
+  int32_t exact_norm;   /* -ksp_lsqr_exact_mat_norm         */
+  int32_t conv_test;    /* MSP_LSQR_CONV_*                  */
+} msp_lsqr_opts;
+
+int msp_lsqr_get_default_opts(msp_lsqr_opts *o);
+/* KSPCreate + KSPSetType(KSPLSQR) + PCNONE (initializeKSP(.., outer_ksp, NULL, ..),
+ * SMSM-global.c:219). */
+int msp_lsqr_create(msp_ctx *ctx, msp_lsqr **lsqr);
+int msp_lsqr_destroy(msp_lsqr **lsqr);
+int msp_lsqr_set_opts(msp_lsqr *lsqr, const msp_lsqr_opts *o);
+int msp_lsqr_get_opts(const msp_lsqr *lsqr, msp_lsqr_opts *o);
+/* KSPSetOperators(outer_ksp, R, R) (utils.c:1066): this process's row blocks of
+ * R, in global block order; every rank passes the same count and column count.
+ * The global operator is the blocks of rank 0, then rank 1, ... */
+int msp_lsqr_set_operators(msp_lsqr *lsqr, int32_t nlocal, msp_dense *const *R);
+/* Ranks that hold the other row blocks (NULL: all blocks are local). */
+int msp_lsqr_set_comm(msp_lsqr *lsqr, msp_comm *comm);
+/* KSPSolve(outer_ksp, b, alpha) with a zero initial guess (utils.c:1067-1068):
+ * b[k] holds the rows of local block k; x (ncols entries) is replicated and
+ * identical on every rank. */
+int msp_lsqr_solve(msp_lsqr *lsqr, msp_vec *const *b, msp_vec *x);
+int msp_lsqr_get_iteration_number(const msp_lsqr *lsqr, int32_t *its);
+/* KSPGetResidualNorm(outer_ksp) (SMSM-global.c:341): LSQR's phibar. */
+int msp_lsqr_get_residual_norm(const msp_lsqr *lsqr, double *rnorm);
+int msp_lsqr_get_converged_reason(const msp_lsqr *lsqr, int32_t *reason);
+/* KSPLSQRGetNorms: ||R^T r|| estimate and ||R||_F (exact or estimated). */
+int msp_lsqr_get_norms(const msp_lsqr *lsqr, double *arnorm, double *anorm);
+int msp_lsqr_get_residual_history(const msp_lsqr *lsqr, const double **hist, int32_t *n);
 
 #ifdef __cplusplus
 }

@@ -15,10 +15,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmsplit_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "msplit.h")
 
-KERNEL_CLASSES = {"spmv": 0, "mdot": 1, "maxpy": 2, "norm": 3, "scale": 4, "other": 5}
+KERNEL_CLASSES = {"spmv": 0, "mdot": 1, "maxpy": 2, "norm": 3, "scale": 4, "other": 5,
+                  "spmm": 6, "dgemv": 7, "dgemvt": 8}
 
 REASONS = {
-    0: "CONVERGED_ITERATING", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
+    0: "CONVERGED_ITERATING", 1: "CONVERGED_RTOL_NORMAL", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
+    4: "CONVERGED_ITS", 9: "CONVERGED_ATOL_NORMAL",
     -2: "DIVERGED_NULL", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
     -5: "DIVERGED_BREAKDOWN", -9: "DIVERGED_NANORINF",
 }
@@ -35,6 +37,15 @@ class KspOpts(C.Structure):
                 ("abstol", C.c_double), ("divtol", C.c_double), ("haptol", C.c_double),
                 ("breakdowntol", C.c_double), ("uirnorm", C.c_int32), ("guess_nonzero", C.c_int32)]
 
+
+class LsqrOpts(C.Structure):
+    _fields_ = [("max_it", C.c_int32), ("rtol", C.c_double), ("abstol", C.c_double), ("divtol", C.c_double),
+                ("exact_norm", C.c_int32), ("conv_test", C.c_int32)]
+
+
+LSQR_CONV = {"default": 0, "lsqr": 1, "skip": 2}
+COMM_ID_BYTES = 128
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int64)
 
 _lib = None
 
@@ -91,6 +102,38 @@ _SIGS = {
     "msp_ksp_get_residual_norm": [_vp, _dp],
     "msp_ksp_get_converged_reason": [_vp, _i32p],
     "msp_ksp_get_residual_history": [_vp, _P(_dp), _i32p],
+    "msp_mat_create_box_stencil_ext": [_vp, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                       _P(_vp)],
+    "msp_dense_create": [_vp, C.c_int64, C.c_int32, _P(_vp)],
+    "msp_dense_destroy": [_P(_vp)],
+    "msp_dense_get_info": [_vp, _P(C.c_int64), _i32p, _P(C.c_int64)],
+    "msp_dense_get_array": [_vp, _P(_vp)],
+    "msp_dense_zero_entries": [_vp],
+    "msp_dense_set_values": [_vp, _dp, C.c_int64],
+    "msp_dense_get_values": [_vp, _dp, C.c_int64],
+    "msp_dense_set_column": [_vp, C.c_int32, C.c_int64, _vp, C.c_int64, C.c_int64],
+    "msp_dense_mult": [_vp, _vp, C.c_int64, C.c_int64, _vp, C.c_int64],
+    "msp_dense_mult_transpose": [_vp, _vp, _vp],
+    "msp_mat_matmult_dense": [_vp, _vp, _vp],
+    "msp_comm_get_unique_id": [_P(C.c_uint8)],
+    "msp_comm_create_rccl": [_vp, C.c_int32, C.c_int32, _P(C.c_uint8), _P(_vp)],
+    "msp_comm_create_host": [_vp, C.c_int32, C.c_int32, ALLGATHER_FN, _vp, _P(_vp)],
+    "msp_comm_destroy": [_P(_vp)],
+    "msp_comm_get_size": [_vp, _i32p, _i32p],
+    "msp_comm_allgather": [_vp, _vp, _vp, C.c_int64],
+    "msp_lsqr_get_default_opts": [_P(LsqrOpts)],
+    "msp_lsqr_create": [_vp, _P(_vp)],
+    "msp_lsqr_destroy": [_P(_vp)],
+    "msp_lsqr_set_opts": [_vp, _P(LsqrOpts)],
+    "msp_lsqr_get_opts": [_vp, _P(LsqrOpts)],
+    "msp_lsqr_set_operators": [_vp, C.c_int32, _P(_vp)],
+    "msp_lsqr_set_comm": [_vp, _vp],
+    "msp_lsqr_solve": [_vp, _P(_vp), _vp],
+    "msp_lsqr_get_iteration_number": [_vp, _i32p],
+    "msp_lsqr_get_residual_norm": [_vp, _dp],
+    "msp_lsqr_get_converged_reason": [_vp, _i32p],
+    "msp_lsqr_get_norms": [_vp, _dp, _dp],
+    "msp_lsqr_get_residual_history": [_vp, _P(_dp), _i32p],
 }
 
 

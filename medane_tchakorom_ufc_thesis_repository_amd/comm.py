@@ -50,6 +50,10 @@ class LocalComm:
     def barrier(self):
         pass
 
+    def lsqr_comm(self, ctx):
+        """Every block is in this process: LSQR adds the block partials itself."""
+        return None
+
 
 class TorchComm:
     """One block per rank over a torch.distributed process group (block id =
@@ -129,3 +133,23 @@ class TorchComm:
 
     def barrier(self):
         self.dist.barrier(group=self.group)
+
+    def lsqr_comm(self, ctx):
+        """The all-gather of LSQR's block partials (petsc.Comm): an RCCL
+        communicator of its own for "nccl" (id broadcast over this group),
+        a host callback over this group's all_gather for "gloo"."""
+        from .petsc import Comm
+        if self.world == 1:
+            return None
+        if self.backend == "nccl":
+            obj = [Comm.unique_id() if self.rank == 0 else None]
+            self.dist.broadcast_object_list(obj, src=0, group=self.group)
+            return Comm.rccl(ctx, self.world, self.rank, obj[0])
+        torch, dist, world, group = self.torch, self.dist, self.world, self.group
+
+        def allgather(a):
+            t = torch.from_numpy(a)
+            outs = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(outs, t, group=group)
+            return torch.cat(outs).numpy()
+        return Comm.host(ctx, self.world, self.rank, allgather)

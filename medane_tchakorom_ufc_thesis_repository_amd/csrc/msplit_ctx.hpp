@@ -1,0 +1,101 @@
+// msplit_ctx.hpp -- the context object and the error/timing helpers shared by
+// the C++/HIP translation units (runtime, dense/LSQR, comm).  Internal only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "msplit.h"
+#include "msplit_internal.h"
+#include "msplit_kernels.h"
+
+#define HIPCHK(call)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (call);                                                                       \
+    if (e_ != hipSuccess) {                                                                       \
+      mspi_set_error(MSP_ERR_LIB, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                     __LINE__);                                                                   \
+      return MSP_ERR_LIB;                                                                         \
+    }                                                                                             \
+  } while (0)
+
+#define KCHK(call)                                                                                  \
+  do {                                                                                              \
+    int e_ = (call);                                                                                \
+    if (e_) {                                                                                       \
+      mspi_set_error(MSP_ERR_LIB, "kernel launch %s failed: %s", #call,                             \
+                     hipGetErrorString((hipError_t)e_));                                            \
+      return MSP_ERR_LIB;                                                                           \
+    }                                                                                               \
+  } while (0)
+
+#define ARGCHK(cond, code, ...)        \
+  do {                                 \
+    if (!(cond)) {                     \
+      mspi_set_error(code, __VA_ARGS__); \
+      return code;                     \
+    }                                  \
+  } while (0)
+
+// ---------------------------------------------------------------- context
+struct TimedRec {
+  int cls;
+  int ev;  // index of the start event in the pool; stop = ev + 1
+  double bytes;
+};
+
+struct msp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  double* dscratch = nullptr;  // device scalars
+  double* hscratch = nullptr;  // pinned host scalars
+  double* partial = nullptr;   // DBR stage-1 partials
+  int64_t partial_cap = 0;     // doubles
+  bool timing = false;
+  std::vector<hipEvent_t> pool;
+  size_t pool_used = 0;
+  std::vector<TimedRec> recs;
+};
+
+static const int kScratch = 4 * MSPI_MAX_GROUP + 64;
+
+// Brackets one logical kernel (possibly two launches) with a pair of events.
+struct KTimer {
+  msp_ctx* c;
+  int ev = -1;
+  KTimer(msp_ctx* ctx, int cls, double bytes) : c(ctx) {
+    if (!c->timing) return;
+    if (c->pool_used + 2 > c->pool.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        c->pool.push_back(e);
+      }
+    }
+    ev = (int)c->pool_used;
+    c->pool_used += 2;
+    (void)hipEventRecord(c->pool[ev], c->stream);
+    c->recs.push_back({cls, ev, bytes});
+  }
+  ~KTimer() {
+    if (ev >= 0) (void)hipEventRecord(c->pool[ev + 1], c->stream);
+  }
+};
+
+
+static inline int ensure_partial(msp_ctx* c, int64_t need) {
+  if (need <= c->partial_cap) return MSP_SUCCESS;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->partial) HIPCHK(hipFree(c->partial));
+  c->partial = nullptr;
+  c->partial_cap = 0;
+  HIPCHK(hipMalloc((void**)&c->partial, (size_t)need * sizeof(double)));
+  c->partial_cap = need;
+  return MSP_SUCCESS;
+}
+
+static inline int64_t nchunks_of(int64_t n) { return (n + MSK_DBR_CHUNK - 1) / MSK_DBR_CHUNK; }
+

@@ -1,0 +1,424 @@
+// msplit_dense.hip -- dense row blocks (MATDENSE) and the tall-skinny kernels of
+// the global-minimization step: R = A S (SpMM), the LSQR products R v and R^T u,
+// and x = S alpha.
+//
+// All of it is HBM-bound f64 streaming: a dense block is column-major with
+// lda a multiple of 512 doubles, so every column starts 4 KiB aligned and a
+// DBR chunk (4096 rows) of a column is 32 KiB contiguous.  The kernels use the
+// same chunk geometry as the GMRES path (lane t owns rows base + j*512 + 2t,
+// +1), so their reductions are the DBR order of oracle/oracle.c (dbr_dot) and
+// the per-row sums are the reference's dgemv/MatMatMult orders: per row,
+// columns (or CSR entries) in order, starting from 0, no FMA contraction.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+
+#include "msplit_ctx.hpp"
+
+namespace msd {
+
+constexpr int kT = 256;
+constexpr int kIters = 8;
+constexpr int kChunk = kT * 2 * kIters;
+constexpr int kMaxCols = 32;  // columns per dot launch (shared reduction slots)
+static_assert(kChunk == MSK_DBR_CHUNK, "DBR chunk must match the oracle");
+
+__device__ __forceinline__ bool stopped(const int* stop) { return stop && *stop; }
+
+__device__ __forceinline__ double wave_butterfly(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------ gemv
+// y = A[:, 0:nc] coef (+ nal * U, VecAXPY skipped when nal == 0), per row
+// ((0 + c0 a0) + c1 a1) + ...; NORM: the DBR partial of ||y||^2 of this chunk.
+template <bool AXPY, bool NORM, bool FULL>
+__device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t lda, int nc,
+                                          const double* __restrict__ coef, double nal, const double* __restrict__ U,
+                                          double* __restrict__ y, int64_t base, int64_t n, double& sq) {
+  double u[2 * kIters];
+#pragma unroll
+  for (int j = 0; j < 2 * kIters; ++j) u[j] = 0.0;
+#pragma unroll 1
+  for (int q = 0; q < nc; ++q) {
+    const double a = coef[q];  // wave-uniform scalar load
+    const double* __restrict__ col = A + (int64_t)q * lda;
+    double p[2 * kIters];
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const int64_t e = base + j * (2 * kT);
+      if (FULL) {
+        const double2 v = *reinterpret_cast<const double2*>(col + e);
+        p[2 * j] = v.x;
+        p[2 * j + 1] = v.y;
+      } else {
+        p[2 * j] = e < n ? col[e] : 0.0;
+        p[2 * j + 1] = e + 1 < n ? col[e + 1] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * kIters; ++j) u[j] = u[j] + a * p[j];
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    const int64_t e = base + j * (2 * kT);
+    double r0 = u[2 * j], r1 = u[2 * j + 1];
+    if (FULL) {
+      if (AXPY && nal != 0.0) {
+        const double2 q = *reinterpret_cast<const double2*>(U + e);
+        r0 = r0 + nal * q.x;
+        r1 = r1 + nal * q.y;
+      }
+      *reinterpret_cast<double2*>(y + e) = make_double2(r0, r1);
+      if (NORM) {
+        acc = acc + r0 * r0;
+        acc = acc + r1 * r1;
+      }
+    } else {
+      if (e < n) {
+        if (AXPY && nal != 0.0) r0 = r0 + nal * U[e];
+        y[e] = r0;
+        if (NORM) acc = acc + r0 * r0;
+      }
+      if (e + 1 < n) {
+        if (AXPY && nal != 0.0) r1 = r1 + nal * U[e + 1];
+        y[e + 1] = r1;
+        if (NORM) acc = acc + r1 * r1;
+      }
+    }
+  }
+  sq = acc;
+}
+
+template <bool AXPY, bool NORM, bool VEC>
+__global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A, int64_t lda, int nc,
+                                                   const double* __restrict__ coef, const double* __restrict__ naldev,
+                                                   const double* __restrict__ U, double* __restrict__ y, int64_t n,
+                                                   double* __restrict__ partial, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  const int t = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const int64_t base = c * kChunk + 2 * t;
+  const double nal = AXPY ? *naldev : 0.0;
+  double sq = 0.0;
+  if (VEC && (c + 1) * kChunk <= n) gemv_body<AXPY, NORM, true>(A, lda, nc, coef, nal, U, y, base, n, sq);
+  else gemv_body<AXPY, NORM, false>(A, lda, nc, coef, nal, U, y, base, n, sq);
+  if (NORM) {
+    __shared__ double red[4];
+    sq = wave_butterfly(sq);
+    if ((t & 63) == 0) red[t >> 6] = sq;
+    __syncthreads();
+    if (t == 0) partial[c] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+// ------------------------------------------------------- scaled column dots
+// w' = w * (*sc) (VecScale, written back to wout) when SCALE, then the DBR
+// stage-1 partials of column_v . w' for v < nc: partial[v*nchunks + c].
+template <bool SCALE, bool VEC>
+__global__ __launch_bounds__(kT) void k_scaled_dot(const double* win, double* wout, const double* __restrict__ scdev,
+                                                   const double* __restrict__ A, int64_t lda, int nc, int64_t n,
+                                                   double* __restrict__ partial, int64_t nchunks,
+                                                   const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  __shared__ double red[kMaxCols][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t c = blockIdx.x;
+  const int64_t base = c * kChunk + 2 * t;
+  const bool full = VEC && (c + 1) * kChunk <= n;
+  const double sc = SCALE ? *scdev : 1.0;
+  double wr[2 * kIters];
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    const int64_t e = base + j * (2 * kT);
+    if (full) {
+      const double2 q = *reinterpret_cast<const double2*>(win + e);
+      wr[2 * j] = q.x;
+      wr[2 * j + 1] = q.y;
+    } else {
+      wr[2 * j] = e < n ? win[e] : 0.0;
+      wr[2 * j + 1] = e + 1 < n ? win[e + 1] : 0.0;
+    }
+    if (SCALE) {
+      wr[2 * j] = wr[2 * j] * sc;
+      wr[2 * j + 1] = wr[2 * j + 1] * sc;
+      if (full) {
+        *reinterpret_cast<double2*>(wout + e) = make_double2(wr[2 * j], wr[2 * j + 1]);
+      } else {
+        if (e < n) wout[e] = wr[2 * j];
+        if (e + 1 < n) wout[e + 1] = wr[2 * j + 1];
+      }
+    }
+  }
+#pragma unroll 1
+  for (int v = 0; v < nc; ++v) {
+    const double* __restrict__ col = A + (int64_t)v * lda;
+    double acc = 0.0;
+    if (full) {
+      double2 q[kIters];
+#pragma unroll
+      for (int j = 0; j < kIters; ++j) q[j] = *reinterpret_cast<const double2*>(col + base + j * (2 * kT));
+#pragma unroll
+      for (int j = 0; j < kIters; ++j) {
+        acc = acc + wr[2 * j] * q[j].x;
+        acc = acc + wr[2 * j + 1] * q[j].y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kIters; ++j) {
+        const int64_t e = base + j * (2 * kT);
+        if (e < n) acc = acc + wr[2 * j] * col[e];
+        if (e + 1 < n) acc = acc + wr[2 * j + 1] * col[e + 1];
+      }
+    }
+    acc = wave_butterfly(acc);
+    if (lane == 0) red[v][wv] = acc;
+  }
+  __syncthreads();
+  if (t < nc) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+}
+
+// ------------------------------------------------------------------ SpMM
+// R[:, 0:nc] = A S[:, 0:nc]: one lane per row, the row's CSR entries read once
+// for all nc columns; per column the MatMult_SeqAIJ order (ascending entries,
+// from 0), as PETSc's MatMatMultNumericAdd_SeqAIJ_SeqDense accumulates.
+template <int CG>
+__global__ __launch_bounds__(kT) void k_spmm(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                             const int32_t* __restrict__ col, const double* __restrict__ val,
+                                             const double* __restrict__ S, int64_t lds, int nc,
+                                             double* __restrict__ R, int64_t ldr) {
+  const int32_t r = blockIdx.x * kT + threadIdx.x;
+  if (r >= nrows) return;
+  double acc[CG];
+#pragma unroll
+  for (int q = 0; q < CG; ++q) acc[q] = 0.0;
+  const int32_t k1 = rowptr[r + 1];
+  for (int32_t k = rowptr[r]; k < k1; ++k) {
+    const double a = val[k];
+    const double* __restrict__ sp = S + col[k];
+#pragma unroll
+    for (int q = 0; q < CG; ++q)
+      if (q < nc) acc[q] = acc[q] + a * sp[(int64_t)q * lds];
+  }
+#pragma unroll
+  for (int q = 0; q < CG; ++q)
+    if (q < nc) R[r + (int64_t)q * ldr] = acc[q];
+}
+
+}  // namespace msd
+
+using namespace msd;
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// ===================================================================== internal
+extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc, int64_t n, const double* coef_dev,
+                               const double* nal_dev, const double* U, double* y, double* partial, double* sumsq_dev,
+                               const int* stop) {
+  if (n <= 0) {
+    if (sumsq_dev) HIPCHK(hipMemsetAsync(sumsq_dev, 0, sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  const int64_t nch = nchunks_of(n);
+  const bool vec = aligned16(A) && (lda % 2 == 0) && aligned16(y) && (!U || aligned16(U));
+  const bool axpy = U != nullptr, norm = sumsq_dev != nullptr;
+  KTimer kt(c, MSP_KERNEL_DGEMV, 8.0 * (double)n * (nc + 1 + (axpy ? 1 : 0)));
+  const dim3 g((unsigned)nch), b(kT);
+#define GEMV(AX, NO, VE) \
+  k_dense_gemv<AX, NO, VE><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, y, n, partial, stop)
+  if (axpy && norm) { if (vec) GEMV(true, true, true); else GEMV(true, true, false); }
+  else if (axpy) { if (vec) GEMV(true, false, true); else GEMV(true, false, false); }
+  else if (norm) { if (vec) GEMV(false, true, true); else GEMV(false, true, false); }
+  else { if (vec) GEMV(false, false, true); else GEMV(false, false, false); }
+#undef GEMV
+  KCHK((int)hipGetLastError());
+  if (norm) KCHK(msk_dot_stage2(partial, nch, 1, sumsq_dev, stop, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wout, const double* sc_dev,
+                                      const double* A, int64_t lda, int nc, int64_t n, double* partial,
+                                      double* out_dev, const int* stop) {
+  if (nc <= 0) return MSP_SUCCESS;
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0) {
+    HIPCHK(hipMemsetAsync(out_dev, 0, (size_t)nc * sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  KTimer kt(c, MSP_KERNEL_DGEMVT, 8.0 * (double)n * (nc + 1 + (sc_dev ? 1 : 0)));
+  const bool vec = aligned16(A) && (lda % 2 == 0) && aligned16(win) && (!sc_dev || aligned16(wout));
+  for (int g0 = 0; g0 < nc; g0 += kMaxCols) {
+    const int g = std::min(kMaxCols, nc - g0);
+    const double* Ag = A + (int64_t)g0 * lda;
+    const bool scale = sc_dev && g0 == 0;          // scale once, later groups read the scaled vector
+    const double* src = (sc_dev && g0 > 0) ? wout : win;
+    const dim3 gr((unsigned)nch), b(kT);
+    if (scale) {
+      if (vec) k_scaled_dot<true, true><<<gr, b, 0, c->stream>>>(src, wout, sc_dev, Ag, lda, g, n, partial, nch, stop);
+      else k_scaled_dot<true, false><<<gr, b, 0, c->stream>>>(src, wout, sc_dev, Ag, lda, g, n, partial, nch, stop);
+    } else {
+      if (vec) k_scaled_dot<false, true><<<gr, b, 0, c->stream>>>(src, nullptr, nullptr, Ag, lda, g, n, partial, nch, stop);
+      else k_scaled_dot<false, false><<<gr, b, 0, c->stream>>>(src, nullptr, nullptr, Ag, lda, g, n, partial, nch, stop);
+    }
+    KCHK((int)hipGetLastError());
+    KCHK(msk_dot_stage2(partial, nch, g, out_dev + g0, stop, c->stream));
+  }
+  return MSP_SUCCESS;
+}
+
+// out[j] = ||column j||^2 (DBR), j < nc
+extern "C" int mspi_dense_colsumsq(msp_ctx* c, const double* A, int64_t lda, int nc, int64_t n, double* partial,
+                                   double* out_dev) {
+  if (nc <= 0) return MSP_SUCCESS;
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0) {
+    HIPCHK(hipMemsetAsync(out_dev, 0, (size_t)nc * sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  KTimer kt(c, MSP_KERNEL_NORM, 8.0 * (double)n * nc);
+  for (int j = 0; j < nc; ++j) {
+    Vecs v = {};
+    v.p[0] = A + (int64_t)j * lda;
+    KCHK(msk_dot_stage1(v.p[0], &v, 1, n, partial, nch, 1, nullptr, c->stream));
+    KCHK(msk_dot_stage2(partial, nch, 1, out_dev + j, nullptr, c->stream));
+  }
+  return MSP_SUCCESS;
+}
+
+// ======================================================================= dense
+static int64_t lda_for(int64_t nrows) { return std::max<int64_t>(512, (nrows + 511) / 512 * 512); }
+
+extern "C" int msp_dense_create(msp_ctx* c, int64_t nrows, int32_t ncols, msp_dense** out) {
+  ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(nrows >= 0 && ncols >= 1, MSP_ERR_ARG_SIZ, "dense block %lld x %d", (long long)nrows, ncols);
+  msp_dense* A = new msp_dense();
+  A->ctx = c;
+  A->nrows = nrows;
+  A->ncols = ncols;
+  A->lda = lda_for(nrows);
+  const size_t bytes = (size_t)(A->lda * ncols + 512) * sizeof(double);
+  if (hipMalloc((void**)&A->d, bytes) != hipSuccess) {
+    delete A;
+    mspi_set_error(MSP_ERR_MEM, "hipMalloc of a %lld x %d dense block failed", (long long)nrows, ncols);
+    return MSP_ERR_MEM;
+  }
+  HIPCHK(hipMemsetAsync(A->d, 0, bytes, c->stream));
+  *out = A;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_destroy(msp_dense** pA) {
+  if (!pA || !*pA) return MSP_SUCCESS;
+  msp_dense* A = *pA;
+  if (A->ctx && A->ctx->stream) (void)hipStreamSynchronize(A->ctx->stream);
+  if (A->d) (void)hipFree(A->d);
+  delete A;
+  *pA = nullptr;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_get_info(const msp_dense* A, int64_t* nrows, int32_t* ncols, int64_t* lda) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "dense is NULL");
+  if (nrows) *nrows = A->nrows;
+  if (ncols) *ncols = A->ncols;
+  if (lda) *lda = A->lda;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_get_array(msp_dense* A, double** p) {
+  ARGCHK(A && p, MSP_ERR_ARG_NULL, "NULL argument");
+  *p = A->d;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_zero_entries(msp_dense* A) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "dense is NULL");
+  HIPCHK(hipMemsetAsync(A->d, 0, (size_t)A->lda * A->ncols * sizeof(double), A->ctx->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_set_values(msp_dense* A, const double* host, int64_t ld) {
+  ARGCHK(A && (host || A->nrows == 0), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(ld >= A->nrows, MSP_ERR_ARG_SIZ, "ld %lld < nrows %lld", (long long)ld, (long long)A->nrows);
+  if (A->nrows == 0) return MSP_SUCCESS;
+  HIPCHK(hipMemcpy2DAsync(A->d, (size_t)A->lda * sizeof(double), host, (size_t)ld * sizeof(double),
+                          (size_t)A->nrows * sizeof(double), (size_t)A->ncols, hipMemcpyHostToDevice,
+                          A->ctx->stream));
+  HIPCHK(hipStreamSynchronize(A->ctx->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_get_values(const msp_dense* A, double* host, int64_t ld) {
+  ARGCHK(A && (host || A->nrows == 0), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(ld >= A->nrows, MSP_ERR_ARG_SIZ, "ld %lld < nrows %lld", (long long)ld, (long long)A->nrows);
+  if (A->nrows == 0) return MSP_SUCCESS;
+  HIPCHK(hipMemcpy2DAsync(host, (size_t)ld * sizeof(double), A->d, (size_t)A->lda * sizeof(double),
+                          (size_t)A->nrows * sizeof(double), (size_t)A->ncols, hipMemcpyDeviceToHost,
+                          A->ctx->stream));
+  HIPCHK(hipStreamSynchronize(A->ctx->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_set_column(msp_dense* A, int32_t j, int64_t row0, const msp_vec* x, int64_t xoff,
+                                    int64_t n) {
+  ARGCHK(A && x, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(j >= 0 && j < A->ncols, MSP_ERR_ARG_OUTOFRANGE, "column %d outside [0,%d)", j, A->ncols);
+  ARGCHK(n >= 0 && row0 >= 0 && row0 + n <= A->nrows && xoff >= 0 && xoff + n <= x->n, MSP_ERR_ARG_OUTOFRANGE,
+         "set_column range out of bounds");
+  return mspi_copy(A->ctx, A->d + (int64_t)j * A->lda + row0, x->d + xoff, n);
+}
+
+extern "C" int msp_dense_mult(msp_dense* A, const msp_vec* alpha, int64_t row0, int64_t n, msp_vec* y, int64_t yoff) {
+  ARGCHK(A && alpha && y, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(alpha->n == A->ncols, MSP_ERR_ARG_SIZ, "alpha has %lld entries, dense block %d columns",
+         (long long)alpha->n, A->ncols);
+  ARGCHK(n >= 0 && row0 >= 0 && row0 + n <= A->nrows && yoff >= 0 && yoff + n <= y->n, MSP_ERR_ARG_OUTOFRANGE,
+         "dense mult range out of bounds");
+  return mspi_dense_gemv(A->ctx, A->d + row0, A->lda, A->ncols, n, alpha->d, nullptr, nullptr, y->d + yoff, nullptr,
+                         nullptr, nullptr);
+}
+
+extern "C" int msp_dense_mult_transpose(msp_dense* A, const msp_vec* u, msp_vec* out) {
+  ARGCHK(A && u && out, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(u->n == A->nrows && out->n == A->ncols, MSP_ERR_ARG_SIZ, "MatMultTranspose sizes");
+  msp_ctx* c = A->ctx;
+  double* partial = nullptr;
+  const int64_t nch = std::max<int64_t>(1, nchunks_of(A->nrows));
+  int rc = mspi_malloc(c, (void**)&partial, (size_t)nch * kMaxCols * sizeof(double));
+  if (rc) return rc;
+  rc = mspi_dense_scaled_dots(c, u->d, nullptr, nullptr, A->d, A->lda, A->ncols, A->nrows, partial, out->d, nullptr);
+  (void)hipStreamSynchronize(c->stream);
+  mspi_free(c, partial);
+  return rc;
+}
+
+extern "C" int msp_mat_matmult_dense(msp_mat* A, const msp_dense* S, msp_dense* R) {
+  ARGCHK(A && S && R, MSP_ERR_ARG_NULL, "NULL argument");
+  int32_t nr, ncol;
+  mspi_mat_dims(A, &nr, &ncol);
+  ARGCHK(ncol == S->nrows && nr == R->nrows && S->ncols == R->ncols, MSP_ERR_ARG_SIZ,
+         "MatMatMult sizes: A %d x %d, S %lld x %d, R %lld x %d", nr, ncol, (long long)S->nrows, S->ncols,
+         (long long)R->nrows, R->ncols);
+  const mspi_csr_view v = mspi_mat_csr(A);
+  ARGCHK(!v.compressed, MSP_ERR_SUP, "MatMatMult with a row-compressed matrix");
+  msp_ctx* c = mspi_mat_ctx(A);
+  if (nr == 0) return MSP_SUCCESS;
+  KTimer kt(c, MSP_KERNEL_SPMM,
+            12.0 * (double)v.nnz + 4.0 * (nr + 1.0) + 8.0 * (double)S->ncols * ((double)S->nrows + (double)nr));
+  const dim3 g((unsigned)((nr + kT - 1) / kT)), b(kT);
+  for (int j0 = 0; j0 < S->ncols; j0 += 32) {
+    const int nc = std::min(32, S->ncols - j0);
+    const double* Sg = S->d + (int64_t)j0 * S->lda;
+    double* Rg = R->d + (int64_t)j0 * R->lda;
+    if (nc <= 8) k_spmm<8><<<g, b, 0, c->stream>>>(nr, v.rowptr, v.col, v.val, Sg, S->lda, nc, Rg, R->lda);
+    else if (nc <= 16) k_spmm<16><<<g, b, 0, c->stream>>>(nr, v.rowptr, v.col, v.val, Sg, S->lda, nc, Rg, R->lda);
+    else k_spmm<32><<<g, b, 0, c->stream>>>(nr, v.rowptr, v.col, v.val, Sg, S->lda, nc, Rg, R->lda);
+    KCHK((int)hipGetLastError());
+  }
+  return MSP_SUCCESS;
+}

@@ -42,6 +42,35 @@ int mspi_d2h_sync(msp_ctx *ctx, void *host, const void *dev, size_t bytes);
 
 int mspi_mat_dims(const msp_mat *A, int32_t *nrows, int32_t *ncols);
 msp_ctx *mspi_mat_ctx(const msp_mat *A);
+typedef struct {
+  const int32_t *rowptr, *col;
+  const double *val;
+  int64_t nnz;
+  int compressed;
+} mspi_csr_view;
+mspi_csr_view mspi_mat_csr(const msp_mat *A);
+
+/* dense row block, column-major, lda a multiple of 512 */
+struct msp_dense {
+  msp_ctx *ctx;
+  int64_t nrows;
+  int32_t ncols;
+  int64_t lda;
+  double *d;
+};
+
+/* y = A[:, 0:nc] coef (+ (*nal_dev) U when U != NULL, skipped when *nal_dev == 0);
+ * sumsq_dev != NULL: also ||y||^2 (DBR; partial holds nchunks doubles). */
+int mspi_dense_gemv(msp_ctx *ctx, const double *A, int64_t lda, int nc, int64_t n, const double *coef_dev,
+                    const double *nal_dev, const double *U, double *y, double *partial, double *sumsq_dev,
+                    const int *stop);
+/* sc_dev != NULL: wout = win * (*sc_dev) first; out_dev[j] = column_j . w (DBR), j < nc.
+ * partial holds nchunks*32 doubles. */
+int mspi_dense_scaled_dots(msp_ctx *ctx, const double *win, double *wout, const double *sc_dev, const double *A,
+                           int64_t lda, int nc, int64_t n, double *partial, double *out_dev, const int *stop);
+/* out_dev[j] = ||column j||^2 (DBR) */
+int mspi_dense_colsumsq(msp_ctx *ctx, const double *A, int64_t lda, int nc, int64_t n, double *partial,
+                        double *out_dev);
 
 /* y = A x ; r = b - A x */
 int mspi_spmv(msp_mat *A, const double *x, double *y);
@@ -98,6 +127,39 @@ int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv,
 int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const double *base, int64_t stride, int64_t n,
                            const double *coef_dev, int nv_expected);
 int mspi_h2d_async(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
+
+/* ---- cross-process all-gather (msplit_comm.hip); comm may be NULL (1 rank) ---- */
+int mspi_comm_allgather(msp_comm *comm, const double *send_dev, double *recv_dev, int64_t count);
+int mspi_comm_size(const msp_comm *comm, int32_t *nranks, int32_t *rank);
+
+/* ---- device-resident KSPLSQR state (msplit_lsqr.hip) ---- */
+typedef struct {
+  int32_t stop;        /* solve over: later kernels return at once */
+  int32_t reason, its, nhist;
+  int32_t i;           /* loop counter of KSPSolve_LSQR */
+  int32_t max_it, conv_test, exact_norm, hist_cap;
+  int32_t s;           /* columns of R */
+  int32_t nblk;        /* row blocks over all ranks */
+  int32_t pad;
+  double rnorm, rnorm0, ttol, arnorm, anorm;
+  double alpha, beta, phibar, rhobar;
+  double uscale;       /* VecScale factor of the newest U (1/beta, or 1 when beta == 0) */
+  double nalpha;       /* -alpha of VecAXPY(U1, -alpha, U) */
+  double rtol, abstol, divtol;
+} mspi_lsqr_state;
+
+typedef struct {
+  mspi_lsqr_state *st;  /* device */
+  double *V, *V1, *W, *X; /* s entries each (X: the solution vector) */
+  double *g;            /* all-gathered block partials, nblk * m */
+  double *hist;         /* hist_cap */
+} mspi_lsqr_dev;
+
+/* one-lane kernels of the LSQR recurrence (g holds nblk values / nblk*s values) */
+int mspi_ls_start(msp_ctx *ctx, mspi_lsqr_dev d);
+int mspi_ls_first(msp_ctx *ctx, mspi_lsqr_dev d, const double *gfrob);
+int mspi_ls_beta(msp_ctx *ctx, mspi_lsqr_dev d);
+int mspi_ls_step(msp_ctx *ctx, mspi_lsqr_dev d);
 
 #ifdef __cplusplus
 }

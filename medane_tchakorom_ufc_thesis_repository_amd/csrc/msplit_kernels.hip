@@ -402,27 +402,37 @@ __device__ __forceinline__ int64_t box_rowptr(int dim, int64_t l, int64_t nx, in
   return 5 * l - missing;
 }
 
+// lo / hi: the block also couples to the neighbour plane below / above (one
+// plane of the slowest direction: z in 3D, mesh lines in 2D), stored as extra
+// columns before / after the block's own: column space [plane_lo | block |
+// plane_hi], still ascending in global order (the rows of the reference's
+// A_block_jacobi, utils.c:30-121 / :247-293, with their column ids shifted).
 __global__ __launch_bounds__(kT) void k_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows,
-                                                    int32_t* __restrict__ rowptr, int32_t* __restrict__ col,
-                                                    double* __restrict__ val) {
+                                                    int lo, int hi, int32_t* __restrict__ rowptr,
+                                                    int32_t* __restrict__ col, double* __restrict__ val) {
   const int64_t stride = (int64_t)gridDim.x * kT;
+  const int64_t P = dim == 3 ? (int64_t)nx * ny : (int64_t)nx;  // slab plane
+  const int64_t ns = dim == 3 ? nz : ny;                           // planes in the block
+  const int64_t off = lo ? P : 0;
   for (int64_t l = (int64_t)blockIdx.x * kT + threadIdx.x; l <= nrows; l += stride) {
-    const int64_t p0 = box_rowptr(dim, l, nx, ny, nz);
+    int64_t p0 = box_rowptr(dim, l, nx, ny, nz);
+    if (lo) p0 += min(l, P);
+    if (hi) p0 += max((int64_t)0, l - (ns - 1) * P);
     rowptr[l] = (int32_t)p0;
     if (l == nrows) continue;
-    const int64_t P = (int64_t)nx * ny;
     const int32_t i = (int32_t)(l % nx);
     const int32_t j = (int32_t)((l / nx) % ny);
-    const int32_t k = dim == 3 ? (int32_t)(l / P) : 0;
+    const int64_t sl = l / P;  // slab-plane index (k in 3D, j in 2D)
+    const int64_t e = l + off;
     int64_t p = p0;
     const double diag = dim == 3 ? 6.0 : 4.0;
-    if (dim == 3 && k > 0) { col[p] = (int32_t)(l - P); val[p++] = -1.0; }
-    if (j > 0) { col[p] = (int32_t)(l - nx); val[p++] = -1.0; }
-    if (i > 0) { col[p] = (int32_t)(l - 1); val[p++] = -1.0; }
-    col[p] = (int32_t)l; val[p++] = diag;
-    if (i < nx - 1) { col[p] = (int32_t)(l + 1); val[p++] = -1.0; }
-    if (j < ny - 1) { col[p] = (int32_t)(l + nx); val[p++] = -1.0; }
-    if (dim == 3 && k < nz - 1) { col[p] = (int32_t)(l + P); val[p++] = -1.0; }
+    if (sl > 0 || lo) { col[p] = (int32_t)(e - P); val[p++] = -1.0; }
+    if (dim == 3 && j > 0) { col[p] = (int32_t)(e - nx); val[p++] = -1.0; }
+    if (i > 0) { col[p] = (int32_t)(e - 1); val[p++] = -1.0; }
+    col[p] = (int32_t)e; val[p++] = diag;
+    if (i < nx - 1) { col[p] = (int32_t)(e + 1); val[p++] = -1.0; }
+    if (dim == 3 && j < ny - 1) { col[p] = (int32_t)(e + nx); val[p++] = -1.0; }
+    if (sl < ns - 1 || hi) { col[p] = (int32_t)(e + P); val[p++] = -1.0; }
   }
 }
 
@@ -539,10 +549,10 @@ extern "C" int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int3
   return (int)hipGetLastError();
 }
 
-extern "C" int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int32_t* rowptr,
-                               int32_t* col, double* val, hipStream_t s) {
+extern "C" int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi,
+                               int32_t* rowptr, int32_t* col, double* val, hipStream_t s) {
   const int g = grid_for(nrows + 1, 8192);
-  k_box_stencil<<<dim3(g), dim3(kT), 0, s>>>(dim, nx, ny, nz, nrows, rowptr, col, val);
+  k_box_stencil<<<dim3(g), dim3(kT), 0, s>>>(dim, nx, ny, nz, nrows, lo, hi, rowptr, col, val);
   return (int)hipGetLastError();
 }
 

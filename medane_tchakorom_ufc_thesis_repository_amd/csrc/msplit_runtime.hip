@@ -17,6 +17,7 @@
 #include "msplit.h"
 #include "msplit_internal.h"
 #include "msplit_kernels.h"
+#include "msplit_ctx.hpp"
 
 // ----------------------------------------------------------------- errors
 static thread_local char g_err[512] = "no error";
@@ -31,57 +32,6 @@ extern "C" void mspi_set_error(int code, const char* fmt, ...) {
 }
 
 extern "C" const char* msp_get_last_error(void) { return g_err; }
-
-#define HIPCHK(call)                                                                              \
-  do {                                                                                            \
-    hipError_t e_ = (call);                                                                       \
-    if (e_ != hipSuccess) {                                                                       \
-      mspi_set_error(MSP_ERR_LIB, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
-                     __LINE__);                                                                   \
-      return MSP_ERR_LIB;                                                                         \
-    }                                                                                             \
-  } while (0)
-
-#define KCHK(call)                                                                                  \
-  do {                                                                                              \
-    int e_ = (call);                                                                                \
-    if (e_) {                                                                                       \
-      mspi_set_error(MSP_ERR_LIB, "kernel launch %s failed: %s", #call,                             \
-                     hipGetErrorString((hipError_t)e_));                                            \
-      return MSP_ERR_LIB;                                                                           \
-    }                                                                                               \
-  } while (0)
-
-#define ARGCHK(cond, code, ...)        \
-  do {                                 \
-    if (!(cond)) {                     \
-      mspi_set_error(code, __VA_ARGS__); \
-      return code;                     \
-    }                                  \
-  } while (0)
-
-// ---------------------------------------------------------------- context
-struct TimedRec {
-  int cls;
-  int ev;  // index of the start event in the pool; stop = ev + 1
-  double bytes;
-};
-
-struct msp_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
-  double* dscratch = nullptr;  // device scalars
-  double* hscratch = nullptr;  // pinned host scalars
-  double* partial = nullptr;   // DBR stage-1 partials
-  int64_t partial_cap = 0;     // doubles
-  bool timing = false;
-  std::vector<hipEvent_t> pool;
-  size_t pool_used = 0;
-  std::vector<TimedRec> recs;
-};
-
-static const int kScratch = 4 * MSPI_MAX_GROUP + 64;
 
 extern "C" int msp_get_device_count(int* count) {
   ARGCHK(count, MSP_ERR_ARG_NULL, "count is NULL");
@@ -178,29 +128,6 @@ extern "C" int msp_ctx_get_kernel_stats(msp_ctx* c, int cls, int64_t* launches, 
   return MSP_SUCCESS;
 }
 
-// Brackets one logical kernel (possibly two launches) with a pair of events.
-struct KTimer {
-  msp_ctx* c;
-  int ev = -1;
-  KTimer(msp_ctx* ctx, int cls, double bytes) : c(ctx) {
-    if (!c->timing) return;
-    if (c->pool_used + 2 > c->pool.size()) {
-      for (int i = 0; i < 256; ++i) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return;
-        c->pool.push_back(e);
-      }
-    }
-    ev = (int)c->pool_used;
-    c->pool_used += 2;
-    (void)hipEventRecord(c->pool[ev], c->stream);
-    c->recs.push_back({cls, ev, bytes});
-  }
-  ~KTimer() {
-    if (ev >= 0) (void)hipEventRecord(c->pool[ev + 1], c->stream);
-  }
-};
-
 extern "C" double* mspi_dev_scratch(msp_ctx* c) { return c->dscratch; }
 extern "C" double* mspi_host_scratch(msp_ctx* c) { return c->hscratch; }
 
@@ -244,19 +171,6 @@ extern "C" int mspi_d2h_sync(msp_ctx* c, void* host, const void* dev, size_t byt
   HIPCHK(hipStreamSynchronize(c->stream));
   return MSP_SUCCESS;
 }
-
-static int ensure_partial(msp_ctx* c, int64_t need) {
-  if (need <= c->partial_cap) return MSP_SUCCESS;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->partial) HIPCHK(hipFree(c->partial));
-  c->partial = nullptr;
-  c->partial_cap = 0;
-  HIPCHK(hipMalloc((void**)&c->partial, (size_t)need * sizeof(double)));
-  c->partial_cap = need;
-  return MSP_SUCCESS;
-}
-
-static inline int64_t nchunks_of(int64_t n) { return (n + MSK_DBR_CHUNK - 1) / MSK_DBR_CHUNK; }
 
 // --------------------------------------------------------------- internal ops
 extern "C" int mspi_mdot(msp_ctx* c, const double* w, int nv, const double* const* V, int64_t n, double* out_dev) {
@@ -420,6 +334,10 @@ extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
   return MSP_SUCCESS;
 }
 extern "C" msp_ctx* mspi_mat_ctx(const msp_mat* A) { return A->ctx; }
+extern "C" mspi_csr_view mspi_mat_csr(const msp_mat* A) {
+  mspi_csr_view v = {A->rowptr, A->col, A->val, A->nnz, A->compressed ? 1 : 0};
+  return v;
+}
 
 static const int32_t kMaxLdsCap = 4096;  // 48 KiB of col+val per 256-row block
 
@@ -528,22 +446,28 @@ extern "C" int msp_mat_create_csr_rows(msp_ctx* c, int32_t nrows, int32_t ncols,
   return MSP_SUCCESS;
 }
 
-extern "C" int msp_mat_create_box_stencil(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, msp_mat** out) {
+extern "C" int msp_mat_create_box_stencil_ext(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
+                                              int32_t hi, msp_mat** out) {
   ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");
   ARGCHK(dim == 2 || dim == 3, MSP_ERR_ARG_WRONG, "dim must be 2 or 3, got %d", dim);
   if (dim == 2) nz = 1;
   ARGCHK(nx > 0 && ny > 0 && nz > 0, MSP_ERR_ARG_SIZ, "box %d x %d x %d", nx, ny, nz);
+  lo = lo ? 1 : 0;
+  hi = hi ? 1 : 0;
   const int64_t nrows = (int64_t)nx * ny * nz;
+  const int64_t plane = dim == 3 ? (int64_t)nx * ny : (int64_t)nx;
+  const int64_t ncols = nrows + (lo + hi) * plane;
   const int64_t deg = dim == 3 ? 7 : 5;
-  ARGCHK(nrows <= INT32_MAX && deg * nrows <= INT32_MAX, MSP_ERR_ARG_OUTOFRANGE,
+  ARGCHK(ncols <= INT32_MAX && deg * nrows <= INT32_MAX, MSP_ERR_ARG_OUTOFRANGE,
          "box of %lld rows exceeds 32-bit PetscInt indexing", (long long)nrows);
   msp_mat* A = new msp_mat();
   A->ctx = c;
   A->nrows = (int32_t)nrows;
-  A->ncols = (int32_t)nrows;
-  // exact nnz: deg*N minus missing neighbours on each face
+  A->ncols = (int32_t)ncols;
+  // exact nnz: deg*N minus missing neighbours on each face, plus the halo couplings
   int64_t nnz = deg * nrows - 2 * (nrows / nx) - 2 * (nrows / ny);
   if (dim == 3) nnz -= 2 * (nrows / nz);
+  nnz += (lo + hi) * plane;
   A->nnz = nnz;
   A->lds_cap = lds_cap_for(deg * 256);
   int rc = mat_alloc(c, A, nrows + 1, nnz);
@@ -551,10 +475,14 @@ extern "C" int msp_mat_create_box_stencil(msp_ctx* c, int dim, int32_t nx, int32
     msp_mat_destroy(&A);
     return rc;
   }
-  KCHK(msk_box_stencil(dim, nx, ny, nz, nrows, A->rowptr, A->col, A->val, c->stream));
+  KCHK(msk_box_stencil(dim, nx, ny, nz, nrows, lo, hi, A->rowptr, A->col, A->val, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   *out = A;
   return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_create_box_stencil(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, msp_mat** out) {
+  return msp_mat_create_box_stencil_ext(c, dim, nx, ny, nz, 0, 0, out);
 }
 
 extern "C" int msp_mat_destroy(msp_mat** pA) {

@@ -1,9 +1,12 @@
-"""Synchronous multisplitting driver over the GPU inner solve.
+"""Synchronous multisplitting drivers over the GPU inner solve.
 
-Mirrors src/synchronous-multisplitting/synchronous-multisplitting.c:
-setup (:101-164), the outer loop (:170-206) and the final report (:208-229),
-generalised from 2 blocks to nb z-slab (3D) or mesh-line (2D) blocks, one per
-GPU.  Each block's inner solve is GMRES on its diagonal block A_ii
+sm_solve mirrors src/synchronous-multisplitting/synchronous-multisplitting.c:
+setup (:101-164), the outer loop (:170-206) and the final report (:208-229);
+smsm_solve mirrors the global-minimization variant,
+src/synchronous-multisplitting-synchronous-minimization-global/
+synchronous-multisplitting-synchronous-minimization-global.c (setup :134-284,
+loop :288-363).  Both are generalised from 2 blocks to nb z-slab (3D) or
+mesh-line (2D) blocks, one per GPU.  Each block's inner solve is GMRES on its diagonal block A_ii
 (inner_solver, utils.c:950-970) running entirely in that GPU's HBM; the only
 traffic between blocks is the boundary-plane exchange and one scalar per block
 per outer iteration (comm.py).
@@ -18,8 +21,8 @@ import math
 import time
 from dataclasses import dataclass, field
 
-from .petsc import Context, Mat, Options, Vec
-from .utils import BlockLayout, block_layout, initializeKSP, inner_solver, updateLocalRHS
+from .petsc import LSQR, Context, DenseMat, Mat, Options, Vec
+from .utils import BlockLayout, block_layout, initializeKSP, initializeOuterKSP, inner_solver, updateLocalRHS
 
 
 class GpuBlock:
@@ -107,6 +110,60 @@ class GpuBlock:
         ln = self.r.norm()
         return ln * ln
 
+    # -- global minimization (SMSM-global) hooks
+    def setup_minimization(self, s: int):
+        """S (the s latest iterates, with the neighbour planes R = A S reads) and
+        R = A S in HBM, and A_ext = this block's rows of A_block_jacobi with the
+        coupling columns (create_redistributed_A_block_jacobi, utils.c:891-921)."""
+        L = self.layout
+        self.s = int(s)
+        self.lo_rows = L.plane if any(nbr < L.b for nbr, *_ in L.recv) else 0
+        self.hi_rows = L.plane if any(nbr > L.b for nbr, *_ in L.recv) else 0
+        dim, bx, by, bz = L.box
+        self.A_ext = Mat.box_stencil_ext(self.ctx, dim, bx, by, bz, self.lo_rows > 0, self.hi_rows > 0)
+        self.S = DenseMat(self.ctx, self.lo_rows + L.nrows + self.hi_rows, self.s)
+        self.R = DenseMat(self.ctx, L.nrows, self.s)
+
+    def store_column(self, k: int):
+        """S(:, k) = x after the k-th inner solve and exchange (MatSetValuesLocal,
+        SMSM-global.c:314-316): own rows and the received neighbour planes."""
+        n = self.layout.nrows
+        self.S.set_column(k, self.lo_rows, self.x)
+        if self.lo_rows:
+            self.S.set_column(k, 0, self.halo, 0, self.lo_rows)
+        if self.hi_rows:
+            self.S.set_column(k, self.lo_rows + n, self.halo, self.lo_rows, self.hi_rows)
+
+    def form_R(self):
+        """R = A S (MatMatMult, SMSM-global.c:325-327)."""
+        self.A_ext.mat_mult_dense(self.S, self.R)
+
+    def apply_alpha(self, alpha: Vec):
+        """x_minimized = S alpha, scattered back into x_i and the neighbour planes
+        (SMSM-global.c:349-352 and utils.c:1076): the planes are computed from
+        the stored neighbour values with the neighbour's own row arithmetic, so
+        they equal what the neighbour computes for those rows."""
+        n = self.layout.nrows
+        self.S.mult(alpha, self.x, row0=self.lo_rows, n=n)
+        if self.lo_rows:
+            self.S.mult(alpha, self.halo, row0=0, n=self.lo_rows, yoff=0)
+        if self.hi_rows:
+            self.S.mult(alpha, self.halo, row0=self.lo_rows + n, n=self.hi_rows, yoff=self.lo_rows)
+
+    def block_residual_sq(self) -> float:
+        """||b_i - A_block x||^2 over the block's full rows (computeFinalResidualNorm,
+        utils.c:575-595): A_ext applied to [plane below | x_i | plane above]."""
+        n = self.layout.nrows
+        xe = Vec(self.ctx, self.lo_rows + n + self.hi_rows)
+        self.x.copy_range_to(0, xe, self.lo_rows, n)
+        if self.lo_rows:
+            self.halo.copy_range_to(0, xe, 0, self.lo_rows)
+        if self.hi_rows:
+            self.halo.copy_range_to(self.lo_rows, xe, self.lo_rows + n, self.hi_rows)
+        self.A_ext.residual(self.b, xe, self.r)
+        ln = self.r.norm()
+        return ln * ln
+
     def error_sq(self) -> float:
         """||x_i - 1||^2 (computeError, utils.c:1045-1059, on this block's rows)."""
         ones = Vec(self.ctx, self.layout.nrows)
@@ -161,5 +218,93 @@ def sm_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_outer: int = 1
     return res
 
 
+class GpuMinimizer:
+    """The outer least-squares step of SMSM-global on the GPUs: one KSPLSQR over
+    R = A S, row-distributed (each rank its blocks' rows; block partials
+    all-gathered, msp_comm), alpha replicated, then x = S alpha on every block
+    (outer_solver_norm_equation, utils.c:1061-1078).  prefix: the reference's
+    outer{b+1}_ options prefix of the lowest local block."""
+
+    def __init__(self, ctx: Context, blocks, comm, opts: Options | None, prefix: str | None = None):
+        self.ctx = ctx
+        self.blocks = blocks
+        b0 = min(blk.layout.b for blk in blocks)
+        self.lsqr = initializeOuterKSP(ctx, prefix if prefix is not None else f"outer{b0 + 1}_", opts)
+        self.lsqr.set_operators([blk.R for blk in blocks])
+        self.comm = comm.lsqr_comm(ctx) if hasattr(comm, "lsqr_comm") else None
+        self.lsqr.set_comm(self.comm)
+        self.alpha = Vec(ctx, blocks[0].s)
+
+    def solve(self, blocks):
+        self.lsqr.solve([blk.b for blk in blocks], self.alpha)
+        for blk in blocks:
+            blk.apply_alpha(self.alpha)
+        return (self.lsqr.get_residual_norm(), self.lsqr.get_iteration_number(),
+                self.lsqr.get_converged_reason())
+
+
+@dataclass
+class SMSMResult:
+    outer_its: int = 0
+    norm0: float = 0.0
+    hist: list = field(default_factory=list)          # outer LSQR residual norms (the stop test's norm)
+    lsqr_its: list = field(default_factory=list)
+    lsqr_reason: list = field(default_factory=list)
+    inner_its: list = field(default_factory=list)     # per outer: s lists of [its of each local block]
+    final_norm: float = float("nan")
+    error: float = float("nan")
+    elapsed: float = 0.0
+
+
+def smsm_solve(blocks, comm, s: int, minimizer, rtol: float, atol: float = 1e-100, max_outer: int = 10000,
+               monitor=None) -> SMSMResult:
+    """SMSM with global minimization (SMSM-global.c:288-363), nb blocks:
+    s times {rhs_i = b_i - A_ij x_j; inner GMRES; exchange; S(:,k) = x},
+    R = A S, alpha = LSQR(R, b), x = S alpha; stop on the LSQR residual norm."""
+    res = SMSMResult()
+    # global_norm_0 = computeFinalResidualNorm at x = 0 (:280)
+    res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
+    for blk in blocks:
+        blk.reset_halo()
+    comm.barrier()
+    t0 = time.perf_counter()
+    while True:
+        its_outer = []
+        for k in range(s):
+            for blk in blocks:
+                blk.update_rhs()                             # updateLocalRHS (:297)
+            its_outer.append([blk.solve() for blk in blocks])  # inner_solver (:299)
+            comm.exchange(blocks)                            # comm_sync_send_and_receive (:301)
+            for blk in blocks:
+                blk.store_column(k)                          # MatSetValuesLocal(S, .., k, x) (:314-316)
+        for blk in blocks:
+            blk.form_R()                                     # R = A S (:325-327)
+        norm, lits, lreason = minimizer.solve(blocks)        # LSQR + x = S alpha (:331-352)
+        res.hist.append(norm)
+        res.lsqr_its.append(lits)
+        res.lsqr_reason.append(lreason)
+        res.inner_its.append(its_outer)
+        res.outer_its += 1
+        if monitor:
+            monitor(res.outer_its, norm, its_outer, lits)
+        if norm <= max(atol, rtol * res.norm0):              # (:342)
+            break
+        if res.outer_its >= max_outer:
+            break
+    comm.barrier()
+    res.elapsed = time.perf_counter() - t0
+    res.final_norm = math.sqrt(comm.ordered_sum(blocks, [blk.block_residual_sq() for blk in blocks]))
+    res.error = math.sqrt(comm.ordered_sum(blocks, [blk.error_sq() for blk in blocks]))
+    return res
+
+
 def make_blocks(ctx: Context, dim, nx, ny, nz, nb, block_ids, opts: Options | None, comm):
     return [GpuBlock(ctx, block_layout(dim, nx, ny, nz, nb, b), opts, comm) for b in block_ids]
+
+
+def make_smsm(ctx: Context, dim, nx, ny, nz, nb, block_ids, s: int, opts: Options | None, comm):
+    """GpuBlocks with the minimization storage, and the GpuMinimizer over them."""
+    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, block_ids, opts, comm)
+    for blk in blocks:
+        blk.setup_minimization(s)
+    return blocks, GpuMinimizer(ctx, blocks, comm, opts)

@@ -16,7 +16,7 @@ from typing import Iterable, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import KspOpts, MsplitError, call
+from ._lib import KspOpts, LsqrOpts, MsplitError, call
 
 PETSC_ERR_SUP = 56
 PETSC_ERR_ARG_WRONG = 62
@@ -287,6 +287,18 @@ class Mat:
         call("msp_mat_create_box_stencil", ctx.h, int(dim), int(nx), int(ny), int(nz), C.byref(h))
         return cls(ctx, h)
 
+    @classmethod
+    def box_stencil_ext(cls, ctx: Context, dim: int, nx: int, ny: int, nz: int, lo: bool, hi: bool) -> "Mat":
+        """Block rows with their coupling to the neighbour plane below/above kept as
+        extra columns ([plane below | own | plane above]): the operator of R = A S."""
+        h = C.c_void_p()
+        call("msp_mat_create_box_stencil_ext", ctx.h, int(dim), int(nx), int(ny), int(nz), 1 if lo else 0,
+             1 if hi else 0, C.byref(h))
+        return cls(ctx, h)
+
+    def mat_mult_dense(self, S: "DenseMat", R: "DenseMat"):        # MatMatMult(A, S, MAT_REUSE_MATRIX, &R)
+        call("msp_mat_matmult_dense", self.h, S.h, R.h)
+
     def get_csr(self):
         rp = np.empty(self.shape[0] + 1, np.int32)
         cl = np.empty(max(self.nnz, 1), np.int32)
@@ -306,6 +318,235 @@ class Mat:
     def destroy(self):
         if getattr(self, "h", None) and self.h.value:
             call("msp_mat_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ----------------------------------------------------------------------- dense
+class DenseMat:
+    """Rows of a MATDENSE matrix in HBM, column-major (create_matrix_dense,
+    utils.c:123-137, + MatZeroEntries)."""
+
+    def __init__(self, ctx: Context, nrows: int, ncols: int):
+        self.ctx = ctx
+        h = C.c_void_p()
+        call("msp_dense_create", ctx.h, int(nrows), int(ncols), C.byref(h))
+        self.h = h
+        self.shape = (int(nrows), int(ncols))
+        lda = C.c_int64()
+        call("msp_dense_get_info", h, None, None, C.byref(lda))
+        self.lda = lda.value
+
+    @classmethod
+    def from_array(cls, ctx: Context, a) -> "DenseMat":
+        a = np.asfortranarray(a, np.float64)
+        M = cls(ctx, a.shape[0], a.shape[1])
+        M.set_values(a)
+        return M
+
+    def set_values(self, a):
+        a = np.asfortranarray(a, np.float64)
+        if a.shape != self.shape:
+            raise MsplitError(60, f"dense values of shape {a.shape}, expected {self.shape}")
+        call("msp_dense_set_values", self.h, _dp(a), max(self.shape[0], 1))
+
+    def get_values(self) -> np.ndarray:
+        a = np.zeros(self.shape, order="F")
+        call("msp_dense_get_values", self.h, _dp(a), max(self.shape[0], 1))
+        return a
+
+    def zero_entries(self):                                          # MatZeroEntries
+        call("msp_dense_zero_entries", self.h)
+
+    def set_column(self, j: int, row0: int, x: Vec, xoff: int = 0, n: int | None = None):
+        """MatSetValuesLocal(S, n rows from row0, 1, &j, x[xoff:xoff+n])."""
+        n = x.n - xoff if n is None else n
+        call("msp_dense_set_column", self.h, int(j), int(row0), x.h, int(xoff), int(n))
+
+    def mult(self, alpha: Vec, y: Vec, row0: int = 0, n: int | None = None, yoff: int = 0):   # MatMult
+        n = self.shape[0] - row0 if n is None else n
+        call("msp_dense_mult", self.h, alpha.h, int(row0), int(n), y.h, int(yoff))
+
+    def mult_transpose(self, u: Vec, out: Vec):                      # MatMultTranspose (local rows)
+        call("msp_dense_mult_transpose", self.h, u.h, out.h)
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_dense_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------ comm
+class Comm:
+    """Cross-process all-gather used by the distributed LSQR (msp_comm)."""
+
+    def __init__(self, h: C.c_void_p, keep=None):
+        self.h = h
+        self._keep = keep
+        n, r = C.c_int32(), C.c_int32()
+        call("msp_comm_get_size", h, C.byref(n), C.byref(r))
+        self.size, self.rank = n.value, r.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+        call("msp_comm_get_unique_id", buf)
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, ctx: Context, nranks: int, rank: int, uid: bytes) -> "Comm":
+        buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        call("msp_comm_create_rccl", ctx.h, int(nranks), int(rank), buf, C.byref(h))
+        return cls(h)
+
+    @classmethod
+    def host(cls, ctx: Context, nranks: int, rank: int, allgather) -> "Comm":
+        """allgather(send: np.ndarray) -> np.ndarray of nranks*len(send) values."""
+        def cb(_user, send, recv, count):
+            try:
+                a = np.ctypeslib.as_array(send, shape=(count,)).copy()
+                out = np.asarray(allgather(a), np.float64).reshape(-1)
+                np.ctypeslib.as_array(recv, shape=(count * nranks,))[:] = out
+                return 0
+            except Exception:  # reported through the C error path
+                return 1
+        fn = _lib.ALLGATHER_FN(cb)
+        h = C.c_void_p()
+        call("msp_comm_create_host", ctx.h, int(nranks), int(rank), fn, None, C.byref(h))
+        return cls(h, keep=fn)
+
+    def allgather(self, send: Vec, recv: Vec, count: int):
+        call("msp_comm_allgather", self.h, send.h, recv.h, int(count))
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_comm_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------ LSQR
+class LSQR:
+    """KSPLSQR with PCNONE over row blocks of a dense operator (the reference's
+    outer solver, outer_solver_norm_equation utils.c:1061-1078; options
+    running_bulk_test_g5k:247-248)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        h = C.c_void_p()
+        call("msp_lsqr_create", ctx.h, C.byref(h))
+        self.h = h
+        self.prefix = ""
+        self._R = []
+        self._comm = None
+
+    def get_opts(self) -> LsqrOpts:
+        o = LsqrOpts()
+        call("msp_lsqr_get_opts", self.h, C.byref(o))
+        return o
+
+    def _set(self, **kw):
+        o = self.get_opts()
+        for k, v in kw.items():
+            setattr(o, k, v)
+        call("msp_lsqr_set_opts", self.h, C.byref(o))
+
+    def set_options_prefix(self, prefix: str | None):
+        self.prefix = prefix or ""
+
+    def set_tolerances(self, rtol=None, abstol=None, divtol=None, max_it=None):
+        kw = {}
+        if rtol is not None:
+            kw["rtol"] = float(rtol)
+        if abstol is not None:
+            kw["abstol"] = float(abstol)
+        if divtol is not None:
+            kw["divtol"] = float(divtol)
+        if max_it is not None:
+            kw["max_it"] = int(max_it)
+        self._set(**kw)
+
+    def set_from_options(self, opts: Options):                      # KSPSetFromOptions
+        p = self.prefix
+        kt = opts.get_string("ksp_type", "lsqr", p)
+        if kt.lower() != "lsqr":
+            raise MsplitError(PETSC_ERR_SUP, f"-{p}ksp_type {kt}: the outer solver on the MI355X path is lsqr")
+        pt = opts.get_string("pc_type", "none", p)
+        if pt.lower() != "none":
+            raise MsplitError(PETSC_ERR_SUP, f"-{p}pc_type {pt}: only none is implemented on the MI355X path")
+        nt = opts.get_string("ksp_norm_type", "unpreconditioned", p).lower()
+        if nt not in ("unpreconditioned", "none"):
+            raise MsplitError(PETSC_ERR_SUP, f"-{p}ksp_norm_type {nt} not supported by LSQR")
+        o = self.get_opts()
+        o.max_it = opts.get_int("ksp_max_it", o.max_it, p)
+        o.rtol = opts.get_real("ksp_rtol", o.rtol, p)
+        o.abstol = opts.get_real("ksp_atol", o.abstol, p)
+        o.divtol = opts.get_real("ksp_divtol", o.divtol, p)
+        if opts.has("ksp_lsqr_exact_mat_norm", p):
+            o.exact_norm = 1 if opts.get_bool("ksp_lsqr_exact_mat_norm", True, p) else 0
+        ct = opts.get_string("ksp_convergence_test", None, p)
+        if ct is not None:
+            if ct.lower() not in _lib.LSQR_CONV:
+                raise MsplitError(PETSC_ERR_ARG_WRONG, f"-{p}ksp_convergence_test {ct}")
+            o.conv_test = _lib.LSQR_CONV[ct.lower()]
+        call("msp_lsqr_set_opts", self.h, C.byref(o))
+
+    def set_operators(self, R: Sequence[DenseMat]):                 # KSPSetOperators(outer_ksp, R, R)
+        self._R = list(R)
+        arr = (C.c_void_p * len(self._R))(*[M.h.value for M in self._R])
+        call("msp_lsqr_set_operators", self.h, len(self._R), arr)
+
+    def set_comm(self, comm: Comm | None):
+        self._comm = comm
+        call("msp_lsqr_set_comm", self.h, comm.h if comm else None)
+
+    def solve(self, b: Sequence[Vec], x: Vec):                      # KSPSolve(outer_ksp, b, alpha)
+        arr = (C.c_void_p * len(b))(*[v.h.value for v in b])
+        call("msp_lsqr_solve", self.h, arr, x.h)
+
+    def get_iteration_number(self) -> int:
+        v = C.c_int32()
+        call("msp_lsqr_get_iteration_number", self.h, C.byref(v))
+        return v.value
+
+    def get_residual_norm(self) -> float:
+        v = C.c_double()
+        call("msp_lsqr_get_residual_norm", self.h, C.byref(v))
+        return v.value
+
+    def get_converged_reason(self) -> int:
+        v = C.c_int32()
+        call("msp_lsqr_get_converged_reason", self.h, C.byref(v))
+        return v.value
+
+    def get_norms(self):                                            # KSPLSQRGetNorms
+        a, b = C.c_double(), C.c_double()
+        call("msp_lsqr_get_norms", self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def get_residual_history(self) -> np.ndarray:
+        p = C.POINTER(C.c_double)()
+        n = C.c_int32()
+        call("msp_lsqr_get_residual_history", self.h, C.byref(p), C.byref(n))
+        return np.ctypeslib.as_array(p, shape=(n.value,)).copy() if n.value else np.zeros(0)
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_lsqr_destroy", C.byref(self.h))
 
     def __del__(self):
         try:

@@ -13,7 +13,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .petsc import KSP, Context, Mat, Options, Vec
+from .petsc import KSP, LSQR, Context, Mat, Options, Vec
 
 
 # ------------------------------------------------------------------ dimensions
@@ -192,6 +192,16 @@ def initializeKSP(ctx: Context, A: Mat, zero_initial_guess: bool, ksp_prefix: st
     ksp.set_operators(A)
     ksp.set_options_prefix(ksp_prefix)
     ksp.set_initial_guess_nonzero(not zero_initial_guess)
+    ksp.set_from_options(opts or Options())
+    return ksp
+
+
+def initializeOuterKSP(ctx: Context, ksp_prefix: str | None, opts: Options | None) -> LSQR:
+    """initializeKSP(comm, &outer_ksp, NULL, .., PETSC_TRUE, "outer1_"/"outer2_", ..)
+    (SMSM-global.c:219): the outer least-squares solver, zero initial guess,
+    configured from the options database (-outer1_ksp_type lsqr ...)."""
+    ksp = LSQR(ctx)
+    ksp.set_options_prefix(ksp_prefix)
     ksp.set_from_options(opts or Options())
     return ksp
 

@@ -651,3 +651,365 @@ done:
   free(rhs); free(r); free(y); free(Abp); free(bbp);
   return rc;
 }
+
+/* ------------------------------------------------------------------------ */
+/* KSPLSQR [PETSc-ext], PCNONE, over a row-distributed dense operator         */
+/* ------------------------------------------------------------------------ */
+
+void orc_lsqr_default_opts(orc_lsqr_opts *o) {
+  o->max_it = 10000;
+  o->rtol = 1e-5;
+  o->abstol = 1e-50;
+  o->divtol = 1e4;
+  o->exact_norm = 0;
+  o->conv_test = ORC_LSQR_CONV_LSQR; /* KSPCreate_LSQR installs KSPLSQRConvergedDefault */
+  o->reduce_mode = ORC_REDUCE_SEQ;
+}
+
+typedef struct {
+  int nblk, s, mode;
+  const int64_t *n;
+} ls_layout;
+
+/* sum over all rows of x[b][i]*y[b][i] (x[b], y[b] stride 1) */
+static double ls_gdot(const ls_layout *L, const double *const *x, const double *const *y) {
+  if (L->mode == ORC_REDUCE_SEQ) {
+    double s = 0.0;
+    for (int b = 0; b < L->nblk; ++b)
+      for (int64_t i = 0; i < L->n[b]; ++i) s += x[b][i] * y[b][i];
+    return s;
+  }
+  double t = 0.0;
+  for (int b = 0; b < L->nblk; ++b) t += dbr_dot(L->n[b], x[b], y[b]);
+  return t;
+}
+
+/* MatMultTranspose(R, u, out): out[j] = column_j . u (reference dgemv 'T' per column) */
+static void ls_mult_transpose(const ls_layout *L, const double *const *R, const int64_t *lda,
+                              const double *const *u, double *out) {
+  const double **col = (const double **)malloc((size_t)L->nblk * sizeof(double *));
+  for (int j = 0; j < L->s; ++j) {
+    for (int b = 0; b < L->nblk; ++b) col[b] = R[b] + (int64_t)j * lda[b];
+    out[j] = ls_gdot(L, col, u);
+  }
+  free(col);
+}
+
+/* MatNorm(R, NORM_FROBENIUS).  SEQ: one sum of squares over the columns in
+ * order (each over all N rows), then sqrt -- PETSc calls BLAS dnrm2 here,
+ * whose scaled evaluation can differ in the last bits; the value only enters
+ * the KSPLSQRConvergedDefault threshold rtol*anorm*rnorm.  DBR: per block the
+ * column sums of squares (DBR) added in column order, then blocks in order. */
+static double ls_frobenius(const ls_layout *L, const double *const *R, const int64_t *lda) {
+  double t = 0.0;
+  if (L->mode == ORC_REDUCE_SEQ) {
+    for (int j = 0; j < L->s; ++j)
+      for (int b = 0; b < L->nblk; ++b) {
+        const double *c = R[b] + (int64_t)j * lda[b];
+        for (int64_t i = 0; i < L->n[b]; ++i) t += c[i] * c[i];
+      }
+    return sqrt(t);
+  }
+  for (int b = 0; b < L->nblk; ++b) {
+    double tb = 0.0;
+    for (int j = 0; j < L->s; ++j) {
+      const double *c = R[b] + (int64_t)j * lda[b];
+      tb += dbr_dot(L->n[b], c, c);
+    }
+    t += tb;
+  }
+  return sqrt(t);
+}
+
+void orc_dense_mult(int64_t n, int s, const double *S, int64_t lda, const double *alpha, double *y) {
+  for (int64_t i = 0; i < n; ++i) {
+    double acc = 0.0;
+    for (int j = 0; j < s; ++j) acc = acc + alpha[j] * S[i + (int64_t)j * lda];
+    y[i] = acc;
+  }
+}
+
+/* VecNorm of an s-vector (one rank holds it whole: sequential) */
+static double ls_snorm(int s, const double *v) {
+  double t = 0.0;
+  for (int j = 0; j < s; ++j) t += v[j] * v[j];
+  return sqrt(t);
+}
+
+/* VecScale(v, a): a == 0 sets, a == 1 leaves v alone */
+static void ls_scale(int64_t n, double *v, double a) {
+  if (a == 0.0) {
+    for (int64_t i = 0; i < n; ++i) v[i] = 0.0;
+  } else if (a != 1.0) {
+    for (int64_t i = 0; i < n; ++i) v[i] = v[i] * a;
+  }
+}
+
+/* VecAXPY(y, a, x): y = y + a*x, nothing when a == 0 */
+static void ls_axpy(int64_t n, double *y, double a, const double *x) {
+  if (a == 0.0) return;
+  for (int64_t i = 0; i < n; ++i) y[i] = y[i] + a * x[i];
+}
+
+/* VecAYPX(y, a, x): y = x + a*y (a == 0: copy, a == 1: y + x) */
+static void ls_aypx(int64_t n, double *y, double a, const double *x) {
+  if (a == 0.0) {
+    for (int64_t i = 0; i < n; ++i) y[i] = x[i];
+  } else if (a == 1.0) {
+    for (int64_t i = 0; i < n; ++i) y[i] = y[i] + x[i];
+  } else {
+    for (int64_t i = 0; i < n; ++i) y[i] = x[i] + a * y[i];
+  }
+}
+
+typedef struct {
+  const orc_lsqr_opts *o;
+  int reason, its, nhist, hist_cap;
+  double rnorm0, ttol, arnorm, anorm;
+  double *hist;
+} ls_state;
+
+/* KSPConvergedDefault (zero initial guess: rnorm0 = rnorm at n = 0), then for the
+ * "lsqr" test KSPLSQRConvergedDefault's normal-equation checks. */
+static void ls_converged(ls_state *k, int n, double rnorm) {
+  k->reason = ORC_CONVERGED_ITERATING;
+  if (k->o->conv_test == ORC_LSQR_CONV_SKIP) {
+    if (n >= k->o->max_it) k->reason = ORC_CONVERGED_ITS;
+    return;
+  }
+  if (n == 0) {
+    k->rnorm0 = rnorm;
+    k->ttol = PMAX(k->o->rtol * k->rnorm0, k->o->abstol);
+  }
+  if (is_bad(rnorm)) {
+    k->reason = ORC_DIVERGED_NANORINF;
+  } else if (rnorm <= k->ttol) {
+    k->reason = (rnorm < k->o->abstol) ? ORC_CONVERGED_ATOL : ORC_CONVERGED_RTOL;
+  } else if (rnorm >= k->o->divtol * k->rnorm0) {
+    k->reason = ORC_DIVERGED_DTOL;
+  }
+  if (k->o->conv_test != ORC_LSQR_CONV_LSQR || n == 0 || k->reason) return;
+  if (k->arnorm < k->o->abstol) k->reason = ORC_CONVERGED_ATOL_NORMAL;
+  else if (k->arnorm < k->o->rtol * k->anorm * rnorm) k->reason = ORC_CONVERGED_RTOL_NORMAL;
+}
+
+static void ls_log(ls_state *k, double r) {
+  if (k->hist && k->nhist < k->hist_cap) k->hist[k->nhist] = r;
+  k->nhist++;
+}
+
+/* KSPSolve(outer_ksp, b, x) -> KSPSolve_LSQR [PETSc-ext] with PCNONE and a zero guess
+ * (outer_solver_norm_equation, utils.c:1061-1078). */
+int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R, const int64_t *lda,
+                   const double *const *rhs, double *x, const orc_lsqr_opts *o, orc_lsqr_result *res,
+                   double *hist, int hist_cap) {
+  if (nblk < 1 || s < 1 || !o) return ORC_ERR_ARG;
+  ls_layout L = {nblk, s, o->reduce_mode, nrows};
+  ls_state k;
+  memset(&k, 0, sizeof(k));
+  k.o = o;
+  k.hist = hist;
+  k.hist_cap = hist_cap;
+  int64_t ntot = 0;
+  for (int b = 0; b < nblk; ++b) ntot += nrows[b];
+  double *ubuf = (double *)calloc((size_t)(2 * ntot + 2), sizeof(double));
+  double *sbuf = (double *)calloc((size_t)(4 * s), sizeof(double));
+  double **U = (double **)malloc((size_t)nblk * sizeof(double *));
+  double **U1 = (double **)malloc((size_t)nblk * sizeof(double *));
+  if (!ubuf || !sbuf || !U || !U1) {
+    free(ubuf); free(sbuf); free(U); free(U1);
+    return ORC_ERR_MEM;
+  }
+  int64_t off = 0;
+  for (int b = 0; b < nblk; off += nrows[b], ++b) {
+    U[b] = ubuf + off;
+    U1[b] = ubuf + ntot + off;
+  }
+  double *V = sbuf, *V1 = sbuf + s, *W = sbuf + 2 * s;
+  double rnorm = 0.0, beta, alpha;
+  for (int j = 0; j < s; ++j) x[j] = 0.0; /* zero initial guess */
+
+  /* u <- b (x is 0) */
+  for (int b = 0; b < nblk; ++b) memcpy(U[b], rhs[b], (size_t)nrows[b] * sizeof(double));
+  rnorm = sqrt(ls_gdot(&L, (const double *const *)U, (const double *const *)U));
+  if (is_bad(rnorm)) { /* KSPCheckNorm */
+    k.reason = ORC_DIVERGED_NANORINF;
+    goto out;
+  }
+  k.its = 0;
+  ls_log(&k, rnorm);
+  ls_converged(&k, 0, rnorm);
+  if (k.reason) goto out;
+
+  beta = rnorm;
+  for (int b = 0; b < nblk; ++b) ls_scale(nrows[b], U[b], 1.0 / beta);
+  ls_mult_transpose(&L, R, lda, (const double *const *)U, V);
+  alpha = ls_snorm(s, V);
+  ls_scale(s, V, 1.0 / alpha);
+  memcpy(W, V, (size_t)s * sizeof(double));
+  k.anorm = o->exact_norm ? ls_frobenius(&L, R, lda) : 0.0;
+  k.arnorm = alpha * beta;
+  double phibar = beta, rhobar = alpha;
+  int i = 0;
+  do {
+    /* U1 = R V - alpha U */
+    for (int b = 0; b < nblk; ++b) orc_dense_mult(nrows[b], s, R[b], lda[b], V, U1[b]);
+    for (int b = 0; b < nblk; ++b) ls_axpy(nrows[b], U1[b], -alpha, U[b]);
+    beta = sqrt(ls_gdot(&L, (const double *const *)U1, (const double *const *)U1));
+    if (is_bad(beta)) {
+      k.reason = ORC_DIVERGED_NANORINF;
+      break;
+    }
+    if (beta > 0.0) {
+      for (int b = 0; b < nblk; ++b) ls_scale(nrows[b], U1[b], 1.0 / beta);
+      if (!o->exact_norm) k.anorm = sqrt(k.anorm * k.anorm + alpha * alpha + beta * beta);
+    }
+    /* V1 = R^T U1 - beta V */
+    ls_mult_transpose(&L, R, lda, (const double *const *)U1, V1);
+    ls_axpy(s, V1, -beta, V);
+    alpha = ls_snorm(s, V1);
+    if (is_bad(alpha)) {
+      k.reason = ORC_DIVERGED_NANORINF;
+      break;
+    }
+    ls_scale(s, V1, 1.0 / alpha);
+    const double rho = sqrt(rhobar * rhobar + beta * beta);
+    const double c = rhobar / rho;
+    const double sn = beta / rho;
+    const double theta = sn * alpha;
+    rhobar = -c * alpha;
+    const double phi = c * phibar;
+    phibar = sn * phibar;
+    const double tau = sn * phi;
+    ls_axpy(s, x, phi / rho, W);        /* x <- x + (phi/rho) w */
+    ls_aypx(s, W, -theta / rho, V1);    /* w <- v1 - (theta/rho) w */
+    k.arnorm = alpha * fabs(tau);
+    rnorm = phibar;
+    k.its++;
+    ls_log(&k, rnorm);
+    ls_converged(&k, i + 1, rnorm);
+    if (k.reason) break;
+    double **t = U; U = U1; U1 = t;     /* SWAP(U1, U), SWAP(V1, V) */
+    double *tv = V; V = V1; V1 = tv;
+    i++;
+  } while (i < o->max_it);
+  if (i >= o->max_it && !k.reason) k.reason = ORC_DIVERGED_ITS;
+out:
+  if (res) {
+    res->its = k.its;
+    res->reason = k.reason;
+    res->rnorm = rnorm;
+    res->arnorm = k.arnorm;
+    res->anorm = k.anorm;
+    res->nhist = k.nhist;
+  }
+  free(ubuf); free(sbuf);
+  free(U);
+  free(U1);
+  return ORC_OK;
+}
+
+/* Synchronous multisplitting with synchronous global minimization (SMSM-global),
+ * src/synchronous-multisplitting-synchronous-minimization-global/
+ * synchronous-multisplitting-synchronous-minimization-global.c, setup :134-284,
+ * loop :288-363, generalised to nb blocks:
+ *   s times: rhs_i = b_i - A_ij x_j (updateLocalRHS, utils.c:943), inner GMRES
+ *            (inner_solver, utils.c:950), exchange, S(:, k) = x           (:295-319)
+ *   R = A S (MatMatMult of the block rows with S, PETSc AIJ x DENSE:
+ *            per row, columns ascending, from 0)                           (:325-327)
+ *   alpha = LSQR(R, b), x = S alpha (outer_solver_norm_equation)           (:331-333)
+ *   stop when the LSQR residual norm <= max(atol, rtol * ||b||)            (:342-347)
+ *   every block takes x = S alpha (scatter of x_minimized)                 (:349-352) */
+int orc_smsm_solve(const orc_smsm_problem *p, const orc_gmres_opts *inner, const orc_lsqr_opts *outer,
+                   orc_smsm_result *res, double *outer_hist, int outer_cap, int *lsqr_its,
+                   int *lsqr_reason, int *inner_its, double *x_out) {
+  const int nb = p->nb, s = p->s;
+  if (nb < 1 || s < 1 || (p->dim != 2 && p->dim != 3)) return ORC_ERR_ARG;
+  if (p->dim == 3 && p->nz % nb) return ORC_ERR_ARG;
+  if (p->dim == 2 && ((int64_t)p->nx * p->ny) % nb) return ORC_ERR_ARG;
+  orc_sm_problem sp = {p->dim, p->nx, p->ny, p->nz, nb, p->rtol, p->atol, p->max_outer};
+  const int64_t N = (int64_t)p->nx * p->ny * (p->dim == 3 ? p->nz : 1);
+  const int mode = inner->reduce_mode;
+  orc_csr *Ab = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
+  orc_csr *Aii = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
+  orc_csr *Aoff = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
+  int64_t *r0 = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
+  int64_t *r1 = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
+  int64_t *nrow = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
+  int64_t *ldab = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
+  double *x = (double *)calloc((size_t)N, sizeof(double));
+  double *u = (double *)malloc((size_t)N * sizeof(double));
+  double *bvec = (double *)calloc((size_t)N, sizeof(double));
+  double *rhs = (double *)calloc((size_t)N, sizeof(double));
+  double *y = (double *)calloc((size_t)N, sizeof(double));
+  double *S = (double *)calloc((size_t)(N * s), sizeof(double));
+  double *Rm = (double *)calloc((size_t)(N * s), sizeof(double));
+  double *alpha = (double *)calloc((size_t)s, sizeof(double));
+  const orc_csr **Abp = (const orc_csr **)calloc((size_t)nb, sizeof(orc_csr *));
+  const double **bbp = (const double **)calloc((size_t)nb, sizeof(double *));
+  const double **Rp = (const double **)calloc((size_t)nb, sizeof(double *));
+  int rc = ORC_OK;
+  if (!Ab || !Aii || !Aoff || !r0 || !r1 || !nrow || !ldab || !x || !u || !bvec || !rhs || !y || !S || !Rm ||
+      !alpha || !Abp || !bbp || !Rp) {
+    rc = ORC_ERR_MEM;
+    goto done;
+  }
+  for (int64_t i = 0; i < N; ++i) u[i] = 1.0;
+  for (int b = 0; b < nb; ++b) {
+    if ((rc = build_block(&sp, b, &Ab[b], &r0[b], &r1[b]))) goto done;
+    if ((rc = orc_split(&Ab[b], r0[b], r1[b], &Aii[b], &Aoff[b]))) goto done;
+    orc_spmv(&Ab[b], u, bvec + r0[b]); /* computeTheRightHandSideWithInitialGuess */
+    Abp[b] = &Ab[b];
+    bbp[b] = bvec + r0[b];
+    Rp[b] = Rm + r0[b];
+    nrow[b] = r1[b] - r0[b];
+    ldab[b] = N;
+  }
+  const double norm0 = orc_final_residual_norm(mode, nb, Abp, x, bbp); /* :280 */
+  orc_gmres_opts io = *inner;
+  io.guess_nonzero = 1;
+  io.uirnorm = 1;
+  int outer_it = 0;
+  int64_t total_inner = 0;
+  for (;;) {
+    for (int k = 0; k < s; ++k) {
+      for (int b = 0; b < nb; ++b) orc_residual(&Aoff[b], bvec + r0[b], x, rhs + r0[b]);
+      for (int b = 0; b < nb; ++b) {
+        orc_gmres_result gr;
+        if ((rc = orc_gmres_solve(&Aii[b], rhs + r0[b], x + r0[b], &io, &gr, NULL, 0))) goto done;
+        if (inner_its && outer_it < outer_cap) inner_its[((int64_t)outer_it * s + k) * nb + b] = gr.its;
+        total_inner += gr.its;
+      }
+      memcpy(S + (int64_t)k * N, x, (size_t)N * sizeof(double)); /* MatSetValuesLocal(S, .., k, x) */
+    }
+    for (int b = 0; b < nb; ++b)
+      for (int k = 0; k < s; ++k) orc_spmv(&Ab[b], S + (int64_t)k * N, Rm + (int64_t)k * N + r0[b]);
+    orc_lsqr_result lr;
+    if ((rc = orc_lsqr_solve(nb, nrow, s, Rp, ldab, bbp, alpha, outer, &lr, NULL, 0))) goto done;
+    orc_dense_mult(N, s, S, N, alpha, x); /* x_minimized = S alpha */
+    const double norm = lr.rnorm;         /* KSPGetResidualNorm(outer_ksp) */
+    if (outer_it < outer_cap) {
+      if (outer_hist) outer_hist[outer_it] = norm;
+      if (lsqr_its) lsqr_its[outer_it] = lr.its;
+      if (lsqr_reason) lsqr_reason[outer_it] = lr.reason;
+    }
+    outer_it++;
+    if (norm <= PMAX(p->atol, p->rtol * norm0)) break;
+    if (p->max_outer > 0 && outer_it >= p->max_outer) break;
+  }
+  if (res) {
+    res->outer_its = outer_it;
+    res->norm0 = norm0;
+    res->final_norm = orc_final_residual_norm(mode, nb, Abp, x, bbp);
+    for (int64_t i = 0; i < N; ++i) y[i] = -1.0 * u[i] + x[i];
+    res->error = orc_norm2(mode, N, y);
+    res->total_inner_its = total_inner;
+  }
+  if (x_out) memcpy(x_out, x, (size_t)N * sizeof(double));
+done:
+  if (Ab)
+    for (int b = 0; b < nb; ++b) { orc_csr_free(&Ab[b]); orc_csr_free(&Aii[b]); orc_csr_free(&Aoff[b]); }
+  free(Ab); free(Aii); free(Aoff); free(r0); free(r1); free(nrow); free(ldab); free(x); free(u); free(bvec);
+  free(rhs); free(y); free(S); free(Rm); free(alpha); free(Abp); free(bbp); free(Rp);
+  return rc;
+}

@@ -18,6 +18,11 @@
  *   - updateLocalRHS      src/utils/utils.c:943-948
  *   - residual reduction  src/utils/utils.c:575-620
  *   - SM outer loop       src/synchronous-multisplitting/synchronous-multisplitting.c:155-206
+ *   - KSPSolve_LSQR / KSPLSQRConvergedDefault (PCNONE)      [PETSc-ext]
+ *   - MatMult / MatMultTranspose / MatNorm(FROBENIUS) of MATDENSE, MatMatMult(AIJ, DENSE) [PETSc-ext]
+ *   - outer_solver_norm_equation src/utils/utils.c:1061-1078
+ *   - SMSM-global loop    src/synchronous-multisplitting-synchronous-minimization-global/
+ *                         synchronous-multisplitting-synchronous-minimization-global.c:288-363
  *
  * Parity status: the assembly and the residual-norm helper are pinned by the
  * reference's own known-answer tests (src/tests/utils_test.c:38-228).  The
@@ -52,6 +57,9 @@ enum { ORC_REDUCE_SEQ = 0, ORC_REDUCE_DBR = 1 };
 /* KSPConvergedReason values (PETSc 3.22.1 include/petscksp.h) */
 enum {
   ORC_CONVERGED_ITERATING = 0,
+  ORC_CONVERGED_RTOL_NORMAL = 1,
+  ORC_CONVERGED_ITS = 4,
+  ORC_CONVERGED_ATOL_NORMAL = 9,
   ORC_CONVERGED_RTOL = 2,
   ORC_CONVERGED_ATOL = 3,
   ORC_CONVERGED_HAPPY_BREAKDOWN = 7,
@@ -143,6 +151,69 @@ typedef struct {
 
 int orc_sm_solve(const orc_sm_problem *p, const orc_gmres_opts *inner, orc_sm_result *res,
                  double *outer_hist, int outer_cap, int *inner_its, double *x_out);
+
+/* --- KSP LSQR (outer least-squares solver of the minimization variants) --- */
+/* The operator is a tall dense matrix R (N x s, column-major) held as nblk
+ * row blocks: block b has nrows[b] rows, leading dimension lda[b] and data
+ * R[b] (column j at R[b] + j*lda[b]).  The right-hand side is split the same
+ * way (rhs[b]).  Reductions over the N rows:
+ *   SEQ  one sequential sum over all N rows, block 0's rows first (the
+ *        reference: every block holds the whole R and runs the same solve);
+ *   DBR  DBR order inside each block, then the block sums added in block
+ *        order from 0.0 (the device order: block-local reduction + all-gather). */
+enum { ORC_LSQR_CONV_DEFAULT = 0, ORC_LSQR_CONV_LSQR = 1, ORC_LSQR_CONV_SKIP = 2 };
+
+typedef struct {
+  int max_it;         /* -ksp_max_it (10000) */
+  double rtol;        /* -ksp_rtol (1e-5) */
+  double abstol;      /* -ksp_atol (1e-50) */
+  double divtol;      /* -ksp_divtol (1e4) */
+  int exact_norm;     /* -ksp_lsqr_exact_mat_norm */
+  int conv_test;      /* -ksp_convergence_test: default | lsqr (KSPCreate_LSQR's choice) | skip */
+  int reduce_mode;    /* ORC_REDUCE_* */
+} orc_lsqr_opts;
+
+typedef struct {
+  int its;
+  int reason;
+  double rnorm;       /* ksp->rnorm = phibar (LSQR's estimate of ||b - R x||) */
+  double arnorm;      /* estimate of ||R^T (b - R x)|| */
+  double anorm;       /* Frobenius norm of R (exact or estimated) */
+  int nhist;
+} orc_lsqr_result;
+
+void orc_lsqr_default_opts(orc_lsqr_opts *o);
+/* KSPSolve(outer_ksp, b, x) with a zero initial guess; x has s entries. */
+int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R, const int64_t *lda,
+                   const double *const *rhs, double *x, const orc_lsqr_opts *o, orc_lsqr_result *res,
+                   double *hist, int hist_cap);
+/* MatMult(S, alpha, y) of a column-major dense block: y[i] = sum_j S[i + j*lda] alpha[j]
+ * (reference dgemv 'N': per row, columns in order, starting from 0). */
+void orc_dense_mult(int64_t n, int s, const double *S, int64_t lda, const double *alpha, double *y);
+
+/* --- SMSM, global minimization ------------------------------------------- */
+typedef struct {
+  int dim, nx, ny, nz, nb;
+  int s;              /* -s: inner solves (basis vectors) per minimization */
+  double rtol;        /* -rtol (outer) */
+  double atol;        /* 1e-100 (SMSM-global.c:33) */
+  int max_outer;      /* safety cap */
+} orc_smsm_problem;
+
+typedef struct {
+  int outer_its;
+  double norm0;       /* global_norm_0 = ||b|| (x = 0) */
+  double final_norm;  /* computeFinalResidualNorm of the last minimized iterate */
+  double error;       /* ||x - u||_2 */
+  int64_t total_inner_its;
+} orc_smsm_result;
+
+/* outer_hist[k]   : the outer LSQR residual norm of outer iteration k (the stop test's norm)
+ * lsqr_its[k]     : its, lsqr_reason[k]: reason of that LSQR solve (may be NULL)
+ * inner_its       : outer_cap * s * nb ints, [k][j][b] (may be NULL) */
+int orc_smsm_solve(const orc_smsm_problem *p, const orc_gmres_opts *inner, const orc_lsqr_opts *outer,
+                   orc_smsm_result *res, double *outer_hist, int outer_cap, int *lsqr_its,
+                   int *lsqr_reason, int *inner_its, double *x_out);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,8 @@ REDUCE_DBR = 1
 DBR_CHUNK = 256 * 2 * 8
 
 REASONS = {
-    0: "CONVERGED_ITERATING", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
+    0: "CONVERGED_ITERATING", 1: "CONVERGED_RTOL_NORMAL", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
+    4: "CONVERGED_ITS", 9: "CONVERGED_ATOL_NORMAL",
     7: "CONVERGED_HAPPY_BREAKDOWN", -2: "DIVERGED_NULL", -3: "DIVERGED_ITS",
     -4: "DIVERGED_DTOL", -5: "DIVERGED_BREAKDOWN", -9: "DIVERGED_NANORINF",
 }
@@ -53,6 +54,23 @@ class SMResult(C.Structure):
     _fields_ = [("outer_its", C.c_int), ("norm0", C.c_double), ("final_norm", C.c_double),
                 ("error", C.c_double), ("total_inner_its", C.c_int64)]
 
+
+class LsqrOpts(C.Structure):
+    _fields_ = [("max_it", C.c_int), ("rtol", C.c_double), ("abstol", C.c_double), ("divtol", C.c_double),
+                ("exact_norm", C.c_int), ("conv_test", C.c_int), ("reduce_mode", C.c_int)]
+
+
+class LsqrResult(C.Structure):
+    _fields_ = [("its", C.c_int), ("reason", C.c_int), ("rnorm", C.c_double), ("arnorm", C.c_double),
+                ("anorm", C.c_double), ("nhist", C.c_int)]
+
+
+class SMSMProblem(C.Structure):
+    _fields_ = [("dim", C.c_int), ("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("nb", C.c_int),
+                ("s", C.c_int), ("rtol", C.c_double), ("atol", C.c_double), ("max_outer", C.c_int)]
+
+
+CONV_DEFAULT, CONV_LSQR, CONV_SKIP = 0, 1, 2
 
 _lib = None
 
@@ -89,6 +107,12 @@ def lib() -> C.CDLL:
         L.orc_final_residual_norm.argtypes = [C.c_int, C.c_int, P(P(CSR)), dp, P(dp)]
         L.orc_final_residual_norm.restype = C.c_double
         L.orc_sm_solve.argtypes = [P(SMProblem), P(GmresOpts), P(SMResult), dp, C.c_int, P(C.c_int), dp]
+        L.orc_lsqr_default_opts.argtypes = [P(LsqrOpts)]
+        L.orc_lsqr_solve.argtypes = [C.c_int, P(C.c_int64), C.c_int, P(dp), P(C.c_int64), P(dp), dp,
+                                     P(LsqrOpts), P(LsqrResult), dp, C.c_int]
+        L.orc_dense_mult.argtypes = [C.c_int64, C.c_int, dp, C.c_int64, dp, dp]
+        L.orc_smsm_solve.argtypes = [P(SMSMProblem), P(GmresOpts), P(LsqrOpts), P(SMResult), dp, C.c_int,
+                                     P(C.c_int), P(C.c_int), P(C.c_int), dp]
         _lib = L
     return _lib
 
@@ -264,3 +288,67 @@ def sm_solve(dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_outer=1000
     return {"outer_its": n, "norm0": res.norm0, "final_norm": res.final_norm, "error": res.error,
             "total_inner_its": res.total_inner_its, "hist": hist[:min(n, cap)].copy(),
             "inner_its": its[:min(n, cap) * nb].reshape(-1, nb).copy(), "x": x}
+
+
+def lsqr_opts(**kw) -> LsqrOpts:
+    o = LsqrOpts()
+    lib().orc_lsqr_default_opts(C.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise KeyError(k)
+        setattr(o, k, v)
+    return o
+
+
+def lsqr(R_blocks, b_blocks, hist_cap=None, **opts):
+    """KSPSolve with KSPLSQR semantics (zero guess, PCNONE) over a dense operator
+    given as row blocks (each an (n_b, s) array).  Returns (x, result-dict)."""
+    o = lsqr_opts(**opts)
+    P = C.POINTER
+    Rs = [np.asfortranarray(R, np.float64) for R in R_blocks]
+    bs = [np.ascontiguousarray(b, np.float64) for b in b_blocks]
+    s = Rs[0].shape[1]
+    nb = len(Rs)
+    nrows = (C.c_int64 * nb)(*[R.shape[0] for R in Rs])
+    lda = (C.c_int64 * nb)(*[max(R.shape[0], 1) for R in Rs])
+    Rarr = (P(C.c_double) * nb)(*[_dp(R) for R in Rs])
+    barr = (P(C.c_double) * nb)(*[_dp(b) for b in bs])
+    x = np.zeros(s)
+    cap = hist_cap if hist_cap is not None else o.max_it + 2
+    hist = np.zeros(max(cap, 1))
+    r = LsqrResult()
+    _check(lib().orc_lsqr_solve(nb, nrows, s, Rarr, lda, barr, _dp(x), C.byref(o), C.byref(r), _dp(hist), cap),
+           "orc_lsqr_solve")
+    return x, {"its": r.its, "reason": r.reason, "rnorm": r.rnorm, "arnorm": r.arnorm, "anorm": r.anorm,
+               "hist": hist[:min(r.nhist, cap)].copy()}
+
+
+def dense_mult(S, alpha) -> np.ndarray:
+    S = np.asfortranarray(S, np.float64)
+    a = np.ascontiguousarray(alpha, np.float64)
+    y = np.zeros(S.shape[0])
+    lib().orc_dense_mult(S.shape[0], S.shape[1], _dp(S), max(S.shape[0], 1), _dp(a), _dp(y))
+    return y
+
+
+def smsm_solve(dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000):
+    """SMSM with global minimization over nb blocks (see oracle.h).  Returns a dict."""
+    p = SMSMProblem(dim, nx, ny, nz if dim == 3 else 1, nb, s, rtol, atol, max_outer)
+    io = gmres_opts(**inner)
+    oo = lsqr_opts(**outer)
+    res = SMResult()
+    cap = max_outer
+    hist = np.zeros(cap)
+    lits = np.zeros(cap, np.int32)
+    lreason = np.zeros(cap, np.int32)
+    its = np.zeros(cap * s * nb, np.int32)
+    N = nx * ny * (nz if dim == 3 else 1)
+    x = np.zeros(N)
+    ip = C.POINTER(C.c_int)
+    _check(lib().orc_smsm_solve(C.byref(p), C.byref(io), C.byref(oo), C.byref(res), _dp(hist), cap,
+                                lits.ctypes.data_as(ip), lreason.ctypes.data_as(ip), its.ctypes.data_as(ip),
+                                _dp(x)), "orc_smsm_solve")
+    n = min(res.outer_its, cap)
+    return {"outer_its": res.outer_its, "norm0": res.norm0, "final_norm": res.final_norm, "error": res.error,
+            "total_inner_its": res.total_inner_its, "hist": hist[:n].copy(), "lsqr_its": lits[:n].copy(),
+            "lsqr_reason": lreason[:n].copy(), "inner_its": its[:n * s * nb].reshape(n, s, nb).copy(), "x": x}

@@ -271,3 +271,139 @@ def gmres(rowptr, col, val, b, x0=None, restart=30, max_it=10000, rtol=1e-5, abs
             break
         guess_zero = False
     return np.array(x), {"its": st["its"], "reason": st["reason"], "rnorm": st["rnorm"], "hist": np.array(hist)}
+
+
+def lsqr(R, b, max_it=10000, rtol=1e-5, abstol=1e-50, divtol=1e4, exact_norm=False, conv_test="lsqr"):
+    """KSPSolve_LSQR [PETSc-ext], PCNONE, zero initial guess, sequential sums:
+    R is a list of rows (each a list of s floats), b a list.  Returns (x, its,
+    reason, rnorm, hist).  Plain Python floats, one statement per PETSc Vec op."""
+    m, s = len(R), len(R[0])
+    hist = []
+
+    def gemv(v):                      # MatMult: per row, columns in order, from 0
+        out = []
+        for i in range(m):
+            acc = 0.0
+            for j in range(s):
+                acc = acc + v[j] * R[i][j]
+            out.append(acc)
+        return out
+
+    def gemvt(u):                     # MatMultTranspose: per column, rows in order
+        out = []
+        for j in range(s):
+            acc = 0.0
+            for i in range(m):
+                acc += R[i][j] * u[i]
+            out.append(acc)
+        return out
+
+    def nrm(v):
+        acc = 0.0
+        for a in v:
+            acc += a * a
+        return math.sqrt(acc)
+
+    def scale(v, a):                  # VecScale special cases
+        if a == 0.0:
+            return [0.0] * len(v)
+        return v if a == 1.0 else [t * a for t in v]
+
+    def axpy(y, a, x):                # VecAXPY, returns early for a == 0
+        return y if a == 0.0 else [yi + a * xi for yi, xi in zip(y, x)]
+
+    def aypx(y, a, x):                # VecAYPX special cases
+        if a == 0.0:
+            return list(x)
+        if a == 1.0:
+            return [yi + xi for yi, xi in zip(y, x)]
+        return [xi + a * yi for yi, xi in zip(y, x)]
+
+    state = {"rnorm0": 0.0, "ttol": 0.0}
+
+    def converged(n, rn, arnorm, anorm):
+        if conv_test == "skip":
+            return 4 if n >= max_it else 0
+        if n == 0:
+            state["rnorm0"] = rn
+            state["ttol"] = max(rtol * rn, abstol)
+        if math.isnan(rn) or math.isinf(rn):
+            return -9
+        if rn <= state["ttol"]:
+            return 3 if rn < abstol else 2
+        if rn >= divtol * state["rnorm0"]:
+            return -4
+        if conv_test != "lsqr" or n == 0:
+            return 0
+        if arnorm < abstol:
+            return 9
+        if arnorm < rtol * anorm * rn:
+            return 1
+        return 0
+
+    x = [0.0] * s
+    u = list(b)
+    rnorm = nrm(u)
+    if math.isnan(rnorm) or math.isinf(rnorm):
+        return x, 0, -9, rnorm, hist
+    hist.append(rnorm)
+    reason = converged(0, rnorm, 0.0, 0.0)
+    if reason:
+        return x, 0, reason, rnorm, hist
+    beta = rnorm
+    u = scale(u, 1.0 / beta)
+    v = gemvt(u)
+    alpha = nrm(v)
+    v = scale(v, 1.0 / alpha)
+    w = list(v)
+    if exact_norm:
+        acc = 0.0
+        for j in range(s):
+            for i in range(m):
+                acc += R[i][j] * R[i][j]
+        anorm = math.sqrt(acc)
+    else:
+        anorm = 0.0
+    arnorm = alpha * beta
+    phibar, rhobar = beta, alpha
+    its = 0
+    i = 0
+    while True:
+        u1 = axpy(gemv(v), -alpha, u)
+        beta = nrm(u1)
+        if math.isnan(beta) or math.isinf(beta):
+            reason = -9
+            break
+        if beta > 0.0:
+            u1 = scale(u1, 1.0 / beta)
+            if not exact_norm:
+                anorm = math.sqrt(anorm * anorm + alpha * alpha + beta * beta)
+        v1 = axpy(gemvt(u1), -beta, v)
+        alpha = nrm(v1)
+        if math.isnan(alpha) or math.isinf(alpha):
+            reason = -9
+            break
+        v1 = scale(v1, 1.0 / alpha)
+        rho = math.sqrt(rhobar * rhobar + beta * beta)
+        c, sn = rhobar / rho, beta / rho
+        theta = sn * alpha
+        rhobar = -c * alpha
+        phi = c * phibar
+        phibar = sn * phibar
+        tau = sn * phi
+        x = axpy(x, phi / rho, w)
+        w = aypx(w, -theta / rho, v1)
+        arnorm = alpha * abs(tau)
+        rnorm = phibar
+        its += 1
+        hist.append(rnorm)
+        reason = converged(i + 1, rnorm, arnorm, anorm)
+        if reason:
+            break
+        u, v = u1, v1
+        i += 1
+        if i >= max_it:
+            break
+    if i >= max_it and not reason:
+        reason = -3
+    return x, its, reason, rnorm, hist

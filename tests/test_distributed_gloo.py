@@ -79,9 +79,89 @@ class OracleBlock:
         ln = self.po.norm2(self.A.residual(self.rhs, self.x), self.po.REDUCE_DBR)
         return ln * ln
 
+    # -- SMSM-global hooks (same arithmetic as oracle.smsm_solve)
+    def setup_minimization(self, s):
+        L = self.layout
+        self.s = s
+        self.lo = L.plane if L.b > 0 else 0
+        self.hi = L.plane if L.b < L.nb - 1 else 0
+        if L.dim == 3:
+            ppb = L.nz // L.nb
+            Ab = self.po.poisson3d_rows(L.nx, L.ny, L.nz, L.b * ppb, (L.b + 1) * ppb)
+        else:
+            Ab = self.po.poisson2d_rows(L.nx, L.ny, L.r0, L.r1)
+        rp, c, v = Ab.arrays()
+        ne = self.lo + L.nrows + self.hi
+        self.A_ext = self.po.Mat.from_arrays(L.nrows, ne, rp, c - (L.r0 - self.lo), v)
+        self.S = np.zeros((ne, s), order="F")
+        self.R = np.zeros((L.nrows, s), order="F")
+
+    def store_column(self, k):
+        n = self.layout.nrows
+        self.S[self.lo:self.lo + n, k] = self.x
+        self.S[:self.lo, k] = self.halo[:self.lo]
+        self.S[self.lo + n:, k] = self.halo[self.lo:self.lo + self.hi]
+
+    def form_R(self):
+        for k in range(self.s):
+            self.R[:, k] = self.A_ext.mult(np.ascontiguousarray(self.S[:, k]))
+
+    def apply_alpha(self, alpha):
+        n = self.layout.nrows
+        xe = self.po.dense_mult(self.S, alpha)
+        self.x = xe[self.lo:self.lo + n].copy()
+        self.halo = np.concatenate([xe[:self.lo], xe[self.lo + n:]])
+
+    def block_residual_sq(self):
+        n = self.layout.nrows
+        xe = np.concatenate([self.halo[:self.lo], self.x, self.halo[self.lo:]])
+        ln = self.po.norm2(self.A_ext.residual(self.b, xe), self.po.REDUCE_DBR)
+        return ln * ln
+
     def error_sq(self):
         e = self.po.norm2(self.x - 1.0, self.po.REDUCE_DBR)
         return e * e
+
+
+class OracleMinimizer:
+    """Test double of multisplitting.GpuMinimizer: every rank gathers all
+    blocks' rows of R and b and runs the oracle's block-ordered LSQR."""
+
+    def __init__(self, po, outer):
+        self.po = po
+        self.outer = outer
+
+    def solve(self, blocks):
+        (blk,) = blocks
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, (blk.R, blk.b))
+        alpha, r = self.po.lsqr([p[0] for p in parts], [p[1] for p in parts], reduce_mode=self.po.REDUCE_DBR,
+                                **self.outer)
+        blk.apply_alpha(alpha)
+        return r["rnorm"], r["its"], r["reason"]
+
+
+OUTER = dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
+
+
+def _smsm_worker(rank, world, port, problem, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import smsm_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        dim, nx, ny, nz, s, rtol = problem
+        blk = OracleBlock(block_layout(dim, nx, ny, nz, world, rank), po)
+        blk.setup_minimization(s)
+        comm = TorchComm()
+        res = smsm_solve([blk], comm, s, OracleMinimizer(po, OUTER), rtol=rtol, max_outer=100)
+        q.put((rank, res.outer_its, res.norm0, list(res.hist), [[k[0] for k in o] for o in res.inner_its],
+               list(res.lsqr_its), res.final_norm, blk.x))
+    finally:
+        dist.destroy_process_group()
 
 
 def _worker(rank, world, port, problem, q):
@@ -110,11 +190,11 @@ def _free_port():
     return p
 
 
-def _run(world, problem):
+def _run(world, problem, target=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, problem, q)) for r in range(world)]
+    procs = [ctx.Process(target=target or _worker, args=(r, world, port, problem, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=600) for _ in range(world)]
@@ -145,3 +225,20 @@ def test_sm_four_ranks_gloo_matches_oracle(oracle):
     assert all(o[1] == ref["outer_its"] for o in out)
     assert np.array_equal(np.array(out[0][3]), ref["hist"])
     assert np.array_equal(np.concatenate([o[5] for o in out]), ref["x"])
+
+
+@pytest.mark.parametrize("world,problem", [(2, (2, 32, 32, 1, 4, 1e-6)), (2, (3, 8, 8, 8, 4, 1e-6)),
+                                           (4, (3, 6, 6, 8, 3, 1e-6))])
+def test_smsm_gloo_matches_oracle(oracle, world, problem):
+    dim, nx, ny, nz, s, rtol = problem
+    out = _run(world, problem, _smsm_worker)
+    ref = oracle.smsm_solve(dim, nx, ny, nz, world, s, rtol, dict(INNER, reduce_mode=oracle.REDUCE_DBR),
+                            dict(OUTER, reduce_mode=oracle.REDUCE_DBR), max_outer=100)
+    for rank, outer, norm0, hist, its, lits, fnorm, x in out:
+        assert outer == ref["outer_its"]
+        assert norm0 == ref["norm0"]
+        assert np.array_equal(np.array(hist), ref["hist"])
+        assert np.array_equal(np.array(its), ref["inner_its"][:, :, rank])
+        assert np.array_equal(np.array(lits), ref["lsqr_its"])
+        assert fnorm == ref["final_norm"]
+    assert np.array_equal(np.concatenate([o[7] for o in out]), ref["x"])
