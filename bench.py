@@ -5,11 +5,17 @@ N = 1 : configs[1] -- 3D 7-pt Poisson 256^3, single-block GMRES(30), pc none,
         one step = one KSPSolve from x0 = 0 with the canonical options
         (running_bulk_test_g5k:64-70: rtol 1e-4, unpreconditioned norm) and a
         fixed max_it = 300 (10 restart cycles).
-N > 1 : synchronous multisplitting, weak scaling: one 256^3 z-slab block per
-        GPU (global 256 x 256 x 256N); one step = one outer iteration
-        (inner GMRES(30) max_it 300 on every block, RCCL boundary-plane
-        exchange, right-hand-side update, residual norm all-gather).
-value = sum over blocks of (rows x GMRES iterations) / max-over-ranks time.
+N > 1 : SMSM with global minimization (configs[2], BASELINE "SMSM 2 blocks on
+        2 MI355X"), weak scaling: one 512 x 512 x 256 z-slab block per GPU
+        (global 512 x 512 x 256N; N = 2 is the 512^3 two-block case).  One
+        step = one outer iteration of SMSM-global.c:288-363 with the campaign
+        options of running_bulk_test_g5k:230-248: s = 20 inner solves
+        (GMRES(30), max_it 20, rtol 1e-20, warm started, RCCL boundary-plane
+        exchange after each), S(:,k) = x, R = A S, LSQR (max_it 70,
+        rtol 1e-15, exact Frobenius norm; block partials all-gathered over
+        RCCL) and x = S alpha.  (--variant sm: plain synchronous
+        multisplitting instead; --variant smsm also runs on one GPU.)
+value = sum over blocks of (rows x inner GMRES iterations) / max-over-ranks time.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]   (N > 1 under
 torch.distributed.run, one rank per GPU, RCCL = backend "nccl").
@@ -30,7 +36,9 @@ METRIC = "DOF-updates/s on 3D 7-pt Poisson GMRES; achieved HBM GB/s vs peak, 1/2
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 KERNEL_NAMES = {"spmv": "k_spmv_lds (CSR MatMult/MatResidual)", "mdot": "k_dot_stage1+2 (VecMDot, DBR)",
                 "maxpy": "k_maxpy (VecMAXPY, CGS update + BuildSoln)", "norm": "k_dot_stage1<1,self>+stage2 (VecNorm)",
-                "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy"}
+                "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy",
+                "spmm": "k_spmm (MatMatMult R = A S)", "dgemv": "k_dense_gemv (LSQR R v - alpha u + norm; S alpha)",
+                "dgemvt": "k_scaled_dot (LSQR scale + R^T u)"}
 
 
 def parse():
@@ -47,6 +55,13 @@ def parse():
     p.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="N>1 exchange backend: nccl (= RCCL, the product) or gloo (single-GPU rehearsal)")
+    p.add_argument("--variant", default=None, choices=["gmres", "sm", "smsm"],
+                   help="gmres (N=1 default), smsm (N>1 default), sm")
+    p.add_argument("--smsm-mesh", type=int, default=512, help="SMSM: nx = ny")
+    p.add_argument("--smsm-planes", type=int, default=256, help="SMSM: z-planes per GPU block")
+    p.add_argument("--s", type=int, default=20, help="SMSM: inner solves per minimization (-s)")
+    p.add_argument("--inner-max-it", type=int, default=20)
+    p.add_argument("--outer-max-it", type=int, default=70)
     return p.parse_args()
 
 
@@ -98,8 +113,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
-    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import GpuBlock
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm, TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import GpuBlock, GpuMinimizer
     from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Context, Mat, Options, Vec
     from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
 
@@ -109,8 +124,11 @@ def main():
     kspopts = (f"-ksp_type gmres -ksp_gmres_restart {args.restart} -pc_type none -ksp_norm_type unpreconditioned "
                f"-ksp_rtol {args.rtol} -ksp_max_it {args.max_it}")
     rows = n * n * n
+    variant = args.variant or ("gmres" if world == 1 else "smsm")
+    if variant == "gmres" and world > 1:
+        raise SystemExit("--variant gmres is the single-GPU workload")
 
-    if world == 1:
+    if variant == "gmres":
         # configs[1]: single-block GMRES(30) on 256^3 (gmres_solution.c:50-70 in 3D)
         A = Mat.box_stencil(ctx, 3, n, n, n)
         ones = Vec(ctx, rows)
@@ -128,7 +146,7 @@ def main():
             ksp.solve(b, x)                     # zero initial guess: x is reset by KSPSolve
             return ksp.get_iteration_number()
         workload = f"3D 7-pt Poisson {n}^3, single-block GMRES({args.restart}) on 1 MI355X (configs[1])"
-    else:
+    elif variant == "sm":
         comm = TorchComm(device=torch.device("cuda", dev) if args.backend == "nccl" else torch.device("cpu"))
         L = block_layout(3, n, n, n * world, world, rank)
         o = Options(kspopts)
@@ -147,6 +165,45 @@ def main():
         workload = (f"3D 7-pt Poisson {n}x{n}x{n * world} synchronous multisplitting, {world} z-slab blocks of "
                     f"{n}^3 (one per MI355X), inner GMRES({args.restart}) max_it {args.max_it}, "
                     f"{'RCCL' if args.backend == 'nccl' else 'gloo (rehearsal)'} halo exchange")
+    else:
+        # configs[2]: SMSM-global (SMSM-global.c:288-363), options of running_bulk_test_g5k:230-248
+        if world > 1:
+            comm = TorchComm(device=torch.device("cuda", dev) if args.backend == "nccl" else torch.device("cpu"))
+        else:
+            comm = LocalComm()
+        n = args.smsm_mesh
+        nz = args.smsm_planes * world
+        rows = n * n * args.smsm_planes
+        kspopts = (f"-inner1_ksp_type gmres -inner1_ksp_gmres_restart {args.restart} -inner1_ksp_atol 1e-100 "
+                   f"-inner1_ksp_max_it {args.inner_max_it} -inner1_ksp_rtol 1e-20 -inner1_pc_type none "
+                   f"-inner1_ksp_norm_type UNPRECONDITIONED "
+                   f"-outer1_ksp_type lsqr -outer1_ksp_convergence_test default -outer1_ksp_lsqr_exact_mat_norm "
+                   f"-outer1_ksp_atol 1e-100 -outer1_ksp_max_it {args.outer_max_it} -outer1_ksp_rtol 1e-15 "
+                   f"-outer1_pc_type none -outer1_ksp_norm_type UNPRECONDITIONED -s {args.s}")
+        o = Options(kspopts)
+        L = block_layout(3, n, n, nz, world, rank)
+        blk = GpuBlock(ctx, L, o, comm, prefix="inner1_")
+        blk.setup_minimization(args.s)
+        mini = GpuMinimizer(ctx, [blk], comm, o, prefix="outer1_")
+        blk.reset_halo()
+        lsqr_its = []
+
+        def step():
+            its = 0
+            for k in range(args.s):
+                blk.update_rhs()                # updateLocalRHS
+                its += blk.solve()              # inner_solver
+                comm.exchange([blk])            # comm_sync_send_and_receive
+                blk.store_column(k)             # S(:, k) = x
+            blk.form_R()                        # R = A S
+            _, lits, _ = mini.solve([blk])      # LSQR, x = S alpha
+            lsqr_its.append(lits)
+            return its
+        workload = (f"3D 7-pt Poisson {n}x{n}x{nz} SMSM-global, {world} z-slab block(s) of {n}x{n}x{args.smsm_planes} "
+                    f"(one per MI355X), s = {args.s} inner GMRES({args.restart}) solves of max_it {args.inner_max_it} "
+                    f"per outer iteration, LSQR max_it {args.outer_max_it}; "
+                    f"{'RCCL' if world > 1 and args.backend == 'nccl' else ('gloo (rehearsal)' if world > 1 else 'single block')} "
+                    f"exchange and all-gathers (configs[2] at N = 2)")
 
     def barrier():
         if world > 1:
@@ -185,9 +242,12 @@ def main():
                "warmup": args.warmup, "ms_per_step": 1e3 * elapsed_max / args.steps, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic: b = A*1 (exact solution u = 1), x0 = 0; device-assembled operator",
-               "config": {"workload": workload, "mesh_per_gpu": [n, n, n], "blocks": world,
+               "config": {"workload": workload, "variant": variant,
+                          "mesh_per_gpu": [n, n, rows // (n * n)], "blocks": world,
                           "ksp": kspopts, "gmres_iterations_per_step_per_block": its_total / args.steps,
                           "parallelism": f"{world} z-slab block(s), one per GPU"}}
+        if variant == "smsm":
+            out["config"]["lsqr_iterations_per_step"] = lsqr_its[-args.steps:]
         if stats:
             total_ms = sum(s["ms"] for s in stats.values())
             dom = max(stats, key=lambda k: stats[k]["ms"])
@@ -207,7 +267,7 @@ def main():
                                   "share": v["ms"] / total_ms if total_ms else None} for k, v in stats.items()}
             alg_bytes = sum(v["bytes"] for v in stats.values())
             out["hbm_alg_GBps_whole_step"] = alg_bytes / (elapsed / 1) / 1e9
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and variant == "gmres" and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, args.restart, args.cpu_sample_its, args.rtol)
         else:
             out["cpu_baseline"] = None

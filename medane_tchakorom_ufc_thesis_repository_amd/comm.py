@@ -135,21 +135,25 @@ class TorchComm:
         self.dist.barrier(group=self.group)
 
     def lsqr_comm(self, ctx):
-        """The all-gather of LSQR's block partials (petsc.Comm): an RCCL
-        communicator of its own for "nccl" (id broadcast over this group),
-        a host callback over this group's all_gather for "gloo"."""
+        """The all-gather of LSQR's block partials (petsc.Comm): with "nccl" an
+        RCCL communicator of its own (id broadcast over this group), enqueued
+        on the context's stream; with "gloo" (or MSPLIT_LSQR_TRANSPORT=host) a
+        host callback over this group's all_gather."""
+        import os
         from .petsc import Comm
         if self.world == 1:
             return None
-        if self.backend == "nccl":
+        transport = os.environ.get("MSPLIT_LSQR_TRANSPORT", "rccl" if self.backend == "nccl" else "host")
+        if transport == "rccl":
             obj = [Comm.unique_id() if self.rank == 0 else None]
             self.dist.broadcast_object_list(obj, src=0, group=self.group)
             return Comm.rccl(ctx, self.world, self.rank, obj[0])
         torch, dist, world, group = self.torch, self.dist, self.world, self.group
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
 
         def allgather(a):
-            t = torch.from_numpy(a)
-            outs = [torch.zeros_like(t) for _ in range(world)]
-            dist.all_gather(outs, t, group=group)
-            return torch.cat(outs).numpy()
+            t = torch.from_numpy(a).to(dev)
+            out = torch.empty(world * t.numel(), dtype=t.dtype, device=dev)
+            dist.all_gather_into_tensor(out, t, group=group)
+            return out.cpu().numpy()
         return Comm.host(ctx, self.world, self.rank, allgather)

@@ -138,11 +138,6 @@ extern "C" int msp_comm_get_size(const msp_comm* m, int32_t* nranks, int32_t* ra
 extern "C" int mspi_comm_allgather(msp_comm* m, const double* send, double* recv, int64_t count) {
   msp_ctx* c = m->ctx;
   if (count <= 0) return MSP_SUCCESS;
-  if (m->nranks == 1) {
-    if (recv != send) HIPCHK(hipMemcpyAsync(recv, send, (size_t)count * sizeof(double), hipMemcpyDeviceToDevice,
-                                            c->stream));
-    return MSP_SUCCESS;
-  }
   if (m->kind == COMM_RCCL) {
     NCCLCHK(rccl().all_gather(send, recv, (size_t)count, ncclDouble, m->nccl, c->stream));
     return MSP_SUCCESS;

@@ -181,3 +181,30 @@ def test_smsm_gpu_bitwise_vs_oracle(ctx, oracle, dim, nx, ny, nz, nb, s, rtol):
     assert np.array_equal(x, ro["x"])
     assert res.final_norm == ro["final_norm"]
     assert res.error == pytest.approx(ro["error"], rel=1e-12)   # per-block vs global DBR of ||x - u||
+
+
+@pytest.mark.parametrize("transport", ["rccl", "host"])
+def test_lsqr_through_comm_single_rank(ctx, oracle, transport):
+    """The cross-rank path of the LSQR (all-gather of block partials) on one
+    rank: an RCCL communicator (ncclAllGather on the context's stream) or the
+    host-callback transport must leave the result bitwise unchanged."""
+    R = RNG.standard_normal((6000, 9))
+    b = RNG.standard_normal(6000)
+    Rs, bs = [R[:2500], R[2500:]], [b[:2500], b[2500:]]
+    if transport == "rccl":
+        comm = Comm.rccl(ctx, 1, 0, Comm.unique_id())
+    else:
+        comm = Comm.host(ctx, 1, 0, lambda a: a)
+    l = LSQR(ctx)
+    l._set(max_it=30, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
+    Ds = [DenseMat.from_array(ctx, M) for M in Rs]
+    l.set_operators(Ds)
+    l.set_comm(comm)
+    x = Vec(ctx, 9)
+    l.solve([Vec.from_array(ctx, v) for v in bs], x)
+    xo, ro = oracle.lsqr(Rs, bs, reduce_mode=oracle.REDUCE_DBR, max_it=30, rtol=1e-15, abstol=1e-100,
+                         exact_norm=1, conv_test=0)
+    assert np.array_equal(x.get_array(), xo)
+    assert np.array_equal(l.get_residual_history(), ro["hist"])
+    l.destroy()
+    comm.destroy()
