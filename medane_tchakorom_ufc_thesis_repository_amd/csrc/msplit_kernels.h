@@ -25,11 +25,12 @@ struct Coefs {
 enum { MSK_SPMV_MULT = 0, MSK_SPMV_RESID = 1, MSK_SPMV_SCALED = 2 };
 
 // tuning flags
-enum { MSK_TUNE_MDOT_REV = 1, MSK_TUNE_SPMV_NT = 2 };
+enum { MSK_TUNE_MDOT_REV = 1, MSK_TUNE_SPMV_NT = 2, MSK_TUNE_SPMV_XCD = 4, MSK_TUNE_SPMV_STAGE1 = 8 };
 
 extern "C" {
 void msk_set_tuning(int flags);
 int msk_get_tuning(void);
+void msk_set_spmv_group(int gb);
 // DBR stage 1 over nv <= 32 vectors (self: ||w||^2).  stop: device flag, skip when set (may be null).
 int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks, int self,
                    const int* stop, hipStream_t s);
@@ -40,9 +41,10 @@ int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, cons
                     const double* adev, int negate, int64_t n, int accum, double* partial, const int* stop,
                     hipStream_t s);
 // mode MULT: y = A x; RESID: y = b - A x; SCALED: sc = *sdev, vout = sc*x (own rows), y = A (sc*x).
+// plane > 0: the operator is a stencil with this many rows per plane (XCD-aware schedule, MSK_TUNE_SPMV_XCD)
 int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
              const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
-             const int* stop, hipStream_t s);
+             const int* stop, int64_t plane, hipStream_t s);
 int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int32_t* rowptr, const int32_t* col,
                   const double* val, const double* x, const double* b, double* y, int resid, hipStream_t s);
 // lo/hi: extra coupling columns to the neighbour plane below/above (column space [lo | block | hi])

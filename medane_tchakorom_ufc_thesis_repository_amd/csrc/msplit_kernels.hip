@@ -13,6 +13,7 @@
 // the speculatively enqueued iterations return at once.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "msplit_kernels.h"
@@ -291,19 +292,43 @@ __global__ __launch_bounds__(kT) void k_maxpy_chunk(const double* win, double* w
 //   SCALED (VecNormalize fused into the next MatMult): sc = *sdev,
 //     vout[r] = x[r]*sc and y = A (sc*x), each product val*(x*sc) rounded
 //     exactly as VecScale followed by MatMult.
-template <int MODE, bool NT>
+// XCD-aware order (stencil operators whose plane is a multiple of 8 row
+// blocks): workgroups are dealt round-robin over the 8 XCDs, so XCD x runs
+// launches x, x+8, ...  Each plane's row blocks are cut into groups of gb
+// blocks; XCD x sweeps its groups (x, x+8, ...) through all planes, plane by
+// plane.  A row block's x-gathers at +-1 plane then hit lines its own XCD read
+// gb blocks earlier (~gb*256 rows of traffic ago, inside the 4 MiB L2), and
+// +-1 line stays inside the group.  Only the schedule changes: every row's sum
+// is the same, so results are bitwise unchanged.
+struct XcdMap {
+  int32_t bp;  // row blocks per plane (0: identity order)
+  int32_t gb;  // row blocks per group, (bp / gb) % 8 == 0
+  int32_t np;  // planes
+};
+
+__device__ __forceinline__ int32_t row_block(XcdMap m) {
+  const int32_t i = blockIdx.x;
+  if (m.bp == 0) return i;
+  const int32_t xcd = i & 7, j = i >> 3;
+  const int32_t span = m.np * m.gb;  // blocks of one group over all planes
+  const int32_t q = j / span, rem = j - q * span;
+  const int32_t k = rem / m.gb, t = rem - k * m.gb;
+  return k * m.bp + (xcd + 8 * q) * m.gb + t;
+}
+
+template <int MODE, bool NT, int SU>
 __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col, const double* __restrict__ val,
                                                   const double* __restrict__ x, const double* __restrict__ b,
                                                   double* __restrict__ y, int32_t lds_cap,
                                                   const double* __restrict__ sdev, double* __restrict__ vout,
-                                                  const int* __restrict__ stop) {
+                                                  const int* __restrict__ stop, XcdMap xm) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* sval = reinterpret_cast<double*>(smem);
   int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
   const int t = threadIdx.x;
-  const int32_t r0 = blockIdx.x * kT;
+  const int32_t r0 = row_block(xm) * kT;
   const int32_t r1 = min(r0 + kT, nrows);
   const int32_t start = rowptr[r0], end = rowptr[r1];
   const int32_t s2 = start & ~1, s4 = start & ~3;
@@ -320,8 +345,41 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
     if (MODE == MSK_SPMV_RESID) bb = b[r];
     if (MODE == MSK_SPMV_SCALED) vout[r] = x[r] * sc;
   }
-  for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = NT ? ld_nt(v2 + i) : v2[i];
-  for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = NT ? ld_nt(c4 + i) : c4[i];
+  if constexpr (SU == 1) {
+    for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = NT ? ld_nt(v2 + i) : v2[i];
+    for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = NT ? ld_nt(c4 + i) : c4[i];
+  } else {
+    // issue SU val and SU/2 col loads per lane before the first LDS write, so a
+    // workgroup's staging costs one memory latency instead of one per slice
+    for (int32_t i0 = t; i0 < n2 || i0 < n4; i0 += SU * kT) {
+      double2 vt[SU];
+      int4 ct[SU / 2 > 0 ? SU / 2 : 1];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int32_t i = i0 + u * kT;
+        if (i < n2) vt[u] = NT ? ld_nt(v2 + i) : v2[i];
+      }
+#pragma unroll
+      for (int u = 0; u < SU / 2; ++u) {
+        const int32_t i = i0 + u * kT;
+        if (i < n4) ct[u] = NT ? ld_nt(c4 + i) : c4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int32_t i = i0 + u * kT;
+        if (i < n2) reinterpret_cast<double2*>(sval)[i] = vt[u];
+      }
+#pragma unroll
+      for (int u = 0; u < SU / 2; ++u) {
+        const int32_t i = i0 + u * kT;
+        if (i < n4) reinterpret_cast<int4*>(scol)[i] = ct[u];
+      }
+      if (i0 + (SU / 2) * kT < n4) {  // col slices beyond SU/2 (rows longer than ~8 entries)
+        for (int32_t i = i0 + (SU / 2) * kT; i < n4 && i < i0 + SU * kT; i += kT)
+          reinterpret_cast<int4*>(scol)[i] = NT ? ld_nt(c4 + i) : c4[i];
+      }
+    }
+  }
   __syncthreads();
   if (r < r1) {
     double s = 0.0;
@@ -462,8 +520,22 @@ using namespace msk;
 
 // Tuning flags (A/B experiments; MSPLIT_TUNING at context creation).
 static int g_tuning = 0;
+static int g_spmv_gb = 0;  // XCD group size override (0: auto)
 extern "C" void msk_set_tuning(int flags) { g_tuning = flags; }
 extern "C" int msk_get_tuning(void) { return g_tuning; }
+extern "C" void msk_set_spmv_group(int gb) { g_spmv_gb = gb; }
+
+static XcdMap xcd_map(int32_t nrows, int64_t plane) {
+  XcdMap m = {0, 0, 0};
+  if (!(g_tuning & MSK_TUNE_SPMV_XCD) || plane <= 0 || plane % kT || nrows % plane) return m;
+  const int32_t bp = (int32_t)(plane / kT);
+  int32_t gb = g_spmv_gb > 0 ? g_spmv_gb : std::min(bp / 8, 64);
+  if (gb <= 0 || bp % gb || (bp / gb) % 8) return m;
+  m.bp = bp;
+  m.gb = gb;
+  m.np = (int32_t)(nrows / plane);
+  return m;
+}
 
 static inline int grid_for(int64_t work, int cap) {
   int64_t g = (work + kT - 1) / kT;
@@ -516,14 +588,22 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
 
 extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
                         const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
-                        const int* stop, hipStream_t s) {
+                        const int* stop, int64_t plane, hipStream_t s) {
   if (nrows <= 0) return 0;
   const unsigned g = (unsigned)((nrows + kT - 1) / kT);
   const size_t lds = (size_t)lds_cap * 12;
+  const XcdMap xm = xcd_map(nrows, plane);
   if (lds_cap > 0) {
     const bool nt = (g_tuning & MSK_TUNE_SPMV_NT) != 0;
-#define LAUNCH_LDS8(M, NTF) \
-  k_spmv_lds8<M, NTF><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev, vout, stop)
+#define LAUNCH_LDS8(M, NTF)                                                                                   \
+  do {                                                                                                         \
+    if (g_tuning & MSK_TUNE_SPMV_STAGE1)                                                                       \
+      k_spmv_lds8<M, NTF, 1><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,   \
+                                                             vout, stop, xm);                                  \
+    else                                                                                                       \
+      k_spmv_lds8<M, NTF, 4><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,   \
+                                                             vout, stop, xm);                                  \
+  } while (0)
     if (mode == MSK_SPMV_RESID) { if (nt) LAUNCH_LDS8(MSK_SPMV_RESID, true); else LAUNCH_LDS8(MSK_SPMV_RESID, false); }
     else if (mode == MSK_SPMV_SCALED) { if (nt) LAUNCH_LDS8(MSK_SPMV_SCALED, true); else LAUNCH_LDS8(MSK_SPMV_SCALED, false); }
     else { if (nt) LAUNCH_LDS8(MSK_SPMV_MULT, true); else LAUNCH_LDS8(MSK_SPMV_MULT, false); }

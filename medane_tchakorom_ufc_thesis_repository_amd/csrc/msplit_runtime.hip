@@ -324,6 +324,7 @@ struct msp_mat {
   double* val = nullptr;      // nnz (+2 pad)
   int32_t lds_cap = 0;        // LDS entries per 256-row block (0: direct kernel)
   bool compressed = false;
+  int64_t plane = 0;          // rows per stencil plane (box-stencil operators), 0 otherwise
   int32_t nlisted = 0;
   int32_t* row_ids = nullptr;
 };
@@ -470,6 +471,7 @@ extern "C" int msp_mat_create_box_stencil_ext(msp_ctx* c, int dim, int32_t nx, i
   nnz += (lo + hi) * plane;
   A->nnz = nnz;
   A->lds_cap = lds_cap_for(deg * 256);
+  A->plane = dim == 3 ? plane : 0;
   int rc = mat_alloc(c, A, nrows + 1, nnz);
   if (rc) {
     msp_mat_destroy(&A);
@@ -540,7 +542,7 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
     return MSP_SUCCESS;
   }
   KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, b, y, A->lds_cap, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT,
-                nullptr, nullptr, nullptr, c->stream));
+                nullptr, nullptr, nullptr, A->plane, c->stream));
   return MSP_SUCCESS;
 }
 
@@ -558,7 +560,7 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
   }
   KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, false) + 8.0 * (double)A->nrows);
   KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, nullptr, y, A->lds_cap, MSK_SPMV_SCALED, sdev, vout, stop,
-                c->stream));
+                A->plane, c->stream));
   return MSP_SUCCESS;
 }
 

@@ -1,10 +1,11 @@
-"""Per-kernel HBM bandwidth of the hot-path kernels on 256^3-sized operands.
+"""Per-kernel HBM bandwidth of the hot-path kernels.
 
 Times each kernel class with the library's HIP-event timing, interleaving
-kernel variants (msk_set_variant) in one process so A/B deltas are not
-cross-process noise.  Prints one JSON object.
+tuning settings (msk_set_tuning flags, msk_set_spmv_group) in one process so
+A/B deltas are not cross-process noise.  Prints one JSON object.
 
-  python tools/microbench.py [--n 256] [--reps 20] [--rounds 3]
+  python tools/microbench.py [--n 256] [--nz 256] [--reps 20] [--rounds 3]
+         [--tunings 0,4] [--groups 0] [--kernels spmv,mdot,maxpy,lsqr]
 """
 from __future__ import annotations
 
@@ -20,28 +21,45 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--n", type=int, default=256, help="nx = ny")
+    ap.add_argument("--nz", type=int, default=None)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="spmv:0;maxpy:0,1;mdot:0")
+    ap.add_argument("--tunings", default="0")
+    ap.add_argument("--groups", default="0", help="SpMV XCD group sizes to sweep (0 = auto)")
+    ap.add_argument("--kernels", default="spmv,mdot,maxpy")
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401
     from medane_tchakorom_ufc_thesis_repository_amd import _lib
-    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Mat, Vec
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import LSQR, Context, DenseMat, Mat, Vec
     L = _lib.load()
-    L.msk_set_variant.argtypes = [ctypes.c_int, ctypes.c_int]
-    L.msk_set_variant.restype = None
-    which = {"spmv": 0, "mdot": 1, "maxpy": 2}
+    L.msk_set_tuning.argtypes = [ctypes.c_int]
+    L.msk_set_tuning.restype = None
+    L.msk_set_spmv_group.argtypes = [ctypes.c_int]
+    L.msk_set_spmv_group.restype = None
+    kernels = args.kernels.split(",")
+    tunings = [int(t) for t in args.tunings.split(",")]
+    groups = [int(g) for g in args.groups.split(",")]
 
     n = args.n
-    N = n ** 3
+    nz = args.nz or n
+    N = n * n * nz
     ctx = Context(0)
-    A = Mat.box_stencil(ctx, 3, n, n, n)
+    A = Mat.box_stencil(ctx, 3, n, n, nz)
     rng = np.random.default_rng(1)
-    V = [Vec.from_array(ctx, rng.uniform(-1, 1, N)) for _ in range(31)]
     w = Vec.from_array(ctx, rng.uniform(-1, 1, N))
     y = Vec(ctx, N)
+    V = [Vec.from_array(ctx, rng.uniform(-1, 1, N)) for _ in range(31)] if ("mdot" in kernels or "maxpy" in kernels) else []
+    if "lsqr" in kernels:
+        s = 20
+        R = DenseMat(ctx, N, s)
+        for j in range(s):
+            R.set_column(j, 0, w)
+        l = LSQR(ctx)
+        l._set(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
+        l.set_operators([R])
+        alpha = Vec(ctx, s)
 
     def timed(fn, cls):
         ctx.reset_kernel_stats()
@@ -49,34 +67,34 @@ def main():
         for _ in range(args.reps):
             fn()
         ctx.set_timing(False)
-        s = ctx.kernel_stats()[cls]
-        return s["bytes"] / (s["ms"] * 1e-3) / 1e9, s["ms"] / s["launches"] * 1e3
+        st = ctx.kernel_stats()
+        s = st[cls]
+        return s["bytes"] / (s["ms"] * 1e-3) / 1e9, s["ms"] / max(s["launches"], 1) * 1e3
 
     res = {}
-    variants = {}
-    for item in args.variants.split(";"):
-        k, vs = item.split(":")
-        variants[k] = [int(v) for v in vs.split(",")]
-    for rnd in range(args.rounds):
-        for v in variants.get("spmv", [0]):
-            L.msk_set_variant(which["spmv"], v)
-            gb, us = timed(lambda: A.mult(w, y), "spmv")
-            res.setdefault(f"spmv/v{v}", []).append((gb, us))
-        for v in variants.get("mdot", [0]):
-            L.msk_set_variant(which["mdot"], v)
-            for k in (1, 8, 16, 30):
-                gb, us = timed(lambda: w.mdot(V[:k]), "mdot")
-                res.setdefault(f"mdot{k}/v{v}", []).append((gb, us))
-        for v in variants.get("maxpy", [0]):
-            L.msk_set_variant(which["maxpy"], v)
-            for k in (1, 8, 16, 30):
-                a = np.full(k, 1e-300)
-                gb, us = timed(lambda: w.maxpy(a, V[:k]), "maxpy")
-                res.setdefault(f"maxpy{k}/v{v}", []).append((gb, us))
-        gb, us = timed(lambda: w.norm(), "norm")
-        res.setdefault("norm", []).append((gb, us))
-        gb, us = timed(lambda: w.scale(1.0000000001), "scale")
-        res.setdefault("scale", []).append((gb, us))
+    for _ in range(args.rounds):
+        for t in tunings:
+            L.msk_set_tuning(t)
+            for g in (groups if "spmv" in kernels else [0]):
+                L.msk_set_spmv_group(g)
+                if "spmv" in kernels:
+                    gb, us = timed(lambda: A.mult(w, y), "spmv")
+                    res.setdefault(f"spmv/t{t}/g{g}", []).append((gb, us))
+            L.msk_set_spmv_group(0)
+            if "mdot" in kernels:
+                for k in (1, 8, 16, 30):
+                    gb, us = timed(lambda: w.mdot(V[:k]), "mdot")
+                    res.setdefault(f"mdot{k}/t{t}", []).append((gb, us))
+            if "maxpy" in kernels:
+                for k in (1, 8, 16, 30):
+                    a = np.full(k, 1e-300)
+                    gb, us = timed(lambda: w.maxpy(a, V[:k]), "maxpy")
+                    res.setdefault(f"maxpy{k}/t{t}", []).append((gb, us))
+            if "lsqr" in kernels:
+                for cls in ("dgemv", "dgemvt"):
+                    gb, us = timed(lambda: l.solve([w], alpha), cls)
+                    res.setdefault(f"lsqr_{cls}/t{t}", []).append((gb, us))
+    L.msk_set_tuning(0)
     out = {k: {"GBps_median": float(np.median([g for g, _ in v])), "GBps_max": float(max(g for g, _ in v)),
                "us_median": float(np.median([u for _, u in v]))} for k, v in res.items()}
     print(json.dumps(out, indent=1))
