@@ -410,6 +410,10 @@ extern "C" int msp_mat_matmult_dense(msp_mat* A, const msp_dense* S, msp_dense* 
   if (nr == 0) return MSP_SUCCESS;
   KTimer kt(c, MSP_KERNEL_SPMM,
             12.0 * (double)v.nnz + 4.0 * (nr + 1.0) + 8.0 * (double)S->ncols * ((double)S->nrows + (double)nr));
+  if (v.lds_cap > 0) {  // CSR slice staged once per row block, columns streamed through it
+    KCHK(msk_spmm(nr, v.rowptr, v.col, v.val, S->d, S->lda, S->ncols, R->d, R->lda, v.lds_cap, c->stream));
+    return MSP_SUCCESS;
+  }
   const dim3 g((unsigned)((nr + kT - 1) / kT)), b(kT);
   for (int j0 = 0; j0 < S->ncols; j0 += 32) {
     const int nc = std::min(32, S->ncols - j0);

@@ -47,6 +47,7 @@ typedef struct {
   const double *val;
   int64_t nnz;
   int compressed;
+  int32_t lds_cap; /* LDS entries per 256-row block for the staged kernels (0: rows too long) */
 } mspi_csr_view;
 mspi_csr_view mspi_mat_csr(const msp_mat *A);
 

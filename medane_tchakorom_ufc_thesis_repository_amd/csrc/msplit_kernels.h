@@ -45,6 +45,9 @@ int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, cons
 int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
              const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
              const int* stop, int64_t plane, hipStream_t s);
+// R[:, 0:nc] = A S[:, 0:nc], column-major S (lds) and R (ldr); needs lds_cap > 0
+int msk_spmm(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* S,
+             int64_t lds, int nc, double* R, int64_t ldr, int32_t lds_cap, hipStream_t s);
 int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int32_t* rowptr, const int32_t* col,
                   const double* val, const double* x, const double* b, double* y, int resid, hipStream_t s);
 // lo/hi: extra coupling columns to the neighbour plane below/above (column space [lo | block | hi])

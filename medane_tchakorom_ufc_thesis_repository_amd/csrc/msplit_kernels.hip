@@ -134,7 +134,16 @@ __global__ __launch_bounds__(kT) void k_dot_stage2(const double* __restrict__ pa
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const double* p = partial + blockIdx.x * nchunks;
   double acc = 0.0;
-  for (int64_t i = t; i < nchunks; i += kT) acc = acc + p[i];
+  int64_t i = t;
+  // 8 loads in flight per lane, added in the same order (lane t: p[t], p[t+256], ...)
+  for (; i + 7 * kT < nchunks; i += 8 * kT) {
+    double q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) q[u] = p[i + u * kT];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = acc + q[u];
+  }
+  for (; i < nchunks; i += kT) acc = acc + p[i];
   acc = wave_butterfly(acc);
   if (lane == 0) red[wv] = acc;
   __syncthreads();
@@ -316,41 +325,16 @@ __device__ __forceinline__ int32_t row_block(XcdMap m) {
   return k * m.bp + (xcd + 8 * q) * m.gb + t;
 }
 
-template <int MODE, bool NT, int SU>
-__global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* __restrict__ rowptr,
-                                                  const int32_t* __restrict__ col, const double* __restrict__ val,
-                                                  const double* __restrict__ x, const double* __restrict__ b,
-                                                  double* __restrict__ y, int32_t lds_cap,
-                                                  const double* __restrict__ sdev, double* __restrict__ vout,
-                                                  const int* __restrict__ stop, XcdMap xm) {
-  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* sval = reinterpret_cast<double*>(smem);
-  int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
-  const int t = threadIdx.x;
-  const int32_t r0 = row_block(xm) * kT;
-  const int32_t r1 = min(r0 + kT, nrows);
-  const int32_t start = rowptr[r0], end = rowptr[r1];
-  const int32_t s2 = start & ~1, s4 = start & ~3;
-  const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
-  const double2* v2 = reinterpret_cast<const double2*>(val + s2);
-  const int4* c4 = reinterpret_cast<const int4*>(col + s4);
-  const int32_t r = r0 + t;
-  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
-  int32_t k0 = 0, k1 = 0;
-  double bb = 0.0;
-  if (r < r1) {
-    k0 = rowptr[r];
-    k1 = rowptr[r + 1];
-    if (MODE == MSK_SPMV_RESID) bb = b[r];
-    if (MODE == MSK_SPMV_SCALED) vout[r] = x[r] * sc;
-  }
+// Stage a row block's val/col slice (16-byte aligned-down views v2/c4 with n2/n4
+// slices) into LDS.  SU > 1: issue SU val and SU/2 col loads per lane before the
+// first LDS write, so staging costs one memory latency instead of one per slice.
+template <bool NT, int SU>
+__device__ __forceinline__ void stage_csr_block(int t, int32_t n2, int32_t n4, const double2* __restrict__ v2,
+                                                const int4* __restrict__ c4, double* sval, int32_t* scol) {
   if constexpr (SU == 1) {
     for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = NT ? ld_nt(v2 + i) : v2[i];
     for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = NT ? ld_nt(c4 + i) : c4[i];
   } else {
-    // issue SU val and SU/2 col loads per lane before the first LDS write, so a
-    // workgroup's staging costs one memory latency instead of one per slice
     for (int32_t i0 = t; i0 < n2 || i0 < n4; i0 += SU * kT) {
       double2 vt[SU];
       int4 ct[SU / 2 > 0 ? SU / 2 : 1];
@@ -380,6 +364,38 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
       }
     }
   }
+}
+
+template <int MODE, bool NT, int SU>
+__global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                  const double* __restrict__ x, const double* __restrict__ b,
+                                                  double* __restrict__ y, int32_t lds_cap,
+                                                  const double* __restrict__ sdev, double* __restrict__ vout,
+                                                  const int* __restrict__ stop, XcdMap xm) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sval = reinterpret_cast<double*>(smem);
+  int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
+  const int t = threadIdx.x;
+  const int32_t r0 = row_block(xm) * kT;
+  const int32_t r1 = min(r0 + kT, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s2 = start & ~1, s4 = start & ~3;
+  const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
+  const double2* v2 = reinterpret_cast<const double2*>(val + s2);
+  const int4* c4 = reinterpret_cast<const int4*>(col + s4);
+  const int32_t r = r0 + t;
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  int32_t k0 = 0, k1 = 0;
+  double bb = 0.0;
+  if (r < r1) {
+    k0 = rowptr[r];
+    k1 = rowptr[r + 1];
+    if (MODE == MSK_SPMV_RESID) bb = b[r];
+    if (MODE == MSK_SPMV_SCALED) vout[r] = x[r] * sc;
+  }
+  stage_csr_block<NT, SU>(t, n2, n4, v2, c4, sval, scol);
   __syncthreads();
   if (r < r1) {
     double s = 0.0;
@@ -398,6 +414,52 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
       }
     }
     y[r] = MODE == MSK_SPMV_RESID ? bb - s : s;
+  }
+}
+
+// R[:, 0:nc] = A S[:, 0:nc] (MatMatMult(AIJ, DENSE)): the row block's CSR slice
+// is staged once, then each column streams through it like one SpMV (per row:
+// entries in order, from 0), so A is read once for all nc columns.
+__global__ __launch_bounds__(kT) void k_spmm_lds8(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                  const double* __restrict__ S, int64_t lds, int nc,
+                                                  double* __restrict__ R, int64_t ldr, int32_t lds_cap) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sval = reinterpret_cast<double*>(smem);
+  int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
+  const int t = threadIdx.x;
+  const int32_t r0 = blockIdx.x * kT;
+  const int32_t r1 = min(r0 + kT, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s2 = start & ~1, s4 = start & ~3;
+  const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
+  const int32_t r = r0 + t;
+  int32_t k0 = 0, k1 = 0;
+  if (r < r1) {
+    k0 = rowptr[r];
+    k1 = rowptr[r + 1];
+  }
+  stage_csr_block<false, 4>(t, n2, n4, reinterpret_cast<const double2*>(val + s2),
+                            reinterpret_cast<const int4*>(col + s4), sval, scol);
+  __syncthreads();
+  if (r >= r1) return;
+#pragma unroll 1
+  for (int q = 0; q < nc; ++q) {
+    const double* __restrict__ x = S + (int64_t)q * lds;
+    double s = 0.0;
+    for (int32_t kb = k0; kb < k1; kb += 8) {
+      double av[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int32_t k = min(kb + u, k1 - 1);
+        av[u] = sval[k - s2];
+        xv[u] = x[scol[k - s4]];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (kb + u < k1) s = s + av[u] * xv[u];
+    }
+    R[r + (int64_t)q * ldr] = s;
   }
 }
 
@@ -616,6 +678,15 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
     else
       k_spmv_direct<MSK_SPMV_MULT><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y, sdev, vout, stop);
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_spmm(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* S,
+                        int64_t lds, int nc, double* R, int64_t ldr, int32_t lds_cap, hipStream_t s) {
+  if (nrows <= 0 || nc <= 0) return 0;
+  if (lds_cap <= 0) return (int)hipErrorInvalidValue;  // rows too long for the LDS stage
+  const unsigned g = (unsigned)((nrows + kT - 1) / kT);
+  k_spmm_lds8<<<dim3(g), dim3(kT), (size_t)lds_cap * 12, s>>>(nrows, rowptr, col, val, S, lds, nc, R, ldr, lds_cap);
   return (int)hipGetLastError();
 }
 

@@ -336,7 +336,7 @@ extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
 }
 extern "C" msp_ctx* mspi_mat_ctx(const msp_mat* A) { return A->ctx; }
 extern "C" mspi_csr_view mspi_mat_csr(const msp_mat* A) {
-  mspi_csr_view v = {A->rowptr, A->col, A->val, A->nnz, A->compressed ? 1 : 0};
+  mspi_csr_view v = {A->rowptr, A->col, A->val, A->nnz, A->compressed ? 1 : 0, A->lds_cap};
   return v;
 }
 

@@ -208,3 +208,25 @@ def test_lsqr_through_comm_single_rank(ctx, oracle, transport):
     assert np.array_equal(l.get_residual_history(), ro["hist"])
     l.destroy()
     comm.destroy()
+
+
+@pytest.mark.parametrize("nnz_per_row", [3, 20])
+def test_matmult_dense_general_csr(ctx, oracle, nnz_per_row):
+    """Random CSR (sorted columns): the LDS-staged SpMM (short rows) and the
+    one-lane-per-row fallback (a 256-row block with more than 4096 entries)."""
+    nr, ncol, s = 700, 900, 11
+    rows, cols = [], []
+    for r in range(nr):
+        c = np.sort(RNG.choice(ncol, size=nnz_per_row, replace=False))
+        rows.append(np.full(nnz_per_row, r))
+        cols.append(c)
+    rp = np.arange(0, nr * nnz_per_row + 1, nnz_per_row, dtype=np.int32)
+    c = np.concatenate(cols).astype(np.int32)
+    v = RNG.standard_normal(c.size)
+    A = Mat.from_csr(ctx, nr, ncol, rp, c, v)
+    S = RNG.standard_normal((ncol, s))
+    Rd = DenseMat(ctx, nr, s)
+    A.mat_mult_dense(DenseMat.from_array(ctx, S), Rd)
+    Ao = oracle.Mat.from_arrays(nr, ncol, rp, c, v)
+    ref = np.stack([Ao.mult(S[:, j]) for j in range(s)], axis=1)
+    assert np.array_equal(Rd.get_values(), ref)
