@@ -74,6 +74,8 @@ typedef struct msp_ksp msp_ksp;
 typedef struct msp_dense msp_dense;
 typedef struct msp_lsqr msp_lsqr;
 typedef struct msp_comm msp_comm;
+typedef struct msp_amsg msp_amsg;
+typedef struct msp_cvd msp_cvd;
 
 /* ---------------------------------------------------------------- context */
 /* One context per GPU: device id + the HIP stream all work is ordered on.
@@ -285,6 +287,65 @@ int msp_lsqr_get_converged_reason(const msp_lsqr *lsqr, int32_t *reason);
 /* KSPLSQRGetNorms: ||R^T r|| estimate and ||R||_F (exact or estimated). */
 int msp_lsqr_get_norms(const msp_lsqr *lsqr, double *arnorm, double *anorm);
 int msp_lsqr_get_residual_history(const msp_lsqr *lsqr, const double **hist, int32_t *n);
+
+/* ------------------------------------------------------- async messages */
+/* Newest-value message slots in POSIX shared memory between the blocks of an
+ * asynchronous run on one node (one process or host thread per GPU).  They
+ * replace the MPI layer of the asynchronous drivers: iterate exchange
+ * (comm_async_test_and_send_prime / comm_async_probe_and_receive_prime,
+ * comm.c:455-554) and the convergence-detection messages (TAG_SEND_RCV_*,
+ * constants.h).  The reference drains every pending message of a kind and uses
+ * the newest; a slot holds exactly that newest message (sequence-locked), so
+ * a send never blocks and a receive never waits.  Iterate payloads (planes)
+ * travel between chain neighbours only (|src - dst| = 1), up to data_cap
+ * doubles.  Exactly one rank creates the region (owner = 1) before the others
+ * open it; the owner unlinks it on destroy.  No GPU is needed except for the
+ * *_vec variants. */
+#define MSP_AMSG_DATA 0          /* TAG_MULTISPLITTING_DATA: (PhaseTag, iteration, plane) */
+#define MSP_AMSG_PARTIAL_CV 1    /* TAG_SEND_RCV_PARTIAL_CV */
+#define MSP_AMSG_VERIFICATION 2  /* TAG_SEND_RCV_VERIFICATION */
+#define MSP_AMSG_RESPONSE 3      /* TAG_SEND_RCV_RESPONSE */
+#define MSP_AMSG_VERDICT 4       /* TAG_SEND_RCV_VERDICT */
+#define MSP_AMSG_NKINDS 5
+int msp_amsg_create(const char *name, int32_t nranks, int32_t rank, int64_t data_cap, int32_t owner, msp_amsg **am);
+int msp_amsg_destroy(msp_amsg **am);
+/* number of ranks that have opened the region (for a start-up barrier) */
+int msp_amsg_attached(const msp_amsg *am, int32_t *n);
+/* up to 6 ints (tags) and, for MSP_AMSG_DATA, n doubles of payload */
+int msp_amsg_send(msp_amsg *am, int32_t dst, int32_t kind, const int32_t *ints, int32_t nints, const double *data,
+                  int64_t n);
+/* got = 1 when a message newer than the last one taken from src arrived; it is copied out */
+int msp_amsg_recv(msp_amsg *am, int32_t src, int32_t kind, int32_t *ints, int32_t nints, double *data, int64_t cap,
+                  int64_t *n, int32_t *got);
+/* the same for a plane v[off : off+n] in HBM (DMA to / from the registered region) */
+int msp_amsg_send_vec(msp_amsg *am, int32_t dst, const int32_t *ints, int32_t nints, const msp_vec *v, int64_t off,
+                      int64_t n);
+int msp_amsg_recv_vec(msp_amsg *am, int32_t src, int32_t *ints, int32_t nints, msp_vec *v, int64_t off, int64_t cap,
+                      int64_t *n, int32_t *got);
+
+/* ------------------------------------------------- convergence detection */
+/* Algorithm 5.15 of Bahi/Contassot-Vivier/Couturier as the reference implements
+ * it (src/utils/conv_detection_prime.c), one instance per block root, over the
+ * amsg slots.  nb[]: spanning-tree neighbours (the reference's 2-block tree,
+ * generalised to the chain of blocks); dep[]: the blocks whose iterates this
+ * block reads.  strict = 0 reproduces the reference exactly (see conv_detect.c);
+ * 1 also lets UnderThreshold veto during verification. */
+#define MSP_CVD_NORMAL 0             /* State, constants.h */
+#define MSP_CVD_WAIT4VERIFICATION 1
+#define MSP_CVD_VERIFICATION 2
+#define MSP_CVD_FINISHED 3
+int msp_cvd_create(msp_amsg *am, int32_t rank, int32_t nnb, const int32_t *nb, int32_t ndep, const int32_t *dep,
+                   int32_t strict, msp_cvd **cvd);
+int msp_cvd_destroy(msp_cvd **cvd);
+/* receive_data_dependency (conv_detection_prime.c:600-632): accept = 1 to take
+ * an iterate of dependency index d stamped (src_tag, src_iter). */
+int msp_cvd_data_received(msp_cvd *cvd, int32_t d, int32_t src_tag, int32_t src_iter, int32_t *accept);
+/* one pass of comm_async_convDetection_prime + receive_partial_CV/verification/
+ * response/verdict (asynchronous-multisplitting_prime.c:368-372) */
+int msp_cvd_step(msp_cvd *cvd, int32_t under_threshold);
+int msp_cvd_get_state(const msp_cvd *cvd, int32_t *state, int32_t *phase_tag);
+/* state, phase_tag, elected, local_cv, pp_begin, pp_end, nb_not_recvd, partial_cv_sent */
+int msp_cvd_get_info(const msp_cvd *cvd, int32_t *info, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -134,6 +134,19 @@ _SIGS = {
     "msp_lsqr_get_converged_reason": [_vp, _i32p],
     "msp_lsqr_get_norms": [_vp, _dp, _dp],
     "msp_lsqr_get_residual_history": [_vp, _P(_dp), _i32p],
+    "msp_amsg_create": [C.c_char_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32, _P(_vp)],
+    "msp_amsg_destroy": [_P(_vp)],
+    "msp_amsg_attached": [_vp, _i32p],
+    "msp_amsg_send": [_vp, C.c_int32, C.c_int32, _i32p, C.c_int32, _dp, C.c_int64],
+    "msp_amsg_recv": [_vp, C.c_int32, C.c_int32, _i32p, C.c_int32, _dp, C.c_int64, _P(C.c_int64), _i32p],
+    "msp_amsg_send_vec": [_vp, C.c_int32, _i32p, C.c_int32, _vp, C.c_int64, C.c_int64],
+    "msp_amsg_recv_vec": [_vp, C.c_int32, _i32p, C.c_int32, _vp, C.c_int64, C.c_int64, _P(C.c_int64), _i32p],
+    "msp_cvd_create": [_vp, C.c_int32, C.c_int32, _i32p, C.c_int32, _i32p, C.c_int32, _P(_vp)],
+    "msp_cvd_destroy": [_P(_vp)],
+    "msp_cvd_data_received": [_vp, C.c_int32, C.c_int32, C.c_int32, _i32p],
+    "msp_cvd_step": [_vp, C.c_int32],
+    "msp_cvd_get_state": [_vp, _i32p, _i32p],
+    "msp_cvd_get_info": [_vp, _i32p, C.c_int32],
 }
 
 

@@ -1,0 +1,142 @@
+"""Asynchronous multisplitting (AM) over the GPU inner solve.
+
+Mirrors src/asynchronous-multisplitting/asynchronous-multisplitting_prime.c:
+setup (:131-330: spanning tree, detection state, ||b||), the loop (:333-392)
+and the final exchange and report (:394-427), generalised from 2 blocks to a
+chain of nb blocks.  Blocks never wait for each other: each one takes the
+newest iterate its neighbours have published (if newer than the last one it
+took), solves, publishes its own boundary plane stamped (PhaseTag, iteration),
+and runs one step of the decentralised convergence detection
+(conv_detection_prime.c, in C: csrc/conv_detect.c).  Messages travel through
+newest-value slots in shared memory (csrc/amsg.c) -- the reference's MPI
+Isend / Iprobe-drain layer (comm.c:455-554) -- between one process per GPU
+(TorchComm) or between the blocks of one process (LocalComm, which runs the
+blocks round-robin: a deterministic schedule the tests replay on the oracle).
+
+Stop test per block (:359): local ||rhs_i - A_ii x_i|| <= max(atol, rtol/sqrt(nb) ||b||)
+(the reference's rtol/sqrt(2) for its 2 blocks), then the detection protocol
+decides the global stop.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+import uuid
+from dataclasses import dataclass, field
+
+from .petsc import AsyncMessages, ConvDetection
+
+
+@dataclass
+class AMResult:
+    iterations: list = field(default_factory=list)     # outer iterations of each local block
+    inner_its: list = field(default_factory=list)      # total inner GMRES iterations of each local block
+    phase_tags: list = field(default_factory=list)
+    norm0: float = 0.0
+    final_norm: float = float("nan")
+    error: float = float("nan")
+    elapsed: float = 0.0
+    trace: list = field(default_factory=list)          # (block, iteration, local norm, state, phase tag)
+
+
+class AsyncBlock:
+    """The asynchronous state of one block root: its message slots, its
+    convergence-detection instance and its counters."""
+
+    def __init__(self, blk, name: str, owner: bool, strict: bool):
+        L = blk.layout
+        self.blk = blk
+        self.am = AsyncMessages(name, L.nb, L.b, max(L.plane, 1), owner)
+        nbrs = [nbr for nbr, *_ in L.recv]            # spanning tree = chain; dependencies = the same blocks
+        self.cvd = ConvDetection(self.am, L.b, nbrs, nbrs, strict)
+        self.it = 0
+        self.inner = 0
+        self.state = ConvDetection.NORMAL
+        self.tag = 0
+        self.local_norm = math.inf
+
+    def iterate(self, norm0: float, rtol: float, atol: float, trace=None):
+        blk, L = self.blk, self.blk.layout
+        # comm_async_probe_and_receive_prime (:335-339): newest iterate of each dependency
+        for d, (nbr, hoff, cnt, _) in enumerate(L.recv):
+            got, (tag, it) = blk.async_recv(self.am, nbr, hoff, cnt)
+            if got and self.cvd.data_received(d, tag, it):
+                blk.async_accept(hoff, cnt)
+        blk.update_rhs()                                              # updateLocalRHS (:341)
+        self.inner += blk.solve()                                     # inner_solver (:344)
+        for nbr, off, cnt in L.send:                                  # comm_async_test_and_send_prime (:347)
+            blk.async_send(self.am, nbr, off, cnt, self.tag, self.it)
+        self.local_norm = math.sqrt(blk.local_residual_sq())          # MatResidual(A_ii, rhs, x), VecNorm (:351-352)
+        under = self.local_norm <= max(atol, rtol / math.sqrt(L.nb) * norm0)   # (:359)
+        self.cvd.step(under)                                          # detection + receives (:368-372)
+        self.it += 1
+        self.state, self.tag = self.cvd.state()
+        if trace is not None:
+            trace.append((L.b, self.it, self.local_norm, self.state, self.tag))
+
+    def close(self):
+        self.cvd.destroy()
+        self.am.destroy()
+
+
+def _channel_name(comm) -> str:
+    name = f"/msplit_am_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+    if getattr(comm, "world", 1) > 1:
+        obj = [name if comm.rank == 0 else None]
+        comm.dist.broadcast_object_list(obj, src=0, group=comm.group)
+        name = obj[0]
+    return name
+
+
+def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: int = 100000,
+             strict: bool = False, record: bool = False, monitor=None) -> AMResult:
+    """The asynchronous multisplitting loop (asynchronous-multisplitting_prime.c:333-392)."""
+    res = AMResult()
+    # global_norm_0 = computeFinalResidualNorm at x = 0 (:322)
+    res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
+    name = _channel_name(comm)
+    ordered = sorted(blocks, key=lambda b: b.layout.b)
+    asyncs = {}
+    owner_here = ordered[0].layout.b == 0
+    if owner_here:                                   # block 0 creates the region, the others open it
+        asyncs[0] = AsyncBlock(ordered[0], name, True, strict)
+    comm.barrier()
+    for blk in ordered:
+        if blk.layout.b not in asyncs:
+            asyncs[blk.layout.b] = AsyncBlock(blk, name, False, strict)
+    comm.barrier()
+    for blk in blocks:                               # x_j = 0; updateLocalRHS before the loop (:329)
+        blk.reset_halo()
+        blk.update_rhs()
+    comm.barrier()
+    trace = [] if record else None
+    t0 = time.perf_counter()
+    active = [asyncs[b.layout.b] for b in ordered]
+    while active:
+        for ab in active:                            # round-robin over the blocks of this process
+            ab.iterate(res.norm0, rtol, atol, trace)
+            if monitor:
+                monitor(ab.blk.layout.b, ab.it, ab.local_norm, ab.state, ab.tag)
+        active = [ab for ab in active if ab.state != ConvDetection.FINISHED]
+        if any(ab.it >= max_iterations for ab in active):
+            raise RuntimeError(f"asynchronous multisplitting did not terminate in {max_iterations} iterations")
+    comm.barrier()
+    res.elapsed = time.perf_counter() - t0
+    comm.exchange(blocks)                            # comm_sync_send_and_receive_final (:396)
+    res.final_norm = math.sqrt(comm.ordered_sum(blocks, [blk.block_residual_sq() for blk in blocks]))
+    res.error = math.sqrt(comm.ordered_sum(blocks, [blk.error_sq() for blk in blocks]))
+    for blk in blocks:
+        ab = asyncs[blk.layout.b]
+        res.iterations.append(ab.it)
+        res.inner_its.append(ab.inner)
+        res.phase_tags.append(ab.tag)
+    res.trace = trace or []
+    comm.barrier()
+    for ab in asyncs.values():
+        if ab.blk.layout.b != 0:
+            ab.close()
+    comm.barrier()
+    if 0 in asyncs:
+        asyncs[0].close()                            # the owner unlinks the region last
+    return res

@@ -1,0 +1,308 @@
+/*
+ * amsg.c -- newest-value message slots between the blocks of an asynchronous
+ * multisplitting run, in POSIX shared memory (one node, one process -- or one
+ * host thread -- per GPU).
+ *
+ * Replaces the MPI point-to-point layer of the asynchronous drivers:
+ *   - iterate exchange: comm_async_test_and_send_prime / _probe_and_receive_prime
+ *     (src/utils/comm.c:455-554): MPI_Isend of (PhaseTag, iteration, x_i), the
+ *     receiver draining every pending message with MPI_Iprobe/MPI_Recv and keeping
+ *     the newest;
+ *   - convergence-detection control (src/utils/conv_detection_prime.c): partial-CV,
+ *     verification, response and verdict messages, each received by the same
+ *     drain-to-newest loop.
+ * A receiver only ever uses the newest message of a (source, kind) pair, so
+ * each pair is one slot holding the newest message, written under a sequence
+ * lock: seq odd while the writer fills it, even when complete; a reader takes
+ * the slot when seq is even, newer than the last one it took, and unchanged
+ * across its copy.  No queue, no allocation, no message can block a sender.
+ *
+ * Iterate payloads are boundary planes: only chain neighbours (|src - dst| = 1,
+ * the z-slab blocks) get a data slot of data_cap doubles.  *_vec variants move
+ * the plane between HBM and the slot (the region is registered with the HIP
+ * runtime, so the copies are DMA transfers).
+ *
+ * Host code only: no GPU is needed for the control messages (the CPU tests use
+ * them across processes).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "msplit.h"
+#include "msplit_internal.h"
+
+#define AMSG_MAGIC 0x4d53504c414d5347ULL /* "MSPLAMSG" */
+#define AMSG_INTS 6
+
+typedef struct {
+  _Atomic uint64_t seq;
+  int32_t ints[AMSG_INTS];
+  int64_t n;
+  uint8_t pad[64 - 8 - 4 * AMSG_INTS - 8];
+} ctrl_slot; /* one cache line */
+
+typedef struct {
+  uint64_t magic;
+  int32_t nranks;
+  int32_t pad0;
+  int64_t data_cap;
+  _Atomic int32_t attached;
+  uint8_t pad[64 - 28];
+} region_header;
+
+struct msp_amsg {
+  char name[128];
+  int32_t nranks, rank, owner;
+  int64_t data_cap;
+  size_t bytes;
+  uint8_t *base;
+  region_header *hdr;
+  ctrl_slot *ctrl;   /* [src][dst][kind] */
+  uint8_t *data;     /* [src][dir] slots of data_bytes */
+  size_t data_bytes; /* header line + data_cap doubles, rounded to 4 KiB */
+  uint64_t *seen;    /* [src][kind] last sequence number taken by this rank */
+  int registered;
+};
+
+static int aerr(int code, const char *msg) {
+  mspi_set_error(code, "%s", msg);
+  return code;
+}
+
+static size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static ctrl_slot *ctrl_at(msp_amsg *m, int src, int dst, int kind) {
+  return m->ctrl + ((size_t)src * m->nranks + dst) * MSP_AMSG_NKINDS + kind;
+}
+
+/* data slot of the (src -> dst) chain link, or NULL */
+static ctrl_slot *data_at(msp_amsg *m, int src, int dst) {
+  int dir;
+  if (dst == src - 1) dir = 0;
+  else if (dst == src + 1) dir = 1;
+  else return NULL;
+  return (ctrl_slot *)(m->data + ((size_t)src * 2 + dir) * m->data_bytes);
+}
+
+int msp_amsg_create(const char *name, int32_t nranks, int32_t rank, int64_t data_cap, int32_t owner,
+                    msp_amsg **out) {
+  if (!name || !out) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
+  if (nranks < 1 || nranks > 4096 || rank < 0 || rank >= nranks || data_cap < 0)
+    return aerr(MSP_ERR_ARG_OUTOFRANGE, "bad amsg sizes");
+  if (strlen(name) >= sizeof(((msp_amsg *)0)->name) || name[0] != '/')
+    return aerr(MSP_ERR_ARG_WRONG, "shared-memory name must start with '/' and be < 128 chars");
+  msp_amsg *m = (msp_amsg *)calloc(1, sizeof(msp_amsg));
+  if (!m) return aerr(MSP_ERR_MEM, "allocation failed");
+  strcpy(m->name, name);
+  m->nranks = nranks;
+  m->rank = rank;
+  m->owner = owner ? 1 : 0;
+  m->data_cap = data_cap;
+  m->data_bytes = round_up(sizeof(ctrl_slot) + (size_t)data_cap * sizeof(double), 4096);
+  const size_t ctrl_bytes = round_up((size_t)nranks * nranks * MSP_AMSG_NKINDS * sizeof(ctrl_slot), 4096);
+  m->bytes = 4096 + ctrl_bytes + (size_t)nranks * 2 * m->data_bytes;
+  int fd;
+  if (m->owner) {
+    shm_unlink(name); /* a stale region of an earlier run */
+    fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd >= 0 && ftruncate(fd, (off_t)m->bytes) != 0) {
+      close(fd);
+      fd = -1;
+    }
+  } else {
+    fd = shm_open(name, O_RDWR, 0600);
+  }
+  if (fd < 0) {
+    free(m);
+    mspi_set_error(MSP_ERR_LIB, "shm_open(%s) failed: %s", name, strerror(errno));
+    return MSP_ERR_LIB;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0 || (size_t)st.st_size < m->bytes) {
+    close(fd);
+    free(m);
+    return aerr(MSP_ERR_ARG_SIZ, "shared-memory region smaller than the layout (sizes differ between ranks?)");
+  }
+  m->base = (uint8_t *)mmap(NULL, m->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (m->base == MAP_FAILED) {
+    free(m);
+    return aerr(MSP_ERR_MEM, "mmap of the shared-memory region failed");
+  }
+  m->hdr = (region_header *)m->base;
+  m->ctrl = (ctrl_slot *)(m->base + 4096);
+  m->data = m->base + 4096 + ctrl_bytes;
+  if (m->owner) {
+    m->hdr->nranks = nranks;
+    m->hdr->data_cap = data_cap;
+    atomic_store_explicit(&m->hdr->attached, 0, memory_order_relaxed);
+    atomic_thread_fence(memory_order_release);
+    m->hdr->magic = AMSG_MAGIC; /* ftruncate zeroed every slot: seq = 0, nothing sent */
+  } else if (m->hdr->magic != AMSG_MAGIC || m->hdr->nranks != nranks || m->hdr->data_cap != data_cap) {
+    munmap(m->base, m->bytes);
+    free(m);
+    return aerr(MSP_ERR_ARG_WRONG, "shared-memory region not initialised by the owner, or different sizes");
+  }
+  m->seen = (uint64_t *)calloc((size_t)nranks * (MSP_AMSG_NKINDS), sizeof(uint64_t));
+  if (!m->seen) {
+    munmap(m->base, m->bytes);
+    free(m);
+    return aerr(MSP_ERR_MEM, "allocation failed");
+  }
+  atomic_fetch_add_explicit(&m->hdr->attached, 1, memory_order_acq_rel);
+  *out = m;
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_attached(const msp_amsg *m, int32_t *n) {
+  if (!m || !n) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
+  *n = atomic_load_explicit(&m->hdr->attached, memory_order_acquire);
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_destroy(msp_amsg **pm) {
+  if (!pm || !*pm) return MSP_SUCCESS;
+  msp_amsg *m = *pm;
+  if (m->registered) mspi_host_unregister(m->base);
+  munmap(m->base, m->bytes);
+  if (m->owner) shm_unlink(m->name);
+  free(m->seen);
+  free(m);
+  *pm = NULL;
+  return MSP_SUCCESS;
+}
+
+static ctrl_slot *slot_for(msp_amsg *m, int src, int dst, int kind) {
+  if (kind == MSP_AMSG_DATA) return data_at(m, src, dst);
+  return ctrl_at(m, src, dst, kind);
+}
+
+/* seqlock writer: seq odd, payload, seq even */
+static void write_begin(ctrl_slot *s) {
+  const uint64_t q = atomic_load_explicit(&s->seq, memory_order_relaxed);
+  atomic_store_explicit(&s->seq, q + 1, memory_order_relaxed);
+  atomic_thread_fence(memory_order_release);
+}
+
+static void write_end(ctrl_slot *s) {
+  const uint64_t q = atomic_load_explicit(&s->seq, memory_order_relaxed);
+  atomic_store_explicit(&s->seq, q + 1, memory_order_release);
+}
+
+static int check_pair(msp_amsg *m, int peer, int kind) {
+  if (peer < 0 || peer >= m->nranks || peer == m->rank) return aerr(MSP_ERR_ARG_OUTOFRANGE, "peer rank out of range");
+  if (kind < 0 || kind >= MSP_AMSG_NKINDS) return aerr(MSP_ERR_ARG_OUTOFRANGE, "unknown message kind");
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_send(msp_amsg *m, int32_t dst, int32_t kind, const int32_t *ints, int32_t nints, const double *data,
+                  int64_t n) {
+  if (!m) return aerr(MSP_ERR_ARG_NULL, "amsg is NULL");
+  int rc = check_pair(m, dst, kind);
+  if (rc) return rc;
+  if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
+  ctrl_slot *s = slot_for(m, m->rank, dst, kind);
+  if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
+  if (kind == MSP_AMSG_DATA ? (n < 0 || n > m->data_cap || (n && !data)) : n != 0)
+    return aerr(MSP_ERR_ARG_SIZ, "payload larger than the data slot");
+  write_begin(s);
+  memset(s->ints, 0, sizeof(s->ints));
+  if (nints) memcpy(s->ints, ints, (size_t)nints * sizeof(int32_t));
+  s->n = n;
+  if (n) memcpy((double *)(s + 1), data, (size_t)n * sizeof(double));
+  write_end(s);
+  return MSP_SUCCESS;
+}
+
+/* seqlock reader; got = 1 when a newer complete message was copied out */
+static int read_slot(msp_amsg *m, int src, int kind, int32_t *ints, int32_t nints, double *data, int64_t cap,
+                     int64_t *n, int32_t *got, msp_vec *v, int64_t voff) {
+  ctrl_slot *s = slot_for(m, src, m->rank, kind);
+  if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
+  uint64_t *seen = m->seen + (size_t)src * MSP_AMSG_NKINDS + kind;
+  *got = 0;
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    const uint64_t s1 = atomic_load_explicit(&s->seq, memory_order_acquire);
+    if ((s1 & 1) || s1 == *seen) return MSP_SUCCESS; /* being written, or nothing new: try next round */
+    int32_t tmp[AMSG_INTS];
+    memcpy(tmp, s->ints, sizeof(tmp));
+    const int64_t len = s->n;
+    if (len < 0 || len > m->data_cap) continue;
+    if (len) {
+      if (len > cap) return aerr(MSP_ERR_ARG_SIZ, "receive buffer smaller than the message");
+      if (v) {
+        int rc = mspi_h2d_sync(v->ctx, v->d + voff, (const double *)(s + 1), (size_t)len * sizeof(double));
+        if (rc) return rc;
+      } else {
+        memcpy(data, (const double *)(s + 1), (size_t)len * sizeof(double));
+      }
+    }
+    atomic_thread_fence(memory_order_acquire);
+    const uint64_t s2 = atomic_load_explicit(&s->seq, memory_order_relaxed);
+    if (s1 != s2) continue; /* overwritten while copying: take the newer one */
+    if (nints) memcpy(ints, tmp, (size_t)nints * sizeof(int32_t));
+    if (n) *n = len;
+    *seen = s1;
+    *got = 1;
+    return MSP_SUCCESS;
+  }
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_recv(msp_amsg *m, int32_t src, int32_t kind, int32_t *ints, int32_t nints, double *data, int64_t cap,
+                  int64_t *n, int32_t *got) {
+  if (!m || !got) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
+  int rc = check_pair(m, src, kind);
+  if (rc) return rc;
+  if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
+  return read_slot(m, src, kind, ints, nints, data, cap, n, got, NULL, 0);
+}
+
+static int ensure_registered(msp_amsg *m) {
+  if (m->registered) return MSP_SUCCESS;
+  int rc = mspi_host_register(m->base, m->bytes);
+  if (rc) return rc;
+  m->registered = 1;
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_send_vec(msp_amsg *m, int32_t dst, const int32_t *ints, int32_t nints, const msp_vec *v, int64_t off,
+                      int64_t n) {
+  if (!m || !v) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
+  int rc = check_pair(m, dst, MSP_AMSG_DATA);
+  if (rc) return rc;
+  if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
+  if (off < 0 || n < 0 || off + n > v->n || n > m->data_cap) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
+  ctrl_slot *s = data_at(m, m->rank, dst);
+  if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
+  if ((rc = ensure_registered(m))) return rc;
+  write_begin(s);
+  memset(s->ints, 0, sizeof(s->ints));
+  if (nints) memcpy(s->ints, ints, (size_t)nints * sizeof(int32_t));
+  s->n = n;
+  if (n && (rc = mspi_d2h_sync(v->ctx, (double *)(s + 1), v->d + off, (size_t)n * sizeof(double)))) {
+    s->n = 0; /* publish an empty message rather than a partial plane */
+    write_end(s);
+    return rc;
+  }
+  write_end(s);
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_recv_vec(msp_amsg *m, int32_t src, int32_t *ints, int32_t nints, msp_vec *v, int64_t off, int64_t cap,
+                      int64_t *n, int32_t *got) {
+  if (!m || !v || !got) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
+  int rc = check_pair(m, src, MSP_AMSG_DATA);
+  if (rc) return rc;
+  if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
+  if (off < 0 || cap < 0 || off + cap > v->n) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
+  if ((rc = ensure_registered(m))) return rc;
+  return read_slot(m, src, MSP_AMSG_DATA, ints, nints, NULL, cap, n, got, v, off);
+}

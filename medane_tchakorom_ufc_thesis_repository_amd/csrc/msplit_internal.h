@@ -128,6 +128,10 @@ int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv,
 int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const double *base, int64_t stride, int64_t n,
                            const double *coef_dev, int nv_expected);
 int mspi_h2d_async(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
+int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
+/* page-lock a host range (shared-memory mailboxes) for DMA */
+int mspi_host_register(void *p, size_t bytes);
+int mspi_host_unregister(void *p);
 
 /* ---- cross-process all-gather (msplit_comm.hip); comm may be NULL (1 rank) ---- */
 int mspi_comm_allgather(msp_comm *comm, const double *send_dev, double *recv_dev, int64_t count);

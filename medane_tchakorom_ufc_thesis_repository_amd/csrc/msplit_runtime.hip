@@ -242,6 +242,22 @@ extern "C" int mspi_h2d_async(msp_ctx* c, void* dev, const void* host, size_t by
   return MSP_SUCCESS;
 }
 
+extern "C" int mspi_h2d_sync(msp_ctx* c, void* dev, const void* host, size_t bytes) {
+  HIPCHK(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_host_register(void* p, size_t bytes) {
+  HIPCHK(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_host_unregister(void* p) {
+  HIPCHK(hipHostUnregister(p));
+  return MSP_SUCCESS;
+}
+
 extern "C" int mspi_mdot_basis(msp_ctx* c, const double* w, int nv, const double* base, int64_t stride, int64_t n,
                                double* out_dev, const int* stop) {
   if (nv <= 0) return MSP_SUCCESS;

@@ -117,12 +117,36 @@ class GpuBlock:
         coupling columns (create_redistributed_A_block_jacobi, utils.c:891-921)."""
         L = self.layout
         self.s = int(s)
+        self._ensure_ext()
+        self.S = DenseMat(self.ctx, self.lo_rows + L.nrows + self.hi_rows, self.s)
+        self.R = DenseMat(self.ctx, L.nrows, self.s)
+
+    def _ensure_ext(self):
+        """A_ext: the block's full rows of A_block_jacobi, coupling columns kept."""
+        if getattr(self, "A_ext", None) is not None:
+            return
+        L = self.layout
         self.lo_rows = L.plane if any(nbr < L.b for nbr, *_ in L.recv) else 0
         self.hi_rows = L.plane if any(nbr > L.b for nbr, *_ in L.recv) else 0
         dim, bx, by, bz = L.box
         self.A_ext = Mat.box_stencil_ext(self.ctx, dim, bx, by, bz, self.lo_rows > 0, self.hi_rows > 0)
-        self.S = DenseMat(self.ctx, self.lo_rows + L.nrows + self.hi_rows, self.s)
-        self.R = DenseMat(self.ctx, L.nrows, self.s)
+
+    # -- asynchronous (AM) hooks: asynchronous.py
+    def async_recv(self, am, nbr, hoff, cnt):
+        """The newest plane of neighbour nbr, into a staging copy of the halo
+        (comm_async_probe_and_receive_prime receives into a temporary buffer)."""
+        if getattr(self, "halo_stage", None) is None:
+            self.halo_stage = Vec(self.ctx, max(self.layout.halo_size, 1))
+        got, ints, _ = am.recv_vec(nbr, 2, self.halo_stage, hoff, cnt)
+        return got, (ints[0], ints[1])
+
+    def async_accept(self, hoff, cnt):
+        """receive_data_dependency accepted it: copy into x_j's plane."""
+        self.halo_stage.copy_range_to(hoff, self.halo, hoff, cnt)
+
+    def async_send(self, am, nbr, off, cnt, tag, it):
+        """comm_async_test_and_send_prime: the plane nbr reads, stamped (PhaseTag, iteration)."""
+        am.send_vec(nbr, [tag, it], self.x, off, cnt)
 
     def store_column(self, k: int):
         """S(:, k) = x after the k-th inner solve and exchange (MatSetValuesLocal,
@@ -153,6 +177,7 @@ class GpuBlock:
     def block_residual_sq(self) -> float:
         """||b_i - A_block x||^2 over the block's full rows (computeFinalResidualNorm,
         utils.c:575-595): A_ext applied to [plane below | x_i | plane above]."""
+        self._ensure_ext()
         n = self.layout.nrows
         xe = Vec(self.ctx, self.lo_rows + n + self.hi_rows)
         self.x.copy_range_to(0, xe, self.lo_rows, n)

@@ -675,3 +675,109 @@ class KSP:
             self.destroy()
         except Exception:
             pass
+
+
+# ------------------------------------------------------------ async messages
+class AsyncMessages:
+    """Newest-value message slots in shared memory between the blocks of an
+    asynchronous run (msp_amsg): the reference's MPI Isend / Iprobe-drain layer
+    (comm.c:455-554, conv_detection_prime.c)."""
+
+    DATA, PARTIAL_CV, VERIFICATION, RESPONSE, VERDICT = range(5)
+
+    def __init__(self, name: str, nranks: int, rank: int, data_cap: int, owner: bool):
+        h = C.c_void_p()
+        call("msp_amsg_create", name.encode(), int(nranks), int(rank), int(data_cap), 1 if owner else 0, C.byref(h))
+        self.h = h
+        self.rank = rank
+        self.nranks = nranks
+
+    def attached(self) -> int:
+        n = C.c_int32()
+        call("msp_amsg_attached", self.h, C.byref(n))
+        return n.value
+
+    def send(self, dst: int, kind: int, ints, data=None):
+        iv = np.ascontiguousarray(ints, np.int32)
+        if data is None:
+            call("msp_amsg_send", self.h, int(dst), int(kind), _ip(iv), iv.size, None, 0)
+        else:
+            d = np.ascontiguousarray(data, np.float64)
+            call("msp_amsg_send", self.h, int(dst), int(kind), _ip(iv), iv.size, _dp(d), d.size)
+
+    def recv(self, src: int, kind: int, nints: int, cap: int = 0):
+        """(got, ints, data): the newest message of (src, kind) not taken yet."""
+        iv = np.zeros(max(nints, 1), np.int32)
+        d = np.zeros(max(cap, 1))
+        n = C.c_int64()
+        got = C.c_int32()
+        call("msp_amsg_recv", self.h, int(src), int(kind), _ip(iv), int(nints), _dp(d), int(cap), C.byref(n),
+             C.byref(got))
+        return bool(got.value), iv[:nints].tolist(), d[:n.value] if got.value else None
+
+    def send_vec(self, dst: int, ints, v: Vec, off: int, n: int):
+        iv = np.ascontiguousarray(ints, np.int32)
+        call("msp_amsg_send_vec", self.h, int(dst), _ip(iv), iv.size, v.h, int(off), int(n))
+
+    def recv_vec(self, src: int, nints: int, v: Vec, off: int, cap: int):
+        iv = np.zeros(max(nints, 1), np.int32)
+        n = C.c_int64()
+        got = C.c_int32()
+        call("msp_amsg_recv_vec", self.h, int(src), _ip(iv), int(nints), v.h, int(off), int(cap), C.byref(n),
+             C.byref(got))
+        return bool(got.value), iv[:nints].tolist(), n.value
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_amsg_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+class ConvDetection:
+    """The reference's decentralised convergence detection (msp_cvd,
+    conv_detection_prime.c) for one block root."""
+
+    NORMAL, WAIT4VERIFICATION, VERIFICATION, FINISHED = range(4)
+
+    def __init__(self, am: AsyncMessages, rank: int, neighbors, dependencies, strict: bool = False):
+        nb = np.ascontiguousarray(neighbors, np.int32)
+        dp = np.ascontiguousarray(dependencies, np.int32)
+        h = C.c_void_p()
+        call("msp_cvd_create", am.h, int(rank), nb.size, _ip(nb) if nb.size else None, dp.size,
+             _ip(dp) if dp.size else None, 1 if strict else 0, C.byref(h))
+        self.h = h
+        self._am = am
+
+    def data_received(self, d: int, tag: int, iteration: int) -> bool:
+        acc = C.c_int32()
+        call("msp_cvd_data_received", self.h, int(d), int(tag), int(iteration), C.byref(acc))
+        return bool(acc.value)
+
+    def step(self, under_threshold: bool):
+        call("msp_cvd_step", self.h, 1 if under_threshold else 0)
+
+    def state(self):
+        s, t = C.c_int32(), C.c_int32()
+        call("msp_cvd_get_state", self.h, C.byref(s), C.byref(t))
+        return s.value, t.value
+
+    def info(self) -> dict:
+        v = np.zeros(8, np.int32)
+        call("msp_cvd_get_info", self.h, _ip(v), 8)
+        keys = ("state", "phase_tag", "elected", "local_cv", "pp_begin", "pp_end", "nb_not_recvd", "partial_cv_sent")
+        return dict(zip(keys, v.tolist()))
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_cvd_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass

@@ -1,0 +1,286 @@
+"""Deterministic replay of asynchronous multisplitting (AM) for the tests.
+
+TEST INFRASTRUCTURE ONLY (imported by tests/ alone).  Restates, independently
+of the product's C code (csrc/amsg.c, csrc/conv_detect.c) and driver
+(asynchronous.py):
+
+  * the AM loop, src/asynchronous-multisplitting/asynchronous-multisplitting_prime.c:333-392
+    (newest iterate per dependency, RHS update, inner GMRES, publish, local
+    residual, threshold rtol/sqrt(nb)*||b||, detection step), and the final
+    synchronous exchange and residual (:394-427);
+  * the convergence detection of src/utils/conv_detection_prime.c (Algorithm 5.15),
+    including its test of the pointer `UnderThreashold` (never false) during
+    verification, over a chain spanning tree;
+  * the drain-to-newest message semantics of comm.c:455-554 and the detection's
+    Iprobe/Recv loops, as newest-value slots,
+
+on the round-robin schedule the product uses when all blocks live in one
+process: blocks iterate in block order, a message is visible as soon as it is
+sent.  The arithmetic is the oracle's (oracle/oracle.c via pyoracle, DBR order),
+so the product must replay it bit for bit.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+NORMAL, WAIT4VERIFICATION, VERIFICATION, FINISHED = 0, 1, 2, 3
+DATA, PARTIAL_CV, VERIFICATION_MSG, RESPONSE, VERDICT = 0, 1, 2, 3, 4
+
+
+class Slots:
+    """Newest message per (src, dst, kind); each receiver remembers what it took."""
+
+    def __init__(self):
+        self.slot = {}
+        self.seen = {}
+
+    def send(self, src, dst, kind, payload):
+        seq = self.slot.get((src, dst, kind), (0, None))[0] + 1
+        self.slot[(src, dst, kind)] = (seq, payload)
+
+    def recv(self, src, dst, kind):
+        seq, payload = self.slot.get((src, dst, kind), (0, None))
+        if seq == 0 or self.seen.get((src, dst, kind)) == seq:
+            return None
+        self.seen[(src, dst, kind)] = seq
+        return payload
+
+
+class Detector:
+    """conv_detection_prime.c for one block root (chain tree)."""
+
+    def __init__(self, rank, neighbors, net: Slots, strict=False):
+        self.rank = rank
+        self.nbrs = list(neighbors)
+        self.net = net
+        self.strict = strict
+        self.phase = 0
+        self.last_iter = [-1] * len(self.nbrs)
+        self.newer = [False] * len(self.nbrs)
+        self.responses = [0] * len(self.nbrs)
+        self.response_sent = False
+        self._initialize_state()
+
+    # -- the reference's helpers
+    def _reinit_pseudo_period(self):
+        self.pp_begin = self.pp_end = False
+        self.newer = [False] * len(self.nbrs)
+
+    def _initialize_state(self):
+        self.not_recvd = len(self.nbrs)
+        self.got_pcv = [False] * len(self.nbrs)
+        self.elected = False
+        self.local_cv = False
+        self.pcv_sent = False
+        self._reinit_pseudo_period()
+        self.state = NORMAL
+
+    def _initialize_verification(self):
+        self._reinit_pseudo_period()
+        self.phase += 1
+        self.responses = [0] * len(self.nbrs)
+        self.response_sent = False
+
+    def _send(self, dst, kind, payload):
+        self.net.send(self.rank, dst, kind, payload)
+
+    def data_received(self, d, tag, it):
+        if self.last_iter[d] < it and (self.state != VERIFICATION or tag == self.phase):
+            self.last_iter[d] = it
+            self.newer[d] = True
+            return True
+        return False
+
+    def step(self, under):
+        self._detect(under)
+        self._recv_partial_cv()
+        self._recv_verification()
+        self._recv_response()
+        self._recv_verdict()
+
+    def _detect(self, under):
+        veto = (not under) if self.strict else False     # the reference compares a pointer with PETSC_FALSE
+        if self.state == NORMAL:
+            if not under:
+                self._reinit_pseudo_period()
+            elif not self.pp_begin:
+                self.pp_begin = True
+            elif self.pp_end:
+                self.local_cv = True
+                if self.not_recvd == 0:
+                    self.elected = True
+                    self._initialize_verification()
+                    for n in self.nbrs:
+                        self._send(n, VERIFICATION_MSG, (self.phase,))
+                    self.state = VERIFICATION
+                elif self.not_recvd == 1:
+                    for i, n in enumerate(self.nbrs):
+                        if not self.got_pcv[i]:
+                            self._send(n, PARTIAL_CV, (self.phase,))
+                            break
+                    self.pcv_sent = True
+                    self.state = WAIT4VERIFICATION
+            elif all(self.newer):
+                self.pp_end = True
+        elif self.state == WAIT4VERIFICATION:
+            if veto:
+                self.local_cv = False
+        elif self.state == VERIFICATION:
+            negative = -1 in self.responses
+            if self.elected:
+                if veto or not self.local_cv or negative:
+                    self.phase += 1
+                    for n in self.nbrs:
+                        self._send(n, VERDICT, (self.phase, -1))
+                    self._initialize_state()
+                elif self.pp_end:
+                    if 0 not in self.responses:
+                        if not negative:
+                            for n in self.nbrs:
+                                self._send(n, VERDICT, (self.phase, 1))
+                            self.state = FINISHED
+                        else:
+                            self.phase += 1
+                            for n in self.nbrs:
+                                self._send(n, VERDICT, (self.phase, -1))
+                            self._initialize_state()
+                elif all(self.newer):
+                    self.pp_end = True
+            elif not self.response_sent:
+                if veto or not self.local_cv or negative:
+                    for i, n in enumerate(self.nbrs):
+                        if not self.got_pcv[i]:
+                            self._send(n, RESPONSE, (self.phase, -1))
+                            break
+                    self.response_sent = True
+                elif self.pp_end:
+                    if self.responses.count(0) == 1:
+                        asking = self.nbrs[self.responses.index(0)]
+                        ok = self.responses.count(1) == len(self.nbrs) - 1
+                        self._send(asking, RESPONSE, (self.phase, 1 if ok else -1))
+                        self.response_sent = True
+                elif all(self.newer):
+                    self.pp_end = True
+
+    def _recv_partial_cv(self):
+        for i, n in enumerate(self.nbrs):
+            m = self.net.recv(n, self.rank, PARTIAL_CV)
+            if m is None or m[0] != self.phase:
+                continue
+            self.got_pcv[i] = True
+            self.not_recvd -= 1
+            if self.not_recvd == 0 and self.pcv_sent and max(self.rank, n) == self.rank:
+                self.elected = True
+                self._initialize_verification()
+                for k in self.nbrs:
+                    self._send(k, VERIFICATION_MSG, (self.phase,))
+                self.state = VERIFICATION
+
+    def _recv_verification(self):
+        for n in self.nbrs:
+            m = self.net.recv(n, self.rank, VERIFICATION_MSG)
+            if m is None or m[0] != self.phase + 1:
+                continue
+            self._initialize_verification()
+            self.state = VERIFICATION
+            for k in self.nbrs:
+                if k != n:
+                    self._send(k, VERIFICATION_MSG, (self.phase,))
+
+    def _recv_response(self):
+        for i, n in enumerate(self.nbrs):
+            m = self.net.recv(n, self.rank, RESPONSE)
+            if m is not None and m[0] == self.phase:
+                self.responses[i] = m[1]
+
+    def _recv_verdict(self):
+        for n in self.nbrs:
+            m = self.net.recv(n, self.rank, VERDICT)
+            if m is None:
+                continue
+            if m[1] == 1:
+                self.state = FINISHED
+            else:
+                self._initialize_state()
+                self.phase = m[0]
+            for k in self.nbrs:
+                if k != n:
+                    self._send(k, VERDICT, (self.phase, m[1]))
+
+
+def am_roundrobin(po, dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_iterations=100000, strict=False):
+    """Replay AM on nb blocks, round-robin.  Returns a dict with per-block
+    iterations / inner iterations / phase tags, the trace of (block, iteration,
+    local norm, state, phase tag), the final iterate, final residual and error."""
+    mode = po.REDUCE_DBR
+    nz = nz if dim == 3 else 1
+    N = nx * ny * nz
+    if dim == 3:
+        plane, rows = nx * ny, N // nb
+    else:
+        plane, rows = ny, N // nb
+    blocks = []
+    for b in range(nb):
+        r0, r1 = b * rows, (b + 1) * rows
+        if dim == 3:
+            ppb = nz // nb
+            Ab = po.poisson3d_rows(nx, ny, nz, b * ppb, (b + 1) * ppb)
+        else:
+            Ab = po.poisson2d_rows(nx, ny, r0, r1)
+        Aii, Aoff = po.split(Ab, r0, r1)
+        bb = Ab.mult(np.ones(N))
+        nbrs = [k for k in (b - 1, b + 1) if 0 <= k < nb]
+        blocks.append(dict(b=b, r0=r0, r1=r1, Ab=Ab, Aii=Aii, Aoff=Aoff, rhs_b=bb, x=np.zeros(rows),
+                           view=np.zeros(N), nbrs=nbrs, it=0, inner=0))
+    net = Slots()
+    dets = [Detector(blk["b"], blk["nbrs"], net, strict) for blk in blocks]
+    norm0 = math.sqrt(sum_ordered([po.norm2(blk["rhs_b"], mode) ** 2 for blk in blocks]))
+    thr = max(atol, rtol / math.sqrt(nb) * norm0)
+    opts = dict(inner, guess_nonzero=1, uirnorm=1, reduce_mode=mode)
+    trace = []
+
+    def plane_for(blk, nbr):         # the plane of blk that nbr's coupling rows read
+        return blk["x"][:plane].copy() if nbr < blk["b"] else blk["x"][rows - plane:].copy()
+
+    def store(blk, nbr, data):       # nbr's plane into blk's view of x
+        lo = nbr * rows + (rows - plane if nbr < blk["b"] else 0)
+        blk["view"][lo:lo + plane] = data
+
+    active = list(range(nb))
+    while active:
+        for bi in active:
+            blk, det = blocks[bi], dets[bi]
+            for d, nbr in enumerate(blk["nbrs"]):
+                m = net.recv(nbr, blk["b"], DATA)
+                if m is not None and det.data_received(d, m[0], m[1]):
+                    store(blk, nbr, m[2])
+            rhs = blk["Aoff"].residual(blk["rhs_b"], blk["view"])
+            blk["x"], r = po.gmres(blk["Aii"], rhs, x0=blk["x"], **opts)
+            blk["inner"] += r["its"]
+            for nbr in blk["nbrs"]:
+                net.send(blk["b"], nbr, DATA, (det.phase, blk["it"], plane_for(blk, nbr)))
+            ln = po.norm2(blk["Aii"].residual(rhs, blk["x"]), mode)
+            det.step(ln <= thr)
+            blk["it"] += 1
+            trace.append((blk["b"], blk["it"], ln, det.state, det.phase))
+            if blk["it"] >= max_iterations:
+                raise RuntimeError("no termination")
+        active = [bi for bi in active if dets[bi].state != FINISHED]
+    x = np.concatenate([blk["x"] for blk in blocks])
+    fin, err = [], []
+    for blk in blocks:                                # final synchronous exchange, full-row residual
+        rr = blk["Ab"].residual(blk["rhs_b"], x)
+        fin.append(po.norm2(rr, mode) ** 2)
+        err.append(po.norm2(blk["x"] - 1.0, mode) ** 2)
+    return {"iterations": [blk["it"] for blk in blocks], "inner_its": [blk["inner"] for blk in blocks],
+            "phase_tags": [d.phase for d in dets], "trace": trace, "x": x, "norm0": norm0,
+            "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}
+
+
+def sum_ordered(values):
+    t = 0.0
+    for v in values:
+        t += v
+    return t
