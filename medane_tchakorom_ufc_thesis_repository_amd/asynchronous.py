@@ -16,6 +16,12 @@ blocks round-robin: a deterministic schedule the tests replay on the oracle).
 Stop test per block (:359): local ||rhs_i - A_ii x_i|| <= max(atol, rtol/sqrt(nb) ||b||)
 (the reference's rtol/sqrt(2) for its 2 blocks), then the detection protocol
 decides the global stop.
+
+variant "amam_local" is src/asynchronous-multisplitting-asynchronous-minimization-local/
+asynchronous-multisplitting-asynchronous-minimization-local_prime.c:371-431: per
+outer iteration s asynchronous inner steps (each stamped with the inner-step
+count), S_i(:,k) = x_i, then the block-local minimization x_i = S_i LSQR(A_ii S_i,
+rhs_i) and one detection step.
 """
 from __future__ import annotations
 
@@ -51,29 +57,52 @@ class AsyncBlock:
         nbrs = [nbr for nbr, *_ in L.recv]            # spanning tree = chain; dependencies = the same blocks
         self.cvd = ConvDetection(self.am, L.b, nbrs, nbrs, strict)
         self.it = 0
+        self.steps = 0                                  # number_of_inner_times_outer_iterations (AMAM)
         self.inner = 0
         self.state = ConvDetection.NORMAL
         self.tag = 0
         self.local_norm = math.inf
 
-    def iterate(self, norm0: float, rtol: float, atol: float, trace=None):
+    def _receive(self):
+        """comm_async_probe_and_receive_prime: newest iterate of each dependency."""
         blk, L = self.blk, self.blk.layout
-        # comm_async_probe_and_receive_prime (:335-339): newest iterate of each dependency
         for d, (nbr, hoff, cnt, _) in enumerate(L.recv):
             got, (tag, it) = blk.async_recv(self.am, nbr, hoff, cnt)
             if got and self.cvd.data_received(d, tag, it):
                 blk.async_accept(hoff, cnt)
-        blk.update_rhs()                                              # updateLocalRHS (:341)
-        self.inner += blk.solve()                                     # inner_solver (:344)
-        for nbr, off, cnt in L.send:                                  # comm_async_test_and_send_prime (:347)
-            blk.async_send(self.am, nbr, off, cnt, self.tag, self.it)
-        self.local_norm = math.sqrt(blk.local_residual_sq())          # MatResidual(A_ii, rhs, x), VecNorm (:351-352)
-        under = self.local_norm <= max(atol, rtol / math.sqrt(L.nb) * norm0)   # (:359)
-        self.cvd.step(under)                                          # detection + receives (:368-372)
+
+    def _publish(self, stamp: int):
+        """comm_async_test_and_send_prime: the planes the neighbours read, (PhaseTag, stamp)."""
+        for nbr, off, cnt in self.blk.layout.send:
+            self.blk.async_send(self.am, nbr, off, cnt, self.tag, stamp)
+
+    def _detect(self, norm0, rtol, atol, trace):
+        blk, L = self.blk, self.blk.layout
+        self.local_norm = math.sqrt(blk.local_residual_sq())          # MatResidual(A_ii, rhs, x), VecNorm
+        under = self.local_norm <= max(atol, rtol / math.sqrt(L.nb) * norm0)
+        self.cvd.step(under)                                          # detection + receives
         self.it += 1
         self.state, self.tag = self.cvd.state()
         if trace is not None:
             trace.append((L.b, self.it, self.local_norm, self.state, self.tag))
+
+    def iterate(self, norm0: float, rtol: float, atol: float, trace=None, variant: str = "am", s: int = 0):
+        blk = self.blk
+        if variant == "am":                                           # asynchronous-multisplitting_prime.c:333-377
+            self._receive()
+            blk.update_rhs()
+            self.inner += blk.solve()
+            self._publish(self.it)
+        else:                                                         # AMAM-local_prime.c:371-404
+            for k in range(s):
+                self._receive()
+                blk.update_rhs()
+                self.inner += blk.solve()
+                self._publish(self.steps)
+                blk.store_local_column(k)
+                self.steps += 1
+            blk.local_minimize()
+        self._detect(norm0, rtol, atol, trace)
 
     def close(self):
         self.cvd.destroy()
@@ -90,8 +119,12 @@ def _channel_name(comm) -> str:
 
 
 def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: int = 100000,
-             strict: bool = False, record: bool = False, monitor=None) -> AMResult:
-    """The asynchronous multisplitting loop (asynchronous-multisplitting_prime.c:333-392)."""
+             strict: bool = False, record: bool = False, monitor=None, variant: str = "am", s: int = 0) -> AMResult:
+    """The asynchronous multisplitting loop (asynchronous-multisplitting_prime.c:333-392);
+    variant "amam_local" adds the block-local minimization every s inner steps
+    (the blocks must have setup_local_minimization(s))."""
+    if variant not in ("am", "amam_local"):
+        raise ValueError(f"unknown asynchronous variant {variant}")
     res = AMResult()
     # global_norm_0 = computeFinalResidualNorm at x = 0 (:322)
     res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
@@ -115,7 +148,7 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
     active = [asyncs[b.layout.b] for b in ordered]
     while active:
         for ab in active:                            # round-robin over the blocks of this process
-            ab.iterate(res.norm0, rtol, atol, trace)
+            ab.iterate(res.norm0, rtol, atol, trace, variant, s)
             if monitor:
                 monitor(ab.blk.layout.b, ab.it, ab.local_norm, ab.state, ab.tag)
         active = [ab for ab in active if ab.state != ConvDetection.FINISHED]

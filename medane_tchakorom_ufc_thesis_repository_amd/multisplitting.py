@@ -131,6 +131,34 @@ class GpuBlock:
         dim, bx, by, bz = L.box
         self.A_ext = Mat.box_stencil_ext(self.ctx, dim, bx, by, bz, self.lo_rows > 0, self.hi_rows > 0)
 
+    # -- local minimization (SMSM-local, AMAM-local) hooks
+    def setup_local_minimization(self, s: int, opts: Options | None, prefix: str | None = None):
+        """S_i (the block's own s latest iterates), R_i = A_ii S_i and a one-block
+        LSQR (create_matrix_dense of N/nb x s, SMSM-local.c / AMAM-local_prime.c:246-253;
+        outer KSP prefix outer{b+1}_)."""
+        self.s = int(s)
+        n = self.layout.nrows
+        self.S_loc = DenseMat(self.ctx, n, self.s)
+        self.R_loc = DenseMat(self.ctx, n, self.s)
+        self.alpha_loc = Vec(self.ctx, self.s)
+        self.lsqr_loc = initializeOuterKSP(self.ctx, prefix if prefix is not None else f"outer{self.layout.b + 1}_",
+                                           opts)
+        self.lsqr_loc.set_operators([self.R_loc])
+
+    def store_local_column(self, k: int):
+        """S_i(:, k) = x_i (MatSetValues(S, .., k, x_i))."""
+        self.S_loc.set_column(k, 0, self.x)
+
+    def local_minimize(self):
+        """R_i = A_ii S_i, rhs_i = b_i - A_ij x_j, alpha = LSQR(R_i, rhs_i), x_i = S_i alpha
+        (SMSM-local.c / AMAM-local_prime.c:400-404)."""
+        self.A.mat_mult_dense(self.S_loc, self.R_loc)
+        self.update_rhs()
+        self.lsqr_loc.solve([self.rhs], self.alpha_loc)
+        self.S_loc.mult(self.alpha_loc, self.x)
+        return (self.lsqr_loc.get_residual_norm(), self.lsqr_loc.get_iteration_number(),
+                self.lsqr_loc.get_converged_reason())
+
     # -- asynchronous (AM) hooks: asynchronous.py
     def async_recv(self, am, nbr, hoff, cnt):
         """The newest plane of neighbour nbr, into a staging copy of the halo
@@ -325,6 +353,65 @@ def smsm_solve(blocks, comm, s: int, minimizer, rtol: float, atol: float = 1e-10
 
 def make_blocks(ctx: Context, dim, nx, ny, nz, nb, block_ids, opts: Options | None, comm):
     return [GpuBlock(ctx, block_layout(dim, nx, ny, nz, nb, b), opts, comm) for b in block_ids]
+
+
+@dataclass
+class LocalMinResult:
+    outer_its: int = 0
+    norm0: float = 0.0
+    hist: list = field(default_factory=list)          # per outer: [local norm of each local block]
+    lsqr_its: list = field(default_factory=list)      # per outer: [LSQR its of each local block]
+    inner_its: list = field(default_factory=list)     # per outer: s lists of [its of each local block]
+    final_norm: float = float("nan")
+    error: float = float("nan")
+    elapsed: float = 0.0
+
+
+def smsm_local_solve(blocks, comm, s: int, rtol: float, atol: float = 1e-100, max_outer: int = 10000,
+                     monitor=None) -> LocalMinResult:
+    """SMSM with local minimization (synchronous-multisplitting-synchronous-minimization-local.c):
+    s times {rhs_i; inner GMRES; exchange; S_i(:,k) = x_i}, then R_i = A_ii S_i,
+    rhs_i, x_i = S_i LSQR(R_i, rhs_i); stop when every block's ||rhs_i - A_ii x_i||
+    <= max(atol, rtol/sqrt(nb) ||b||) (comm_sync_convergence_detection, comm.c:235-250)."""
+    res = LocalMinResult()
+    res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
+    nb = blocks[0].layout.nb
+    thr = max(atol, rtol / math.sqrt(nb) * res.norm0)
+    for blk in blocks:
+        blk.reset_halo()
+    comm.barrier()
+    t0 = time.perf_counter()
+    while True:
+        its_outer = []
+        for k in range(s):
+            for blk in blocks:
+                blk.update_rhs()
+            its_outer.append([blk.solve() for blk in blocks])
+            comm.exchange(blocks)
+            for blk in blocks:
+                blk.store_local_column(k)
+        norms, lits = [], []
+        for blk in blocks:
+            _, li, _ = blk.local_minimize()
+            lits.append(li)
+            norms.append(math.sqrt(blk.local_residual_sq()))      # MatResidual(A_ii, rhs_i, x_i)
+        res.hist.append(norms)
+        res.lsqr_its.append(lits)
+        res.inner_its.append(its_outer)
+        res.outer_its += 1
+        if monitor:
+            monitor(res.outer_its, norms, its_outer, lits)
+        conv = [1.0 if n <= thr else 0.0 for n in norms]
+        if comm.ordered_sum(blocks, conv) == float(nb):           # every block converged
+            break
+        if res.outer_its >= max_outer:
+            break
+    comm.barrier()
+    res.elapsed = time.perf_counter() - t0
+    comm.exchange(blocks)                                        # comm_sync_send_and_receive_final
+    res.final_norm = math.sqrt(comm.ordered_sum(blocks, [blk.block_residual_sq() for blk in blocks]))
+    res.error = math.sqrt(comm.ordered_sum(blocks, [blk.error_sq() for blk in blocks]))
+    return res
 
 
 def make_smsm(ctx: Context, dim, nx, ny, nz, nb, block_ids, s: int, opts: Options | None, comm):

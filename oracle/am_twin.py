@@ -210,8 +210,10 @@ class Detector:
                     self._send(k, VERDICT, (self.phase, m[1]))
 
 
-def am_roundrobin(po, dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_iterations=100000, strict=False):
-    """Replay AM on nb blocks, round-robin.  Returns a dict with per-block
+def am_roundrobin(po, dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_iterations=100000, strict=False,
+                  variant="am", s=0, outer: dict | None = None):
+    """Replay AM (or, variant "amam_local", AMAM-local: s inner steps then the
+    block-local LSQR minimization, AMAM-local_prime.c:371-431) on nb blocks, round-robin.  Returns a dict with per-block
     iterations / inner iterations / phase tags, the trace of (block, iteration,
     local norm, state, phase tag), the final iterate, final residual and error."""
     mode = po.REDUCE_DBR
@@ -248,19 +250,40 @@ def am_roundrobin(po, dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_i
         lo = nbr * rows + (rows - plane if nbr < blk["b"] else 0)
         blk["view"][lo:lo + plane] = data
 
+    outer = dict(outer or {}, reduce_mode=mode)
+
+    def receive(blk, det):
+        for d, nbr in enumerate(blk["nbrs"]):
+            m = net.recv(nbr, blk["b"], DATA)
+            if m is not None and det.data_received(d, m[0], m[1]):
+                store(blk, nbr, m[2])
+
+    def inner_step(blk, det, stamp):
+        rhs = blk["Aoff"].residual(blk["rhs_b"], blk["view"])
+        blk["x"], r = po.gmres(blk["Aii"], rhs, x0=blk["x"], **opts)
+        blk["inner"] += r["its"]
+        for nbr in blk["nbrs"]:
+            net.send(blk["b"], nbr, DATA, (det.phase, stamp, plane_for(blk, nbr)))
+        return rhs
+
     active = list(range(nb))
     while active:
         for bi in active:
             blk, det = blocks[bi], dets[bi]
-            for d, nbr in enumerate(blk["nbrs"]):
-                m = net.recv(nbr, blk["b"], DATA)
-                if m is not None and det.data_received(d, m[0], m[1]):
-                    store(blk, nbr, m[2])
-            rhs = blk["Aoff"].residual(blk["rhs_b"], blk["view"])
-            blk["x"], r = po.gmres(blk["Aii"], rhs, x0=blk["x"], **opts)
-            blk["inner"] += r["its"]
-            for nbr in blk["nbrs"]:
-                net.send(blk["b"], nbr, DATA, (det.phase, blk["it"], plane_for(blk, nbr)))
+            if variant == "am":
+                receive(blk, det)
+                rhs = inner_step(blk, det, blk["it"])
+            else:
+                S = np.zeros((rows, s), order="F")
+                for k in range(s):
+                    receive(blk, det)
+                    inner_step(blk, det, blk.setdefault("steps", 0))
+                    S[:, k] = blk["x"]
+                    blk["steps"] += 1
+                R = np.stack([blk["Aii"].mult(np.ascontiguousarray(S[:, k])) for k in range(s)], axis=1)
+                rhs = blk["Aoff"].residual(blk["rhs_b"], blk["view"])
+                alpha, _ = po.lsqr([R], [rhs], **outer)
+                blk["x"] = po.dense_mult(S, alpha)
             ln = po.norm2(blk["Aii"].residual(rhs, blk["x"]), mode)
             det.step(ln <= thr)
             blk["it"] += 1
@@ -284,3 +307,69 @@ def sum_ordered(values):
     for v in values:
         t += v
     return t
+
+
+def smsm_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000):
+    """SMSM with block-local minimization (synchronous-multisplitting-synchronous-
+    minimization-local.c): s times {rhs_i, inner GMRES, exchange, S_i(:,k) = x_i},
+    R_i = A_ii S_i, rhs_i, x_i = S_i LSQR(R_i, rhs_i); stop when every block's
+    ||rhs_i - A_ii x_i|| <= max(atol, rtol/sqrt(nb) ||b||).  Oracle arithmetic (DBR)."""
+    mode = po.REDUCE_DBR
+    nz = nz if dim == 3 else 1
+    N = nx * ny * nz
+    rows = N // nb
+    blocks = []
+    for b in range(nb):
+        r0, r1 = b * rows, (b + 1) * rows
+        if dim == 3:
+            ppb = nz // nb
+            Ab = po.poisson3d_rows(nx, ny, nz, b * ppb, (b + 1) * ppb)
+        else:
+            Ab = po.poisson2d_rows(nx, ny, r0, r1)
+        Aii, Aoff = po.split(Ab, r0, r1)
+        blocks.append(dict(r0=r0, Ab=Ab, Aii=Aii, Aoff=Aoff, rhs_b=Ab.mult(np.ones(N))))
+    x = np.zeros(N)        # every block's own rows
+    view = np.zeros(N)     # what the blocks last exchanged (x_j of updateLocalRHS)
+    norm0 = math.sqrt(sum_ordered([po.norm2(blk["rhs_b"], mode) ** 2 for blk in blocks]))
+    thr = max(atol, rtol / math.sqrt(nb) * norm0)
+    opts = dict(inner, guess_nonzero=1, uirnorm=1, reduce_mode=mode)
+    outer = dict(outer, reduce_mode=mode)
+    hist, lits_all, inner_all = [], [], []
+    outer_its = 0
+    while True:
+        S = [np.zeros((rows, s), order="F") for _ in range(nb)]
+        its_outer = []
+        for k in range(s):
+            rhs = [blk["Aoff"].residual(blk["rhs_b"], view) for blk in blocks]
+            its = []
+            xn = x.copy()
+            for b, blk in enumerate(blocks):
+                xb, r = po.gmres(blk["Aii"], rhs[b], x0=x[blk["r0"]:blk["r0"] + rows], **opts)
+                xn[blk["r0"]:blk["r0"] + rows] = xb
+                its.append(r["its"])
+            x = xn
+            view = x.copy()                              # the exchange: every block sees every x_j
+            its_outer.append(its)
+            for b, blk in enumerate(blocks):
+                S[b][:, k] = x[blk["r0"]:blk["r0"] + rows]
+        norms, lits = [], []
+        xn = x.copy()
+        for b, blk in enumerate(blocks):
+            R = np.stack([blk["Aii"].mult(np.ascontiguousarray(S[b][:, k])) for k in range(s)], axis=1)
+            rhs = blk["Aoff"].residual(blk["rhs_b"], view)
+            alpha, r = po.lsqr([R], [rhs], **outer)
+            xb = po.dense_mult(S[b], alpha)
+            xn[blk["r0"]:blk["r0"] + rows] = xb
+            lits.append(r["its"])
+            norms.append(po.norm2(blk["Aii"].residual(rhs, xb), mode))
+        x = xn                                           # own rows minimized; view unchanged until the next exchange
+        hist.append(norms)
+        lits_all.append(lits)
+        inner_all.append(its_outer)
+        outer_its += 1
+        if all(n <= thr for n in norms) or outer_its >= max_outer:
+            break
+    fin = [po.norm2(blk["Ab"].residual(blk["rhs_b"], x), mode) ** 2 for blk in blocks]
+    err = [po.norm2(x[blk["r0"]:blk["r0"] + rows] - 1.0, mode) ** 2 for blk in blocks]
+    return {"outer_its": outer_its, "norm0": norm0, "hist": hist, "lsqr_its": lits_all, "inner_its": inner_all,
+            "x": x, "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}

@@ -229,6 +229,81 @@ class _Block:
     def error_sq(self):
         return self.po.norm2(self.x - 1.0, self.po.REDUCE_DBR) ** 2
 
+    # local minimization (SMSM-local / AMAM-local), oracle arithmetic
+    def setup_local_minimization(self, s, outer):
+        self.s, self.outer = s, dict(outer, reduce_mode=self.po.REDUCE_DBR)
+        self.S = np.zeros((self.layout.nrows, s), order="F")
+
+    def store_local_column(self, k):
+        self.S[:, k] = self.x
+
+    def local_minimize(self):
+        R = np.stack([self.A.mult(np.ascontiguousarray(self.S[:, k])) for k in range(self.s)], axis=1)
+        self.update_rhs()
+        alpha, r = self.po.lsqr([R], [self.rhs], **self.outer)
+        self.x = self.po.dense_mult(self.S, alpha)
+        return r["rnorm"], r["its"], r["reason"]
+
+
+OUTER = dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
+
+
+def _local_worker(rank, world, port, problem, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    import torch.distributed as dist
+    from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import smsm_local_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        variant, dim, nx, ny, nz, s, rtol, max_it = problem
+        blk = _Block(block_layout(dim, nx, ny, nz, world, rank), po, dict(restart=30, max_it=max_it, rtol=1e-20))
+        blk.setup_local_minimization(s, OUTER)
+        if variant == "smsm_local":
+            res = smsm_local_solve([blk], TorchComm(), s, rtol=rtol, max_outer=100)
+            q.put((rank, res.outer_its, res.norm0, [h[0] for h in res.hist], res.final_norm, blk.x))
+        else:
+            res = am_solve([blk], TorchComm(), rtol=rtol, max_iterations=20000, variant="amam_local", s=s)
+            q.put((rank, res.iterations[0], res.norm0, res.phase_tags[0], res.final_norm, blk.x))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, problem, target):
+    from test_distributed_gloo import _free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, problem, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("world,problem", [(2, (3, 8, 8, 8, 4, 1e-6, 20)), (3, (3, 6, 6, 9, 3, 1e-6, 20))])
+def test_smsm_local_gloo_matches_twin(oracle, world, problem):
+    dim, nx, ny, nz, s, rtol, max_it = problem
+    out = _run(world, ("smsm_local",) + problem, _local_worker)
+    tw = am_twin.smsm_local(oracle, dim, nx, ny, nz, world, s, rtol, dict(restart=30, max_it=max_it, rtol=1e-20),
+                            OUTER)
+    for rank, outer, norm0, hist, fnorm, x in out:
+        assert outer == tw["outer_its"] and norm0 == tw["norm0"] and fnorm == tw["final_norm"]
+        assert hist == [h[rank] for h in tw["hist"]]
+    assert np.array_equal(np.concatenate([o[5] for o in out]), tw["x"])
+
+
+def test_amam_local_gloo_terminates(oracle):
+    out = _run(2, ("amam_local", 3, 8, 8, 8, 4, 1e-6, 5), _local_worker)
+    assert out[0][4] == out[1][4] and out[0][4] <= 1e-3 * out[0][2]
+    assert out[0][3] == out[1][3]
+
 
 def _am_worker(rank, world, port, problem, q):
     sys.path.insert(0, ROOT)
