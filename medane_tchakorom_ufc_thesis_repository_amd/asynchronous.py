@@ -21,7 +21,11 @@ variant "amam_local" is src/asynchronous-multisplitting-asynchronous-minimizatio
 asynchronous-multisplitting-asynchronous-minimization-local_prime.c:371-431: per
 outer iteration s asynchronous inner steps (each stamped with the inner-step
 count), S_i(:,k) = x_i, then the block-local minimization x_i = S_i LSQR(A_ii S_i,
-rhs_i) and one detection step.
+rhs_i) and one detection step.  variant "amam_semi_local" is
+asynchronous-multisplitting-asynchronous-minimization-semi-local_prime.c:350-420: each
+inner step is followed by a second receive and S_i(:,k) = [neighbour planes | x_i];
+then R_i = A_block S_i, alpha_i = LSQR(R_i, b_i) and x_minimized = S_i alpha_i, which
+the reference computes but never scatters back, and the detection step.
 """
 from __future__ import annotations
 
@@ -93,6 +97,16 @@ class AsyncBlock:
             blk.update_rhs()
             self.inner += blk.solve()
             self._publish(self.it)
+        elif variant == "amam_semi_local":                            # AMAM-semi-local_prime.c:350-420
+            for k in range(s):
+                self._receive()
+                blk.update_rhs()
+                self.inner += blk.solve()
+                self._publish(self.steps)
+                self._receive()
+                blk.store_column(k)
+                self.steps += 1
+            blk.semi_local_minimize(apply=False)
         else:                                                         # AMAM-local_prime.c:371-404
             for k in range(s):
                 self._receive()
@@ -123,7 +137,7 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
     """The asynchronous multisplitting loop (asynchronous-multisplitting_prime.c:333-392);
     variant "amam_local" adds the block-local minimization every s inner steps
     (the blocks must have setup_local_minimization(s))."""
-    if variant not in ("am", "amam_local"):
+    if variant not in ("am", "amam_local", "amam_semi_local"):
         raise ValueError(f"unknown asynchronous variant {variant}")
     res = AMResult()
     # global_norm_0 = computeFinalResidualNorm at x = 0 (:322)

@@ -58,6 +58,7 @@ class GpuBlock:
         self.A_off.residual(y, mones, self.b)            # b = y - A_ij (-1) = y + A_ij 1
         del ones, y, mones
         self.prefix = prefix if prefix is not None else f"inner{layout.b + 1}_"
+        self.opts = opts
         self.ksp = initializeKSP(ctx, self.A, False, self.prefix, opts)
         self.last_its = 0
 
@@ -158,6 +159,27 @@ class GpuBlock:
         self.S_loc.mult(self.alpha_loc, self.x)
         return (self.lsqr_loc.get_residual_norm(), self.lsqr_loc.get_iteration_number(),
                 self.lsqr_loc.get_converged_reason())
+
+    # -- semi-local minimization (SMSM-semi-local, AMAM-semi-local)
+    def semi_local_minimize(self, apply: bool = True):
+        """R_i = A_block S_i (own rows of the global R), alpha_i = LSQR(R_i, b_i)
+        (outer_solver_norm_equation_modify, utils.c:1080-1103), x_minimized = S_i alpha_i
+        over the block's rows and neighbour planes; apply: x_i and the halo take it
+        (SMSM-semi-local.c:332-335; the asynchronous variant never applies it)."""
+        if getattr(self, "lsqr_semi", None) is None:
+            self.lsqr_semi = initializeOuterKSP(self.ctx, f"outer{self.layout.b + 1}_", self.opts)
+            self.lsqr_semi.set_operators([self.R])
+            self.alpha_semi = Vec(self.ctx, self.s)
+        self.form_R()
+        self.lsqr_semi.solve([self.b], self.alpha_semi)
+        if apply:
+            self.apply_alpha(self.alpha_semi)
+        else:                                                  # computed and dropped, as the reference does
+            if getattr(self, "xmin_scratch", None) is None:
+                self.xmin_scratch = Vec(self.ctx, self.lo_rows + self.layout.nrows + self.hi_rows)
+            self.S.mult(self.alpha_semi, self.xmin_scratch)
+        return (self.lsqr_semi.get_residual_norm(), self.lsqr_semi.get_iteration_number(),
+                self.lsqr_semi.get_converged_reason())
 
     # -- asynchronous (AM) hooks: asynchronous.py
     def async_recv(self, am, nbr, hoff, cnt):
@@ -409,6 +431,55 @@ def smsm_local_solve(blocks, comm, s: int, rtol: float, atol: float = 1e-100, ma
     comm.barrier()
     res.elapsed = time.perf_counter() - t0
     comm.exchange(blocks)                                        # comm_sync_send_and_receive_final
+    res.final_norm = math.sqrt(comm.ordered_sum(blocks, [blk.block_residual_sq() for blk in blocks]))
+    res.error = math.sqrt(comm.ordered_sum(blocks, [blk.error_sq() for blk in blocks]))
+    return res
+
+
+def smsm_semi_local_solve(blocks, comm, s: int, rtol: float, atol: float = 1e-100, max_outer: int = 10000,
+                          monitor=None) -> LocalMinResult:
+    """SMSM with semi-local minimization (synchronous-multisplitting-synchronous-minimization-
+    semi-local.c:288-345): s times {rhs_i; inner GMRES; exchange; S_i(:,k) = x over the
+    block's rows and neighbour planes}, R_i = A_block S_i, alpha_i = LSQR(R_i, b_i); the
+    local test on the last inner iterate; x_i and the block's view of its neighbours
+    <- S_i alpha_i; stop when every block passes (comm_sync_convergence_detection)."""
+    res = LocalMinResult()
+    res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
+    nb = blocks[0].layout.nb
+    thr = max(atol, rtol / math.sqrt(nb) * res.norm0)
+    for blk in blocks:
+        blk.reset_halo()
+    comm.barrier()
+    t0 = time.perf_counter()
+    while True:
+        its_outer = []
+        for k in range(s):
+            for blk in blocks:
+                blk.update_rhs()
+            its_outer.append([blk.solve() for blk in blocks])
+            comm.exchange(blocks)
+            for blk in blocks:
+                blk.store_column(k)
+        norms, lits = [], []
+        for blk in blocks:
+            norms.append(math.sqrt(blk.local_residual_sq()))      # last inner iterate (:336-337)
+        for blk in blocks:
+            _, li, _ = blk.semi_local_minimize(apply=True)
+            lits.append(li)
+        res.hist.append(norms)
+        res.lsqr_its.append(lits)
+        res.inner_its.append(its_outer)
+        res.outer_its += 1
+        if monitor:
+            monitor(res.outer_its, norms, its_outer, lits)
+        conv = [1.0 if n <= thr else 0.0 for n in norms]
+        if comm.ordered_sum(blocks, conv) == float(nb):
+            break
+        if res.outer_its >= max_outer:
+            break
+    comm.barrier()
+    res.elapsed = time.perf_counter() - t0
+    comm.exchange(blocks)
     res.final_norm = math.sqrt(comm.ordered_sum(blocks, [blk.block_residual_sq() for blk in blocks]))
     res.error = math.sqrt(comm.ordered_sum(blocks, [blk.error_sq() for blk in blocks]))
     return res

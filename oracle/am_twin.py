@@ -373,3 +373,152 @@ def smsm_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=
     err = [po.norm2(x[blk["r0"]:blk["r0"] + rows] - 1.0, mode) ** 2 for blk in blocks]
     return {"outer_its": outer_its, "norm0": norm0, "hist": hist, "lsqr_its": lits_all, "inner_its": inner_all,
             "x": x, "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}
+
+
+def _blocks_ext(po, dim, nx, ny, nz, nb):
+    """Block rows with the ext column space [plane below | own | plane above]."""
+    nz = nz if dim == 3 else 1
+    N = nx * ny * nz
+    rows = N // nb
+    plane = nx * ny if dim == 3 else ny
+    out = []
+    for b in range(nb):
+        r0, r1 = b * rows, (b + 1) * rows
+        if dim == 3:
+            ppb = nz // nb
+            Ab = po.poisson3d_rows(nx, ny, nz, b * ppb, (b + 1) * ppb)
+        else:
+            Ab = po.poisson2d_rows(nx, ny, r0, r1)
+        Aii, Aoff = po.split(Ab, r0, r1)
+        lo = plane if b > 0 else 0
+        hi = plane if b < nb - 1 else 0
+        rp, c, v = Ab.arrays()
+        Aext = po.Mat.from_arrays(rows, lo + rows + hi, rp, c - (r0 - lo), v)
+        out.append(dict(b=b, r0=r0, r1=r1, lo=lo, hi=hi, Ab=Ab, Aii=Aii, Aoff=Aoff, Aext=Aext,
+                        rhs_b=Ab.mult(np.ones(N)), x=np.zeros(rows), view=np.zeros(N),
+                        nbrs=[k for k in (b - 1, b + 1) if 0 <= k < nb], it=0, inner=0, steps=0))
+    return out, N, rows, plane
+
+
+def _ext_col(blk, rows):
+    r0, lo, hi = blk["r0"], blk["lo"], blk["hi"]
+    return np.concatenate([blk["view"][r0 - lo:r0], blk["x"], blk["view"][r0 + rows:r0 + rows + hi]])
+
+
+def _apply_ext(blk, xe, rows):
+    r0, lo, hi = blk["r0"], blk["lo"], blk["hi"]
+    blk["x"] = xe[lo:lo + rows].copy()
+    blk["view"][r0 - lo:r0] = xe[:lo]
+    blk["view"][r0 + rows:r0 + rows + hi] = xe[lo + rows:]
+
+
+def smsm_semi_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000):
+    """SMSM with semi-local minimization (synchronous-multisplitting-synchronous-
+    minimization-semi-local.c): s times {rhs_i, inner GMRES, exchange, S_i(:,k) = x
+    over the block's rows and neighbour planes}, R_i = A_block S_i (own rows),
+    alpha_i = LSQR(R_i, b_i), local test on the last inner iterate, then x_i and the
+    block's view of its neighbours <- S_i alpha_i; stop when every block passes."""
+    mode = po.REDUCE_DBR
+    blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb)
+    norm0 = math.sqrt(sum_ordered([po.norm2(blk["rhs_b"], mode) ** 2 for blk in blocks]))
+    thr = max(atol, rtol / math.sqrt(nb) * norm0)
+    opts = dict(inner, guess_nonzero=1, uirnorm=1, reduce_mode=mode)
+    outer = dict(outer, reduce_mode=mode)
+    hist, lits_all = [], []
+    outer_its = 0
+    while True:
+        S = [np.zeros((blk["lo"] + rows + blk["hi"], s), order="F") for blk in blocks]
+        rhs = [None] * nb
+        for k in range(s):
+            for blk in blocks:
+                rhs[blk["b"]] = blk["Aoff"].residual(blk["rhs_b"], blk["view"])
+            for blk in blocks:
+                blk["x"], r = po.gmres(blk["Aii"], rhs[blk["b"]], x0=blk["x"], **opts)
+            for blk in blocks:                              # exchange
+                for nbr in blk["nbrs"]:
+                    o = blocks[nbr]
+                    blk["view"][o["r0"]:o["r0"] + rows] = o["x"]
+            for blk in blocks:
+                S[blk["b"]][:, k] = _ext_col(blk, rows)
+        norms, lits, alphas = [], [], []
+        for blk in blocks:
+            R = np.stack([blk["Aext"].mult(np.ascontiguousarray(S[blk["b"]][:, k])) for k in range(s)], axis=1)
+            alpha, r = po.lsqr([R], [blk["rhs_b"]], **outer)
+            alphas.append(alpha)
+            lits.append(r["its"])
+            norms.append(po.norm2(blk["Aii"].residual(rhs[blk["b"]], blk["x"]), mode))
+        for blk, alpha in zip(blocks, alphas):
+            _apply_ext(blk, po.dense_mult(S[blk["b"]], alpha), rows)
+        hist.append(norms)
+        lits_all.append(lits)
+        outer_its += 1
+        if all(n <= thr for n in norms) or outer_its >= max_outer:
+            break
+    for blk in blocks:                                      # final exchange
+        for nbr in blk["nbrs"]:
+            o = blocks[nbr]
+            blk["view"][o["r0"]:o["r0"] + rows] = o["x"]
+    x = np.concatenate([blk["x"] for blk in blocks])
+    fin = [po.norm2(blk["Ab"].residual(blk["rhs_b"], x), mode) ** 2 for blk in blocks]
+    err = [po.norm2(blk["x"] - 1.0, mode) ** 2 for blk in blocks]
+    return {"outer_its": outer_its, "norm0": norm0, "hist": hist, "lsqr_its": lits_all, "x": x,
+            "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}
+
+
+def amam_semi_local_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100,
+                               max_iterations=100000, strict=False):
+    """AMAM with semi-local minimization (asynchronous-multisplitting-asynchronous-
+    minimization-semi-local_prime.c:350-420), round-robin: s asynchronous inner
+    steps, each followed by a second receive and S_i(:,k) = [neighbour planes | x_i];
+    R_i = A_block S_i, alpha_i = LSQR(R_i, b_i), x_minimized = S_i alpha_i -- which
+    the reference computes but never scatters back (the iterate is unchanged) --;
+    the local test on the last inner iterate; one detection step."""
+    mode = po.REDUCE_DBR
+    blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb)
+    net = Slots()
+    dets = [Detector(blk["b"], blk["nbrs"], net, strict) for blk in blocks]
+    norm0 = math.sqrt(sum_ordered([po.norm2(blk["rhs_b"], mode) ** 2 for blk in blocks]))
+    thr = max(atol, rtol / math.sqrt(nb) * norm0)
+    opts = dict(inner, guess_nonzero=1, uirnorm=1, reduce_mode=mode)
+    outer = dict(outer, reduce_mode=mode)
+    trace = []
+
+    def receive(blk, det):
+        for d, nbr in enumerate(blk["nbrs"]):
+            m = net.recv(nbr, blk["b"], DATA)
+            if m is not None and det.data_received(d, m[0], m[1]):
+                lo = nbr * rows + (rows - plane if nbr < blk["b"] else 0)
+                blk["view"][lo:lo + plane] = m[2]
+
+    active = list(range(nb))
+    while active:
+        for bi in active:
+            blk, det = blocks[bi], dets[bi]
+            S = np.zeros((blk["lo"] + rows + blk["hi"], s), order="F")
+            for k in range(s):
+                receive(blk, det)
+                rhs = blk["Aoff"].residual(blk["rhs_b"], blk["view"])
+                blk["x"], r = po.gmres(blk["Aii"], rhs, x0=blk["x"], **opts)
+                blk["inner"] += r["its"]
+                for nbr in blk["nbrs"]:
+                    pl = blk["x"][:plane].copy() if nbr < blk["b"] else blk["x"][rows - plane:].copy()
+                    net.send(blk["b"], nbr, DATA, (det.phase, blk["steps"], pl))
+                receive(blk, det)
+                S[:, k] = _ext_col(blk, rows)
+                blk["steps"] += 1
+            R = np.stack([blk["Aext"].mult(np.ascontiguousarray(S[:, k])) for k in range(s)], axis=1)
+            alpha, _ = po.lsqr([R], [blk["rhs_b"]], **outer)
+            po.dense_mult(S, alpha)                         # x_minimized, not used by the reference
+            ln = po.norm2(blk["Aii"].residual(rhs, blk["x"]), mode)
+            det.step(ln <= thr)
+            blk["it"] += 1
+            trace.append((blk["b"], blk["it"], ln, det.state, det.phase))
+            if blk["it"] >= max_iterations:
+                raise RuntimeError("no termination")
+        active = [bi for bi in active if dets[bi].state != FINISHED]
+    x = np.concatenate([blk["x"] for blk in blocks])
+    fin = [po.norm2(blk["Ab"].residual(blk["rhs_b"], x), mode) ** 2 for blk in blocks]
+    err = [po.norm2(blk["x"] - 1.0, mode) ** 2 for blk in blocks]
+    return {"iterations": [blk["it"] for blk in blocks], "inner_its": [blk["inner"] for blk in blocks],
+            "phase_tags": [d.phase for d in dets], "trace": trace, "x": x, "norm0": norm0,
+            "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}

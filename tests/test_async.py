@@ -342,3 +342,12 @@ def test_am_multiprocess_gloo_terminates(world, problem):
     assert all(o[4] == out[0][4] for o in out)                       # one global final residual
     assert out[0][4] <= 10 * rtol * norm0
     assert len({o[2] for o in out}) == 1                             # same phase tag at the verdict
+
+
+def test_semi_local_twins_converge(oracle):
+    outer = dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
+    r = am_twin.smsm_semi_local(oracle, 2, 24, 20, 1, 2, 4, 1e-6, dict(restart=30, max_it=20, rtol=1e-20), outer)
+    assert r["final_norm"] <= 1e-4 * r["norm0"]
+    r = am_twin.amam_semi_local_roundrobin(oracle, 3, 6, 6, 9, 3, 3, 1e-6, dict(restart=30, max_it=5, rtol=1e-20),
+                                           outer)
+    assert r["final_norm"] <= 1e-4 * r["norm0"] and len(set(r["phase_tags"])) == 1

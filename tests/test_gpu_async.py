@@ -79,3 +79,35 @@ def test_smsm_local_gpu_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s):
     assert res.hist == tw["hist"] and res.lsqr_its == tw["lsqr_its"] and res.inner_its == tw["inner_its"]
     assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
     assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,nb,s", [(2, 24, 20, 1, 2, 4), (3, 8, 8, 8, 2, 4), (3, 6, 6, 9, 3, 3)])
+def test_smsm_semi_local_gpu_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s):
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import smsm_semi_local_solve
+    opts = Options(" ".join(f"-inner{b + 1}_ksp_max_it 20 -inner{b + 1}_ksp_rtol 1e-20 -inner{b + 1}_pc_type none"
+                            for b in range(nb)) + " " + _outer_opts(nb))
+    comm = LocalComm()
+    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, range(nb), opts, comm)
+    for blk in blocks:
+        blk.setup_minimization(s)
+    res = smsm_semi_local_solve(blocks, comm, s, rtol=1e-6, max_outer=100)
+    tw = am_twin.smsm_semi_local(oracle, dim, nx, ny, nz, nb, s, 1e-6, dict(restart=30, max_it=20, rtol=1e-20), OUTER)
+    assert res.outer_its == tw["outer_its"] and res.hist == tw["hist"] and res.lsqr_its == tw["lsqr_its"]
+    assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
+    assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,nb,s,max_it", [(2, 24, 20, 1, 2, 4, 5), (3, 6, 6, 9, 3, 3, 3)])
+def test_amam_semi_local_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s, max_it):
+    opts = Options(" ".join(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 "
+                            f"-inner{b + 1}_pc_type none" for b in range(nb)) + " " + _outer_opts(nb))
+    comm = LocalComm()
+    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, range(nb), opts, comm)
+    for blk in blocks:
+        blk.setup_minimization(s)
+    res = am_solve(blocks, comm, rtol=1e-6, record=True, variant="amam_semi_local", s=s)
+    tw = am_twin.amam_semi_local_roundrobin(oracle, dim, nx, ny, nz, nb, s, 1e-6,
+                                            dict(restart=30, max_it=max_it, rtol=1e-20), OUTER)
+    assert res.iterations == tw["iterations"] and res.trace == tw["trace"]
+    assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
+    assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
