@@ -1,0 +1,259 @@
+/* petsc_msplit_ksp.c -- KSPType "msplitgmres": KSPGMRES(restart) with PCNONE on the MI355X. */
+#include <petsc/private/kspimpl.h>
+#include "msplit.h"
+
+typedef struct {
+  msp_ctx *ctx;
+  msp_mat *A;
+  msp_ksp *ksp;
+  msp_vec *b, *x;
+  PetscInt restart;
+  PetscReal haptol, breakdowntol;
+} KSP_MSplit;
+
+#define MSPCall(e) do { int _rc = (e); PetscCheck(!_rc, PETSC_COMM_SELF, _rc, "%s", msp_get_last_error()); } while (0)
+
+static PetscErrorCode KSPSetUp_MSplitGMRES(KSP ksp)
+{
+  KSP_MSplit        *ms = (KSP_MSplit *)ksp->data;
+  Mat                A, Ad;
+  PetscInt           n, nr;
+  const PetscInt    *ia, *ja;
+  const PetscScalar *aa;
+  PetscBool          done;
+
+  PetscFunctionBegin;
+  PetscCall(KSPGetOperators(ksp, &A, NULL));
+  /* npb = 1: the block's operator is one rank's diagonal AIJ block (utils.c:473) */
+  PetscCall(MatMPIAIJGetSeqAIJ(A, &Ad, NULL, NULL));          /* or A itself when it is MATSEQAIJ */
+  PetscCall(MatGetRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &nr, &ia, &ja, &done));
+  PetscCall(MatSeqAIJGetArrayRead(Ad, &aa));
+  if (!ms->ctx) MSPCall(msp_ctx_create(0, NULL, &ms->ctx));   /* device = local rank % ndev in practice */
+  MSPCall(msp_mat_destroy(&ms->A));
+  MSPCall(msp_mat_create_csr(ms->ctx, (int32_t)nr, (int32_t)nr, ia, ja, aa, &ms->A));
+  PetscCall(MatSeqAIJRestoreArrayRead(Ad, &aa));
+  PetscCall(MatRestoreRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &n, &ia, &ja, &done));
+  if (!ms->ksp) MSPCall(msp_ksp_create(ms->ctx, &ms->ksp));
+  MSPCall(msp_ksp_set_operators(ms->ksp, ms->A));
+  if (!ms->b) {
+    MSPCall(msp_vec_create(ms->ctx, nr, &ms->b));
+    MSPCall(msp_vec_create(ms->ctx, nr, &ms->x));
+  }
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static PetscErrorCode KSPSolve_MSplitGMRES(KSP ksp)
+{
+  KSP_MSplit        *ms = (KSP_MSplit *)ksp->data;
+  msp_ksp_opts       o;
+  const PetscScalar *b;
+  PetscScalar       *x;
+  PetscInt           n;
+  int32_t            its, reason;
+  double             rnorm;
+  KSPConvergedDefaultCtx *cctx = (KSPConvergedDefaultCtx *)ksp->cnvP;
+
+  PetscFunctionBegin;
+  MSPCall(msp_ksp_get_default_opts(&o));
+  o.restart       = (int32_t)ms->restart;
+  o.max_it        = (int32_t)ksp->max_it;
+  o.rtol          = ksp->rtol;
+  o.abstol        = ksp->abstol;
+  o.divtol        = ksp->divtol;
+  o.haptol        = ms->haptol;
+  o.breakdowntol  = ms->breakdowntol;
+  o.uirnorm       = cctx ? (int32_t)cctx->initialrtol : 0;   /* KSPConvergedDefaultSetUIRNorm */
+  o.guess_nonzero = ksp->guess_zero ? 0 : 1;
+  MSPCall(msp_ksp_set_opts(ms->ksp, &o));
+  PetscCall(VecGetLocalSize(ksp->vec_rhs, &n));
+  PetscCall(VecGetArrayRead(ksp->vec_rhs, &b));
+  MSPCall(msp_vec_set_values(ms->b, 0, n, b));
+  PetscCall(VecRestoreArrayRead(ksp->vec_rhs, &b));
+  PetscCall(VecGetArray(ksp->vec_sol, &x));
+  if (!ksp->guess_zero) MSPCall(msp_vec_set_values(ms->x, 0, n, x));
+  MSPCall(msp_ksp_solve(ms->ksp, ms->b, ms->x));
+  MSPCall(msp_vec_get_values(ms->x, 0, n, x));
+  PetscCall(VecRestoreArray(ksp->vec_sol, &x));
+  MSPCall(msp_ksp_get_iteration_number(ms->ksp, &its));
+  MSPCall(msp_ksp_get_residual_norm(ms->ksp, &rnorm));
+  MSPCall(msp_ksp_get_converged_reason(ms->ksp, &reason));
+  ksp->its    = its;
+  ksp->rnorm  = rnorm;
+  ksp->reason = (KSPConvergedReason)reason;                  /* same numbering as petscksp.h */
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static PetscErrorCode KSPSetFromOptions_MSplitGMRES(KSP ksp, PetscOptionItems *PetscOptionsObject)
+{
+  KSP_MSplit *ms = (KSP_MSplit *)ksp->data;
+  PetscFunctionBegin;
+  PetscOptionsHeadBegin(PetscOptionsObject, "KSP MSplit GMRES Options");
+  PetscCall(PetscOptionsInt("-ksp_gmres_restart", "Krylov directions", NULL, ms->restart, &ms->restart, NULL));
+  PetscCall(PetscOptionsReal("-ksp_gmres_haptol", "happy breakdown tolerance", NULL, ms->haptol, &ms->haptol, NULL));
+  PetscCall(PetscOptionsReal("-ksp_gmres_breakdown_tolerance", "restart breakdown tolerance", NULL, ms->breakdowntol,
+                             &ms->breakdowntol, NULL));
+  PetscOptionsHeadEnd();
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static PetscErrorCode KSPDestroy_MSplitGMRES(KSP ksp)
+{
+  KSP_MSplit *ms = (KSP_MSplit *)ksp->data;
+  PetscFunctionBegin;
+  msp_vec_destroy(&ms->b);
+  msp_vec_destroy(&ms->x);
+  msp_ksp_destroy(&ms->ksp);
+  msp_mat_destroy(&ms->A);
+  msp_ctx_destroy(&ms->ctx);
+  PetscCall(PetscFree(ksp->data));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+PetscErrorCode KSPCreate_MSplitGMRES(KSP ksp)
+{
+  KSP_MSplit *ms;
+  PetscFunctionBegin;
+  PetscCall(PetscNew(&ms));
+  ms->restart = 30; ms->haptol = 1.0e-30; ms->breakdowntol = 0.1;
+  ksp->data = (void *)ms;
+  PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_PRECONDITIONED, PC_LEFT, 3));
+  PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_UNPRECONDITIONED, PC_RIGHT, 2));
+  ksp->ops->setup          = KSPSetUp_MSplitGMRES;
+  ksp->ops->solve          = KSPSolve_MSplitGMRES;
+  ksp->ops->setfromoptions = KSPSetFromOptions_MSplitGMRES;
+  ksp->ops->destroy        = KSPDestroy_MSplitGMRES;
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+/* ------------------------------------------------------------------------ */
+/* KSPType "msplitlsqr": KSPLSQR with PCNONE and a zero guess on the MI355X, the
+ * outer solver of the minimization variants (outer_solver_norm_equation,
+ * utils.c:1061-1078).  The operator is the block's MATDENSE/MATMPIDENSE R (one
+ * rank per block, as the reference runs it); it is copied to HBM at KSPSetUp
+ * (the drivers call KSPSetOperators every outer iteration, SMSM-global.c:331). */
+typedef struct {
+  msp_ctx *ctx;
+  msp_dense *R;
+  msp_lsqr *lsqr;
+  msp_vec *b, *x;
+  PetscBool exact_norm;
+} KSP_MSplitLSQR;
+
+static PetscErrorCode KSPSetUp_MSplitLSQR(KSP ksp)
+{
+  KSP_MSplitLSQR    *ms = (KSP_MSplitLSQR *)ksp->data;
+  Mat                A, Al;
+  PetscInt           m, n, lda;
+  const PetscScalar *a;
+  PetscBool          isdense;
+
+  PetscFunctionBegin;
+  PetscCall(KSPGetOperators(ksp, &A, NULL));
+  PetscCall(PetscObjectTypeCompare((PetscObject)A, MATMPIDENSE, &isdense));
+  if (isdense) PetscCall(MatDenseGetLocalMatrix(A, &Al));
+  else Al = A;
+  PetscCall(MatGetSize(Al, &m, &n));
+  PetscCall(MatDenseGetLDA(Al, &lda));
+  if (!ms->ctx) MSPCall(msp_ctx_create(0, NULL, &ms->ctx));
+  MSPCall(msp_dense_destroy(&ms->R));
+  MSPCall(msp_dense_create(ms->ctx, m, (int32_t)n, &ms->R));
+  PetscCall(MatDenseGetArrayRead(Al, &a));
+  MSPCall(msp_dense_set_values(ms->R, a, lda));
+  PetscCall(MatDenseRestoreArrayRead(Al, &a));
+  if (!ms->lsqr) MSPCall(msp_lsqr_create(ms->ctx, &ms->lsqr));
+  MSPCall(msp_lsqr_set_operators(ms->lsqr, 1, &ms->R));
+  MSPCall(msp_vec_destroy(&ms->b));
+  MSPCall(msp_vec_destroy(&ms->x));
+  MSPCall(msp_vec_create(ms->ctx, m, &ms->b));
+  MSPCall(msp_vec_create(ms->ctx, n, &ms->x));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static PetscErrorCode KSPSolve_MSplitLSQR(KSP ksp)
+{
+  KSP_MSplitLSQR    *ms = (KSP_MSplitLSQR *)ksp->data;
+  msp_lsqr_opts      o;
+  const PetscScalar *b;
+  PetscScalar       *x;
+  PetscInt           m, n;
+  int32_t            its, reason;
+  double             rnorm;
+
+  PetscFunctionBegin;
+  MSPCall(msp_lsqr_get_default_opts(&o));
+  o.max_it     = (int32_t)ksp->max_it;
+  o.rtol       = ksp->rtol;
+  o.abstol     = ksp->abstol;
+  o.divtol     = ksp->divtol;
+  o.exact_norm = ms->exact_norm ? 1 : 0;
+  if (ksp->converged == KSPConvergedDefault) o.conv_test = MSP_LSQR_CONV_DEFAULT;   /* -ksp_convergence_test default */
+  else if (ksp->converged == KSPConvergedSkip) o.conv_test = MSP_LSQR_CONV_SKIP;
+  else o.conv_test = MSP_LSQR_CONV_LSQR;                                          /* KSPLSQRConvergedDefault */
+  MSPCall(msp_lsqr_set_opts(ms->lsqr, &o));
+  PetscCall(VecGetLocalSize(ksp->vec_rhs, &m));
+  PetscCall(VecGetArrayRead(ksp->vec_rhs, &b));
+  MSPCall(msp_vec_set_values(ms->b, 0, m, b));
+  PetscCall(VecRestoreArrayRead(ksp->vec_rhs, &b));
+  MSPCall(msp_lsqr_solve(ms->lsqr, &ms->b, ms->x));               /* zero initial guess */
+  PetscCall(VecGetLocalSize(ksp->vec_sol, &n));
+  PetscCall(VecGetArray(ksp->vec_sol, &x));
+  MSPCall(msp_vec_get_values(ms->x, 0, n, x));
+  PetscCall(VecRestoreArray(ksp->vec_sol, &x));
+  MSPCall(msp_lsqr_get_iteration_number(ms->lsqr, &its));
+  MSPCall(msp_lsqr_get_residual_norm(ms->lsqr, &rnorm));
+  MSPCall(msp_lsqr_get_converged_reason(ms->lsqr, &reason));
+  ksp->its    = its;
+  ksp->rnorm  = rnorm;                                             /* KSPGetResidualNorm, SMSM-global.c:341 */
+  ksp->reason = (KSPConvergedReason)reason;
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static PetscErrorCode KSPSetFromOptions_MSplitLSQR(KSP ksp, PetscOptionItems *PetscOptionsObject)
+{
+  KSP_MSplitLSQR *ms = (KSP_MSplitLSQR *)ksp->data;
+  PetscFunctionBegin;
+  PetscOptionsHeadBegin(PetscOptionsObject, "KSP MSplit LSQR Options");
+  PetscCall(PetscOptionsBool("-ksp_lsqr_exact_mat_norm", "exact Frobenius norm of the operator", NULL,
+                             ms->exact_norm, &ms->exact_norm, NULL));
+  PetscOptionsHeadEnd();
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static PetscErrorCode KSPDestroy_MSplitLSQR(KSP ksp)
+{
+  KSP_MSplitLSQR *ms = (KSP_MSplitLSQR *)ksp->data;
+  PetscFunctionBegin;
+  msp_vec_destroy(&ms->b);
+  msp_vec_destroy(&ms->x);
+  msp_lsqr_destroy(&ms->lsqr);
+  msp_dense_destroy(&ms->R);
+  msp_ctx_destroy(&ms->ctx);
+  PetscCall(PetscFree(ksp->data));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+PetscErrorCode KSPCreate_MSplitLSQR(KSP ksp)
+{
+  KSP_MSplitLSQR *ms;
+  PetscFunctionBegin;
+  PetscCall(PetscNew(&ms));
+  ksp->data = (void *)ms;
+  PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_UNPRECONDITIONED, PC_LEFT, 3));
+  PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_NONE, PC_LEFT, 1));
+  PetscCall(KSPSetConvergenceTest(ksp, KSPLSQRConvergedDefault, NULL, NULL)); /* as KSPCreate_LSQR */
+  ksp->ops->setup          = KSPSetUp_MSplitLSQR;
+  ksp->ops->solve          = KSPSolve_MSplitLSQR;
+  ksp->ops->setfromoptions = KSPSetFromOptions_MSplitLSQR;
+  ksp->ops->destroy        = KSPDestroy_MSplitLSQR;
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+/* Call once after PetscInitialize (or load as a PETSc dynamic library):
+ *   -inner1_ksp_type msplitgmres ... -outer1_ksp_type msplitlsqr ... */
+PetscErrorCode MSplitRegisterAll(void)
+{
+  PetscFunctionBegin;
+  PetscCall(KSPRegister("msplitgmres", KSPCreate_MSplitGMRES));
+  PetscCall(KSPRegister("msplitlsqr", KSPCreate_MSplitLSQR));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
