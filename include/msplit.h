@@ -124,6 +124,15 @@ int msp_mat_create_box_stencil(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, in
  * operator of R = A S in the minimization variants (SMSM-global.c:326). */
 int msp_mat_create_box_stencil_ext(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
                                    int32_t hi, msp_mat **A);
+/* The convection-diffusion operator of BASELINE configs[4] (build-defined; the
+ * reference has only Poisson): h^2 (-Lap u + beta . grad u), first-order upwind,
+ * constant beta given as cell Peclet numbers peclet[d] = beta_d h / 2 (x fastest;
+ * in 2D x and the line direction).  Lower neighbour in d: -1 - 2 max(P_d, 0);
+ * upper: -1 + 2 min(P_d, 0); diagonal 2*dim + 2 sum |P_d| (summed x, y, z).
+ * peclet = NULL or zeros gives the Poisson stencil bit for bit.  Same block /
+ * column layout as msp_mat_create_box_stencil_ext. */
+int msp_mat_create_box_convdiff(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo, int32_t hi,
+                                const double *peclet, msp_mat **A);
 int msp_mat_destroy(msp_mat **A);
 int msp_mat_get_info(const msp_mat *A, int32_t *nrows, int32_t *ncols, int64_t *nnz);
 /* Download the CSR (host buffers of nrows+1 / nnz entries); synchronising. */

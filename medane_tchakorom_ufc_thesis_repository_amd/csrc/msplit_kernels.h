@@ -20,6 +20,10 @@ struct Vecs {
 struct Coefs {
   double a[MSK_MAX_GROUP];
 };
+// constant 7-point stencil values: slow-, y-, x-, diagonal, x+, y+, slow+
+struct BoxCoef {
+  double c[7];
+};
 
 // SpMV modes
 enum { MSK_SPMV_MULT = 0, MSK_SPMV_RESID = 1, MSK_SPMV_SCALED = 2 };
@@ -51,7 +55,7 @@ int msk_spmm(int32_t nrows, const int32_t* rowptr, const int32_t* col, const dou
 int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int32_t* rowptr, const int32_t* col,
                   const double* val, const double* x, const double* b, double* y, int resid, hipStream_t s);
 // lo/hi: extra coupling columns to the neighbour plane below/above (column space [lo | block | hi])
-int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi, int32_t* rowptr,
-                    int32_t* col, double* val, hipStream_t s);
+int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi, const BoxCoef* cf,
+                    int32_t* rowptr, int32_t* col, double* val, hipStream_t s);
 int msk_blas1(int op, double* y, const double* x, const double* z, double alpha, int64_t n, hipStream_t s);
 }

@@ -527,8 +527,10 @@ __device__ __forceinline__ int64_t box_rowptr(int dim, int64_t l, int64_t nx, in
 // columns before / after the block's own: column space [plane_lo | block |
 // plane_hi], still ascending in global order (the rows of the reference's
 // A_block_jacobi, utils.c:30-121 / :247-293, with their column ids shifted).
+// coef: the 7 constant stencil values (slow-, y-, x-, diagonal, x+, y+, slow+);
+// the Poisson operator is {-1,-1,-1,6,-1,-1,-1} (3D) / {-1,0,-1,4,-1,0,-1} (2D).
 __global__ __launch_bounds__(kT) void k_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows,
-                                                    int lo, int hi, int32_t* __restrict__ rowptr,
+                                                    int lo, int hi, BoxCoef cf, int32_t* __restrict__ rowptr,
                                                     int32_t* __restrict__ col, double* __restrict__ val) {
   const int64_t stride = (int64_t)gridDim.x * kT;
   const int64_t P = dim == 3 ? (int64_t)nx * ny : (int64_t)nx;  // slab plane
@@ -545,14 +547,13 @@ __global__ __launch_bounds__(kT) void k_box_stencil(int dim, int32_t nx, int32_t
     const int64_t sl = l / P;  // slab-plane index (k in 3D, j in 2D)
     const int64_t e = l + off;
     int64_t p = p0;
-    const double diag = dim == 3 ? 6.0 : 4.0;
-    if (sl > 0 || lo) { col[p] = (int32_t)(e - P); val[p++] = -1.0; }
-    if (dim == 3 && j > 0) { col[p] = (int32_t)(e - nx); val[p++] = -1.0; }
-    if (i > 0) { col[p] = (int32_t)(e - 1); val[p++] = -1.0; }
-    col[p] = (int32_t)e; val[p++] = diag;
-    if (i < nx - 1) { col[p] = (int32_t)(e + 1); val[p++] = -1.0; }
-    if (dim == 3 && j < ny - 1) { col[p] = (int32_t)(e + nx); val[p++] = -1.0; }
-    if (sl < ns - 1 || hi) { col[p] = (int32_t)(e + P); val[p++] = -1.0; }
+    if (sl > 0 || lo) { col[p] = (int32_t)(e - P); val[p++] = cf.c[0]; }
+    if (dim == 3 && j > 0) { col[p] = (int32_t)(e - nx); val[p++] = cf.c[1]; }
+    if (i > 0) { col[p] = (int32_t)(e - 1); val[p++] = cf.c[2]; }
+    col[p] = (int32_t)e; val[p++] = cf.c[3];
+    if (i < nx - 1) { col[p] = (int32_t)(e + 1); val[p++] = cf.c[4]; }
+    if (dim == 3 && j < ny - 1) { col[p] = (int32_t)(e + nx); val[p++] = cf.c[5]; }
+    if (sl < ns - 1 || hi) { col[p] = (int32_t)(e + P); val[p++] = cf.c[6]; }
   }
 }
 
@@ -701,9 +702,9 @@ extern "C" int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int3
 }
 
 extern "C" int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi,
-                               int32_t* rowptr, int32_t* col, double* val, hipStream_t s) {
+                               const BoxCoef* cf, int32_t* rowptr, int32_t* col, double* val, hipStream_t s) {
   const int g = grid_for(nrows + 1, 8192);
-  k_box_stencil<<<dim3(g), dim3(kT), 0, s>>>(dim, nx, ny, nz, nrows, lo, hi, rowptr, col, val);
+  k_box_stencil<<<dim3(g), dim3(kT), 0, s>>>(dim, nx, ny, nz, nrows, lo, hi, *cf, rowptr, col, val);
   return (int)hipGetLastError();
 }
 

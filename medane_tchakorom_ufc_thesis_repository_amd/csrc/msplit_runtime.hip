@@ -463,8 +463,29 @@ extern "C" int msp_mat_create_csr_rows(msp_ctx* c, int32_t nrows, int32_t ncols,
   return MSP_SUCCESS;
 }
 
-extern "C" int msp_mat_create_box_stencil_ext(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
-                                              int32_t hi, msp_mat** out) {
+// The 7 stencil values of the upwind convection-diffusion operator h^2 (-Lap u + beta . grad u)
+// in cell Peclet numbers P_d = beta_d h / 2 (x fastest; 2D: x and the line direction y):
+//   lower neighbour in d: -1 - 2 max(P_d, 0), upper: -1 + 2 min(P_d, 0),
+//   diagonal ((2*dim + 2|Px|) + 2|Py|) (+ 2|Pz| in 3D); P = 0 is the Poisson operator, exactly.
+static BoxCoef box_coefs(int dim, const double* P) {
+  const double px = P ? P[0] : 0.0, py = P ? P[1] : 0.0, pz = (P && dim == 3) ? P[2] : 0.0;
+  auto cm = [](double p) { return -1.0 - 2.0 * (p > 0.0 ? p : 0.0); };
+  auto cp = [](double p) { return -1.0 + 2.0 * (p < 0.0 ? p : 0.0); };
+  BoxCoef c;
+  if (dim == 3) {
+    c.c[0] = cm(pz); c.c[1] = cm(py); c.c[2] = cm(px);
+    c.c[3] = ((6.0 + 2.0 * fabs(px)) + 2.0 * fabs(py)) + 2.0 * fabs(pz);
+    c.c[4] = cp(px); c.c[5] = cp(py); c.c[6] = cp(pz);
+  } else {
+    c.c[0] = cm(py); c.c[1] = 0.0; c.c[2] = cm(px);
+    c.c[3] = (4.0 + 2.0 * fabs(px)) + 2.0 * fabs(py);
+    c.c[4] = cp(px); c.c[5] = 0.0; c.c[6] = cp(py);
+  }
+  return c;
+}
+
+extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
+                                           int32_t hi, const double* peclet, msp_mat** out) {
   ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");
   ARGCHK(dim == 2 || dim == 3, MSP_ERR_ARG_WRONG, "dim must be 2 or 3, got %d", dim);
   if (dim == 2) nz = 1;
@@ -493,10 +514,18 @@ extern "C" int msp_mat_create_box_stencil_ext(msp_ctx* c, int dim, int32_t nx, i
     msp_mat_destroy(&A);
     return rc;
   }
-  KCHK(msk_box_stencil(dim, nx, ny, nz, nrows, lo, hi, A->rowptr, A->col, A->val, c->stream));
+  ARGCHK(!peclet || (std::isfinite(peclet[0]) && std::isfinite(peclet[1]) && std::isfinite(peclet[2])),
+         MSP_ERR_ARG_WRONG, "Peclet numbers must be finite");
+  const BoxCoef cf = box_coefs(dim, peclet);
+  KCHK(msk_box_stencil(dim, nx, ny, nz, nrows, lo, hi, &cf, A->rowptr, A->col, A->val, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   *out = A;
   return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_create_box_stencil_ext(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
+                                              int32_t hi, msp_mat** out) {
+  return msp_mat_create_box_convdiff(c, dim, nx, ny, nz, lo, hi, nullptr, out);
 }
 
 extern "C" int msp_mat_create_box_stencil(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, msp_mat** out) {

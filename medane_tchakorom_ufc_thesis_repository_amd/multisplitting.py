@@ -35,7 +35,8 @@ class GpuBlock:
         self.layout = layout
         n = layout.nrows
         dim, bx, by, bz = layout.box
-        self.A = Mat.box_stencil(ctx, dim, bx, by, bz)
+        self.peclet = tuple(getattr(layout, "peclet", (0.0, 0.0, 0.0)))
+        self.A = Mat.box_convdiff(ctx, dim, bx, by, bz, False, False, self.peclet)
         row_ids, rowptr, col, val = layout.coupling
         self.A_off = Mat.from_csr_rows(ctx, n, layout.halo_size, row_ids, rowptr, col, val)
         self.halo, self.halo_t = comm.alloc(ctx, layout.halo_size)
@@ -48,15 +49,12 @@ class GpuBlock:
         self.rhs = Vec(ctx, n)
         self.r = Vec(ctx, n)
         # computeTheRightHandSideWithInitialGuess (utils.c:623-650): b_i = A_block u, u = 1,
-        # as A_ii u + A_ij u_halo (integer-valued rows: exact in any order)
-        ones = Vec(ctx, n)
+        # over the block's full rows in ascending-column order (MatMult_SeqAIJ)
+        self._ensure_ext()
+        ones = Vec(ctx, self.lo_rows + n + self.hi_rows)
         ones.set(1.0)
-        y = Vec(ctx, n)
-        self.A.mult(ones, y)
-        mones = Vec(ctx, layout.halo_size)
-        mones.set(-1.0)
-        self.A_off.residual(y, mones, self.b)            # b = y - A_ij (-1) = y + A_ij 1
-        del ones, y, mones
+        self.A_ext.mult(ones, self.b)
+        del ones
         self.prefix = prefix if prefix is not None else f"inner{layout.b + 1}_"
         self.opts = opts
         self.ksp = initializeKSP(ctx, self.A, False, self.prefix, opts)
@@ -130,7 +128,8 @@ class GpuBlock:
         self.lo_rows = L.plane if any(nbr < L.b for nbr, *_ in L.recv) else 0
         self.hi_rows = L.plane if any(nbr > L.b for nbr, *_ in L.recv) else 0
         dim, bx, by, bz = L.box
-        self.A_ext = Mat.box_stencil_ext(self.ctx, dim, bx, by, bz, self.lo_rows > 0, self.hi_rows > 0)
+        self.A_ext = Mat.box_convdiff(self.ctx, dim, bx, by, bz, self.lo_rows > 0, self.hi_rows > 0,
+                                      getattr(self, "peclet", (0.0, 0.0, 0.0)))
 
     # -- local minimization (SMSM-local, AMAM-local) hooks
     def setup_local_minimization(self, s: int, opts: Options | None, prefix: str | None = None):
@@ -373,8 +372,9 @@ def smsm_solve(blocks, comm, s: int, minimizer, rtol: float, atol: float = 1e-10
     return res
 
 
-def make_blocks(ctx: Context, dim, nx, ny, nz, nb, block_ids, opts: Options | None, comm):
-    return [GpuBlock(ctx, block_layout(dim, nx, ny, nz, nb, b), opts, comm) for b in block_ids]
+def make_blocks(ctx: Context, dim, nx, ny, nz, nb, block_ids, opts: Options | None, comm, peclet=None):
+    """GpuBlocks of the Poisson operator, or (peclet) the upwind convection-diffusion one."""
+    return [GpuBlock(ctx, block_layout(dim, nx, ny, nz, nb, b, peclet), opts, comm) for b in block_ids]
 
 
 @dataclass
@@ -485,9 +485,9 @@ def smsm_semi_local_solve(blocks, comm, s: int, rtol: float, atol: float = 1e-10
     return res
 
 
-def make_smsm(ctx: Context, dim, nx, ny, nz, nb, block_ids, s: int, opts: Options | None, comm):
+def make_smsm(ctx: Context, dim, nx, ny, nz, nb, block_ids, s: int, opts: Options | None, comm, peclet=None):
     """GpuBlocks with the minimization storage, and the GpuMinimizer over them."""
-    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, block_ids, opts, comm)
+    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, block_ids, opts, comm, peclet)
     for blk in blocks:
         blk.setup_minimization(s)
     return blocks, GpuMinimizer(ctx, blocks, comm, opts)

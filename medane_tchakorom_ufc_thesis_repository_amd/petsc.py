@@ -296,6 +296,15 @@ class Mat:
              1 if hi else 0, C.byref(h))
         return cls(ctx, h)
 
+    @classmethod
+    def box_convdiff(cls, ctx: Context, dim: int, nx: int, ny: int, nz: int, lo: bool, hi: bool, peclet) -> "Mat":
+        """The upwind convection-diffusion stencil (msp_mat_create_box_convdiff): BASELINE configs[4]'s operator."""
+        pe = np.ascontiguousarray(peclet, np.float64)
+        h = C.c_void_p()
+        call("msp_mat_create_box_convdiff", ctx.h, int(dim), int(nx), int(ny), int(nz), 1 if lo else 0,
+             1 if hi else 0, _dp(pe), C.byref(h))
+        return cls(ctx, h)
+
     def mat_mult_dense(self, S: "DenseMat", R: "DenseMat"):        # MatMatMult(A, S, MAT_REUSE_MATRIX, &R)
         call("msp_mat_matmult_dense", self.h, S.h, R.h)
 

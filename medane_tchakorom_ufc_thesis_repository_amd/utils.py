@@ -111,6 +111,7 @@ class BlockLayout:
     send: list = field(default_factory=list)   # (nbr, local_off, count)
     halo_size: int = 0
     coupling: tuple = ()                        # (row_ids, rowptr, col(halo idx), val)
+    peclet: tuple = (0.0, 0.0, 0.0)             # operator: Poisson (0) or upwind convection-diffusion
 
     @property
     def nrows(self):
@@ -124,11 +125,28 @@ class BlockLayout:
         return 2, self.ny, self.nrows // self.ny, 1
 
 
-def block_layout(dim, nx, ny, nz, nb, b) -> BlockLayout:
+def convdiff_coefs(dim, peclet=None):
+    """The 7 stencil values (slow-, y-, x-, diagonal, x+, y+, slow+) of the upwind
+    convection-diffusion operator h^2(-Lap u + beta.grad u) in cell Peclet numbers
+    P_d = beta_d h / 2 (x fastest; 2D: x and the line direction).  P = 0 is the
+    reference's Poisson stencil exactly (msplit.h, msp_mat_create_box_convdiff)."""
+    px, py, pz = (tuple(float(v) for v in peclet) + (0.0, 0.0, 0.0))[:3] if peclet is not None else (0.0, 0.0, 0.0)
+    if dim == 2:
+        pz = 0.0
+    cm = lambda p: -1.0 - 2.0 * max(p, 0.0)
+    cp = lambda p: -1.0 + 2.0 * min(p, 0.0)
+    if dim == 3:
+        return [cm(pz), cm(py), cm(px), ((6.0 + 2.0 * abs(px)) + 2.0 * abs(py)) + 2.0 * abs(pz),
+                cp(px), cp(py), cp(pz)]
+    return [cm(py), 0.0, cm(px), (4.0 + 2.0 * abs(px)) + 2.0 * abs(py), cp(px), 0.0, cp(py)]
+
+
+def block_layout(dim, nx, ny, nz, nb, b, peclet=None) -> BlockLayout:
     """Slab partition of the reference's stencil into nb blocks.
     dim 3: nx x ny x nz grid, block b = planes [b*nz/nb, (b+1)*nz/nb).
     dim 2: m = nx mesh lines x n = ny mesh columns (poisson2DMatrix numbering),
-    block b = rows [b*N/nb, (b+1)*N/nb), whole mesh lines only."""
+    block b = rows [b*N/nb, (b+1)*N/nb), whole mesh lines only.
+    peclet: the convection-diffusion operator's coupling values instead of -1."""
     if dim == 3:
         if nz % nb:
             raise ValueError(f"nz={nz} must be divisible by the number of blocks {nb}")
@@ -160,24 +178,28 @@ def block_layout(dim, nx, ny, nz, nb, b) -> BlockLayout:
         hi_off = off
         off += plane
     L.halo_size = off
+    L.peclet = tuple(peclet) if peclet is not None else (0.0, 0.0, 0.0)
+    cf = convdiff_coefs(dim, peclet)
     # coupling rows: row l couples to halo lo_off + l (below) and/or hi_off + (l - (nloc-plane)) (above);
     # halo numbering is ascending in global column, so per-row column order is PETSc's.
-    ent_r, ent_c = [], []
+    ent_r, ent_c, ent_v = [], [], []
     if rows_lo.size:
         ent_r.append(rows_lo)
         ent_c.append(lo_off + rows_lo)
+        ent_v.append(np.full(rows_lo.size, cf[0]))
     if rows_hi.size:
         ent_r.append(rows_hi)
         ent_c.append(hi_off + (rows_hi - (nloc - plane)))
+        ent_v.append(np.full(rows_hi.size, cf[6]))
     if ent_r:
         r = np.concatenate(ent_r)
         c = np.concatenate(ent_c)
+        v = np.concatenate(ent_v)
         order = np.lexsort((c, r))
-        r, c = r[order], c[order]
+        r, c, v = r[order], c[order], v[order]
         row_ids, counts = np.unique(r, return_counts=True)
         rowptr = np.concatenate([[0], np.cumsum(counts)])
-        L.coupling = (row_ids.astype(np.int32), rowptr.astype(np.int32), c.astype(np.int32),
-                      np.full(c.size, -1.0))
+        L.coupling = (row_ids.astype(np.int32), rowptr.astype(np.int32), c.astype(np.int32), v)
     else:
         L.coupling = (np.zeros(0, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32), np.zeros(0))
     return L

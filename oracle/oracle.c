@@ -134,6 +134,47 @@ int orc_poisson2d_complete(int m, int n, orc_csr *A) {
  * MatCreateSubMatrix(A_block, own rows, cols of block i).  Here the diagonal
  * block gets local columns and every off-block column goes to one coupling
  * matrix (global ids), which for 2 blocks is exactly the reference's A_ij. */
+static double cd_lower(double p) { return -1.0 - 2.0 * (p > 0.0 ? p : 0.0); }
+static double cd_upper(double p) { return -1.0 + 2.0 * (p < 0.0 ? p : 0.0); }
+
+int orc_convdiff_rows(int dim, int nx, int ny, int nz, int64_t row0, int64_t row1, const double *P, orc_csr *A) {
+  if (dim != 2 && dim != 3) return ORC_ERR_ARG;
+  const int64_t n = row1 - row0;
+  const int64_t N = (int64_t)nx * ny * (dim == 3 ? nz : 1);
+  if (n < 0 || row0 < 0 || row1 > N) return ORC_ERR_ARG;
+  int rc = csr_alloc(A, n, N, 7 * n);
+  if (rc) return rc;
+  const double px = P[0], py = P[1], pz = dim == 3 ? P[2] : 0.0;
+  int64_t p = 0;
+  A->rowptr[0] = 0;
+  for (int64_t g = row0; g < row1; ++g) {
+    const int64_t l = g - row0;
+    if (dim == 3) {
+      const int64_t i = g % nx, j = (g / nx) % ny, k = g / ((int64_t)nx * ny), pl = (int64_t)nx * ny;
+      const double diag = ((6.0 + 2.0 * fabs(px)) + 2.0 * fabs(py)) + 2.0 * fabs(pz);
+      if (k > 0) { A->col[p] = (int32_t)(g - pl); A->val[p++] = cd_lower(pz); }
+      if (j > 0) { A->col[p] = (int32_t)(g - nx); A->val[p++] = cd_lower(py); }
+      if (i > 0) { A->col[p] = (int32_t)(g - 1); A->val[p++] = cd_lower(px); }
+      A->col[p] = (int32_t)g; A->val[p++] = diag;
+      if (i < nx - 1) { A->col[p] = (int32_t)(g + 1); A->val[p++] = cd_upper(px); }
+      if (j < ny - 1) { A->col[p] = (int32_t)(g + nx); A->val[p++] = cd_upper(py); }
+      if (k < nz - 1) { A->col[p] = (int32_t)(g + pl); A->val[p++] = cd_upper(pz); }
+    } else {
+      /* nx = m mesh lines, ny = n mesh columns (poisson2DMatrix numbering): line = g / n */
+      const int64_t m = nx, nn = ny, line = g / nn, c = g % nn;
+      const double diag = (4.0 + 2.0 * fabs(px)) + 2.0 * fabs(py);
+      if (line > 0) { A->col[p] = (int32_t)(g - nn); A->val[p++] = cd_lower(py); }
+      if (c > 0) { A->col[p] = (int32_t)(g - 1); A->val[p++] = cd_lower(px); }
+      A->col[p] = (int32_t)g; A->val[p++] = diag;
+      if (c < nn - 1) { A->col[p] = (int32_t)(g + 1); A->val[p++] = cd_upper(px); }
+      if (line < m - 1) { A->col[p] = (int32_t)(g + nn); A->val[p++] = cd_upper(py); }
+    }
+    A->rowptr[l + 1] = (int32_t)p;
+  }
+  A->nnz = p;
+  return ORC_OK;
+}
+
 int orc_split(const orc_csr *Ab, int64_t c0, int64_t c1, orc_csr *Aii, orc_csr *Aoff) {
   int64_t nin = 0, nout = 0;
   for (int64_t k = 0; k < Ab->nnz; ++k) {
@@ -550,16 +591,19 @@ double orc_final_residual_norm(int mode, int nb, const orc_csr *const *Ab, const
 }
 
 static int build_block(const orc_sm_problem *p, int b, orc_csr *Ablock, int64_t *r0, int64_t *r1) {
+  const int cd = p->peclet[0] != 0.0 || p->peclet[1] != 0.0 || p->peclet[2] != 0.0;
   if (p->dim == 3) {
     const int ppb = p->nz / p->nb;
     const int64_t nxny = (int64_t)p->nx * p->ny;
     *r0 = (int64_t)b * ppb * nxny;
     *r1 = (int64_t)(b + 1) * ppb * nxny;
+    if (cd) return orc_convdiff_rows(3, p->nx, p->ny, p->nz, *r0, *r1, p->peclet, Ablock);
     return orc_poisson3d_rows(p->nx, p->ny, p->nz, b * ppb, (b + 1) * ppb, Ablock);
   }
   const int64_t N = (int64_t)p->nx * p->ny, rbs = N / p->nb;
   *r0 = b * rbs;
   *r1 = (b + 1) * rbs;
+  if (cd) return orc_convdiff_rows(2, p->nx, p->ny, 1, *r0, *r1, p->peclet, Ablock);
   return orc_poisson2d_rows(p->nx, p->ny, *r0, *r1, Ablock);
 }
 
@@ -927,7 +971,8 @@ int orc_smsm_solve(const orc_smsm_problem *p, const orc_gmres_opts *inner, const
   if (nb < 1 || s < 1 || (p->dim != 2 && p->dim != 3)) return ORC_ERR_ARG;
   if (p->dim == 3 && p->nz % nb) return ORC_ERR_ARG;
   if (p->dim == 2 && ((int64_t)p->nx * p->ny) % nb) return ORC_ERR_ARG;
-  orc_sm_problem sp = {p->dim, p->nx, p->ny, p->nz, nb, p->rtol, p->atol, p->max_outer};
+  orc_sm_problem sp = {p->dim, p->nx, p->ny, p->nz, nb, p->rtol, p->atol, p->max_outer,
+                       {p->peclet[0], p->peclet[1], p->peclet[2]}};
   const int64_t N = (int64_t)p->nx * p->ny * (p->dim == 3 ? p->nz : 1);
   const int mode = inner->reduce_mode;
   orc_csr *Ab = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));

@@ -88,6 +88,12 @@ int orc_poisson3d_rows(int nx, int ny, int nz, int z0, int z1, orc_csr *A);
 int orc_poisson2d_rows(int m, int n, int64_t row0, int64_t row1, orc_csr *A);
 /* poisson2DMatrix_complete: full N = m*n square matrix, Ii = i*m + j. */
 int orc_poisson2d_complete(int m, int n, orc_csr *A);
+/* Convection-diffusion rows (BASELINE configs[4]; build-defined, the reference has only
+ * Poisson): h^2(-Lap u + beta.grad u), first-order upwind, peclet[d] = beta_d h / 2, x fastest.
+ * dim 3: rows of planes [z0,z1) of nx*ny*nz; dim 2: rows [row0,row1) of the m = ny... see oracle.c.
+ * Lower neighbour in d: -1 - 2 max(P_d,0); upper: -1 + 2 min(P_d,0); diagonal
+ * ((2 dim + 2|Px|) + 2|Py|) (+ 2|Pz|).  Global columns, ascending. */
+int orc_convdiff_rows(int dim, int nx, int ny, int nz, int64_t row0, int64_t row1, const double *peclet, orc_csr *A);
 /* Block split: A_ii = columns in [c0,c1) shifted by -c0; A_off = the other columns (kept global). */
 int orc_split(const orc_csr *Ablock, int64_t c0, int64_t c1, orc_csr *Aii, orc_csr *Aoff);
 
@@ -139,6 +145,7 @@ typedef struct {
   double rtol;        /* -rtol (outer) */
   double atol;        /* 1e-100 (synchronous-multisplitting.c:34) */
   int max_outer;      /* safety cap (the reference loops until convergence) */
+  double peclet[3];   /* 0: the reference's Poisson operator; else orc_convdiff_rows */
 } orc_sm_problem;
 
 typedef struct {
@@ -198,6 +205,7 @@ typedef struct {
   double rtol;        /* -rtol (outer) */
   double atol;        /* 1e-100 (SMSM-global.c:33) */
   int max_outer;      /* safety cap */
+  double peclet[3];   /* as orc_sm_problem */
 } orc_smsm_problem;
 
 typedef struct {

@@ -47,7 +47,8 @@ class GmresResult(C.Structure):
 
 class SMProblem(C.Structure):
     _fields_ = [("dim", C.c_int), ("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("nb", C.c_int),
-                ("rtol", C.c_double), ("atol", C.c_double), ("max_outer", C.c_int)]
+                ("rtol", C.c_double), ("atol", C.c_double), ("max_outer", C.c_int),
+                ("peclet", C.c_double * 3)]
 
 
 class SMResult(C.Structure):
@@ -67,7 +68,8 @@ class LsqrResult(C.Structure):
 
 class SMSMProblem(C.Structure):
     _fields_ = [("dim", C.c_int), ("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("nb", C.c_int),
-                ("s", C.c_int), ("rtol", C.c_double), ("atol", C.c_double), ("max_outer", C.c_int)]
+                ("s", C.c_int), ("rtol", C.c_double), ("atol", C.c_double), ("max_outer", C.c_int),
+                ("peclet", C.c_double * 3)]
 
 
 CONV_DEFAULT, CONV_LSQR, CONV_SKIP = 0, 1, 2
@@ -93,6 +95,7 @@ def lib() -> C.CDLL:
             getattr(L, name).argtypes = [C.c_int] * 5 + [P(CSR)]
         L.orc_poisson2d_rows.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, P(CSR)]
         L.orc_poisson2d_complete.argtypes = [C.c_int, C.c_int, P(CSR)]
+        L.orc_convdiff_rows.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, dp, P(CSR)]
         L.orc_split.argtypes = [P(CSR), C.c_int64, C.c_int64, P(CSR), P(CSR)]
         L.orc_spmv.argtypes = [P(CSR), dp, dp]
         L.orc_residual.argtypes = [P(CSR), dp, dp, dp]
@@ -205,6 +208,15 @@ def poisson2d_complete(m, n) -> Mat:
     return Mat(c)
 
 
+def convdiff_rows(dim, nx, ny, nz, row0, row1, peclet) -> Mat:
+    """Rows [row0,row1) of the upwind convection-diffusion operator (see oracle.h)."""
+    csr = CSR()
+    pe = np.ascontiguousarray(peclet, np.float64)
+    _check(lib().orc_convdiff_rows(dim, nx, ny, nz if dim == 3 else 1, row0, row1, _dp(pe), C.byref(csr)),
+           "orc_convdiff_rows")
+    return Mat(csr)
+
+
 def split(A: Mat, c0: int, c1: int):
     a, o = CSR(), CSR()
     _check(lib().orc_split(C.byref(A.csr), c0, c1, C.byref(a), C.byref(o)), "orc_split")
@@ -272,9 +284,9 @@ def final_residual_norm(Ablocks, x, bblocks, mode=REDUCE_SEQ) -> float:
     return lib().orc_final_residual_norm(mode, len(Ablocks), Aarr, _dp(x), barr)
 
 
-def sm_solve(dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_outer=10000):
+def sm_solve(dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_outer=10000, peclet=(0.0, 0.0, 0.0)):
     """Synchronous multisplitting over nb blocks (see oracle.h).  Returns a dict."""
-    p = SMProblem(dim, nx, ny, nz if dim == 3 else 1, nb, rtol, atol, max_outer)
+    p = SMProblem(dim, nx, ny, nz if dim == 3 else 1, nb, rtol, atol, max_outer, (C.c_double * 3)(*peclet))
     o = gmres_opts(**inner)
     res = SMResult()
     cap = max_outer
@@ -331,9 +343,10 @@ def dense_mult(S, alpha) -> np.ndarray:
     return y
 
 
-def smsm_solve(dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000):
+def smsm_solve(dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000,
+               peclet=(0.0, 0.0, 0.0)):
     """SMSM with global minimization over nb blocks (see oracle.h).  Returns a dict."""
-    p = SMSMProblem(dim, nx, ny, nz if dim == 3 else 1, nb, s, rtol, atol, max_outer)
+    p = SMSMProblem(dim, nx, ny, nz if dim == 3 else 1, nb, s, rtol, atol, max_outer, (C.c_double * 3)(*peclet))
     io = gmres_opts(**inner)
     oo = lsqr_opts(**outer)
     res = SMResult()
