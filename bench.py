@@ -62,7 +62,13 @@ def parse():
     p.add_argument("--s", type=int, default=20, help="SMSM: inner solves per minimization (-s)")
     p.add_argument("--inner-max-it", type=int, default=20)
     p.add_argument("--outer-max-it", type=int, default=70)
-    return p.parse_args()
+    p.add_argument("--peclet", default=None,
+                   help="Px,Py,Pz: the upwind convection-diffusion operator (configs[4]) instead of Poisson")
+    a = p.parse_args()
+    a.peclet = tuple(float(v) for v in a.peclet.split(",")) if a.peclet else None
+    if a.peclet is not None and len(a.peclet) != 3:
+        raise SystemExit("--peclet takes three cell Peclet numbers Px,Py,Pz")
+    return a
 
 
 def cpu_baseline(n: int, restart: int, its: int, rtol: float):
@@ -130,7 +136,7 @@ def main():
 
     if variant == "gmres":
         # configs[1]: single-block GMRES(30) on 256^3 (gmres_solution.c:50-70 in 3D)
-        A = Mat.box_stencil(ctx, 3, n, n, n)
+        A = Mat.box_convdiff(ctx, 3, n, n, n, False, False, args.peclet or (0.0, 0.0, 0.0))
         ones = Vec(ctx, rows)
         ones.set(1.0)
         b = Vec(ctx, rows)
@@ -148,7 +154,7 @@ def main():
         workload = f"3D 7-pt Poisson {n}^3, single-block GMRES({args.restart}) on 1 MI355X (configs[1])"
     elif variant == "sm":
         comm = TorchComm(device=torch.device("cuda", dev) if args.backend == "nccl" else torch.device("cpu"))
-        L = block_layout(3, n, n, n * world, world, rank)
+        L = block_layout(3, n, n, n * world, world, rank, args.peclet)
         o = Options(kspopts)
         blk = GpuBlock(ctx, L, None, comm, prefix="")
         blk.ksp.set_from_options(o)
@@ -181,7 +187,7 @@ def main():
                    f"-outer1_ksp_atol 1e-100 -outer1_ksp_max_it {args.outer_max_it} -outer1_ksp_rtol 1e-15 "
                    f"-outer1_pc_type none -outer1_ksp_norm_type UNPRECONDITIONED -s {args.s}")
         o = Options(kspopts)
-        L = block_layout(3, n, n, nz, world, rank)
+        L = block_layout(3, n, n, nz, world, rank, args.peclet)
         blk = GpuBlock(ctx, L, o, comm, prefix="inner1_")
         blk.setup_minimization(args.s)
         mini = GpuMinimizer(ctx, [blk], comm, o, prefix="outer1_")
@@ -204,6 +210,11 @@ def main():
                     f"per outer iteration, LSQR max_it {args.outer_max_it}; "
                     f"{'RCCL' if world > 1 and args.backend == 'nccl' else ('gloo (rehearsal)' if world > 1 else 'single block')} "
                     f"exchange and all-gathers (configs[2] at N = 2)")
+
+    if args.peclet is not None:
+        workload = workload.replace("7-pt Poisson", "7-pt upwind convection-diffusion (cell Peclet "
+                                    + ",".join(f"{v:g}" for v in args.peclet) + ")")
+        workload = workload.replace("(configs[1])", "(configs[1] shape, configs[4] operator)")
 
     def barrier():
         if world > 1:
@@ -267,7 +278,7 @@ def main():
                                   "share": v["ms"] / total_ms if total_ms else None} for k, v in stats.items()}
             alg_bytes = sum(v["bytes"] for v in stats.values())
             out["hbm_alg_GBps_whole_step"] = alg_bytes / (elapsed / 1) / 1e9
-        if world == 1 and variant == "gmres" and not args.no_cpu_baseline:
+        if world == 1 and variant == "gmres" and not args.no_cpu_baseline and args.peclet is None:
             out["cpu_baseline"] = cpu_baseline(n, args.restart, args.cpu_sample_its, args.rtol)
         else:
             out["cpu_baseline"] = None

@@ -210,8 +210,20 @@ class Detector:
                     self._send(k, VERDICT, (self.phase, m[1]))
 
 
+def _block_rows(po, dim, nx, ny, nz, nb, b, peclet=None):
+    """Block b's rows of the reference operator (Poisson) or the convection-diffusion one."""
+    N = nx * ny * (nz if dim == 3 else 1)
+    rows = N // nb
+    if peclet is not None and any(peclet):
+        return po.convdiff_rows(dim, nx, ny, nz, b * rows, (b + 1) * rows, peclet)
+    if dim == 3:
+        ppb = nz // nb
+        return po.poisson3d_rows(nx, ny, nz, b * ppb, (b + 1) * ppb)
+    return po.poisson2d_rows(nx, ny, b * rows, (b + 1) * rows)
+
+
 def am_roundrobin(po, dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_iterations=100000, strict=False,
-                  variant="am", s=0, outer: dict | None = None):
+                  variant="am", s=0, outer: dict | None = None, peclet=None):
     """Replay AM (or, variant "amam_local", AMAM-local: s inner steps then the
     block-local LSQR minimization, AMAM-local_prime.c:371-431) on nb blocks, round-robin.  Returns a dict with per-block
     iterations / inner iterations / phase tags, the trace of (block, iteration,
@@ -226,11 +238,7 @@ def am_roundrobin(po, dim, nx, ny, nz, nb, rtol, inner: dict, atol=1e-100, max_i
     blocks = []
     for b in range(nb):
         r0, r1 = b * rows, (b + 1) * rows
-        if dim == 3:
-            ppb = nz // nb
-            Ab = po.poisson3d_rows(nx, ny, nz, b * ppb, (b + 1) * ppb)
-        else:
-            Ab = po.poisson2d_rows(nx, ny, r0, r1)
+        Ab = _block_rows(po, dim, nx, ny, nz, nb, b, peclet)
         Aii, Aoff = po.split(Ab, r0, r1)
         bb = Ab.mult(np.ones(N))
         nbrs = [k for k in (b - 1, b + 1) if 0 <= k < nb]
@@ -309,7 +317,8 @@ def sum_ordered(values):
     return t
 
 
-def smsm_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000):
+def smsm_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000,
+               peclet=None):
     """SMSM with block-local minimization (synchronous-multisplitting-synchronous-
     minimization-local.c): s times {rhs_i, inner GMRES, exchange, S_i(:,k) = x_i},
     R_i = A_ii S_i, rhs_i, x_i = S_i LSQR(R_i, rhs_i); stop when every block's
@@ -321,11 +330,7 @@ def smsm_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=
     blocks = []
     for b in range(nb):
         r0, r1 = b * rows, (b + 1) * rows
-        if dim == 3:
-            ppb = nz // nb
-            Ab = po.poisson3d_rows(nx, ny, nz, b * ppb, (b + 1) * ppb)
-        else:
-            Ab = po.poisson2d_rows(nx, ny, r0, r1)
+        Ab = _block_rows(po, dim, nx, ny, nz, nb, b, peclet)
         Aii, Aoff = po.split(Ab, r0, r1)
         blocks.append(dict(r0=r0, Ab=Ab, Aii=Aii, Aoff=Aoff, rhs_b=Ab.mult(np.ones(N))))
     x = np.zeros(N)        # every block's own rows
@@ -375,7 +380,7 @@ def smsm_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=
             "x": x, "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}
 
 
-def _blocks_ext(po, dim, nx, ny, nz, nb):
+def _blocks_ext(po, dim, nx, ny, nz, nb, peclet=None):
     """Block rows with the ext column space [plane below | own | plane above]."""
     nz = nz if dim == 3 else 1
     N = nx * ny * nz
@@ -384,11 +389,7 @@ def _blocks_ext(po, dim, nx, ny, nz, nb):
     out = []
     for b in range(nb):
         r0, r1 = b * rows, (b + 1) * rows
-        if dim == 3:
-            ppb = nz // nb
-            Ab = po.poisson3d_rows(nx, ny, nz, b * ppb, (b + 1) * ppb)
-        else:
-            Ab = po.poisson2d_rows(nx, ny, r0, r1)
+        Ab = _block_rows(po, dim, nx, ny, nz, nb, b, peclet)
         Aii, Aoff = po.split(Ab, r0, r1)
         lo = plane if b > 0 else 0
         hi = plane if b < nb - 1 else 0
@@ -412,14 +413,15 @@ def _apply_ext(blk, xe, rows):
     blk["view"][r0 + rows:r0 + rows + hi] = xe[lo + rows:]
 
 
-def smsm_semi_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000):
+def smsm_semi_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000,
+                    peclet=None):
     """SMSM with semi-local minimization (synchronous-multisplitting-synchronous-
     minimization-semi-local.c): s times {rhs_i, inner GMRES, exchange, S_i(:,k) = x
     over the block's rows and neighbour planes}, R_i = A_block S_i (own rows),
     alpha_i = LSQR(R_i, b_i), local test on the last inner iterate, then x_i and the
     block's view of its neighbours <- S_i alpha_i; stop when every block passes."""
     mode = po.REDUCE_DBR
-    blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb)
+    blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb, peclet)
     norm0 = math.sqrt(sum_ordered([po.norm2(blk["rhs_b"], mode) ** 2 for blk in blocks]))
     thr = max(atol, rtol / math.sqrt(nb) * norm0)
     opts = dict(inner, guess_nonzero=1, uirnorm=1, reduce_mode=mode)
@@ -466,7 +468,7 @@ def smsm_semi_local(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, 
 
 
 def amam_semi_local_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100,
-                               max_iterations=100000, strict=False):
+                               max_iterations=100000, strict=False, peclet=None):
     """AMAM with semi-local minimization (asynchronous-multisplitting-asynchronous-
     minimization-semi-local_prime.c:350-420), round-robin: s asynchronous inner
     steps, each followed by a second receive and S_i(:,k) = [neighbour planes | x_i];
@@ -474,7 +476,7 @@ def amam_semi_local_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, ou
     the reference computes but never scatters back (the iterate is unchanged) --;
     the local test on the last inner iterate; one detection step."""
     mode = po.REDUCE_DBR
-    blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb)
+    blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb, peclet)
     net = Slots()
     dets = [Detector(blk["b"], blk["nbrs"], net, strict) for blk in blocks]
     norm0 = math.sqrt(sum_ordered([po.norm2(blk["rhs_b"], mode) ** 2 for blk in blocks]))

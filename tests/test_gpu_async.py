@@ -111,3 +111,37 @@ def test_amam_semi_local_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny
     assert res.iterations == tw["iterations"] and res.trace == tw["trace"]
     assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
     assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
+
+
+PE = (0.5, 0.25, -0.3)
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,nb,max_it", [(3, 8, 8, 8, 2, 5), (3, 6, 6, 12, 4, 3), (2, 24, 20, 1, 3, 5)])
+def test_am_convdiff_gpu_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, max_it):
+    """AM on the convection-diffusion operator (BASELINE configs[4]'s system)."""
+    opts = Options(" ".join(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 "
+                            f"-inner{b + 1}_pc_type none" for b in range(nb)))
+    comm = LocalComm()
+    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, range(nb), opts, comm, PE)
+    res = am_solve(blocks, comm, rtol=1e-6, record=True)
+    tw = am_twin.am_roundrobin(oracle, dim, nx, ny, nz, nb, 1e-6, dict(restart=30, max_it=max_it, rtol=1e-20),
+                               peclet=PE)
+    assert res.norm0 == tw["norm0"] and res.iterations == tw["iterations"] and res.trace == tw["trace"]
+    assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
+    assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
+
+
+def test_amam_semi_local_convdiff_gpu_bitwise_vs_twin(ctx, oracle):
+    dim, nx, ny, nz, nb, s, max_it = 3, 8, 8, 8, 2, 4, 5
+    opts = Options(" ".join(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 "
+                            f"-inner{b + 1}_pc_type none" for b in range(nb)) + " " + _outer_opts(nb))
+    comm = LocalComm()
+    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, range(nb), opts, comm, PE)
+    for blk in blocks:
+        blk.setup_minimization(s)
+    res = am_solve(blocks, comm, rtol=1e-6, record=True, variant="amam_semi_local", s=s)
+    tw = am_twin.amam_semi_local_roundrobin(oracle, dim, nx, ny, nz, nb, s, 1e-6,
+                                            dict(restart=30, max_it=max_it, rtol=1e-20), OUTER, peclet=PE)
+    assert res.iterations == tw["iterations"] and res.trace == tw["trace"]
+    assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
+    assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
