@@ -76,6 +76,7 @@ typedef struct msp_lsqr msp_lsqr;
 typedef struct msp_comm msp_comm;
 typedef struct msp_amsg msp_amsg;
 typedef struct msp_cvd msp_cvd;
+typedef struct msp_abcast msp_abcast;
 
 /* ---------------------------------------------------------------- context */
 /* One context per GPU: device id + the HIP stream all work is ordered on.
@@ -331,6 +332,29 @@ int msp_amsg_send_vec(msp_amsg *am, int32_t dst, const int32_t *ints, int32_t ni
                       int64_t n);
 int msp_amsg_recv_vec(msp_amsg *am, int32_t src, int32_t *ints, int32_t nints, msp_vec *v, int64_t off, int64_t cap,
                       int64_t *n, int32_t *got);
+
+/* ------------------------------------------- async minimization broadcast */
+/* Newest-value broadcast of each block's rows of R (AMAM-global), in POSIX
+ * shared memory.  Replaces comm_async_test_and_send_min and
+ * comm_async_probe_and_receive_min (comm.c:288-351; used at
+ * asynchronous-multisplitting-asynchronous-minimization-global_prime.c:422-428):
+ * publish sends this rank's nrows x ncols block unless the buffer it would fill
+ * is still being read (the reference's "previous MPI_Isend not complete":
+ * published = 0); fetch copies source src's newest block if it is newer than
+ * the last one taken (got = 1), else leaves the destination as it was.  Two
+ * buffers per source, a reader/writer word per buffer: no torn copies.
+ * cap = the largest nrows x ncols any rank publishes.  One rank creates the
+ * region (owner = 1) before the others open it. */
+int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t cap, int32_t owner, msp_abcast **bc);
+int msp_abcast_destroy(msp_abcast **bc);
+/* host payloads: column j at data + j*ld */
+int msp_abcast_publish(msp_abcast *bc, const double *data, int64_t nrows, int32_t ncols, int64_t ld,
+                       int32_t *published);
+int msp_abcast_fetch(msp_abcast *bc, int32_t src, double *data, int64_t nrows, int32_t ncols, int64_t ld,
+                     int32_t *got);
+/* a dense block in HBM (DMA to / from the registered region) */
+int msp_abcast_publish_dense(msp_abcast *bc, const msp_dense *D, int32_t *published);
+int msp_abcast_fetch_dense(msp_abcast *bc, int32_t src, msp_dense *D, int32_t *got);
 
 /* ------------------------------------------------- convergence detection */
 /* Algorithm 5.15 of Bahi/Contassot-Vivier/Couturier as the reference implements

@@ -26,6 +26,12 @@ asynchronous-multisplitting-asynchronous-minimization-semi-local_prime.c:350-420
 inner step is followed by a second receive and S_i(:,k) = [neighbour planes | x_i];
 then R_i = A_block S_i, alpha_i = LSQR(R_i, b_i) and x_minimized = S_i alpha_i, which
 the reference computes but never scatters back, and the detection step.
+variant "amam_global" is asynchronous-multisplitting-asynchronous-minimization-
+global_prime.c:370-470: the same inner steps, then R_i = A_block S_i is sent to
+every block and the newest rows of every other block are taken (newest-value
+broadcast, csrc/abcast.c), alpha = LSQR over the replicated R and the global b,
+x_minimized = S_i alpha replaces x_i and the block's view of its neighbours, and
+the local test is ||b_i - A_block x_minimized|| (:437-438).
 """
 from __future__ import annotations
 
@@ -35,7 +41,7 @@ import time
 import uuid
 from dataclasses import dataclass, field
 
-from .petsc import AsyncMessages, ConvDetection
+from .petsc import AsyncBroadcast, AsyncMessages, ConvDetection
 
 
 @dataclass
@@ -54,10 +60,11 @@ class AsyncBlock:
     """The asynchronous state of one block root: its message slots, its
     convergence-detection instance and its counters."""
 
-    def __init__(self, blk, name: str, owner: bool, strict: bool):
+    def __init__(self, blk, name: str, owner: bool, strict: bool, bcast_cap: int = 0):
         L = blk.layout
         self.blk = blk
         self.am = AsyncMessages(name, L.nb, L.b, max(L.plane, 1), owner)
+        self.bcast = AsyncBroadcast(name + "_R", L.nb, L.b, bcast_cap, owner) if bcast_cap else None
         nbrs = [nbr for nbr, *_ in L.recv]            # spanning tree = chain; dependencies = the same blocks
         self.cvd = ConvDetection(self.am, L.b, nbrs, nbrs, strict)
         self.it = 0
@@ -80,9 +87,10 @@ class AsyncBlock:
         for nbr, off, cnt in self.blk.layout.send:
             self.blk.async_send(self.am, nbr, off, cnt, self.tag, stamp)
 
-    def _detect(self, norm0, rtol, atol, trace):
+    def _detect(self, norm0, rtol, atol, trace, block_norm: bool = False):
         blk, L = self.blk, self.blk.layout
-        self.local_norm = math.sqrt(blk.local_residual_sq())          # MatResidual(A_ii, rhs, x), VecNorm
+        # MatResidual(A_ii, rhs, x) + VecNorm; AMAM-global: MatResidual(A_block, b_i, x_minimized)
+        self.local_norm = math.sqrt(blk.block_residual_sq() if block_norm else blk.local_residual_sq())
         under = self.local_norm <= max(atol, rtol / math.sqrt(L.nb) * norm0)
         self.cvd.step(under)                                          # detection + receives
         self.it += 1
@@ -97,8 +105,8 @@ class AsyncBlock:
             blk.update_rhs()
             self.inner += blk.solve()
             self._publish(self.it)
-        elif variant == "amam_semi_local":                            # AMAM-semi-local_prime.c:350-420
-            for k in range(s):
+        elif variant in ("amam_semi_local", "amam_global"):          # AMAM-semi-local_prime.c:350-420,
+            for k in range(s):                                        # AMAM-global_prime.c:378-413
                 self._receive()
                 blk.update_rhs()
                 self.inner += blk.solve()
@@ -106,7 +114,10 @@ class AsyncBlock:
                 self._receive()
                 blk.store_column(k)
                 self.steps += 1
-            blk.semi_local_minimize(apply=False)
+            if variant == "amam_global":
+                blk.global_async_minimize(self.bcast)
+            else:
+                blk.semi_local_minimize(apply=False)
         else:                                                         # AMAM-local_prime.c:371-404
             for k in range(s):
                 self._receive()
@@ -116,11 +127,13 @@ class AsyncBlock:
                 blk.store_local_column(k)
                 self.steps += 1
             blk.local_minimize()
-        self._detect(norm0, rtol, atol, trace)
+        self._detect(norm0, rtol, atol, trace, block_norm=variant == "amam_global")
 
     def close(self):
         self.cvd.destroy()
         self.am.destroy()
+        if self.bcast is not None:
+            self.bcast.destroy()
 
 
 def _channel_name(comm) -> str:
@@ -136,22 +149,27 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
              strict: bool = False, record: bool = False, monitor=None, variant: str = "am", s: int = 0) -> AMResult:
     """The asynchronous multisplitting loop (asynchronous-multisplitting_prime.c:333-392);
     variant "amam_local" adds the block-local minimization every s inner steps
-    (the blocks must have setup_local_minimization(s))."""
-    if variant not in ("am", "amam_local", "amam_semi_local"):
+    (the blocks must have setup_local_minimization(s)), "amam_semi_local" the
+    semi-local one (setup_minimization(s)), "amam_global" the global one
+    (setup_global_async_minimization(s))."""
+    if variant not in ("am", "amam_local", "amam_semi_local", "amam_global"):
         raise ValueError(f"unknown asynchronous variant {variant}")
     res = AMResult()
     # global_norm_0 = computeFinalResidualNorm at x = 0 (:322)
     res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
     name = _channel_name(comm)
     ordered = sorted(blocks, key=lambda b: b.layout.b)
+    cap = 0
+    if variant == "amam_global":                     # the largest block of R any block broadcasts
+        cap = max(R.shape[0] * R.shape[1] for R in ordered[0].R_rep)
     asyncs = {}
     owner_here = ordered[0].layout.b == 0
-    if owner_here:                                   # block 0 creates the region, the others open it
-        asyncs[0] = AsyncBlock(ordered[0], name, True, strict)
+    if owner_here:                                   # block 0 creates the regions, the others open them
+        asyncs[0] = AsyncBlock(ordered[0], name, True, strict, cap)
     comm.barrier()
     for blk in ordered:
         if blk.layout.b not in asyncs:
-            asyncs[blk.layout.b] = AsyncBlock(blk, name, False, strict)
+            asyncs[blk.layout.b] = AsyncBlock(blk, name, False, strict, cap)
     comm.barrier()
     for blk in blocks:                               # x_j = 0; updateLocalRHS before the loop (:329)
         blk.reset_halo()

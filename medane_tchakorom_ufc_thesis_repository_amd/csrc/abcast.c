@@ -1,0 +1,281 @@
+/*
+ * abcast.c -- newest-value broadcast of each block's rows of R between the
+ * blocks of an asynchronous run with global minimization, in POSIX shared
+ * memory (one node, one process -- or one host thread -- per GPU).
+ *
+ * Replaces comm_async_test_and_send_min / comm_async_probe_and_receive_min
+ * (src/utils/comm.c:288-351) as AMAM-global uses them
+ * (asynchronous-multisplitting-asynchronous-minimization-global_prime.c:422-428):
+ *   - the sender MPI_Isends its rows of R, unless its previous send has not
+ *     completed (MPI_Test), in which case this round sends nothing;
+ *   - the receiver drains every pending message and copies the newest into
+ *     its replicated R, or keeps what it had (zeros before the first one).
+ * Each source has two buffers.  A publish fills the one that is not the
+ * newest and then makes it the newest; a fetch copies the newest one out.
+ * Per buffer, a reader-count / writer-bit word admits either readers or the
+ * writer, never both, so a fetch never sees a half-written R and a publish
+ * that would overwrite a buffer still being read is skipped -- the reference's
+ * "previous send not complete".  Payloads move HBM <-> the registered region
+ * by DMA.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "msplit.h"
+#include "msplit_internal.h"
+
+#define ABC_MAGIC 0x4d53504142434153ULL /* "MSPABCAS" */
+#define ABC_WRITER 0x80000000u
+
+typedef struct {
+  _Atomic int32_t newest;   /* buffer index of the newest complete payload, -1 before the first */
+  int32_t pad0;
+  _Atomic uint32_t lock[2]; /* ABC_WRITER | reader count */
+  uint64_t version[2];      /* publish number of the payload each buffer holds */
+  int64_t nrows[2], ncols[2];
+  uint64_t published;       /* publishes so far (written by the source only) */
+  uint8_t pad[128 - 8 - 8 - 16 - 32 - 8];
+} src_line;
+
+typedef struct {
+  uint64_t magic;
+  int32_t nranks;
+  int32_t pad0;
+  int64_t cap;
+  uint8_t pad[64 - 24];
+} abc_header;
+
+struct msp_abcast {
+  char name[128];
+  int32_t nranks, rank, owner;
+  int64_t cap;
+  size_t bytes, buf_bytes;
+  uint8_t *base;
+  src_line *lines;
+  uint8_t *bufs;   /* [src][2] buffers of cap doubles */
+  uint64_t *seen;  /* [src] version last fetched */
+  int registered;
+};
+
+static int berr(int code, const char *msg) {
+  mspi_set_error(code, "%s", msg);
+  return code;
+}
+
+static size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static double *buf_at(msp_abcast *b, int src, int k) {
+  return (double *)(b->bufs + ((size_t)src * 2 + (size_t)k) * b->buf_bytes);
+}
+
+int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t cap, int32_t owner, msp_abcast **out) {
+  if (!name || !out) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  if (nranks < 1 || nranks > 4096 || rank < 0 || rank >= nranks || cap < 0)
+    return berr(MSP_ERR_ARG_OUTOFRANGE, "bad abcast sizes");
+  if (strlen(name) >= sizeof(((msp_abcast *)0)->name) || name[0] != '/')
+    return berr(MSP_ERR_ARG_WRONG, "shared-memory name must start with '/' and be < 128 chars");
+  msp_abcast *b = (msp_abcast *)calloc(1, sizeof(msp_abcast));
+  if (!b) return berr(MSP_ERR_MEM, "allocation failed");
+  strcpy(b->name, name);
+  b->nranks = nranks;
+  b->rank = rank;
+  b->owner = owner ? 1 : 0;
+  b->cap = cap;
+  b->buf_bytes = round_up((size_t)(cap > 0 ? cap : 1) * sizeof(double), 4096);
+  const size_t lines_bytes = round_up((size_t)nranks * sizeof(src_line), 4096);
+  b->bytes = 4096 + lines_bytes + (size_t)nranks * 2 * b->buf_bytes;
+  int fd;
+  if (b->owner) {
+    shm_unlink(name);
+    fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd >= 0 && ftruncate(fd, (off_t)b->bytes) != 0) {
+      close(fd);
+      fd = -1;
+    }
+  } else {
+    fd = shm_open(name, O_RDWR, 0600);
+  }
+  if (fd < 0) {
+    free(b);
+    mspi_set_error(MSP_ERR_LIB, "shm_open(%s) failed: %s", name, strerror(errno));
+    return MSP_ERR_LIB;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0 || (size_t)st.st_size < b->bytes) {
+    close(fd);
+    free(b);
+    return berr(MSP_ERR_ARG_SIZ, "shared-memory region smaller than the layout (sizes differ between ranks?)");
+  }
+  b->base = (uint8_t *)mmap(NULL, b->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (b->base == MAP_FAILED) {
+    free(b);
+    return berr(MSP_ERR_MEM, "mmap of the shared-memory region failed");
+  }
+  abc_header *h = (abc_header *)b->base;
+  b->lines = (src_line *)(b->base + 4096);
+  b->bufs = b->base + 4096 + lines_bytes;
+  if (b->owner) {
+    h->nranks = nranks;
+    h->cap = cap;
+    for (int r = 0; r < nranks; ++r) atomic_store_explicit(&b->lines[r].newest, -1, memory_order_relaxed);
+    atomic_thread_fence(memory_order_release);
+    h->magic = ABC_MAGIC;
+  } else if (h->magic != ABC_MAGIC || h->nranks != nranks || h->cap != cap) {
+    munmap(b->base, b->bytes);
+    free(b);
+    return berr(MSP_ERR_ARG_WRONG, "shared-memory region not initialised by the owner, or different sizes");
+  }
+  b->seen = (uint64_t *)calloc((size_t)nranks, sizeof(uint64_t));
+  if (!b->seen) {
+    munmap(b->base, b->bytes);
+    free(b);
+    return berr(MSP_ERR_MEM, "allocation failed");
+  }
+  *out = b;
+  return MSP_SUCCESS;
+}
+
+int msp_abcast_destroy(msp_abcast **pb) {
+  if (!pb || !*pb) return MSP_SUCCESS;
+  msp_abcast *b = *pb;
+  if (b->registered) mspi_host_unregister(b->base);
+  munmap(b->base, b->bytes);
+  if (b->owner) shm_unlink(b->name);
+  free(b->seen);
+  free(b);
+  *pb = NULL;
+  return MSP_SUCCESS;
+}
+
+static int ensure_registered(msp_abcast *b) {
+  if (b->registered) return MSP_SUCCESS;
+  int rc = mspi_host_register(b->base, b->bytes);
+  if (rc) return rc;
+  b->registered = 1;
+  return MSP_SUCCESS;
+}
+
+/* one payload of nrows x ncols, column j at src + j*ld, either in HBM (ctx != NULL) or host memory */
+typedef struct {
+  msp_ctx *ctx;
+  double *p;
+  int64_t nrows, ld;
+  int32_t ncols;
+} abc_view;
+
+static int copy_out(const abc_view *v, double *dst) {
+  int rc = MSP_SUCCESS;
+  for (int32_t j = 0; j < v->ncols && !rc; ++j) {
+    const double *col = v->p + (size_t)j * v->ld;
+    double *d = dst + (size_t)j * v->nrows;
+    if (v->ctx) rc = mspi_d2h_sync(v->ctx, d, col, (size_t)v->nrows * sizeof(double));
+    else memcpy(d, col, (size_t)v->nrows * sizeof(double));
+  }
+  return rc;
+}
+
+static int copy_in(const abc_view *v, const double *srcp) {
+  int rc = MSP_SUCCESS;
+  for (int32_t j = 0; j < v->ncols && !rc; ++j) {
+    double *col = v->p + (size_t)j * v->ld;
+    const double *s = srcp + (size_t)j * v->nrows;
+    if (v->ctx) rc = mspi_h2d_sync(v->ctx, col, s, (size_t)v->nrows * sizeof(double));
+    else memcpy(col, s, (size_t)v->nrows * sizeof(double));
+  }
+  return rc;
+}
+
+static int publish(msp_abcast *b, const abc_view *v, int32_t *published) {
+  *published = 0;
+  if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
+    return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
+  if (v->nrows * (int64_t)v->ncols > b->cap) return berr(MSP_ERR_ARG_SIZ, "payload larger than the broadcast slot");
+  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
+  if (rc) return rc;
+  src_line *L = &b->lines[b->rank];
+  const int32_t newest = atomic_load_explicit(&L->newest, memory_order_acquire);
+  const int w = newest == 0 ? 1 : 0;
+  uint32_t expect = 0;
+  if (!atomic_compare_exchange_strong_explicit(&L->lock[w], &expect, ABC_WRITER, memory_order_acq_rel,
+                                               memory_order_relaxed))
+    return MSP_SUCCESS; /* a reader still holds it: the previous send has not completed */
+  if ((rc = copy_out(v, buf_at(b, b->rank, w)))) {
+    atomic_store_explicit(&L->lock[w], 0u, memory_order_release);
+    return rc;
+  }
+  L->nrows[w] = v->nrows;
+  L->ncols[w] = v->ncols;
+  L->version[w] = ++L->published;
+  atomic_store_explicit(&L->lock[w], 0u, memory_order_release);
+  atomic_store_explicit(&L->newest, w, memory_order_release);
+  *published = 1;
+  return MSP_SUCCESS;
+}
+
+static int fetch(msp_abcast *b, int32_t src, const abc_view *v, int32_t *got) {
+  *got = 0;
+  if (src < 0 || src >= b->nranks || src == b->rank) return berr(MSP_ERR_ARG_OUTOFRANGE, "source rank out of range");
+  if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
+    return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
+  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
+  if (rc) return rc;
+  src_line *L = &b->lines[src];
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    const int32_t k = atomic_load_explicit(&L->newest, memory_order_acquire);
+    if (k < 0) return MSP_SUCCESS; /* nothing sent yet */
+    uint32_t cur = atomic_load_explicit(&L->lock[k], memory_order_relaxed);
+    if (cur & ABC_WRITER) continue; /* the source moved on and is refilling it: look again */
+    if (!atomic_compare_exchange_weak_explicit(&L->lock[k], &cur, cur + 1, memory_order_acq_rel, memory_order_relaxed))
+      continue;
+    const uint64_t ver = L->version[k];
+    if (ver == b->seen[src]) {
+      atomic_fetch_sub_explicit(&L->lock[k], 1u, memory_order_release);
+      return MSP_SUCCESS; /* nothing newer */
+    }
+    if (L->nrows[k] != v->nrows || L->ncols[k] != v->ncols) {
+      atomic_fetch_sub_explicit(&L->lock[k], 1u, memory_order_release);
+      return berr(MSP_ERR_ARG_SIZ, "received block has a different shape");
+    }
+    rc = copy_in(v, buf_at(b, src, k));
+    atomic_fetch_sub_explicit(&L->lock[k], 1u, memory_order_release);
+    if (rc) return rc;
+    b->seen[src] = ver;
+    *got = 1;
+    return MSP_SUCCESS;
+  }
+  return MSP_SUCCESS; /* the source kept refilling: try next round */
+}
+
+int msp_abcast_publish(msp_abcast *b, const double *data, int64_t nrows, int32_t ncols, int64_t ld,
+                       int32_t *published) {
+  if (!b || !published) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  const abc_view v = {NULL, (double *)data, nrows, ld, ncols};
+  return publish(b, &v, published);
+}
+
+int msp_abcast_fetch(msp_abcast *b, int32_t src, double *data, int64_t nrows, int32_t ncols, int64_t ld,
+                     int32_t *got) {
+  if (!b || !got) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  const abc_view v = {NULL, data, nrows, ld, ncols};
+  return fetch(b, src, &v, got);
+}
+
+int msp_abcast_publish_dense(msp_abcast *b, const msp_dense *D, int32_t *published) {
+  if (!b || !D || !published) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  const abc_view v = {D->ctx, D->d, D->nrows, D->lda, D->ncols};
+  return publish(b, &v, published);
+}
+
+int msp_abcast_fetch_dense(msp_abcast *b, int32_t src, msp_dense *D, int32_t *got) {
+  if (!b || !D || !got) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  const abc_view v = {D->ctx, D->d, D->nrows, D->lda, D->ncols};
+  return fetch(b, src, &v, got);
+}

@@ -180,6 +180,53 @@ class GpuBlock:
         return (self.lsqr_semi.get_residual_norm(), self.lsqr_semi.get_iteration_number(),
                 self.lsqr_semi.get_converged_reason())
 
+    # -- global asynchronous minimization (AMAM-global)
+    def setup_global_async_minimization(self, s: int, opts: Options | None = None, prefix: str | None = None):
+        """AMAM-global_prime.c:238-330: S over the block's rows and neighbour planes,
+        this block's rows of R, the replicated R -- every block's rows, zero until
+        that block's first message arrives (MatZeroEntries(R)) --, the global b and
+        the outer LSQR over the nb row blocks in block order."""
+        L = self.layout
+        self.setup_minimization(s)
+        self.R_rep, self.b_all = [], []
+        for j in range(L.nb):
+            if j == L.b:
+                self.R_rep.append(self.R)
+                self.b_all.append(self.b)
+                continue
+            Lj = block_layout(L.dim, L.nx, L.ny, L.nz, L.nb, j, L.peclet)
+            R = DenseMat(self.ctx, Lj.nrows, self.s)
+            R.zero_entries()
+            self.R_rep.append(R)
+            lo = any(nbr < j for nbr, *_ in Lj.recv)
+            hi = any(nbr > j for nbr, *_ in Lj.recv)
+            A = Mat.box_convdiff(self.ctx, *Lj.box, lo, hi, L.peclet)   # b_j = A_block_j 1 (utils.c:623-650)
+            ones = Vec(self.ctx, (Lj.plane if lo else 0) + Lj.nrows + (Lj.plane if hi else 0))
+            ones.set(1.0)
+            bj = Vec(self.ctx, Lj.nrows)
+            A.mult(ones, bj)
+            self.b_all.append(bj)
+            del A, ones
+        self.lsqr_glob = initializeOuterKSP(self.ctx, prefix if prefix is not None else f"outer{L.b + 1}_",
+                                            opts if opts is not None else self.opts)
+        self.lsqr_glob.set_operators(self.R_rep)
+        self.alpha_glob = Vec(self.ctx, self.s)
+
+    def global_async_minimize(self, bcast):
+        """AMAM-global_prime.c:415-440: R_i = A_block S, send it (comm_async_test_and_send_min),
+        take the newest rows of every other block (comm_async_probe_and_receive_min),
+        alpha = LSQR(R, b) over the replicated R (outer_solver_norm_equation,
+        utils.c:1061-1078), x_minimized = S alpha into x_i and the neighbour planes."""
+        self.form_R()
+        bcast.publish_dense(self.R)
+        for j, R in enumerate(self.R_rep):
+            if j != self.layout.b:
+                bcast.fetch_dense(j, R)
+        self.lsqr_glob.solve(self.b_all, self.alpha_glob)
+        self.apply_alpha(self.alpha_glob)
+        return (self.lsqr_glob.get_residual_norm(), self.lsqr_glob.get_iteration_number(),
+                self.lsqr_glob.get_converged_reason())
+
     # -- asynchronous (AM) hooks: asynchronous.py
     def async_recv(self, am, nbr, hoff, cnt):
         """The newest plane of neighbour nbr, into a staging copy of the halo

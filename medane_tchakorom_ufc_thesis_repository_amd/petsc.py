@@ -747,6 +747,57 @@ class AsyncMessages:
             pass
 
 
+class AsyncBroadcast:
+    """Newest-value broadcast of each block's rows of R in shared memory
+    (msp_abcast): comm_async_test_and_send_min / comm_async_probe_and_receive_min
+    (comm.c:288-351) as AMAM-global uses them."""
+
+    def __init__(self, name: str, nranks: int, rank: int, cap: int, owner: bool):
+        h = C.c_void_p()
+        call("msp_abcast_create", name.encode(), int(nranks), int(rank), int(cap), 1 if owner else 0, C.byref(h))
+        self.h = h
+        self.rank = rank
+        self.nranks = nranks
+
+    def publish(self, data: np.ndarray) -> bool:
+        """Host block (nrows x ncols, column-major); False = the previous send is still being read."""
+        d = np.asfortranarray(data, np.float64)
+        nrows, ncols = d.shape
+        ok = C.c_int32()
+        call("msp_abcast_publish", self.h, _dp(d), int(nrows), int(ncols), int(max(nrows, 1)), C.byref(ok))
+        return bool(ok.value)
+
+    def fetch(self, src: int, out: np.ndarray) -> bool:
+        """Copy src's newest block into out (Fortran-ordered float64) if it is newer than the last one taken."""
+        if not (out.flags.f_contiguous and out.dtype == np.float64):
+            raise ValueError("out must be a Fortran-ordered float64 array")
+        nrows, ncols = out.shape
+        got = C.c_int32()
+        call("msp_abcast_fetch", self.h, int(src), _dp(out), int(nrows), int(ncols), int(max(nrows, 1)),
+             C.byref(got))
+        return bool(got.value)
+
+    def publish_dense(self, D: "DenseMat") -> bool:
+        ok = C.c_int32()
+        call("msp_abcast_publish_dense", self.h, D.h, C.byref(ok))
+        return bool(ok.value)
+
+    def fetch_dense(self, src: int, D: "DenseMat") -> bool:
+        got = C.c_int32()
+        call("msp_abcast_fetch_dense", self.h, int(src), D.h, C.byref(got))
+        return bool(got.value)
+
+    def destroy(self):
+        if getattr(self, "h", None) and self.h.value:
+            call("msp_abcast_destroy", C.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
 class ConvDetection:
     """The reference's decentralised convergence detection (msp_cvd,
     conv_detection_prime.c) for one block root."""

@@ -524,3 +524,78 @@ def amam_semi_local_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, ou
     return {"iterations": [blk["it"] for blk in blocks], "inner_its": [blk["inner"] for blk in blocks],
             "phase_tags": [d.phase for d in dets], "trace": trace, "x": x, "norm0": norm0,
             "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}
+
+
+def amam_global_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100,
+                           max_iterations=100000, strict=False, peclet=None):
+    """AMAM with global minimization (asynchronous-multisplitting-asynchronous-
+    minimization-global_prime.c:370-470), round-robin: s asynchronous inner steps,
+    each followed by a second receive and S_i(:,k) = [neighbour planes | x_i];
+    R_i = A_block S_i is broadcast, every other block's newest R rows are taken
+    (zeros before the first), alpha = LSQR(R, b) over all nb row blocks in block
+    order, x_minimized = S_i alpha replaces x_i and the view of the neighbour
+    planes, the local test is ||b_i - A_block x_minimized||, one detection step."""
+    mode = po.REDUCE_DBR
+    blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb, peclet)
+    net = Slots()
+    dets = [Detector(blk["b"], blk["nbrs"], net, strict) for blk in blocks]
+    norm0 = math.sqrt(sum_ordered([po.norm2(blk["rhs_b"], mode) ** 2 for blk in blocks]))
+    thr = max(atol, rtol / math.sqrt(nb) * norm0)
+    opts = dict(inner, guess_nonzero=1, uirnorm=1, reduce_mode=mode)
+    outer = dict(outer, reduce_mode=mode)
+    published = [None] * nb                                 # newest R rows each block sent
+    for blk in blocks:
+        blk["Rrep"] = [np.zeros((rows, s), order="F") for _ in range(nb)]
+        blk["taken"] = [0] * nb
+    versions = [0] * nb
+    b_all = [blk["rhs_b"] for blk in blocks]
+    trace, lsqr_its = [], []
+
+    def receive(blk, det):
+        for d, nbr in enumerate(blk["nbrs"]):
+            m = net.recv(nbr, blk["b"], DATA)
+            if m is not None and det.data_received(d, m[0], m[1]):
+                lo = nbr * rows + (rows - plane if nbr < blk["b"] else 0)
+                blk["view"][lo:lo + plane] = m[2]
+
+    active = list(range(nb))
+    while active:
+        for bi in active:
+            blk, det = blocks[bi], dets[bi]
+            S = np.zeros((blk["lo"] + rows + blk["hi"], s), order="F")
+            for k in range(s):
+                receive(blk, det)
+                rhs = blk["Aoff"].residual(blk["rhs_b"], blk["view"])
+                blk["x"], r = po.gmres(blk["Aii"], rhs, x0=blk["x"], **opts)
+                blk["inner"] += r["its"]
+                for nbr in blk["nbrs"]:
+                    pl = blk["x"][:plane].copy() if nbr < blk["b"] else blk["x"][rows - plane:].copy()
+                    net.send(blk["b"], nbr, DATA, (det.phase, blk["steps"], pl))
+                receive(blk, det)
+                S[:, k] = _ext_col(blk, rows)
+                blk["steps"] += 1
+            R = np.asfortranarray(np.stack([blk["Aext"].mult(np.ascontiguousarray(S[:, k])) for k in range(s)],
+                                           axis=1))
+            blk["Rrep"][bi] = R
+            published[bi] = R.copy()                        # comm_async_test_and_send_min
+            versions[bi] += 1
+            for j in range(nb):                             # comm_async_probe_and_receive_min
+                if j != bi and versions[j] > blk["taken"][j]:
+                    blk["Rrep"][j] = published[j].copy()
+                    blk["taken"][j] = versions[j]
+            alpha, lr = po.lsqr(blk["Rrep"], b_all, **outer)
+            lsqr_its.append(lr["its"])
+            _apply_ext(blk, po.dense_mult(S, alpha), rows)
+            ln = po.norm2(blk["Aext"].residual(blk["rhs_b"], _ext_col(blk, rows)), mode)
+            det.step(ln <= thr)
+            blk["it"] += 1
+            trace.append((blk["b"], blk["it"], ln, det.state, det.phase))
+            if blk["it"] >= max_iterations:
+                raise RuntimeError("no termination")
+        active = [bi for bi in active if dets[bi].state != FINISHED]
+    x = np.concatenate([blk["x"] for blk in blocks])
+    fin = [po.norm2(blk["Ab"].residual(blk["rhs_b"], x), mode) ** 2 for blk in blocks]
+    err = [po.norm2(blk["x"] - 1.0, mode) ** 2 for blk in blocks]
+    return {"iterations": [blk["it"] for blk in blocks], "inner_its": [blk["inner"] for blk in blocks],
+            "phase_tags": [d.phase for d in dets], "trace": trace, "x": x, "norm0": norm0, "lsqr_its": lsqr_its,
+            "final_norm": math.sqrt(sum_ordered(fin)), "error": math.sqrt(sum_ordered(err))}

@@ -14,7 +14,7 @@ import pytest
 
 import am_twin
 from medane_tchakorom_ufc_thesis_repository_amd._lib import MsplitError
-from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncMessages, ConvDetection
+from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncBroadcast, AsyncMessages, ConvDetection
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -83,6 +83,71 @@ def test_amsg_cross_process_seqlock():
     if got:
         last = ints[0]
     assert last == n and taken >= 1
+    r.destroy()
+
+
+def test_abcast_newest_value_semantics():
+    """comm_async_test_and_send_min / _probe_and_receive_min: the newest R block
+    of each source, zeros (untouched) before the first one, per receiver."""
+    name = _name()
+    a = AsyncBroadcast(name, 3, 0, 40, owner=True)
+    b = AsyncBroadcast(name, 3, 1, 40, owner=False)
+    c = AsyncBroadcast(name, 3, 2, 40, owner=False)
+    out = np.zeros((8, 5), order="F")
+    assert b.fetch(0, out) is False and not out.any()                  # nothing sent: R keeps its zeros
+    blocks = [np.asfortranarray(np.arange(40.0).reshape(8, 5) + 100 * k) for k in range(3)]
+    for blk in blocks:
+        assert a.publish(blk)                                          # no reader holds a buffer
+    assert b.fetch(0, out) and np.array_equal(out, blocks[-1])         # the newest only
+    assert b.fetch(0, out) is False                                    # taken
+    assert c.fetch(0, out) and np.array_equal(out, blocks[-1])         # per receiver
+    assert b.publish(np.ones((8, 5))) and a.fetch(1, out) and np.array_equal(out, np.ones((8, 5)))
+    with pytest.raises(MsplitError):
+        a.publish(np.zeros((9, 5)))                                    # larger than the slot
+    a.publish(np.zeros((4, 5)))
+    with pytest.raises(MsplitError):
+        b.fetch(0, np.zeros((8, 5), order="F"))                        # shape differs from what was sent
+    with pytest.raises(MsplitError):
+        a.fetch(0, out)                                                # not from itself
+    with pytest.raises(MsplitError):
+        AsyncBroadcast(name, 3, 1, 41, owner=False)                    # layout mismatch
+    c.destroy()
+    b.destroy()
+    a.destroy()
+
+
+def _bwriter(name, n_msgs, rows, cols):
+    sys.path.insert(0, ROOT)
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncBroadcast as AB
+    w = AB(name, 2, 1, rows * cols, owner=False)
+    skipped = 0
+    for k in range(1, n_msgs + 1):
+        while not w.publish(np.full((rows, cols), float(k), order="F")):
+            skipped += 1
+            if k < n_msgs:
+                break                                                  # skipped send, as MPI_Test would
+    w.destroy()
+
+
+def test_abcast_cross_process_no_torn_blocks():
+    """A writer process publishes blocks as fast as it can; every block the
+    reader takes is whole (a reader in a buffer keeps the writer out of it)
+    and versions only increase; the last one always arrives."""
+    name, rows, cols, n = _name(), 5000, 8, 1500
+    r = AsyncBroadcast(name, 2, 0, rows * cols, owner=True)
+    p = mp.get_context("spawn").Process(target=_bwriter, args=(name, n, rows, cols))
+    p.start()
+    out = np.zeros((rows, cols), order="F")
+    last, taken = 0, 0
+    while last < n:
+        if r.fetch(1, out):
+            v = out[0, 0]
+            assert np.all(out == v) and v > last
+            last, taken = v, taken + 1
+        elif p.exitcode not in (None, 0):
+            break
+    p.join(timeout=60)
+    assert p.exitcode == 0 and last == n and taken >= 1
     r.destroy()
 
 
@@ -156,11 +221,7 @@ class _Block:
     def __init__(self, layout, po, inner):
         self.po, self.layout, self.inner = po, layout, inner
         L = layout
-        if L.dim == 3:
-            ppb = L.nz // L.nb
-            Ab = po.poisson3d_rows(L.nx, L.ny, L.nz, L.b * ppb, (L.b + 1) * ppb)
-        else:
-            Ab = po.poisson2d_rows(L.nx, L.ny, L.r0, L.r1)
+        Ab = am_twin._block_rows(po, L.dim, L.nx, L.ny, L.nz, L.nb, L.b, L.peclet)
         self.A, _ = po.split(Ab, L.r0, L.r1)
         row_ids, crp, cc, cv = L.coupling
         rp = np.zeros(L.nrows + 1, np.int64)
@@ -228,6 +289,37 @@ class _Block:
 
     def error_sq(self):
         return self.po.norm2(self.x - 1.0, self.po.REDUCE_DBR) ** 2
+
+    def copy_halo_from(self, by_id):                                 # LocalComm exchange
+        for nbr, hoff, cnt, nbr_off in self.layout.recv:
+            self.halo[hoff:hoff + cnt] = by_id[nbr].x[nbr_off:nbr_off + cnt]
+
+    # global asynchronous minimization (AMAM-global), oracle arithmetic
+    def setup_global_async_minimization(self, s, outer):
+        L, po = self.layout, self.po
+        self.s, self.outer = s, dict(outer, reduce_mode=po.REDUCE_DBR)
+        self.S = np.zeros((self.lo + L.nrows + self.hi, s), order="F")
+        self.R_rep = [np.zeros((L.nrows, s), order="F") for _ in range(L.nb)]
+        self.b_all = [am_twin._block_rows(po, L.dim, L.nx, L.ny, L.nz, L.nb, j, L.peclet).mult(
+            np.ones(L.nrows * L.nb)) for j in range(L.nb)]
+
+    def store_column(self, k):
+        self.S[:, k] = np.concatenate([self.halo[:self.lo], self.x, self.halo[self.lo:self.lo + self.hi]])
+
+    def global_async_minimize(self, bcast):
+        L, po = self.layout, self.po
+        R = np.stack([self.A_ext.mult(np.ascontiguousarray(self.S[:, k])) for k in range(self.s)], axis=1)
+        self.R_rep[L.b] = np.asfortranarray(R)
+        bcast.publish(self.R_rep[L.b])
+        for j in range(L.nb):
+            if j != L.b:
+                bcast.fetch(j, self.R_rep[j])
+        alpha, r = po.lsqr(self.R_rep, self.b_all, **self.outer)
+        xe = po.dense_mult(self.S, alpha)
+        self.x = xe[self.lo:self.lo + L.nrows].copy()
+        self.halo[:self.lo] = xe[:self.lo]
+        self.halo[self.lo:self.lo + self.hi] = xe[self.lo + L.nrows:]
+        return r["rnorm"], r["its"], r["reason"]
 
     # local minimization (SMSM-local / AMAM-local), oracle arithmetic
     def setup_local_minimization(self, s, outer):
@@ -342,6 +434,59 @@ def test_am_multiprocess_gloo_terminates(world, problem):
     assert all(o[4] == out[0][4] for o in out)                       # one global final residual
     assert out[0][4] <= 10 * rtol * norm0
     assert len({o[2] for o in out}) == 1                             # same phase tag at the verdict
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,nb,s,max_it,peclet", [(3, 8, 8, 8, 2, 4, 5, None),
+                                                               (3, 6, 6, 9, 3, 3, 3, None),
+                                                               (2, 24, 20, 1, 2, 4, 5, (0.5, 0.25, 0.0))])
+def test_amam_global_roundrobin_host_matches_twin(oracle, dim, nx, ny, nz, nb, s, max_it, peclet):
+    """The product driver (am_solve, variant amam_global: msp_abcast broadcast of R,
+    C detection) over CPU test-double blocks, round-robin in one process, against
+    the twin's independent restatement of the loop: bit for bit."""
+    from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
+    inner = dict(restart=30, max_it=max_it, rtol=1e-20)
+    blocks = [_Block(block_layout(dim, nx, ny, nz, nb, b, peclet), oracle, inner) for b in range(nb)]
+    for blk in blocks:
+        blk.setup_global_async_minimization(s, OUTER)
+    res = am_solve(blocks, LocalComm(), rtol=1e-6, record=True, variant="amam_global", s=s)
+    tw = am_twin.amam_global_roundrobin(oracle, dim, nx, ny, nz, nb, s, 1e-6, inner, OUTER, peclet=peclet)
+    assert res.norm0 == tw["norm0"] and res.iterations == tw["iterations"] and res.inner_its == tw["inner_its"]
+    assert res.trace == tw["trace"]
+    assert np.array_equal(np.concatenate([blk.x for blk in blocks]), tw["x"])
+    assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
+
+
+def _global_worker(rank, world, port, problem, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    import torch.distributed as dist
+    from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        dim, nx, ny, nz, s, rtol, max_it = problem
+        blk = _Block(block_layout(dim, nx, ny, nz, world, rank), po, dict(restart=30, max_it=max_it, rtol=1e-20))
+        blk.setup_global_async_minimization(s, OUTER)
+        res = am_solve([blk], TorchComm(), rtol=rtol, max_iterations=20000, variant="amam_global", s=s)
+        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.error))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_amam_global_multiprocess_gloo_terminates(world):
+    """One process per block, truly asynchronous (R broadcast through shared
+    memory while the others compute): the detection terminates every block
+    in the same phase, with one global final residual."""
+    out = _run(world, (3, 6, 6, 12, 3, 1e-6, 5), _global_worker)
+    assert all(o[3] == out[0][3] for o in out)
+    assert all(o[4] == out[0][4] for o in out)
+    assert out[0][4] <= 1e-2 * out[0][3]
+    assert len({o[2] for o in out}) == 1
 
 
 def test_semi_local_twins_converge(oracle):

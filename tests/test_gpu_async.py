@@ -145,3 +145,25 @@ def test_amam_semi_local_convdiff_gpu_bitwise_vs_twin(ctx, oracle):
     assert res.iterations == tw["iterations"] and res.trace == tw["trace"]
     assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
     assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
+
+
+@pytest.mark.parametrize("dim,nx,ny,nz,nb,s,max_it,peclet", [(2, 24, 20, 1, 2, 4, 5, None),
+                                                               (3, 8, 8, 8, 2, 4, 5, None),
+                                                               (3, 6, 6, 9, 3, 3, 3, None),
+                                                               (3, 8, 8, 8, 4, 4, 5, PE)])
+def test_amam_global_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s, max_it, peclet):
+    """AMAM-global (configs[3]/[4]'s algorithm): R rows broadcast through msp_abcast,
+    LSQR over the replicated R, x_minimized into x_i and the neighbour view."""
+    opts = Options(" ".join(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 "
+                            f"-inner{b + 1}_pc_type none" for b in range(nb)) + " " + _outer_opts(nb))
+    comm = LocalComm()
+    blocks = make_blocks(ctx, dim, nx, ny, nz, nb, range(nb), opts, comm, peclet)
+    for blk in blocks:
+        blk.setup_global_async_minimization(s)
+    res = am_solve(blocks, comm, rtol=1e-6, record=True, variant="amam_global", s=s)
+    tw = am_twin.amam_global_roundrobin(oracle, dim, nx, ny, nz, nb, s, 1e-6,
+                                        dict(restart=30, max_it=max_it, rtol=1e-20), OUTER, peclet=peclet)
+    assert res.norm0 == tw["norm0"] and res.iterations == tw["iterations"] and res.inner_its == tw["inner_its"]
+    assert res.trace == tw["trace"]
+    assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])
+    assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
