@@ -27,6 +27,20 @@ static_assert(kChunk == MSK_DBR_CHUNK, "DBR chunk must match the oracle");
 
 __device__ __forceinline__ bool stopped(const int* stop) { return stop && *stop; }
 
+// Column loads: VEC 0 = scalar (unaligned / ragged), 1 = 16-byte default policy,
+// 2 = 16-byte non-temporal (the default: the columns of S and R stream through
+// once per launch and dwarf the MALL; msplit_kernels.hip, MSK_TUNE_VEC_TEMPORAL).
+typedef double dx2 __attribute__((ext_vector_type(2)));
+template <int VEC>
+__device__ __forceinline__ double2 ld_col(const double* p) {
+  if constexpr (VEC == 2) {
+    const dx2 v = __builtin_nontemporal_load(reinterpret_cast<const dx2*>(p));
+    return make_double2(v.x, v.y);
+  } else {
+    return *reinterpret_cast<const double2*>(p);
+  }
+}
+
 __device__ __forceinline__ double wave_butterfly(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
@@ -36,7 +50,7 @@ __device__ __forceinline__ double wave_butterfly(double v) {
 // ------------------------------------------------------------------ gemv
 // y = A[:, 0:nc] coef (+ nal * U, VecAXPY skipped when nal == 0), per row
 // ((0 + c0 a0) + c1 a1) + ...; NORM: the DBR partial of ||y||^2 of this chunk.
-template <bool AXPY, bool NORM, bool FULL>
+template <bool AXPY, bool NORM, bool FULL, int VEC>
 __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t lda, int nc,
                                           const double* __restrict__ coef, double nal, const double* __restrict__ U,
                                           double* __restrict__ y, int64_t base, int64_t n, double& sq) {
@@ -52,7 +66,7 @@ __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t 
     for (int j = 0; j < kIters; ++j) {
       const int64_t e = base + j * (2 * kT);
       if (FULL) {
-        const double2 v = *reinterpret_cast<const double2*>(col + e);
+        const double2 v = ld_col<VEC>(col + e);
         p[2 * j] = v.x;
         p[2 * j + 1] = v.y;
       } else {
@@ -95,7 +109,7 @@ __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t 
   sq = acc;
 }
 
-template <bool AXPY, bool NORM, bool VEC>
+template <bool AXPY, bool NORM, int VEC>
 __global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A, int64_t lda, int nc,
                                                    const double* __restrict__ coef, const double* __restrict__ naldev,
                                                    const double* __restrict__ U, double* __restrict__ y, int64_t n,
@@ -106,8 +120,8 @@ __global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A,
   const int64_t base = c * kChunk + 2 * t;
   const double nal = AXPY ? *naldev : 0.0;
   double sq = 0.0;
-  if (VEC && (c + 1) * kChunk <= n) gemv_body<AXPY, NORM, true>(A, lda, nc, coef, nal, U, y, base, n, sq);
-  else gemv_body<AXPY, NORM, false>(A, lda, nc, coef, nal, U, y, base, n, sq);
+  if (VEC && (c + 1) * kChunk <= n) gemv_body<AXPY, NORM, true, VEC>(A, lda, nc, coef, nal, U, y, base, n, sq);
+  else gemv_body<AXPY, NORM, false, VEC>(A, lda, nc, coef, nal, U, y, base, n, sq);
   if (NORM) {
     __shared__ double red[4];
     sq = wave_butterfly(sq);
@@ -120,7 +134,7 @@ __global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A,
 // ------------------------------------------------------- scaled column dots
 // w' = w * (*sc) (VecScale, written back to wout) when SCALE, then the DBR
 // stage-1 partials of column_v . w' for v < nc: partial[v*nchunks + c].
-template <bool SCALE, bool VEC>
+template <bool SCALE, int VEC>
 __global__ __launch_bounds__(kT) void k_scaled_dot(const double* win, double* wout, const double* __restrict__ scdev,
                                                    const double* __restrict__ A, int64_t lda, int nc, int64_t n,
                                                    double* __restrict__ partial, int64_t nchunks,
@@ -162,7 +176,7 @@ __global__ __launch_bounds__(kT) void k_scaled_dot(const double* win, double* wo
     if (full) {
       double2 q[kIters];
 #pragma unroll
-      for (int j = 0; j < kIters; ++j) q[j] = *reinterpret_cast<const double2*>(col + base + j * (2 * kT));
+      for (int j = 0; j < kIters; ++j) q[j] = ld_col<VEC>(col + base + j * (2 * kT));
 #pragma unroll
       for (int j = 0; j < kIters; ++j) {
         acc = acc + wr[2 * j] * q[j].x;
@@ -225,16 +239,20 @@ extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc,
     return MSP_SUCCESS;
   }
   const int64_t nch = nchunks_of(n);
-  const bool vec = aligned16(A) && (lda % 2 == 0) && aligned16(y) && (!U || aligned16(U));
+  const int vec = !(aligned16(A) && (lda % 2 == 0) && aligned16(y) && (!U || aligned16(U))) ? 0
+                  : (msk_get_tuning() & MSK_TUNE_VEC_TEMPORAL) ? 1 : 2;
   const bool axpy = U != nullptr, norm = sumsq_dev != nullptr;
   KTimer kt(c, MSP_KERNEL_DGEMV, 8.0 * (double)n * (nc + 1 + (axpy ? 1 : 0)));
   const dim3 g((unsigned)nch), b(kT);
 #define GEMV(AX, NO, VE) \
   k_dense_gemv<AX, NO, VE><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, y, n, partial, stop)
-  if (axpy && norm) { if (vec) GEMV(true, true, true); else GEMV(true, true, false); }
-  else if (axpy) { if (vec) GEMV(true, false, true); else GEMV(true, false, false); }
-  else if (norm) { if (vec) GEMV(false, true, true); else GEMV(false, true, false); }
-  else { if (vec) GEMV(false, false, true); else GEMV(false, false, false); }
+#define GEMV3(AX, NO) \
+  if (vec == 2) GEMV(AX, NO, 2); else if (vec == 1) GEMV(AX, NO, 1); else GEMV(AX, NO, 0);
+  if (axpy && norm) { GEMV3(true, true) }
+  else if (axpy) { GEMV3(true, false) }
+  else if (norm) { GEMV3(false, true) }
+  else { GEMV3(false, false) }
+#undef GEMV3
 #undef GEMV
   KCHK((int)hipGetLastError());
   if (norm) KCHK(msk_dot_stage2(partial, nch, 1, sumsq_dev, stop, c->stream));
@@ -251,20 +269,25 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
     return MSP_SUCCESS;
   }
   KTimer kt(c, MSP_KERNEL_DGEMVT, 8.0 * (double)n * (nc + 1 + (sc_dev ? 1 : 0)));
-  const bool vec = aligned16(A) && (lda % 2 == 0) && aligned16(win) && (!sc_dev || aligned16(wout));
+  const int vec = !(aligned16(A) && (lda % 2 == 0) && aligned16(win) && (!sc_dev || aligned16(wout))) ? 0
+                  : (msk_get_tuning() & MSK_TUNE_VEC_TEMPORAL) ? 1 : 2;
   for (int g0 = 0; g0 < nc; g0 += kMaxCols) {
     const int g = std::min(kMaxCols, nc - g0);
     const double* Ag = A + (int64_t)g0 * lda;
     const bool scale = sc_dev && g0 == 0;          // scale once, later groups read the scaled vector
     const double* src = (sc_dev && g0 > 0) ? wout : win;
     const dim3 gr((unsigned)nch), b(kT);
+#define SDOT(SC, VE, WO, SD) k_scaled_dot<SC, VE><<<gr, b, 0, c->stream>>>(src, WO, SD, Ag, lda, g, n, partial, nch, stop)
     if (scale) {
-      if (vec) k_scaled_dot<true, true><<<gr, b, 0, c->stream>>>(src, wout, sc_dev, Ag, lda, g, n, partial, nch, stop);
-      else k_scaled_dot<true, false><<<gr, b, 0, c->stream>>>(src, wout, sc_dev, Ag, lda, g, n, partial, nch, stop);
+      if (vec == 2) SDOT(true, 2, wout, sc_dev);
+      else if (vec == 1) SDOT(true, 1, wout, sc_dev);
+      else SDOT(true, 0, wout, sc_dev);
     } else {
-      if (vec) k_scaled_dot<false, true><<<gr, b, 0, c->stream>>>(src, nullptr, nullptr, Ag, lda, g, n, partial, nch, stop);
-      else k_scaled_dot<false, false><<<gr, b, 0, c->stream>>>(src, nullptr, nullptr, Ag, lda, g, n, partial, nch, stop);
+      if (vec == 2) SDOT(false, 2, nullptr, nullptr);
+      else if (vec == 1) SDOT(false, 1, nullptr, nullptr);
+      else SDOT(false, 0, nullptr, nullptr);
     }
+#undef SDOT
     KCHK((int)hipGetLastError());
     KCHK(msk_dot_stage2(partial, nch, g, out_dev + g0, stop, c->stream));
   }

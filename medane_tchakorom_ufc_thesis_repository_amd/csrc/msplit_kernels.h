@@ -29,7 +29,14 @@ struct BoxCoef {
 enum { MSK_SPMV_MULT = 0, MSK_SPMV_RESID = 1, MSK_SPMV_SCALED = 2 };
 
 // tuning flags
-enum { MSK_TUNE_MDOT_REV = 1, MSK_TUNE_SPMV_NT = 2, MSK_TUNE_SPMV_XCD = 4, MSK_TUNE_SPMV_STAGE1 = 8 };
+enum {
+  MSK_TUNE_MDOT_REV = 1,
+  MSK_TUNE_SPMV_NT = 2,
+  MSK_TUNE_SPMV_XCD = 4,
+  MSK_TUNE_SPMV_STAGE1 = 8,
+  MSK_TUNE_VEC_TEMPORAL = 16,       // default-policy (not non-temporal) basis loads in MDot / MAXPY / dense
+  MSK_TUNE_MAXPY_TEMPORAL_ST = 64  // default-policy store of w in MAXPY
+};
 
 extern "C" {
 void msk_set_tuning(int flags);

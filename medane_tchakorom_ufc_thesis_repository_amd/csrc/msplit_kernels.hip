@@ -55,14 +55,16 @@ __device__ __forceinline__ double wave_butterfly(double v) {
 // elements base + j*512 + 2t, +1 (j = 0..7) in order, wave butterfly, then
 // (w0 + w1) + (w2 + w3).  partial[v * nchunks + c].  w stays in registers and
 // each vector streams 32 KiB contiguous per workgroup.
-template <int NV, bool SELF>
-__global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w, Vecs V, int64_t n,
-                                                   double* __restrict__ partial, int64_t nchunks,
-                                                   const int* __restrict__ stop, int rev) {
-  if (stopped(stop)) return;
-  __shared__ double red[NV][4];
+// VAR: bit 0 = non-temporal loads of the basis vectors (the default: each
+// vector streams through once per kernel and is far larger than the 256 MiB
+// MALL, so caching it only evicts lines others still need; +8-16 % per kernel,
+// +7.7 % per GMRES step on 256^3, same-box A/B); bit 2 = non-temporal store
+// of w in MAXPY.  Results are identical.
+template <int NV, bool SELF, int VAR>
+__device__ __forceinline__ void dot_chunk(const double* __restrict__ w, const Vecs& V, int64_t n,
+                                          double* __restrict__ partial, int64_t nchunks, int rev, int64_t c,
+                                          double (&red)[NV][4]) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int64_t c = blockIdx.x;
   const int64_t base = c * kChunk + 2 * t;
   const bool full = (c + 1) * kChunk <= n;
   double wr[2 * kIters];
@@ -104,7 +106,10 @@ __global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w,
       if (full) {
         double2 q[kIters];
 #pragma unroll
-        for (int j = 0; j < kIters; ++j) q[j] = *reinterpret_cast<const double2*>(y + base + j * (2 * kT));
+        for (int j = 0; j < kIters; ++j) {
+          const double2* pq = reinterpret_cast<const double2*>(y + base + j * (2 * kT));
+          q[j] = (VAR & 1) ? ld_nt(pq) : *pq;
+        }
 #pragma unroll
         for (int j = 0; j < kIters; ++j) {
           acc = acc + wr[2 * j] * q[j].x;
@@ -124,6 +129,15 @@ __global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w,
   }
   __syncthreads();
   if (t < NV) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+}
+
+template <int NV, bool SELF, int VAR>
+__global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w, Vecs V, int64_t n,
+                                                   double* __restrict__ partial, int64_t nchunks,
+                                                   const int* __restrict__ stop, int rev) {
+  if (stopped(stop)) return;
+  __shared__ double red[NV][4];
+  dot_chunk<NV, SELF, VAR>(w, V, n, partial, nchunks, rev, blockIdx.x, red);
 }
 
 // Stage 2: workgroup v folds the nchunks partials of vector v the same way.
@@ -171,7 +185,7 @@ __device__ __forceinline__ double group_sum(const double (&a)[G], const double (
   }
 }
 
-template <int G, bool FULL>
+template <int G, bool FULL, int VAR>
 __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs& V, const Coefs& A,
                                             const double* __restrict__ adev, int negate, int g, int64_t base,
                                             int64_t n) {
@@ -190,7 +204,8 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs&
 #pragma unroll
     for (int q = 0; q < G; ++q) {
       if (FULL) {
-        const double2 v = *reinterpret_cast<const double2*>(vp[q] + e);
+        const double2* pv = reinterpret_cast<const double2*>(vp[q] + e);
+        const double2 v = (VAR & 1) ? ld_nt(pv) : *pv;
         p0[q] = v.x;
         p1[q] = v.y;
       } else {
@@ -209,7 +224,7 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs&
   }
 }
 
-template <bool ACCUM, bool NORM, bool FULL>
+template <bool ACCUM, bool NORM, bool FULL, int VAR>
 __device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win, double* __restrict__ wout,
                                                  const Vecs& V, const Coefs& A, const double* __restrict__ adev,
                                                  int negate, int nv, int64_t base, int64_t n, double& sq) {
@@ -230,11 +245,11 @@ __device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win,
     }
   }
   const int jrem = nv & 3;
-  if (jrem == 3) chunk_group<3, FULL>(u, V, A, adev, negate, 0, base, n);
-  else if (jrem == 2) chunk_group<2, FULL>(u, V, A, adev, negate, 0, base, n);
-  else if (jrem == 1) chunk_group<1, FULL>(u, V, A, adev, negate, 0, base, n);
+  if (jrem == 3) chunk_group<3, FULL, VAR>(u, V, A, adev, negate, 0, base, n);
+  else if (jrem == 2) chunk_group<2, FULL, VAR>(u, V, A, adev, negate, 0, base, n);
+  else if (jrem == 1) chunk_group<1, FULL, VAR>(u, V, A, adev, negate, 0, base, n);
 #pragma unroll 1
-  for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL>(u, V, A, adev, negate, g, base, n);
+  for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL, VAR>(u, V, A, adev, negate, g, base, n);
   double acc = 0.0;
 #pragma unroll
   for (int j = 0; j < kIters; ++j) {
@@ -246,7 +261,14 @@ __device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win,
         r0 = q.x + r0;
         r1 = q.y + r1;
       }
-      *reinterpret_cast<double2*>(wout + e) = make_double2(r0, r1);
+      if constexpr ((VAR & 4) != 0) {
+        dx2 o;
+        o.x = r0;
+        o.y = r1;
+        __builtin_nontemporal_store(o, reinterpret_cast<dx2*>(wout + e));
+      } else {
+        *reinterpret_cast<double2*>(wout + e) = make_double2(r0, r1);
+      }
       if (NORM) {
         acc = acc + r0 * r0;
         acc = acc + r1 * r1;
@@ -267,7 +289,7 @@ __device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win,
   sq = acc;
 }
 
-template <bool ACCUM, bool NORM>
+template <bool ACCUM, bool NORM, int VAR>
 __global__ __launch_bounds__(kT) void k_maxpy_chunk(const double* win, double* wout, Vecs V, Coefs A,
                                                     const double* __restrict__ adev, int negate, int nv,
                                                     const int* __restrict__ nvdev, int64_t n,
@@ -279,8 +301,8 @@ __global__ __launch_bounds__(kT) void k_maxpy_chunk(const double* win, double* w
   const int64_t c = blockIdx.x;
   const int64_t base = c * kChunk + 2 * t;
   double sq = 0.0;
-  if ((c + 1) * kChunk <= n) maxpy_chunk_body<ACCUM, NORM, true>(win, wout, V, A, adev, negate, nv, base, n, sq);
-  else maxpy_chunk_body<ACCUM, NORM, false>(win, wout, V, A, adev, negate, nv, base, n, sq);
+  if ((c + 1) * kChunk <= n) maxpy_chunk_body<ACCUM, NORM, true, VAR>(win, wout, V, A, adev, negate, nv, base, n, sq);
+  else maxpy_chunk_body<ACCUM, NORM, false, VAR>(win, wout, V, A, adev, negate, nv, base, n, sq);
   if (NORM) {
     __shared__ double red[4];
     sq = wave_butterfly(sq);
@@ -607,22 +629,28 @@ static inline int grid_for(int64_t work, int cap) {
   return (int)g;
 }
 
-template <int NV>
+// basis-vector load policy: non-temporal unless MSK_TUNE_VEC_TEMPORAL (A/B)
+static inline int vec_var() { return (g_tuning & MSK_TUNE_VEC_TEMPORAL) ? 0 : 1; }
+
+template <int NV, int VAR>
 static void dot1_dispatch(int nv, const double* w, const Vecs& V, int64_t n, double* partial, int64_t nchunks,
                           const int* stop, hipStream_t s) {
   if (nv == NV) {
-    k_dot_stage1<NV, false><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, V, n, partial, nchunks, stop,
-                                                                          (g_tuning & MSK_TUNE_MDOT_REV) ? 1 : 0);
+    k_dot_stage1<NV, false, VAR><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(
+        w, V, n, partial, nchunks, stop, (g_tuning & MSK_TUNE_MDOT_REV) ? 1 : 0);
   } else if constexpr (NV < MSK_MAX_GROUP) {
-    dot1_dispatch<NV + 1>(nv, w, V, n, partial, nchunks, stop, s);
+    dot1_dispatch<NV + 1, VAR>(nv, w, V, n, partial, nchunks, stop, s);
   }
 }
 
 extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
                               int self, const int* stop, hipStream_t s) {
   if (nchunks <= 0) return 0;
-  if (self) k_dot_stage1<1, true><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, *V, n, partial, nchunks, stop, 0);
-  else dot1_dispatch<1>(nv, w, *V, n, partial, nchunks, stop, s);
+  const int var = vec_var();
+  if (self)
+    k_dot_stage1<1, true, 0><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, *V, n, partial, nchunks, stop, 0);
+  else if (var) dot1_dispatch<1, 1>(nv, w, *V, n, partial, nchunks, stop, s);
+  else dot1_dispatch<1, 0>(nv, w, *V, n, partial, nchunks, stop, s);
   return (int)hipGetLastError();
 }
 
@@ -636,16 +664,26 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
                                const Coefs* A, const double* adev, int negate, int64_t n, int accum, double* partial,
                                const int* stop, hipStream_t s) {
   if (n <= 0 || (nv <= 0 && !nvdev)) return 0;
+  // non-temporal store of w too unless MSK_TUNE_MAXPY_TEMPORAL_ST (+0.4 % per step)
+  const int var = vec_var() | ((g_tuning & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4);
   const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
-  if (partial)
-    k_maxpy_chunk<false, true><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n, partial,
-                                                            stop);
-  else if (accum)
-    k_maxpy_chunk<true, false><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n, partial,
-                                                            stop);
-  else
-    k_maxpy_chunk<false, false><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n, partial,
-                                                             stop);
+#define MSK_MAXPY_LAUNCH(V_)                                                                                     \
+  if (partial)                                                                                                  \
+    k_maxpy_chunk<false, true, V_><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n,   \
+                                                                partial, stop);                                \
+  else if (accum)                                                                                               \
+    k_maxpy_chunk<true, false, V_><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n,   \
+                                                                partial, stop);                                \
+  else                                                                                                          \
+    k_maxpy_chunk<false, false, V_><<<dim3(g), dim3(kT), 0, s>>>(win, wout, *V, *A, adev, negate, nv, nvdev, n,  \
+                                                                 partial, stop);
+  switch (var) {
+    case 0: MSK_MAXPY_LAUNCH(0) break;
+    case 1: MSK_MAXPY_LAUNCH(1) break;
+    case 4: MSK_MAXPY_LAUNCH(4) break;
+    default: MSK_MAXPY_LAUNCH(5) break;
+  }
+#undef MSK_MAXPY_LAUNCH
   return (int)hipGetLastError();
 }
 
