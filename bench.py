@@ -283,7 +283,10 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    if variant == "smsm":
+        mini.close()                            # the LSQR communicator before the process group
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

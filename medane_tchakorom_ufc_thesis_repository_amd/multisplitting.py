@@ -356,6 +356,15 @@ class GpuMinimizer:
         self.lsqr.set_comm(self.comm)
         self.alpha = Vec(ctx, blocks[0].s)
 
+    def close(self):
+        """Release the cross-rank communicator while the process group still runs
+        (ncclCommDestroy is collective-free, but must precede the runtime's teardown)."""
+        self.ctx.synchronize()
+        if self.comm is not None:
+            self.lsqr.set_comm(None)
+            self.comm.destroy()
+            self.comm = None
+
     def solve(self, blocks):
         self.lsqr.solve([blk.b for blk in blocks], self.alpha)
         for blk in blocks:

@@ -398,9 +398,10 @@ class DenseMat:
 class Comm:
     """Cross-process all-gather used by the distributed LSQR (msp_comm)."""
 
-    def __init__(self, h: C.c_void_p, keep=None):
+    def __init__(self, h: C.c_void_p, keep=None, ctx: Context | None = None):
         self.h = h
         self._keep = keep
+        self._ctx = ctx          # msp_comm synchronises the context's stream on destroy: keep it alive
         n, r = C.c_int32(), C.c_int32()
         call("msp_comm_get_size", h, C.byref(n), C.byref(r))
         self.size, self.rank = n.value, r.value
@@ -416,7 +417,7 @@ class Comm:
         buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)
         h = C.c_void_p()
         call("msp_comm_create_rccl", ctx.h, int(nranks), int(rank), buf, C.byref(h))
-        return cls(h)
+        return cls(h, ctx=ctx)
 
     @classmethod
     def host(cls, ctx: Context, nranks: int, rank: int, allgather) -> "Comm":
@@ -432,7 +433,7 @@ class Comm:
         fn = _lib.ALLGATHER_FN(cb)
         h = C.c_void_p()
         call("msp_comm_create_host", ctx.h, int(nranks), int(rank), fn, None, C.byref(h))
-        return cls(h, keep=fn)
+        return cls(h, keep=fn, ctx=ctx)
 
     def allgather(self, send: Vec, recv: Vec, count: int):
         call("msp_comm_allgather", self.h, send.h, recv.h, int(count))
