@@ -54,6 +54,8 @@ class AMResult:
     error: float = float("nan")
     elapsed: float = 0.0
     trace: list = field(default_factory=list)          # (block, iteration, local norm, state, phase tag)
+    timers: dict = field(default_factory=dict)         # host seconds per phase, summed over local blocks
+    converged: bool = True                             # False: stopped at max_iterations (stop_at_limit)
 
 
 class AsyncBlock:
@@ -73,6 +75,13 @@ class AsyncBlock:
         self.state = ConvDetection.NORMAL
         self.tag = 0
         self.local_norm = math.inf
+        self.timers = {"solve": 0.0, "exchange": 0.0, "minimize": 0.0, "detect": 0.0}
+
+    def _timed(self, key, fn, *args):
+        t0 = time.perf_counter()
+        r = fn(*args)
+        self.timers[key] += time.perf_counter() - t0
+        return r
 
     def _receive(self):
         """comm_async_probe_and_receive_prime: newest iterate of each dependency."""
@@ -100,34 +109,35 @@ class AsyncBlock:
 
     def iterate(self, norm0: float, rtol: float, atol: float, trace=None, variant: str = "am", s: int = 0):
         blk = self.blk
+        T = self._timed
         if variant == "am":                                           # asynchronous-multisplitting_prime.c:333-377
-            self._receive()
+            T("exchange", self._receive)
             blk.update_rhs()
-            self.inner += blk.solve()
-            self._publish(self.it)
+            self.inner += T("solve", blk.solve)
+            T("exchange", self._publish, self.it)
         elif variant in ("amam_semi_local", "amam_global"):          # AMAM-semi-local_prime.c:350-420,
             for k in range(s):                                        # AMAM-global_prime.c:378-413
-                self._receive()
+                T("exchange", self._receive)
                 blk.update_rhs()
-                self.inner += blk.solve()
-                self._publish(self.steps)
-                self._receive()
+                self.inner += T("solve", blk.solve)
+                T("exchange", self._publish, self.steps)
+                T("exchange", self._receive)
                 blk.store_column(k)
                 self.steps += 1
             if variant == "amam_global":
-                blk.global_async_minimize(self.bcast)
+                T("minimize", blk.global_async_minimize, self.bcast)
             else:
-                blk.semi_local_minimize(apply=False)
+                T("minimize", blk.semi_local_minimize, False)
         else:                                                         # AMAM-local_prime.c:371-404
             for k in range(s):
-                self._receive()
+                T("exchange", self._receive)
                 blk.update_rhs()
-                self.inner += blk.solve()
-                self._publish(self.steps)
+                self.inner += T("solve", blk.solve)
+                T("exchange", self._publish, self.steps)
                 blk.store_local_column(k)
                 self.steps += 1
-            blk.local_minimize()
-        self._detect(norm0, rtol, atol, trace, block_norm=variant == "amam_global")
+            T("minimize", blk.local_minimize)
+        T("detect", self._detect, norm0, rtol, atol, trace, variant == "amam_global")
 
     def close(self):
         self.cvd.destroy()
@@ -146,12 +156,15 @@ def _channel_name(comm) -> str:
 
 
 def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: int = 100000,
-             strict: bool = False, record: bool = False, monitor=None, variant: str = "am", s: int = 0) -> AMResult:
+             strict: bool = False, record: bool = False, monitor=None, variant: str = "am", s: int = 0,
+             stop_at_limit: bool = False) -> AMResult:
     """The asynchronous multisplitting loop (asynchronous-multisplitting_prime.c:333-392);
     variant "amam_local" adds the block-local minimization every s inner steps
     (the blocks must have setup_local_minimization(s)), "amam_semi_local" the
     semi-local one (setup_minimization(s)), "amam_global" the global one
-    (setup_global_async_minimization(s))."""
+    (setup_global_async_minimization(s)).  At max_iterations the run raises, or
+    (stop_at_limit, for timing runs) every block stops and the result says
+    converged = False."""
     if variant not in ("am", "amam_local", "amam_semi_local", "amam_global"):
         raise ValueError(f"unknown asynchronous variant {variant}")
     res = AMResult()
@@ -185,7 +198,10 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
                 monitor(ab.blk.layout.b, ab.it, ab.local_norm, ab.state, ab.tag)
         active = [ab for ab in active if ab.state != ConvDetection.FINISHED]
         if any(ab.it >= max_iterations for ab in active):
-            raise RuntimeError(f"asynchronous multisplitting did not terminate in {max_iterations} iterations")
+            if not stop_at_limit:
+                raise RuntimeError(f"asynchronous multisplitting did not terminate in {max_iterations} iterations")
+            res.converged = False
+            break
     comm.barrier()
     res.elapsed = time.perf_counter() - t0
     comm.exchange(blocks)                            # comm_sync_send_and_receive_final (:396)
@@ -196,6 +212,8 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
         res.iterations.append(ab.it)
         res.inner_its.append(ab.inner)
         res.phase_tags.append(ab.tag)
+        for k, v in ab.timers.items():
+            res.timers[k] = res.timers.get(k, 0.0) + v
     res.trace = trace or []
     comm.barrier()
     for ab in asyncs.values():
