@@ -210,10 +210,10 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
     rc = mspi_spmv_scaled(k->A, k->tmp, &k->g.st->scale, VV(k, it), VV(k, it + 1), stop);
     /* CGS: h = VecMDot(VV(it+1), VV(0..it)); T = VV(it+1) - sum h_j VV(j); ||T||^2 */
     if (!rc) rc = mspi_mdot_basis(c, VV(k, it + 1), it + 1, k->basis, k->stride, k->n, k->g.h, stop);
+    /* then h(it+1) = ||T||^2 and the Hessenberg column update */
     if (!rc)
-      rc = mspi_maxpy_norm_basis(c, VV(k, it + 1), k->tmp, it + 1, k->basis, k->stride, k->n, k->g.h,
-                                 &k->g.h[it + 1], stop);
-    if (!rc) rc = mspi_gm_iter_update(c, k->g);
+      rc = mspi_maxpy_norm_update(c, VV(k, it + 1), k->tmp, it + 1, k->basis, k->stride, k->n, k->g, it,
+                                  k->o.restart, stop);
   }
   /* KSPGMRESBuildSoln: back-solve (one lane), then x += sum nrs_j VV(j) */
   if (!rc) rc = mspi_gm_build(c, k->g);

@@ -154,6 +154,132 @@ __global__ void k_iter_update(mspi_gmres_dev g) {
   if (itn && (st->reason || st->its >= st->max_it)) log_res(g, res);
 }
 
+// The same step fused with the stage-2 DBR reduction of ||w||^2 (the partials the
+// norm-fused CGS VecMAXPY left): one launch instead of two, and the serial
+// recurrence reads the column, cc and ss from LDS (staged by all lanes) instead of
+// one dependent global load after another.  The sum is k_dot_stage2's, the
+// recurrence k_iter_update's statement for statement: results are identical.
+constexpr int kUT = 256;
+
+__device__ inline double fold_partials(const double* __restrict__ p, int64_t nchunks, double* red) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double acc = 0.0;
+  int64_t i = t;
+  for (; i + 7 * kUT < nchunks; i += 8 * kUT) {  // k_dot_stage2's order: lane t adds p[t], p[t+256], ...
+    double q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) q[u] = p[i + u * kUT];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = acc + q[u];
+  }
+  for (; i < nchunks; i += kUT) acc = acc + p[i];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+  if (lane == 0) red[wv] = acc;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(kUT) void k_norm_update(mspi_gmres_dev g, const double* __restrict__ partial,
+                                                     int64_t nchunks) {
+  mspi_gmres_state* st = g.st;
+  if (st->stop) return;  // uniform: every lane reads the same flag
+  __shared__ double red[4];
+  extern __shared__ double lds[];  // hh column (m+2), cc (m+2), ss (m+2)
+  const int t = threadIdx.x;
+  const int it = st->it, m2 = st->m + 2;
+  const double sumsq = fold_partials(partial, nchunks, red);
+  double* lh = lds;
+  double* lc = lds + m2;
+  double* ls = lds + 2 * m2;
+  for (int j = t; j <= it; j += kUT) {
+    lh[j] = g.h[j];
+    lc[j] = g.cc[j];
+    ls[j] = g.ss[j];
+  }
+  __syncthreads();
+  __shared__ int ncol;
+  if (t == 0) {
+    g.h[it + 1] = sumsq;
+    ncol = 0;
+    bool nan_dot = false;
+    for (int j = 0; j <= it; ++j)
+      if (bad(lh[j])) nan_dot = true;
+    double* hh = lh;  // the column, built in LDS: hh[j] = 0 - (-h[j])
+    double res = st->res;
+    int hapend = 0;
+    bool done = false;
+    if (nan_dot) {
+      st->reason = MSP_DIVERGED_NANORINF;
+      for (int j = 0; j <= it; ++j) hh[j] = 0.0;
+      ncol = it + 1;
+    } else {
+      for (int j = 0; j <= it; ++j) {
+        double v = 0.0;
+        v -= -hh[j];
+        hh[j] = v;
+      }
+      const double tt = sqrt(sumsq);
+      if (bad(tt)) {
+        st->reason = MSP_DIVERGED_NANORINF;
+        st->stop = st->skip_build = 1;
+        ncol = it + 1;
+        done = true;
+      } else {
+        st->scale = (tt != 0.0) ? 1.0 / tt : 1.0;
+        hh[it + 1] = tt;
+        double hapbnd = fabs(tt / g.grs[it]);
+        if (hapbnd > st->haptol) hapbnd = st->haptol;
+        if (tt < hapbnd) hapend = 1;
+        // KSPGMRESUpdateHessenberg on the LDS column
+        for (int j = 1; j <= it; ++j) {
+          const double a = hh[j - 1];
+          hh[j - 1] = lc[j - 1] * a + ls[j - 1] * hh[j];
+          hh[j] = lc[j - 1] * hh[j] - (ls[j - 1] * a);
+        }
+        if (!hapend) {
+          const double r = sqrt(hh[it] * hh[it] + hh[it + 1] * hh[it + 1]);
+          if (r == 0.0) {
+            st->reason = MSP_DIVERGED_NULL;
+          } else {
+            const double c = hh[it] / r, sn = hh[it + 1] / r;
+            g.cc[it] = c;
+            g.ss[it] = sn;
+            const double grs = g.grs[it];
+            g.grs[it + 1] = -(sn * grs);
+            g.grs[it] = c * grs;
+            hh[it] = c * hh[it] + sn * hh[it + 1];
+            res = fabs(g.grs[it + 1]);
+          }
+        } else {
+          res = 0.0;
+        }
+        ncol = it + 2;
+        st->it = it + 1;
+        st->its++;
+        st->rnorm = res;
+        st->res = res;
+        if (!st->reason) {
+          converged(g, st->its, res);
+          if (hapend && !st->reason) st->reason = MSP_DIVERGED_BREAKDOWN;
+        }
+      }
+    }
+    if (!done) {
+      const int itn = st->it;
+      if (!st->reason && itn < st->m && st->its < st->max_it) {
+        log_res(g, res);
+      } else {
+        st->stop = 1;
+        if (itn && (st->reason || st->its >= st->max_it)) log_res(g, res);
+      }
+    }
+  }
+  __syncthreads();
+  double* col = &HHD(0, it);
+  for (int j = t; j < ncol; j += kUT) col[j] = lh[j];
+}
+
 // KSPGMRESBuildSoln(GRS(0), x, x, ksp, it - 1): back-solve in place (nrs
 // aliases GRS); the x update is the accumulate-MAXPY that follows.
 __global__ void k_build(mspi_gmres_dev g) {
@@ -202,6 +328,17 @@ extern "C" int mspi_gm_iter_update(msp_ctx* ctx, mspi_gmres_dev g) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     mspi_set_error(MSP_ERR_LIB, "k_iter_update: %s", hipGetErrorString(e));
+    return MSP_ERR_LIB;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_gm_norm_update(msp_ctx* ctx, mspi_gmres_dev g, const double* partial, int64_t nchunks, int m) {
+  const size_t lds = (size_t)3 * (m + 2) * sizeof(double);
+  k_norm_update<<<1, kUT, lds, mspi_stream(ctx)>>>(g, partial, nchunks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    mspi_set_error(MSP_ERR_LIB, "k_norm_update: %s", hipGetErrorString(e));
     return MSP_ERR_LIB;
   }
   return MSP_SUCCESS;

@@ -119,6 +119,11 @@ typedef struct {
 int mspi_gm_cycle_start(msp_ctx *ctx, mspi_gmres_dev g, const double *sumsq_dev);
 int mspi_gm_iter_update(msp_ctx *ctx, mspi_gmres_dev g);
 int mspi_gm_build(msp_ctx *ctx, mspi_gmres_dev g);
+/* fold the ||w||^2 partials (stage-2 DBR) and run the Hessenberg update, one launch */
+int mspi_gm_norm_update(msp_ctx *ctx, mspi_gmres_dev g, const double *partial, int64_t nchunks, int m);
+/* CGS VecMAXPY + ||w||^2 partials, then mspi_gm_norm_update (h(it+1) = ||w||^2) */
+int mspi_maxpy_norm_update(msp_ctx *ctx, const double *win, double *wout, int nv, const double *base, int64_t stride,
+                           int64_t n, mspi_gmres_dev g, int it, int m, const int *stop);
 /* data-path pieces with a stop flag; basis = VV(j) at base + j*stride */
 int mspi_spmv_scaled(msp_mat *A, const double *x, const double *sdev, double *vout, double *y, const int *stop);
 int mspi_mdot_basis(msp_ctx *ctx, const double *w, int nv, const double *base, int64_t stride, int64_t n,

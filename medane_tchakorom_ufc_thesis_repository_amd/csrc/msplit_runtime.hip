@@ -296,6 +296,31 @@ extern "C" int mspi_maxpy_norm_basis(msp_ctx* c, const double* win, double* wout
   return MSP_SUCCESS;
 }
 
+// CGS VecMAXPY with the fused ||w||^2 partials, then one launch that folds them and
+// runs the Hessenberg update (k_norm_update).  MSK_TUNE_GM_UNFUSED: the separate
+// stage-2 and one-lane update launches (A/B).
+extern "C" int mspi_maxpy_norm_update(msp_ctx* c, const double* win, double* wout, int nv, const double* base,
+                                      int64_t stride, int64_t n, mspi_gmres_dev g, int it, int m, const int* stop) {
+  if (msk_get_tuning() & MSK_TUNE_GM_UNFUSED) {
+    int rc = mspi_maxpy_norm_basis(c, win, wout, nv, base, stride, n, g.h, g.h + it + 1, stop);
+    return rc ? rc : mspi_gm_iter_update(c, g);
+  }
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0 || nv <= 0) {
+    mspi_set_error(MSP_ERR_ARG_SIZ, "maxpy_norm on an empty basis");
+    return MSP_ERR_ARG_SIZ;
+  }
+  {
+    KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n * (nv + 2));
+    Vecs vg = {};
+    vg.base = base;
+    vg.stride = stride;
+    Coefs cf = {};
+    KCHK(msk_maxpy_chunk(win, wout, &vg, nv, nullptr, &cf, g.h, 1, n, 0, c->partial, stop, c->stream));
+  }
+  return mspi_gm_norm_update(c, g, c->partial, nch, m);
+}
+
 extern "C" int mspi_maxpy_accum_basis(msp_ctx* c, double* x, const int* nvdev, const double* base, int64_t stride,
                                       int64_t n, const double* coef_dev, int nv_expected) {
   if (n <= 0) return MSP_SUCCESS;
