@@ -332,6 +332,13 @@ int msp_amsg_send_vec(msp_amsg *am, int32_t dst, const int32_t *ints, int32_t ni
                       int64_t n);
 int msp_amsg_recv_vec(msp_amsg *am, int32_t src, int32_t *ints, int32_t nints, msp_vec *v, int64_t off, int64_t cap,
                       int64_t *n, int32_t *got);
+/* Device slots (the xGMI mailboxes of SURVEY.md section 8e): this rank's
+ * outgoing planes live in its own HBM, exported by HIP IPC; *_vec then move a
+ * plane HBM -> sender's slot and sender's slot -> receiver's HBM (peer copy over
+ * xGMI), with the same sequence words.  Every rank enables before the first
+ * send; close_peers (every rank) must precede destroy (which frees the slots). */
+int msp_amsg_enable_device(msp_amsg *am, msp_ctx *ctx);
+int msp_amsg_close_peers(msp_amsg *am);
 
 /* ------------------------------------------- async minimization broadcast */
 /* Newest-value broadcast of each block's rows of R (AMAM-global), in POSIX
@@ -355,6 +362,11 @@ int msp_abcast_fetch(msp_abcast *bc, int32_t src, double *data, int64_t nrows, i
 /* a dense block in HBM (DMA to / from the registered region) */
 int msp_abcast_publish_dense(msp_abcast *bc, const msp_dense *D, int32_t *published);
 int msp_abcast_fetch_dense(msp_abcast *bc, int32_t src, msp_dense *D, int32_t *got);
+/* device buffers: the published blocks stay in the sender's HBM (HIP IPC), a fetch
+ * is a peer copy over xGMI; enable on every rank before the first publish,
+ * close_peers on every rank before destroy */
+int msp_abcast_enable_device(msp_abcast *bc, msp_ctx *ctx);
+int msp_abcast_close_peers(msp_abcast *bc);
 
 /* ------------------------------------------------- convergence detection */
 /* Algorithm 5.15 of Bahi/Contassot-Vivier/Couturier as the reference implements

@@ -56,6 +56,7 @@ class AMResult:
     trace: list = field(default_factory=list)          # (block, iteration, local norm, state, phase tag)
     timers: dict = field(default_factory=dict)         # host seconds per phase, summed over local blocks
     converged: bool = True                             # False: stopped at max_iterations (stop_at_limit)
+    transport: str = "host"                            # "device" (HBM slots, xGMI) or "host" (shared memory)
 
 
 class AsyncBlock:
@@ -139,6 +140,17 @@ class AsyncBlock:
             T("minimize", blk.local_minimize)
         T("detect", self._detect, norm0, rtol, atol, trace, variant == "amam_global")
 
+    def enable_device(self):
+        """Device slots / buffers in this block's HBM (xGMI peer copies between GPUs)."""
+        self.am.enable_device(self.blk.ctx)
+        if self.bcast is not None:
+            self.bcast.enable_device(self.blk.ctx)
+
+    def close_peers(self):
+        self.am.close_peers()
+        if self.bcast is not None:
+            self.bcast.close_peers()
+
     def close(self):
         self.cvd.destroy()
         self.am.destroy()
@@ -157,14 +169,15 @@ def _channel_name(comm) -> str:
 
 def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: int = 100000,
              strict: bool = False, record: bool = False, monitor=None, variant: str = "am", s: int = 0,
-             stop_at_limit: bool = False) -> AMResult:
+             stop_at_limit: bool = False, transport: str | None = None) -> AMResult:
     """The asynchronous multisplitting loop (asynchronous-multisplitting_prime.c:333-392);
     variant "amam_local" adds the block-local minimization every s inner steps
     (the blocks must have setup_local_minimization(s)), "amam_semi_local" the
     semi-local one (setup_minimization(s)), "amam_global" the global one
     (setup_global_async_minimization(s)).  At max_iterations the run raises, or
     (stop_at_limit, for timing runs) every block stops and the result says
-    converged = False."""
+    converged = False.  transport: "device" (payloads in the senders' HBM, peer copies
+    over xGMI; the default for GpuBlocks) or "host" (staged through shared memory)."""
     if variant not in ("am", "amam_local", "amam_semi_local", "amam_global"):
         raise ValueError(f"unknown asynchronous variant {variant}")
     res = AMResult()
@@ -184,6 +197,14 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
         if blk.layout.b not in asyncs:
             asyncs[blk.layout.b] = AsyncBlock(blk, name, False, strict, cap)
     comm.barrier()
+    if transport is None:
+        transport = "device" if all(getattr(b, "async_transport", "host") == "device" for b in ordered) else "host"
+    if transport not in ("device", "host"):
+        raise ValueError(f"unknown transport {transport}")
+    if transport == "device":                        # every block exports its slots before anyone sends
+        for ab in asyncs.values():
+            ab.enable_device()
+        comm.barrier()
     for blk in blocks:                               # x_j = 0; updateLocalRHS before the loop (:329)
         blk.reset_halo()
         blk.update_rhs()
@@ -215,6 +236,10 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
         for k, v in ab.timers.items():
             res.timers[k] = res.timers.get(k, 0.0) + v
     res.trace = trace or []
+    res.transport = transport
+    comm.barrier()
+    for ab in asyncs.values():                       # unmap the peers' slots before anyone frees its own
+        ab.close_peers()
     comm.barrier()
     for ab in asyncs.values():
         if ab.blk.layout.b != 0:

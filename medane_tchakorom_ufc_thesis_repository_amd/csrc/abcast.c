@@ -16,7 +16,9 @@
  * writer, never both, so a fetch never sees a half-written R and a publish
  * that would overwrite a buffer still being read is skipped -- the reference's
  * "previous send not complete".  Payloads move HBM <-> the registered region
- * by DMA.
+ * by DMA, or, with device buffers enabled (msp_abcast_enable_device), stay in
+ * the sender's HBM (HIP IPC): a publish is one HBM -> HBM copy, a fetch one
+ * peer copy over xGMI; the lock words stay in shared memory.
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -52,6 +54,14 @@ typedef struct {
   uint8_t pad[64 - 24];
 } abc_header;
 
+typedef struct {
+  _Atomic int32_t ready;
+  int32_t pid;
+  uint64_t rawptr; /* valid in the exporting process only */
+  uint8_t handle[MSPI_IPC_HANDLE_BYTES];
+  uint8_t pad[128 - 16 - MSPI_IPC_HANDLE_BYTES];
+} abc_ipc;
+
 struct msp_abcast {
   char name[128];
   int32_t nranks, rank, owner;
@@ -62,6 +72,11 @@ struct msp_abcast {
   uint8_t *bufs;   /* [src][2] buffers of cap doubles */
   uint64_t *seen;  /* [src] version last fetched */
   int registered;
+  abc_ipc *ipc;    /* [rank] exported device buffers */
+  msp_ctx *dctx;   /* device buffers enabled */
+  double *dbufs;   /* this rank's 2 x cap device buffers */
+  double **peer;   /* [src] resolved device buffers */
+  uint8_t *opened; /* [src] came from hipIpcOpenMemHandle */
 };
 
 static int berr(int code, const char *msg) {
@@ -90,7 +105,8 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
   b->cap = cap;
   b->buf_bytes = round_up((size_t)(cap > 0 ? cap : 1) * sizeof(double), 4096);
   const size_t lines_bytes = round_up((size_t)nranks * sizeof(src_line), 4096);
-  b->bytes = 4096 + lines_bytes + (size_t)nranks * 2 * b->buf_bytes;
+  const size_t ipc_bytes = round_up((size_t)nranks * sizeof(abc_ipc), 4096);
+  b->bytes = 4096 + lines_bytes + (size_t)nranks * 2 * b->buf_bytes + ipc_bytes;
   int fd;
   if (b->owner) {
     shm_unlink(name);
@@ -122,6 +138,7 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
   abc_header *h = (abc_header *)b->base;
   b->lines = (src_line *)(b->base + 4096);
   b->bufs = b->base + 4096 + lines_bytes;
+  b->ipc = (abc_ipc *)(b->bufs + (size_t)nranks * 2 * b->buf_bytes);
   if (b->owner) {
     h->nranks = nranks;
     h->cap = cap;
@@ -143,9 +160,67 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
   return MSP_SUCCESS;
 }
 
+int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx) {
+  if (!b || !ctx) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  if (b->dctx) return MSP_SUCCESS;
+  b->peer = (double **)calloc((size_t)b->nranks, sizeof(double *));
+  b->opened = (uint8_t *)calloc((size_t)b->nranks, 1);
+  if (!b->peer || !b->opened) return berr(MSP_ERR_MEM, "allocation failed");
+  void *p = NULL;
+  int rc = mspi_dev_alloc(ctx, (size_t)2 * (size_t)(b->cap > 0 ? b->cap : 1) * sizeof(double), &p);
+  if (rc) return rc;
+  abc_ipc *e = &b->ipc[b->rank];
+  if ((rc = mspi_ipc_export(p, e->handle))) {
+    mspi_dev_free(p);
+    return rc;
+  }
+  b->dbufs = (double *)p;
+  b->dctx = ctx;
+  e->pid = (int32_t)getpid();
+  e->rawptr = (uint64_t)(uintptr_t)p;
+  atomic_store_explicit(&e->ready, 1, memory_order_release);
+  return MSP_SUCCESS;
+}
+
+int msp_abcast_close_peers(msp_abcast *b) {
+  if (!b) return berr(MSP_ERR_ARG_NULL, "abcast is NULL");
+  if (!b->peer) return MSP_SUCCESS;
+  for (int r = 0; r < b->nranks; ++r) {
+    if (b->opened[r]) mspi_ipc_close(b->peer[r]);
+    b->peer[r] = NULL;
+    b->opened[r] = 0;
+  }
+  return MSP_SUCCESS;
+}
+
+static int peer_bufs(msp_abcast *b, int src, double **out) {
+  *out = b->peer[src];
+  if (*out) return MSP_SUCCESS;
+  abc_ipc *e = &b->ipc[src];
+  if (!atomic_load_explicit(&e->ready, memory_order_acquire)) return MSP_SUCCESS;
+  if (e->pid == (int32_t)getpid()) {
+    b->peer[src] = (double *)(uintptr_t)e->rawptr;
+  } else {
+    void *p = NULL;
+    int rc = mspi_ipc_open(b->dctx, e->handle, &p);
+    if (rc) return rc;
+    b->peer[src] = (double *)p;
+    b->opened[src] = 1;
+  }
+  *out = b->peer[src];
+  return MSP_SUCCESS;
+}
+
 int msp_abcast_destroy(msp_abcast **pb) {
   if (!pb || !*pb) return MSP_SUCCESS;
   msp_abcast *b = *pb;
+  msp_abcast_close_peers(b);
+  if (b->dbufs) {
+    atomic_store_explicit(&b->ipc[b->rank].ready, 0, memory_order_release);
+    mspi_dev_free(b->dbufs);
+  }
+  free(b->peer);
+  free(b->opened);
   if (b->registered) mspi_host_unregister(b->base);
   munmap(b->base, b->bytes);
   if (b->owner) shm_unlink(b->name);
@@ -195,10 +270,11 @@ static int copy_in(const abc_view *v, const double *srcp) {
 
 static int publish(msp_abcast *b, const abc_view *v, int32_t *published) {
   *published = 0;
+  if (b->dctx && !v->ctx) return berr(MSP_ERR_ARG_WRONG, "device buffers enabled: publish a dense block in HBM");
   if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
     return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
   if (v->nrows * (int64_t)v->ncols > b->cap) return berr(MSP_ERR_ARG_SIZ, "payload larger than the broadcast slot");
-  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
+  int rc = (v->ctx && !b->dctx) ? ensure_registered(b) : MSP_SUCCESS;
   if (rc) return rc;
   src_line *L = &b->lines[b->rank];
   const int32_t newest = atomic_load_explicit(&L->newest, memory_order_acquire);
@@ -207,7 +283,14 @@ static int publish(msp_abcast *b, const abc_view *v, int32_t *published) {
   if (!atomic_compare_exchange_strong_explicit(&L->lock[w], &expect, ABC_WRITER, memory_order_acq_rel,
                                                memory_order_relaxed))
     return MSP_SUCCESS; /* a reader still holds it: the previous send has not completed */
-  if ((rc = copy_out(v, buf_at(b, b->rank, w)))) {
+  if (b->dctx) {
+    const size_t rowb = (size_t)v->nrows * sizeof(double);
+    rc = mspi_d2d_sync(b->dctx, b->dbufs + (size_t)w * (size_t)b->cap, rowb, v->p, (size_t)v->ld * sizeof(double),
+                       rowb, (size_t)v->ncols);
+  } else {
+    rc = copy_out(v, buf_at(b, b->rank, w));
+  }
+  if (rc) {
     atomic_store_explicit(&L->lock[w], 0u, memory_order_release);
     return rc;
   }
@@ -222,11 +305,17 @@ static int publish(msp_abcast *b, const abc_view *v, int32_t *published) {
 
 static int fetch(msp_abcast *b, int32_t src, const abc_view *v, int32_t *got) {
   *got = 0;
+  if (b->dctx && !v->ctx) return berr(MSP_ERR_ARG_WRONG, "device buffers enabled: fetch into a dense block in HBM");
   if (src < 0 || src >= b->nranks || src == b->rank) return berr(MSP_ERR_ARG_OUTOFRANGE, "source rank out of range");
   if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
     return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
-  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
+  int rc = (v->ctx && !b->dctx) ? ensure_registered(b) : MSP_SUCCESS;
   if (rc) return rc;
+  double *pbuf = NULL;
+  if (b->dctx) {
+    if ((rc = peer_bufs(b, src, &pbuf))) return rc;
+    if (!pbuf) return MSP_SUCCESS; /* src has not enabled its buffers: nothing sent yet */
+  }
   src_line *L = &b->lines[src];
   for (int attempt = 0; attempt < 64; ++attempt) {
     const int32_t k = atomic_load_explicit(&L->newest, memory_order_acquire);
@@ -244,7 +333,13 @@ static int fetch(msp_abcast *b, int32_t src, const abc_view *v, int32_t *got) {
       atomic_fetch_sub_explicit(&L->lock[k], 1u, memory_order_release);
       return berr(MSP_ERR_ARG_SIZ, "received block has a different shape");
     }
-    rc = copy_in(v, buf_at(b, src, k));
+    if (pbuf) {
+      const size_t rowb = (size_t)v->nrows * sizeof(double);
+      rc = mspi_d2d_sync(b->dctx, v->p, (size_t)v->ld * sizeof(double), pbuf + (size_t)k * (size_t)b->cap, rowb, rowb,
+                         (size_t)v->ncols);
+    } else {
+      rc = copy_in(v, buf_at(b, src, k));
+    }
     atomic_fetch_sub_explicit(&L->lock[k], 1u, memory_order_release);
     if (rc) return rc;
     b->seen[src] = ver;

@@ -20,7 +20,10 @@
  * Iterate payloads are boundary planes: only chain neighbours (|src - dst| = 1,
  * the z-slab blocks) get a data slot of data_cap doubles.  *_vec variants move
  * the plane between HBM and the slot (the region is registered with the HIP
- * runtime, so the copies are DMA transfers).
+ * runtime, so the copies are DMA transfers).  With device slots enabled
+ * (msp_amsg_enable_device) the sequence word stays here but the payload lives
+ * in the sender's HBM, exported by HIP IPC: a send is one HBM -> HBM copy into
+ * the sender's slot, a receive one copy out of it over xGMI (msplit_ipc.hip).
  *
  * Host code only: no GPU is needed for the control messages (the CPU tests use
  * them across processes).
@@ -57,6 +60,15 @@ typedef struct {
   uint8_t pad[64 - 28];
 } region_header;
 
+/* one per rank, after the data slots: the rank's exported device slots */
+typedef struct {
+  _Atomic int32_t ready;
+  int32_t pid;
+  uint64_t rawptr; /* valid in the exporting process only */
+  uint8_t handle[MSPI_IPC_HANDLE_BYTES];
+  uint8_t pad[128 - 16 - MSPI_IPC_HANDLE_BYTES];
+} ipc_entry;
+
 struct msp_amsg {
   char name[128];
   int32_t nranks, rank, owner;
@@ -69,6 +81,11 @@ struct msp_amsg {
   size_t data_bytes; /* header line + data_cap doubles, rounded to 4 KiB */
   uint64_t *seen;    /* [src][kind] last sequence number taken by this rank */
   int registered;
+  ipc_entry *ipc;    /* [rank] */
+  msp_ctx *dctx;     /* device slots enabled: the context their copies run on */
+  double *dslots;    /* this rank's 2 x data_cap device slots (dir 0: to rank-1, 1: to rank+1) */
+  double **peer;     /* [src] resolved device slots of src (NULL: not yet) */
+  uint8_t *opened;   /* [src] peer[src] came from hipIpcOpenMemHandle */
 };
 
 static int aerr(int code, const char *msg) {
@@ -107,7 +124,8 @@ int msp_amsg_create(const char *name, int32_t nranks, int32_t rank, int64_t data
   m->data_cap = data_cap;
   m->data_bytes = round_up(sizeof(ctrl_slot) + (size_t)data_cap * sizeof(double), 4096);
   const size_t ctrl_bytes = round_up((size_t)nranks * nranks * MSP_AMSG_NKINDS * sizeof(ctrl_slot), 4096);
-  m->bytes = 4096 + ctrl_bytes + (size_t)nranks * 2 * m->data_bytes;
+  const size_t ipc_bytes = round_up((size_t)nranks * sizeof(ipc_entry), 4096);
+  m->bytes = 4096 + ctrl_bytes + (size_t)nranks * 2 * m->data_bytes + ipc_bytes;
   int fd;
   if (m->owner) {
     shm_unlink(name); /* a stale region of an earlier run */
@@ -139,6 +157,7 @@ int msp_amsg_create(const char *name, int32_t nranks, int32_t rank, int64_t data
   m->hdr = (region_header *)m->base;
   m->ctrl = (ctrl_slot *)(m->base + 4096);
   m->data = m->base + 4096 + ctrl_bytes;
+  m->ipc = (ipc_entry *)(m->data + (size_t)nranks * 2 * m->data_bytes);
   if (m->owner) {
     m->hdr->nranks = nranks;
     m->hdr->data_cap = data_cap;
@@ -167,9 +186,68 @@ int msp_amsg_attached(const msp_amsg *m, int32_t *n) {
   return MSP_SUCCESS;
 }
 
+int msp_amsg_enable_device(msp_amsg *m, msp_ctx *ctx) {
+  if (!m || !ctx) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
+  if (m->dctx) return MSP_SUCCESS;
+  m->peer = (double **)calloc((size_t)m->nranks, sizeof(double *));
+  m->opened = (uint8_t *)calloc((size_t)m->nranks, 1);
+  if (!m->peer || !m->opened) return aerr(MSP_ERR_MEM, "allocation failed");
+  void *p = NULL;
+  int rc = mspi_dev_alloc(ctx, (size_t)2 * (size_t)(m->data_cap > 0 ? m->data_cap : 1) * sizeof(double), &p);
+  if (rc) return rc;
+  ipc_entry *e = &m->ipc[m->rank];
+  if ((rc = mspi_ipc_export(p, e->handle))) {
+    mspi_dev_free(p);
+    return rc;
+  }
+  m->dslots = (double *)p;
+  m->dctx = ctx;
+  e->pid = (int32_t)getpid();
+  e->rawptr = (uint64_t)(uintptr_t)p;
+  atomic_store_explicit(&e->ready, 1, memory_order_release);
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_close_peers(msp_amsg *m) {
+  if (!m) return aerr(MSP_ERR_ARG_NULL, "amsg is NULL");
+  if (!m->peer) return MSP_SUCCESS;
+  for (int r = 0; r < m->nranks; ++r) {
+    if (m->opened[r]) mspi_ipc_close(m->peer[r]);
+    m->peer[r] = NULL;
+    m->opened[r] = 0;
+  }
+  return MSP_SUCCESS;
+}
+
+/* the device slots of src, opened on first use; NULL while src has not enabled them */
+static int peer_slots(msp_amsg *m, int src, double **out) {
+  *out = m->peer[src];
+  if (*out) return MSP_SUCCESS;
+  ipc_entry *e = &m->ipc[src];
+  if (!atomic_load_explicit(&e->ready, memory_order_acquire)) return MSP_SUCCESS;
+  if (e->pid == (int32_t)getpid()) {
+    m->peer[src] = (double *)(uintptr_t)e->rawptr; /* same process: the allocation itself */
+  } else {
+    void *p = NULL;
+    int rc = mspi_ipc_open(m->dctx, e->handle, &p);
+    if (rc) return rc;
+    m->peer[src] = (double *)p;
+    m->opened[src] = 1;
+  }
+  *out = m->peer[src];
+  return MSP_SUCCESS;
+}
+
 int msp_amsg_destroy(msp_amsg **pm) {
   if (!pm || !*pm) return MSP_SUCCESS;
   msp_amsg *m = *pm;
+  msp_amsg_close_peers(m);
+  if (m->dslots) {
+    atomic_store_explicit(&m->ipc[m->rank].ready, 0, memory_order_release);
+    mspi_dev_free(m->dslots);
+  }
+  free(m->peer);
+  free(m->opened);
   if (m->registered) mspi_host_unregister(m->base);
   munmap(m->base, m->bytes);
   if (m->owner) shm_unlink(m->name);
@@ -178,6 +256,9 @@ int msp_amsg_destroy(msp_amsg **pm) {
   *pm = NULL;
   return MSP_SUCCESS;
 }
+
+/* the slot direction of this rank's messages to dst (0: dst = rank - 1, 1: dst = rank + 1) */
+static int dst_rank_dir(const msp_amsg *m, int dst) { return dst == m->rank - 1 ? 0 : 1; }
 
 static ctrl_slot *slot_for(msp_amsg *m, int src, int dst, int kind) {
   if (kind == MSP_AMSG_DATA) return data_at(m, src, dst);
@@ -210,6 +291,7 @@ int msp_amsg_send(msp_amsg *m, int32_t dst, int32_t kind, const int32_t *ints, i
   if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
   ctrl_slot *s = slot_for(m, m->rank, dst, kind);
   if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
+  if (kind == MSP_AMSG_DATA && m->dctx) return aerr(MSP_ERR_ARG_WRONG, "device slots enabled: send planes with *_vec");
   if (kind == MSP_AMSG_DATA ? (n < 0 || n > m->data_cap || (n && !data)) : n != 0)
     return aerr(MSP_ERR_ARG_SIZ, "payload larger than the data slot");
   write_begin(s);
@@ -228,6 +310,14 @@ static int read_slot(msp_amsg *m, int src, int kind, int32_t *ints, int32_t nint
   if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
   uint64_t *seen = m->seen + (size_t)src * MSP_AMSG_NKINDS + kind;
   *got = 0;
+  const double *dsrc = NULL; /* device slots: the payload in src's HBM */
+  if (v && m->dctx) {
+    double *ps = NULL;
+    int rc = peer_slots(m, src, &ps);
+    if (rc) return rc;
+    if (!ps) return MSP_SUCCESS; /* src has not enabled its slots: nothing sent yet */
+    dsrc = ps + (size_t)(m->rank == src - 1 ? 0 : 1) * (size_t)m->data_cap;
+  }
   for (int attempt = 0; attempt < 8; ++attempt) {
     const uint64_t s1 = atomic_load_explicit(&s->seq, memory_order_acquire);
     if ((s1 & 1) || s1 == *seen) return MSP_SUCCESS; /* being written, or nothing new: try next round */
@@ -237,7 +327,11 @@ static int read_slot(msp_amsg *m, int src, int kind, int32_t *ints, int32_t nint
     if (len < 0 || len > m->data_cap) continue;
     if (len) {
       if (len > cap) return aerr(MSP_ERR_ARG_SIZ, "receive buffer smaller than the message");
-      if (v) {
+      if (dsrc) {
+        const size_t bytes = (size_t)len * sizeof(double);
+        int rc = mspi_d2d_sync(m->dctx, v->d + voff, bytes, dsrc, bytes, bytes, 1);
+        if (rc) return rc;
+      } else if (v) {
         int rc = mspi_h2d_sync(v->ctx, v->d + voff, (const double *)(s + 1), (size_t)len * sizeof(double));
         if (rc) return rc;
       } else {
@@ -262,6 +356,7 @@ int msp_amsg_recv(msp_amsg *m, int32_t src, int32_t kind, int32_t *ints, int32_t
   int rc = check_pair(m, src, kind);
   if (rc) return rc;
   if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
+  if (kind == MSP_AMSG_DATA && m->dctx) return aerr(MSP_ERR_ARG_WRONG, "device slots enabled: receive planes with *_vec");
   return read_slot(m, src, kind, ints, nints, data, cap, n, got, NULL, 0);
 }
 
@@ -282,11 +377,22 @@ int msp_amsg_send_vec(msp_amsg *m, int32_t dst, const int32_t *ints, int32_t nin
   if (off < 0 || n < 0 || off + n > v->n || n > m->data_cap) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
   ctrl_slot *s = data_at(m, m->rank, dst);
   if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
-  if ((rc = ensure_registered(m))) return rc;
+  if (!m->dctx && (rc = ensure_registered(m))) return rc;
   write_begin(s);
   memset(s->ints, 0, sizeof(s->ints));
   if (nints) memcpy(s->ints, ints, (size_t)nints * sizeof(int32_t));
   s->n = n;
+  if (m->dctx) {
+    double *slot = m->dslots + (size_t)dst_rank_dir(m, dst) * (size_t)m->data_cap;
+    const size_t bytes = (size_t)n * sizeof(double);
+    if (n && (rc = mspi_d2d_sync(m->dctx, slot, bytes, v->d + off, bytes, bytes, 1))) {
+      s->n = 0;
+      write_end(s);
+      return rc;
+    }
+    write_end(s);
+    return MSP_SUCCESS;
+  }
   if (n && (rc = mspi_d2h_sync(v->ctx, (double *)(s + 1), v->d + off, (size_t)n * sizeof(double)))) {
     s->n = 0; /* publish an empty message rather than a partial plane */
     write_end(s);
@@ -303,6 +409,6 @@ int msp_amsg_recv_vec(msp_amsg *m, int32_t src, int32_t *ints, int32_t nints, ms
   if (rc) return rc;
   if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
   if (off < 0 || cap < 0 || off + cap > v->n) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
-  if ((rc = ensure_registered(m))) return rc;
+  if (!m->dctx && (rc = ensure_registered(m))) return rc;
   return read_slot(m, src, MSP_AMSG_DATA, ints, nints, NULL, cap, n, got, v, off);
 }

@@ -134,6 +134,16 @@ int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const doub
                            const double *coef_dev, int nv_expected);
 int mspi_h2d_async(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
+/* ---- HBM mailboxes shared between processes (msplit_ipc.hip) ---- */
+#define MSPI_IPC_HANDLE_BYTES 64
+int mspi_dev_alloc(msp_ctx *ctx, size_t bytes, void **p); /* zeroed */
+int mspi_dev_free(void *p);
+int mspi_ipc_export(void *p, uint8_t *handle);
+int mspi_ipc_open(msp_ctx *ctx, const uint8_t *handle, void **p);
+int mspi_ipc_close(void *p);
+/* height rows of width bytes, pitched, device to device; synchronises the context's stream */
+int mspi_d2d_sync(msp_ctx *ctx, void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
+                  size_t height);
 /* page-lock a host range (shared-memory mailboxes) for DMA */
 int mspi_host_register(void *p, size_t bytes);
 int mspi_host_unregister(void *p);

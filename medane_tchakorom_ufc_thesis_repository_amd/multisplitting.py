@@ -30,6 +30,8 @@ class GpuBlock:
     coupling rows A_ij, b_i, x_i, the local right-hand side, the halo and the
     inner KSP (prefix inner{b+1}_, synchronous-multisplitting.c:129-143)."""
 
+    async_transport = "device"   # asynchronous.py: planes and R rows through HBM slots (xGMI peer copies)
+
     def __init__(self, ctx: Context, layout: BlockLayout, opts: Options | None, comm, prefix: str | None = None):
         self.ctx = ctx
         self.layout = layout

@@ -729,6 +729,14 @@ class AsyncMessages:
         iv = np.ascontiguousarray(ints, np.int32)
         call("msp_amsg_send_vec", self.h, int(dst), _ip(iv), iv.size, v.h, int(off), int(n))
 
+    def enable_device(self, ctx: Context):
+        """Device slots: planes stay in the sender's HBM (HIP IPC), received by peer copy over xGMI."""
+        call("msp_amsg_enable_device", self.h, ctx.h)
+        self._ctx = ctx
+
+    def close_peers(self):
+        call("msp_amsg_close_peers", self.h)
+
     def recv_vec(self, src: int, nints: int, v: Vec, off: int, cap: int):
         iv = np.zeros(max(nints, 1), np.int32)
         n = C.c_int64()
@@ -777,6 +785,14 @@ class AsyncBroadcast:
         call("msp_abcast_fetch", self.h, int(src), _dp(out), int(nrows), int(ncols), int(max(nrows, 1)),
              C.byref(got))
         return bool(got.value)
+
+    def enable_device(self, ctx: Context):
+        """Device buffers: published blocks stay in the sender's HBM (HIP IPC)."""
+        call("msp_abcast_enable_device", self.h, ctx.h)
+        self._ctx = ctx
+
+    def close_peers(self):
+        call("msp_abcast_close_peers", self.h)
 
     def publish_dense(self, D: "DenseMat") -> bool:
         ok = C.c_int32()

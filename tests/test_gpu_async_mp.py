@@ -1,0 +1,153 @@
+"""The asynchronous transports across processes on the GPU: device slots and
+buffers in the sender's HBM, opened by the receivers through HIP IPC (the
+xGMI mailboxes; on the one-GPU box both processes share cuda:0, so the peer
+copies are same-device copies through the IPC mapping).  Two processes per
+test, spawned fresh (no fork of a GPU-initialised parent)."""
+import multiprocessing as mp
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from test_distributed_gloo import _free_port
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _transport_worker(rank, name, n_msgs, n, q):
+    sys.path.insert(0, ROOT)
+    import time
+    import torch  # noqa: F401
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncBroadcast, AsyncMessages, Context, DenseMat, Vec
+    ctx = Context(0)
+    if rank == 1:
+        t0 = time.time()
+        while True:                                   # the owner (rank 0) creates the regions first
+            try:
+                am = AsyncMessages(name, 2, 1, n, owner=False)
+                bc = AsyncBroadcast(name + "_R", 2, 1, n * 3, owner=False)
+                break
+            except Exception:
+                if time.time() - t0 > 60:
+                    raise
+                time.sleep(0.05)
+    else:
+        am = AsyncMessages(name, 2, 0, n, owner=True)
+        bc = AsyncBroadcast(name + "_R", 2, 0, n * 3, owner=True)
+    am.enable_device(ctx)
+    bc.enable_device(ctx)
+    while am.attached() < 2:
+        time.sleep(0.01)
+    ok = True
+    if rank == 1:                                     # the writer: planes and dense blocks stamped k
+        v = Vec(ctx, n)
+        D = DenseMat(ctx, n, 3)
+        for k in range(1, n_msgs + 1):
+            v.set(float(k))
+            am.send_vec(0, [k, k], v, 0, n)
+            if k % 10 == 0 or k == n_msgs:
+                for j in range(3):
+                    D.set_column(j, 0, v)
+                while not bc.publish_dense(D):
+                    pass
+        am.send(0, AsyncMessages.VERDICT, [n_msgs, 1])
+        got_done = False
+        while not got_done:                           # wait for the reader before unmapping anything
+            got_done = am.recv(0, AsyncMessages.VERDICT, 1)[0]
+            time.sleep(0.01)
+        am.close_peers()
+        bc.close_peers()
+        am.destroy()
+        bc.destroy()
+        q.put((rank, ok, 0, 0))
+        return
+    y = Vec(ctx, n)
+    R = DenseMat(ctx, n, 3)
+    last, taken, last_r, done = 0, 0, 0, False
+    while not done or last < n_msgs or last_r < n_msgs:
+        got, ints, _ = am.recv_vec(1, 2, y, 0, n)
+        if got:
+            a = y.get_array()
+            ok = ok and ints[0] == ints[1] > last and bool(np.all(a == float(ints[0])))
+            last, taken = ints[0], taken + 1
+        if bc.fetch_dense(1, R):
+            a = R.get_values()
+            ok = ok and bool(np.all(a == a[0, 0])) and a[0, 0] > last_r
+            last_r = a[0, 0]
+        done = done or am.recv(1, AsyncMessages.VERDICT, 2)[0]
+    am.close_peers()                                  # unmap the writer's slots, then let it free them
+    bc.close_peers()
+    am.send(1, AsyncMessages.VERDICT, [1])
+    time.sleep(0.5)
+    am.destroy()
+    bc.destroy()
+    q.put((rank, ok, taken, last))
+
+
+def test_device_slots_cross_process_whole_and_newest():
+    """Every plane and block a receiver takes from the sender's HBM is whole and
+    newer than the last, and the last one always arrives."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/msplit_ipc_{os.getpid()}"
+    n, n_msgs = 1 << 16, 400
+    procs = [ctx.Process(target=_transport_worker, args=(r, name, n_msgs, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0][1] and out[1][1]
+    assert out[0][3] == n_msgs and out[0][2] >= 1
+
+
+def _am_worker(rank, world, port, problem, q):
+    sys.path.insert(0, ROOT)
+    import torch  # noqa: F401
+    import torch.distributed as dist
+    from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import make_blocks
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Options
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        variant, dim, nx, ny, nz, s, max_it, rtol = problem
+        b = rank
+        opts = Options(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 -inner{b + 1}_pc_type none "
+                       f"-outer{b + 1}_ksp_type lsqr -outer{b + 1}_ksp_convergence_test default "
+                       f"-outer{b + 1}_ksp_lsqr_exact_mat_norm -outer{b + 1}_ksp_atol 1e-100 "
+                       f"-outer{b + 1}_ksp_max_it 70 -outer{b + 1}_ksp_rtol 1e-15")
+        ctx = Context(0)
+        comm = TorchComm()
+        (blk,) = make_blocks(ctx, dim, nx, ny, nz, world, [rank], opts, comm)
+        if variant == "amam_global":
+            blk.setup_global_async_minimization(s)
+        res = am_solve([blk], comm, rtol=rtol, max_iterations=20000, variant=variant, s=s)
+        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.transport))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("problem", [("am", 3, 8, 8, 16, 0, 5, 1e-6), ("amam_global", 3, 8, 8, 16, 4, 5, 1e-6)])
+def test_am_two_processes_device_transport(problem):
+    """One process per block, truly asynchronous, planes (and for AMAM-global the
+    R rows) through HBM slots opened by IPC: the detection ends every block in
+    the same phase with one global final residual below the threshold."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_am_worker, args=(r, 2, port, problem, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=600) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(o[5] == "device" for o in out)
+    assert out[0][3] == out[1][3] and out[0][4] == out[1][4]
+    assert out[0][4] <= 1e-4 * out[0][3]
+    assert out[0][2] == out[1][2]

@@ -1,8 +1,10 @@
 """Measurement of the asynchronous rows on one GPU.
 
-1. Transport: the newest-value slots (msp_amsg, a boundary plane HBM -> shared
-   memory -> HBM) and the R-row broadcast (msp_abcast, a dense block), GB/s of
-   payload per send + receive pair, both ends in this process.
+1. Transport: the newest-value slots (msp_amsg, a boundary plane) and the
+   R-row broadcast (msp_abcast, a dense block), GB/s of payload per send +
+   receive pair, both ends in this process: host-staged (HBM -> shared memory
+   -> HBM) and through HBM slots (on one GPU a same-device copy; between GPUs
+   the receive is a peer copy over xGMI).
 2. AM / AMAM-global on nb z-slab blocks of one GPU, round-robin (LocalComm):
    DOF-updates/s of the inner GMRES and the share of host time in each phase
    (solve, exchange, minimize, detect).
@@ -25,43 +27,57 @@ sys.path.insert(0, ROOT)
 
 
 def transport(ctx, n_plane: int, rows: int, s: int, reps: int):
+    """Payload GB/s of one send + receive, host-staged and through HBM slots."""
     from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncBroadcast, AsyncMessages, DenseMat, Vec
     import numpy as np
     out = {}
-    name = f"/msplit_tb_{os.getpid()}_{uuid.uuid4().hex[:8]}"
-    a = AsyncMessages(name, 2, 0, n_plane, owner=True)
-    b = AsyncMessages(name, 2, 1, n_plane, owner=False)
     x = Vec.from_array(ctx, np.arange(n_plane, dtype=np.float64))
     y = Vec(ctx, n_plane)
-    a.send_vec(1, [0, 0], x, 0, n_plane)
-    b.recv_vec(0, 2, y, 0, n_plane)                       # registers the region (first use)
-    t0 = time.perf_counter()
-    for k in range(reps):
-        a.send_vec(1, [0, k + 1], x, 0, n_plane)
-        got, _, _ = b.recv_vec(0, 2, y, 0, n_plane)
-        assert got
-    dt = (time.perf_counter() - t0) / reps
-    out["amsg_plane"] = {"doubles": n_plane, "us_per_send_recv": dt * 1e6, "GBps": 8 * n_plane / dt / 1e9}
-    b.destroy()
-    a.destroy()
-    name = f"/msplit_tb_{os.getpid()}_{uuid.uuid4().hex[:8]}"
-    p = AsyncBroadcast(name, 2, 0, rows * s, owner=True)
-    q = AsyncBroadcast(name, 2, 1, rows * s, owner=False)
     R = DenseMat(ctx, rows, s)
     for j in range(s):
         R.set_column(j, 0, Vec.from_array(ctx, np.full(rows, float(j))))
     R2 = DenseMat(ctx, rows, s)
-    p.publish_dense(R)
-    q.fetch_dense(0, R2)
-    t0 = time.perf_counter()
-    nrep = max(2, reps // 10)
-    for _ in range(nrep):
-        assert p.publish_dense(R)
-        assert q.fetch_dense(0, R2)
-    dt = (time.perf_counter() - t0) / nrep
-    out["abcast_R"] = {"rows": rows, "cols": s, "ms_per_publish_fetch": dt * 1e3, "GBps": 8 * rows * s / dt / 1e9}
-    q.destroy()
-    p.destroy()
+    for mode in ("host", "device"):
+        name = f"/msplit_tb_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+        a = AsyncMessages(name, 2, 0, n_plane, owner=True)
+        b = AsyncMessages(name, 2, 1, n_plane, owner=False)
+        if mode == "device":
+            a.enable_device(ctx)
+            b.enable_device(ctx)
+        a.send_vec(1, [0, 0], x, 0, n_plane)
+        b.recv_vec(0, 2, y, 0, n_plane)                   # first use: registration / IPC resolution
+        t0 = time.perf_counter()
+        for k in range(reps):
+            a.send_vec(1, [0, k + 1], x, 0, n_plane)
+            got, _, _ = b.recv_vec(0, 2, y, 0, n_plane)
+            assert got
+        dt = (time.perf_counter() - t0) / reps
+        out[f"amsg_plane_{mode}"] = {"doubles": n_plane, "us_per_send_recv": dt * 1e6,
+                                     "GBps": 8 * n_plane / dt / 1e9}
+        b.close_peers()
+        a.close_peers()
+        b.destroy()
+        a.destroy()
+        name = f"/msplit_tb_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+        p = AsyncBroadcast(name, 2, 0, rows * s, owner=True)
+        q = AsyncBroadcast(name, 2, 1, rows * s, owner=False)
+        if mode == "device":
+            p.enable_device(ctx)
+            q.enable_device(ctx)
+        p.publish_dense(R)
+        q.fetch_dense(0, R2)
+        nrep = max(2, reps // 10)
+        t0 = time.perf_counter()
+        for _ in range(nrep):
+            assert p.publish_dense(R)
+            assert q.fetch_dense(0, R2)
+        dt = (time.perf_counter() - t0) / nrep
+        out[f"abcast_R_{mode}"] = {"rows": rows, "cols": s, "ms_per_publish_fetch": dt * 1e3,
+                                   "GBps": 8 * rows * s / dt / 1e9}
+        q.close_peers()
+        p.close_peers()
+        q.destroy()
+        p.destroy()
     return out
 
 
@@ -76,6 +92,7 @@ def main():
     ap.add_argument("--s", type=int, default=4)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rtol", type=float, default=1e-6)
+    ap.add_argument("--transport", default="device", choices=["device", "host"])
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
     from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
@@ -100,11 +117,11 @@ def main():
             blk.setup_global_async_minimization(args.s)
     ctx.synchronize()
     res = am_solve(blocks, comm, rtol=args.rtol, max_iterations=args.max_iterations, variant=args.variant,
-                   s=args.s, stop_at_limit=True)
+                   s=args.s, stop_at_limit=True, transport=args.transport)
     inner_total = sum(res.inner_its)
     tot = sum(res.timers.values())
-    out["solve"] = {"variant": args.variant, "mesh": [n, n, args.planes * nb], "blocks": nb,
-                    "rows_per_block": rows, "iterations": res.iterations, "inner_its": res.inner_its,
+    out["solve"] = {"variant": args.variant, "transport": res.transport, "mesh": [n, n, args.planes * nb],
+                    "blocks": nb, "rows_per_block": rows, "iterations": res.iterations, "inner_its": res.inner_its,
                     "converged": res.converged, "final_norm_rel": res.final_norm / res.norm0,
                     "elapsed_s": res.elapsed, "DOF_updates_per_s": rows * inner_total / res.elapsed,
                     "phase_share": {k: v / tot for k, v in res.timers.items()} if tot else {},
