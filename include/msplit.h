@@ -257,6 +257,16 @@ int msp_comm_destroy(msp_comm **comm);
 int msp_comm_get_size(const msp_comm *comm, int32_t *nranks, int32_t *rank);
 /* recv[r*count + i] = rank r's send[i]; recv has nranks*count entries. */
 int msp_comm_allgather(msp_comm *comm, const msp_vec *send, msp_vec *recv, int64_t count);
+/* Boundary exchange between chain neighbours (comm_sync_send_and_receive,
+ * comm.c:126-141; only the planes the neighbours' coupling rows read):
+ * src[lo_src:+count] -> rank-1, src[hi_src:+count] -> rank+1; from rank-1 into
+ * dst[lo_dst:+count], from rank+1 into dst[hi_dst:+count].  RCCL send/recv in
+ * one group on the context's stream; host transport through the all-gather. */
+int msp_comm_exchange_neighbors(msp_comm *comm, const msp_vec *src, int64_t lo_src, int64_t hi_src, msp_vec *dst,
+                                int64_t lo_dst, int64_t hi_dst, int64_t count);
+/* out[i] = sum over ranks of in[i] in rank order (host arrays): the outer residual
+ * Allreduce of synchronous-multisplitting.c:192, bitwise the same on every rank. */
+int msp_comm_sum_ordered(msp_comm *comm, const double *in, double *out, int32_t n);
 
 /* ------------------------------------------------------------------- LSQR */
 /* KSPLSQR options (the outer solver of the minimization variants,

@@ -26,6 +26,10 @@ struct RcclApi {
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
   const char* (*get_error_string)(ncclResult_t) = nullptr;
 };
 
@@ -42,7 +46,12 @@ RcclApi& rccl() {
   api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
   api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
   api.get_error_string = (decltype(api.get_error_string))dlsym(h, "ncclGetErrorString");
-  api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_gather && api.get_error_string;
+  api.send = (decltype(api.send))dlsym(h, "ncclSend");
+  api.recv = (decltype(api.recv))dlsym(h, "ncclRecv");
+  api.group_start = (decltype(api.group_start))dlsym(h, "ncclGroupStart");
+  api.group_end = (decltype(api.group_end))dlsym(h, "ncclGroupEnd");
+  api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_gather && api.get_error_string &&
+           api.send && api.recv && api.group_start && api.group_end;
   return api;
 }
 
@@ -176,4 +185,94 @@ extern "C" int msp_comm_allgather(msp_comm* m, const msp_vec* send, msp_vec* rec
          "allgather of %lld per rank: send %lld, recv %lld", (long long)count, (long long)send->n,
          (long long)recv->n);
   return mspi_comm_allgather(m, send->d, recv->d, count);
+}
+
+// Boundary exchange between chain neighbours (comm_sync_send_and_receive,
+// comm.c:126-141, for the z-slab blocks): src[lo_src : +count] goes to rank-1
+// and src[hi_src : +count] to rank+1; rank-1's plane lands in dst[lo_dst : +count]
+// and rank+1's in dst[hi_dst : +count].  RCCL: one ncclGroupStart/End of the
+// sends and receives on the context's stream (xGMI).  Host transport: an
+// all-gather of every rank's two planes, each rank keeping its neighbours'.
+extern "C" int msp_comm_exchange_neighbors(msp_comm* m, const msp_vec* src, int64_t lo_src, int64_t hi_src,
+                                           msp_vec* dst, int64_t lo_dst, int64_t hi_dst, int64_t count) {
+  ARGCHK(m && src && dst, MSP_ERR_ARG_NULL, "NULL argument");
+  const bool lo = m->rank > 0, hi = m->rank < m->nranks - 1;
+  ARGCHK(count >= 0, MSP_ERR_ARG_OUTOFRANGE, "negative count");
+  ARGCHK((!lo || (lo_src >= 0 && lo_src + count <= src->n && lo_dst >= 0 && lo_dst + count <= dst->n)) &&
+             (!hi || (hi_src >= 0 && hi_src + count <= src->n && hi_dst >= 0 && hi_dst + count <= dst->n)),
+         MSP_ERR_ARG_OUTOFRANGE, "plane ranges outside the vectors");
+  msp_ctx* c = m->ctx;
+  if (count == 0 || m->nranks == 1) return MSP_SUCCESS;
+  if (m->kind == COMM_RCCL) {
+    NCCLCHK(rccl().group_start());
+    if (lo) {
+      NCCLCHK(rccl().send(src->d + lo_src, (size_t)count, ncclDouble, m->rank - 1, m->nccl, c->stream));
+      NCCLCHK(rccl().recv(dst->d + lo_dst, (size_t)count, ncclDouble, m->rank - 1, m->nccl, c->stream));
+    }
+    if (hi) {
+      NCCLCHK(rccl().send(src->d + hi_src, (size_t)count, ncclDouble, m->rank + 1, m->nccl, c->stream));
+      NCCLCHK(rccl().recv(dst->d + hi_dst, (size_t)count, ncclDouble, m->rank + 1, m->nccl, c->stream));
+    }
+    NCCLCHK(rccl().group_end());
+    return MSP_SUCCESS;
+  }
+  // host transport: [lo plane | hi plane] of every rank, gathered
+  double* pk = nullptr;
+  double* all = nullptr;
+  HIPCHK(hipMallocAsync((void**)&pk, (size_t)2 * count * sizeof(double), c->stream));
+  HIPCHK(hipMallocAsync((void**)&all, (size_t)2 * count * m->nranks * sizeof(double), c->stream));
+  const size_t bytes = (size_t)count * sizeof(double);
+  int rc = MSP_SUCCESS;
+  if (lo) HIPCHK(hipMemcpyAsync(pk, src->d + lo_src, bytes, hipMemcpyDeviceToDevice, c->stream));
+  if (hi) HIPCHK(hipMemcpyAsync(pk + count, src->d + hi_src, bytes, hipMemcpyDeviceToDevice, c->stream));
+  rc = mspi_comm_allgather(m, pk, all, 2 * count);
+  if (!rc && lo)  // rank-1 sent its hi plane
+    rc = hipMemcpyAsync(dst->d + lo_dst, all + (size_t)(m->rank - 1) * 2 * count + count, bytes,
+                        hipMemcpyDeviceToDevice, c->stream) == hipSuccess ? MSP_SUCCESS : MSP_ERR_LIB;
+  if (!rc && hi)  // rank+1 sent its lo plane
+    rc = hipMemcpyAsync(dst->d + hi_dst, all + (size_t)(m->rank + 1) * 2 * count, bytes, hipMemcpyDeviceToDevice,
+                        c->stream) == hipSuccess ? MSP_SUCCESS : MSP_ERR_LIB;
+  (void)hipFreeAsync(pk, c->stream);
+  (void)hipFreeAsync(all, c->stream);
+  if (rc == MSP_ERR_LIB) mspi_set_error(MSP_ERR_LIB, "device copy of a received plane failed");
+  return rc;
+}
+
+// The outer-residual reduction (the Allreduce over the block roots,
+// synchronous-multisplitting.c:192): out[i] = sum over ranks of in[i], added in
+// rank order from 0.0 on every rank, so every rank holds the same bits whatever
+// the collective's algorithm.  Host arrays; synchronises the context's stream.
+extern "C" int msp_comm_sum_ordered(msp_comm* m, const double* in, double* out, int32_t n) {
+  ARGCHK(m && (n == 0 || (in && out)), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(n >= 0, MSP_ERR_ARG_OUTOFRANGE, "negative count");
+  if (n == 0) return MSP_SUCCESS;
+  msp_ctx* c = m->ctx;
+  const size_t per = (size_t)n * sizeof(double);
+  double* d = nullptr;
+  HIPCHK(hipMallocAsync((void**)&d, per * (1 + (size_t)m->nranks), c->stream));
+  HIPCHK(hipMemcpyAsync(d, in, per, hipMemcpyHostToDevice, c->stream));
+  int rc = mspi_comm_allgather(m, d, d + n, n);
+  double* h = (double*)malloc(per * (size_t)m->nranks);
+  if (!rc && !h) {
+    mspi_set_error(MSP_ERR_MEM, "allocation failed");
+    rc = MSP_ERR_MEM;
+  }
+  if (!rc && hipMemcpyAsync(h, d + n, per * m->nranks, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+    mspi_set_error(MSP_ERR_LIB, "copy of the gathered values failed");
+    rc = MSP_ERR_LIB;
+  }
+  (void)hipFreeAsync(d, c->stream);
+  if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) {
+    mspi_set_error(MSP_ERR_LIB, "stream synchronisation failed");
+    rc = MSP_ERR_LIB;
+  }
+  if (!rc) {
+    for (int32_t i = 0; i < n; ++i) {
+      double acc = 0.0;
+      for (int32_t r = 0; r < m->nranks; ++r) acc += h[(size_t)r * n + i];
+      out[i] = acc;
+    }
+  }
+  free(h);
+  return rc;
 }

@@ -438,6 +438,19 @@ class Comm:
     def allgather(self, send: Vec, recv: Vec, count: int):
         call("msp_comm_allgather", self.h, send.h, recv.h, int(count))
 
+    def exchange_neighbors(self, src: Vec, lo_src: int, hi_src: int, dst: Vec, lo_dst: int, hi_dst: int,
+                           count: int):
+        """comm_sync_send_and_receive for chain neighbours: planes to rank-1 / rank+1 and back."""
+        call("msp_comm_exchange_neighbors", self.h, src.h, int(lo_src), int(hi_src), dst.h, int(lo_dst),
+             int(hi_dst), int(count))
+
+    def sum_ordered(self, values) -> np.ndarray:
+        """Sum over ranks, in rank order (the outer-residual Allreduce)."""
+        a = np.ascontiguousarray(values, np.float64).reshape(-1)
+        out = np.zeros_like(a)
+        call("msp_comm_sum_ordered", self.h, _dp(a), _dp(out), a.size)
+        return out
+
     def destroy(self):
         if getattr(self, "h", None) and self.h.value:
             call("msp_comm_destroy", C.byref(self.h))

@@ -151,3 +151,52 @@ def test_am_two_processes_device_transport(problem):
     assert out[0][3] == out[1][3] and out[0][4] == out[1][4]
     assert out[0][4] <= 1e-4 * out[0][3]
     assert out[0][2] == out[1][2]
+
+
+def _comm_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Vec
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ctx = Context(0)
+        os.environ["MSPLIT_LSQR_TRANSPORT"] = "host"
+        comm = TorchComm().lsqr_comm(ctx)               # the host-callback msp_comm over gloo
+        n, p = 40, 6
+        src = Vec.from_array(ctx, 1000.0 * rank + np.arange(n, dtype=np.float64))
+        dst = Vec.from_array(ctx, np.full(2 * p, -1.0))
+        comm.exchange_neighbors(src, 0, n - p, dst, 0, p, p)   # first plane down, last plane up
+        got = dst.get_array()
+        s = comm.sum_ordered(np.array([rank + 0.1, 2.0 ** -rank]))
+        q.put((rank, got, s))
+        comm.destroy()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_exchange_neighbors_host_transport_three_ranks():
+    """msp_comm_exchange_neighbors / msp_comm_sum_ordered across three processes
+    (host transport over gloo): each rank receives exactly its neighbours'
+    boundary planes and every rank holds the same rank-ordered sum."""
+    world, n, p = 3, 40, 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for rank, got, s in out:
+        lo = 1000.0 * (rank - 1) + np.arange(n - p, n) if rank > 0 else np.full(p, -1.0)
+        hi = 1000.0 * (rank + 1) + np.arange(p) if rank < world - 1 else np.full(p, -1.0)
+        assert np.array_equal(got, np.concatenate([lo, hi]))
+        exp0 = 0.0
+        for r in range(world):
+            exp0 += r + 0.1
+        assert s[0] == exp0 and s[1] == 1.0 + 0.5 + 0.25

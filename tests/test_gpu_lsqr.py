@@ -230,3 +230,16 @@ def test_matmult_dense_general_csr(ctx, oracle, nnz_per_row):
     Ao = oracle.Mat.from_arrays(nr, ncol, rp, c, v)
     ref = np.stack([Ao.mult(S[:, j]) for j in range(s)], axis=1)
     assert np.array_equal(Rd.get_values(), ref)
+
+
+@pytest.mark.parametrize("transport", ["rccl", "host"])
+def test_comm_exchange_and_sum_single_rank(ctx, transport):
+    """One rank has no neighbours: the exchange leaves dst alone; the ordered sum is the identity."""
+    comm = Comm.rccl(ctx, 1, 0, Comm.unique_id()) if transport == "rccl" else Comm.host(ctx, 1, 0, lambda a: a)
+    src = Vec.from_array(ctx, np.arange(10.0))
+    dst = Vec.from_array(ctx, np.full(6, -1.0))
+    comm.exchange_neighbors(src, 0, 7, dst, 0, 3, 3)
+    assert np.array_equal(dst.get_array(), np.full(6, -1.0))
+    v = np.array([1.5, -2.0, 3e-300])
+    assert np.array_equal(comm.sum_ordered(v), v)
+    comm.destroy()
