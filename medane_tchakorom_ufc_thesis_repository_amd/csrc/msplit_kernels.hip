@@ -185,7 +185,7 @@ __device__ __forceinline__ double group_sum(const double (&a)[G], const double (
   }
 }
 
-template <int G, bool FULL, int VAR>
+template <int G, bool FULL, int VAR, int J0, int JN>
 __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs& V, const Coefs& A,
                                             const double* __restrict__ adev, int negate, int g, int64_t base,
                                             int64_t n) {
@@ -198,7 +198,7 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs&
     vp[q] = vec_at(V, g + q);
   }
 #pragma unroll
-  for (int j = 0; j < kIters; ++j) {
+  for (int j = J0; j < J0 + JN; ++j) {
     const int64_t e = base + j * (2 * kT);
     double p0[G], p1[G];
 #pragma unroll
@@ -224,13 +224,17 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs&
   }
 }
 
-template <bool ACCUM, bool NORM, bool FULL, int VAR>
-__device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win, double* __restrict__ wout,
-                                                 const Vecs& V, const Coefs& A, const double* __restrict__ adev,
-                                                 int negate, int nv, int64_t base, int64_t n, double& sq) {
+// One slice [J0, J0+JN) of the lane's 8 double2 positions: load w, run every
+// vector group over it, store and add its squares to acc in j order.  The
+// chunk is one slice (VAR bit 3 clear) or two halves one after the other (set:
+// half the registers, twice the waves per SIMD); per element nothing changes.
+template <bool ACCUM, bool NORM, bool FULL, int VAR, int J0, int JN>
+__device__ __forceinline__ void maxpy_slice(const double* __restrict__ win, double* __restrict__ wout,
+                                            const Vecs& V, const Coefs& A, const double* __restrict__ adev,
+                                            int negate, int nv, int64_t base, int64_t n, double& acc) {
   double u[2 * kIters];
 #pragma unroll
-  for (int j = 0; j < kIters; ++j) {
+  for (int j = J0; j < J0 + JN; ++j) {
     const int64_t e = base + j * (2 * kT);
     if (ACCUM) {
       u[2 * j] = 0.0;
@@ -245,14 +249,13 @@ __device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win,
     }
   }
   const int jrem = nv & 3;
-  if (jrem == 3) chunk_group<3, FULL, VAR>(u, V, A, adev, negate, 0, base, n);
-  else if (jrem == 2) chunk_group<2, FULL, VAR>(u, V, A, adev, negate, 0, base, n);
-  else if (jrem == 1) chunk_group<1, FULL, VAR>(u, V, A, adev, negate, 0, base, n);
+  if (jrem == 3) chunk_group<3, FULL, VAR, J0, JN>(u, V, A, adev, negate, 0, base, n);
+  else if (jrem == 2) chunk_group<2, FULL, VAR, J0, JN>(u, V, A, adev, negate, 0, base, n);
+  else if (jrem == 1) chunk_group<1, FULL, VAR, J0, JN>(u, V, A, adev, negate, 0, base, n);
 #pragma unroll 1
-  for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL, VAR>(u, V, A, adev, negate, g, base, n);
-  double acc = 0.0;
+  for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL, VAR, J0, JN>(u, V, A, adev, negate, g, base, n);
 #pragma unroll
-  for (int j = 0; j < kIters; ++j) {
+  for (int j = J0; j < J0 + JN; ++j) {
     const int64_t e = base + j * (2 * kT);
     double r0 = u[2 * j], r1 = u[2 * j + 1];
     if (FULL) {
@@ -285,6 +288,19 @@ __device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win,
         if (NORM) acc = acc + r1 * r1;
       }
     }
+  }
+}
+
+template <bool ACCUM, bool NORM, bool FULL, int VAR>
+__device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win, double* __restrict__ wout,
+                                                 const Vecs& V, const Coefs& A, const double* __restrict__ adev,
+                                                 int negate, int nv, int64_t base, int64_t n, double& sq) {
+  double acc = 0.0;
+  if constexpr ((VAR & 8) != 0) {
+    maxpy_slice<ACCUM, NORM, FULL, VAR, 0, kIters / 2>(win, wout, V, A, adev, negate, nv, base, n, acc);
+    maxpy_slice<ACCUM, NORM, FULL, VAR, kIters / 2, kIters / 2>(win, wout, V, A, adev, negate, nv, base, n, acc);
+  } else {
+    maxpy_slice<ACCUM, NORM, FULL, VAR, 0, kIters>(win, wout, V, A, adev, negate, nv, base, n, acc);
   }
   sq = acc;
 }
@@ -665,7 +681,8 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
                                const int* stop, hipStream_t s) {
   if (n <= 0 || (nv <= 0 && !nvdev)) return 0;
   // non-temporal store of w too unless MSK_TUNE_MAXPY_TEMPORAL_ST (+0.4 % per step)
-  const int var = vec_var() | ((g_tuning & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4);
+  const int var = vec_var() | ((g_tuning & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4) |
+                  ((g_tuning & MSK_TUNE_MAXPY_HALVES) ? 8 : 0);
   const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
 #define MSK_MAXPY_LAUNCH(V_)                                                                                     \
   if (partial)                                                                                                  \
@@ -681,6 +698,8 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
     case 0: MSK_MAXPY_LAUNCH(0) break;
     case 1: MSK_MAXPY_LAUNCH(1) break;
     case 4: MSK_MAXPY_LAUNCH(4) break;
+    case 5: MSK_MAXPY_LAUNCH(5) break;
+    case 13: MSK_MAXPY_LAUNCH(13) break;
     default: MSK_MAXPY_LAUNCH(5) break;
   }
 #undef MSK_MAXPY_LAUNCH
