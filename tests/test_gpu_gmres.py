@@ -123,3 +123,39 @@ def test_sm_driver_bitwise_vs_oracle(ctx, oracle, dim, nx, ny, nz, nb):
     x = np.concatenate([blk.x.get_array() for blk in blocks])
     assert np.array_equal(x, ro["x"])
     assert abs(res.error - ro["error"]) <= 1e-12 * max(1.0, ro["error"])
+
+
+def _random_csr(rng, n, max_row):
+    """Nonsymmetric, diagonally dominant, ragged rows (0..max_row off-diagonals), sorted columns."""
+    rows, cols, vals = [], [], []
+    for r in range(n):
+        k = int(rng.integers(0, max_row + 1))
+        c = np.unique(np.concatenate([[r], rng.integers(0, n, k)]))
+        v = rng.uniform(-1, 1, c.size)
+        v[c == r] = 1.0 + np.abs(v).sum()
+        rows.append(np.full(c.size, r))
+        cols.append(c)
+        vals.append(v)
+    cols, vals = np.concatenate(cols), np.concatenate(vals)
+    rp = np.concatenate([[0], np.cumsum([x.size for x in rows])])
+    return rp.astype(np.int32), cols.astype(np.int32), vals
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_gmres_random_operators_bitwise(ctx, oracle, seed):
+    """General CSR (not a stencil): ragged rows up to 70 entries (the LDS staging's
+    long-row path), random restart / max_it / guess, against the DBR oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(50, 6000))
+    rp, c, v = _random_csr(rng, n, [3, 8, 70][seed % 3])
+    A = Mat.from_csr(ctx, n, n, rp, c, v)
+    O = oracle.Mat.from_arrays(n, n, rp, c, v)
+    b = rng.uniform(-1, 1, n)
+    o = dict(restart=int(rng.integers(1, 41)), max_it=int(rng.integers(1, 120)),
+             rtol=[1e-30, 1e-8, 1e-3, 1e-30][seed % 4])
+    nonzero = bool(rng.integers(0, 2))
+    x0 = rng.uniform(-1, 1, n) if nonzero else None
+    xg, rg = _gpu_gmres(ctx, A, b, x0, _opts_str(o, nonzero))
+    xo, ro = oracle.gmres(O, b, x0=x0, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=1 if nonzero else 0, **o)
+    assert (rg["its"], rg["reason"]) == (ro["its"], ro["reason"])
+    assert np.array_equal(rg["hist"], ro["hist"]) and np.array_equal(xg, xo)
