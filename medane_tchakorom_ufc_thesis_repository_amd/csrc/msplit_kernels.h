@@ -37,7 +37,8 @@ enum {
   MSK_TUNE_VEC_TEMPORAL = 16,       // default-policy (not non-temporal) basis loads in MDot / MAXPY / dense
   MSK_TUNE_MAXPY_TEMPORAL_ST = 64,  // default-policy store of w in MAXPY
   MSK_TUNE_GM_UNFUSED = 128,        // separate ||w||^2 stage-2 and one-lane Hessenberg update launches
-  MSK_TUNE_MAXPY_HALVES = 256       // MAXPY: each chunk in two halves (fewer registers, more waves)
+  MSK_TUNE_MAXPY_HALVES = 256,      // MAXPY: each chunk in two halves (fewer registers, more waves)
+  MSK_TUNE_SPMV_ZCHUNK = 512        // SpMV: XCD x takes the x-th eighth of the row blocks, in order
 };
 
 extern "C" {

@@ -356,6 +356,7 @@ struct XcdMap {
 __device__ __forceinline__ int32_t row_block(XcdMap m) {
   const int32_t i = blockIdx.x;
   if (m.bp == 0) return i;
+  if (m.bp < 0) return (i & 7) * m.np + (i >> 3);  // z-chunks: XCD x sweeps rows [x N/8, (x+1) N/8) in order
   const int32_t xcd = i & 7, j = i >> 3;
   const int32_t span = m.np * m.gb;  // blocks of one group over all planes
   const int32_t q = j / span, rem = j - q * span;
@@ -628,6 +629,14 @@ extern "C" void msk_set_spmv_group(int gb) { g_spmv_gb = gb; }
 
 static XcdMap xcd_map(int32_t nrows, int64_t plane) {
   XcdMap m = {0, 0, 0};
+  if (g_tuning & MSK_TUNE_SPMV_ZCHUNK) {  // A/B: each XCD a contiguous eighth of the rows
+    const int32_t nblk = (nrows + kT - 1) / kT;
+    if (nblk % 8 == 0) {
+      m.bp = -1;
+      m.np = nblk / 8;
+    }
+    return m;
+  }
   if (!(g_tuning & MSK_TUNE_SPMV_XCD) || plane <= 0 || plane % kT || nrows % plane) return m;
   const int32_t bp = (int32_t)(plane / kT);
   int32_t gb = g_spmv_gb > 0 ? g_spmv_gb : std::min(bp / 8, 64);
