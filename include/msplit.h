@@ -374,8 +374,10 @@ int msp_abcast_publish_dense(msp_abcast *bc, const msp_dense *D, int32_t *publis
 int msp_abcast_fetch_dense(msp_abcast *bc, int32_t src, msp_dense *D, int32_t *got);
 /* device buffers: the published blocks stay in the sender's HBM (HIP IPC), a fetch
  * is a peer copy over xGMI; enable on every rank before the first publish,
- * close_peers on every rank before destroy */
-int msp_abcast_enable_device(msp_abcast *bc, msp_ctx *ctx);
+ * close_peers on every rank before destroy.  nbuf = 2 (a publish fills the
+ * buffer readers are not using) or 1 (half the HBM: a publish waits until no
+ * reader holds the newest block, and readers skip a block being rewritten). */
+int msp_abcast_enable_device(msp_abcast *bc, msp_ctx *ctx, int32_t nbuf);
 int msp_abcast_close_peers(msp_abcast *bc);
 
 /* ------------------------------------------------- convergence detection */

@@ -68,6 +68,7 @@ class AsyncBlock:
         self.blk = blk
         self.am = AsyncMessages(name, L.nb, L.b, max(L.plane, 1), owner)
         self.bcast = AsyncBroadcast(name + "_R", L.nb, L.b, bcast_cap, owner) if bcast_cap else None
+        self.bcast_cap = bcast_cap
         nbrs = [nbr for nbr, *_ in L.recv]            # spanning tree = chain; dependencies = the same blocks
         self.cvd = ConvDetection(self.am, L.b, nbrs, nbrs, strict)
         self.it = 0
@@ -141,10 +142,18 @@ class AsyncBlock:
         T("detect", self._detect, norm0, rtol, atol, trace, variant == "amam_global")
 
     def enable_device(self):
-        """Device slots / buffers in this block's HBM (xGMI peer copies between GPUs)."""
+        """Device slots / buffers in this block's HBM (xGMI peer copies between GPUs).  The R
+        broadcast takes two buffers, or one when two would not leave a quarter of the free HBM
+        (configs[3] scale: DESIGN.md section 6.5); MSPLIT_ABCAST_NBUF forces 1 or 2."""
         self.am.enable_device(self.blk.ctx)
         if self.bcast is not None:
-            self.bcast.enable_device(self.blk.ctx)
+            nbuf = int(os.environ.get("MSPLIT_ABCAST_NBUF", "0"))
+            if nbuf not in (1, 2):
+                import torch
+                free, _ = torch.cuda.mem_get_info(self.blk.ctx.device)
+                nbuf = 2 if 2 * 8 * self.bcast_cap <= 0.75 * free else 1
+            self.bcast.enable_device(self.blk.ctx, nbuf)
+            self.bcast_nbuf = nbuf
 
     def close_peers(self):
         self.am.close_peers()

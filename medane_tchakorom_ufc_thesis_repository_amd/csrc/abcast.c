@@ -74,7 +74,8 @@ struct msp_abcast {
   int registered;
   abc_ipc *ipc;    /* [rank] exported device buffers */
   msp_ctx *dctx;   /* device buffers enabled */
-  double *dbufs;   /* this rank's 2 x cap device buffers */
+  double *dbufs;   /* this rank's nbuf_dev x cap device buffers */
+  int nbuf_dev;    /* 2, or 1 where HBM is short: a publish then waits out the readers of the newest block */
   double **peer;   /* [src] resolved device buffers */
   uint8_t *opened; /* [src] came from hipIpcOpenMemHandle */
 };
@@ -160,15 +161,17 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
   return MSP_SUCCESS;
 }
 
-int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx) {
+int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   if (!b || !ctx) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  if (nbuf != 1 && nbuf != 2) return berr(MSP_ERR_ARG_OUTOFRANGE, "nbuf must be 1 or 2");
   if (b->dctx) return MSP_SUCCESS;
   b->peer = (double **)calloc((size_t)b->nranks, sizeof(double *));
   b->opened = (uint8_t *)calloc((size_t)b->nranks, 1);
   if (!b->peer || !b->opened) return berr(MSP_ERR_MEM, "allocation failed");
   void *p = NULL;
-  int rc = mspi_dev_alloc(ctx, (size_t)2 * (size_t)(b->cap > 0 ? b->cap : 1) * sizeof(double), &p);
+  int rc = mspi_dev_alloc(ctx, (size_t)nbuf * (size_t)(b->cap > 0 ? b->cap : 1) * sizeof(double), &p);
   if (rc) return rc;
+  b->nbuf_dev = nbuf;
   abc_ipc *e = &b->ipc[b->rank];
   if ((rc = mspi_ipc_export(p, e->handle))) {
     mspi_dev_free(p);
@@ -278,7 +281,8 @@ static int publish(msp_abcast *b, const abc_view *v, int32_t *published) {
   if (rc) return rc;
   src_line *L = &b->lines[b->rank];
   const int32_t newest = atomic_load_explicit(&L->newest, memory_order_acquire);
-  const int w = newest == 0 ? 1 : 0;
+  /* the buffer that is not the newest; with one device buffer, the newest itself (free of readers) */
+  const int w = (b->dctx && b->nbuf_dev == 1) ? 0 : (newest == 0 ? 1 : 0);
   uint32_t expect = 0;
   if (!atomic_compare_exchange_strong_explicit(&L->lock[w], &expect, ABC_WRITER, memory_order_acq_rel,
                                                memory_order_relaxed))

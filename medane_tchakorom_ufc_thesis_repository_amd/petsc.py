@@ -799,9 +799,9 @@ class AsyncBroadcast:
              C.byref(got))
         return bool(got.value)
 
-    def enable_device(self, ctx: Context):
-        """Device buffers: published blocks stay in the sender's HBM (HIP IPC)."""
-        call("msp_abcast_enable_device", self.h, ctx.h)
+    def enable_device(self, ctx: Context, nbuf: int = 2):
+        """Device buffers: published blocks stay in the sender's HBM (HIP IPC); nbuf 1 halves their HBM."""
+        call("msp_abcast_enable_device", self.h, ctx.h, int(nbuf))
         self._ctx = ctx
 
     def close_peers(self):

@@ -154,9 +154,12 @@ def test_amam_semi_local_convdiff_gpu_bitwise_vs_twin(ctx, oracle):
                                                                (3, 8, 8, 8, 2, 4, 5, None),
                                                                (3, 6, 6, 9, 3, 3, 3, None),
                                                                (3, 8, 8, 8, 4, 4, 5, PE)])
-def test_amam_global_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s, max_it, peclet):
+def test_amam_global_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s, max_it, peclet, monkeypatch):
     """AMAM-global (configs[3]/[4]'s algorithm): R rows broadcast through msp_abcast,
-    LSQR over the replicated R, x_minimized into x_i and the neighbour view."""
+    LSQR over the replicated R, x_minimized into x_i and the neighbour view (one
+    device buffer per block on the 3-block case, two otherwise)."""
+    if nb == 3:
+        monkeypatch.setenv("MSPLIT_ABCAST_NBUF", "1")
     opts = Options(" ".join(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 "
                             f"-inner{b + 1}_pc_type none" for b in range(nb)) + " " + _outer_opts(nb))
     comm = LocalComm()

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _transport_worker(rank, name, n_msgs, n, q):
+def _transport_worker(rank, name, n_msgs, n, q, nbuf=2):
     sys.path.insert(0, ROOT)
     import time
     import torch  # noqa: F401
@@ -38,7 +38,7 @@ def _transport_worker(rank, name, n_msgs, n, q):
         am = AsyncMessages(name, 2, 0, n, owner=True)
         bc = AsyncBroadcast(name + "_R", 2, 0, n * 3, owner=True)
     am.enable_device(ctx)
-    bc.enable_device(ctx)
+    bc.enable_device(ctx, nbuf)
     while am.attached() < 2:
         time.sleep(0.01)
     ok = True
@@ -87,14 +87,16 @@ def _transport_worker(rank, name, n_msgs, n, q):
     q.put((rank, ok, taken, last))
 
 
-def test_device_slots_cross_process_whole_and_newest():
+@pytest.mark.parametrize("nbuf", [2, 1])
+def test_device_slots_cross_process_whole_and_newest(nbuf):
     """Every plane and block a receiver takes from the sender's HBM is whole and
-    newer than the last, and the last one always arrives."""
+    newer than the last, and the last one always arrives (R broadcast with two
+    device buffers, or one)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    name = f"/msplit_ipc_{os.getpid()}"
+    name = f"/msplit_ipc_{os.getpid()}_{nbuf}"
     n, n_msgs = 1 << 16, 400
-    procs = [ctx.Process(target=_transport_worker, args=(r, name, n_msgs, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_transport_worker, args=(r, name, n_msgs, n, q, nbuf)) for r in range(2)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=300) for _ in range(2)])
