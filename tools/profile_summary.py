@@ -1,0 +1,77 @@
+"""Write profiles/r01/README.md and profiles/r01/final/* from a tools/gpu_round.sh run directory.
+
+  python tools/profile_summary.py gpurun_out/<run> [--tag r01]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run")
+    ap.add_argument("--tag", default="r01")
+    a = ap.parse_args()
+    run = a.run
+    D = os.path.join(ROOT, "profiles", a.tag, "final")
+    os.makedirs(D, exist_ok=True)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), os.path.join(run, "pmc_fetch"),
+                    os.path.join(run, "pmc_write"), "--n", "256", "--out", os.path.join(D, "traffic.json")],
+                   check=True, stdout=subprocess.DEVNULL)
+    shutil.copy(os.path.join(D, "traffic.json"), os.path.join(ROOT, "profiles", "traffic.json"))
+    shutil.copy(os.path.join(run, "bench.json"), os.path.join(D, "bench.json"))
+    shutil.copy(os.path.join(run, "bench_trace.json"), os.path.join(D, "bench_under_rocprof.json"))
+    shutil.copy(os.path.join(run, "trace", "run_kernel_stats.csv"), os.path.join(D, "rocprofv3_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(os.path.join(D, "rocprofv3_kernel_stats.csv"))))
+    b = json.loads(open(os.path.join(D, "bench.json")).read().strip().splitlines()[-1])
+    bt = json.loads(open(os.path.join(D, "bench_under_rocprof.json")).read().strip().splitlines()[-1])
+    tr = json.load(open(os.path.join(D, "traffic.json")))
+    mx = [r for r in rows if r["Name"] == "k_maxpy_chunk"][0]
+    rf = b["roofline"]
+    L = [f"# Round {a.tag[1:]} profiles (MI355X, gfx950, ROCm 7.2)", "",
+         f"Command: `bash tools/gpu_round.sh {os.path.basename(run)}` = pytest -m gpu; `python bench.py`; "
+         "`rocprofv3 --kernel-trace --stats -T -- python3 bench.py --steps 3 --no-cpu-baseline`;",
+         "two PMC passes (`--pmc FETCH_SIZE`, `--pmc WRITE_SIZE`) of `bench.py --steps 1 --warmup 0 --no-timing`, "
+         "reduced by `tools/pmc_traffic.py` (read = 2 x FETCH_SIZE on gfx950, write = WRITE_SIZE). "
+         "Summary written by `tools/profile_summary.py`.", "",
+         f"bench.py (N=1, 256^3, GMRES(30), 300 iterations/step): **{b['value']:.4g} DOF-updates/s**, "
+         f"{b['ms_per_step']:.1f} ms/step; under rocprof: {bt['value']:.4g}.",
+         f"cpu_baseline (oracle, 1 thread): {b['cpu_baseline']['value']:.3g} DOF-updates/s.", "",
+         "## rocprofv3 --stats (4 solves = 1 warmup + 3 timed)", "",
+         "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
+    for r in rows:
+        L.append(f"| {r['Name']} | {r['Calls']} | {int(r['TotalDurationNs']) / 1e6:.2f} | "
+                 f"{float(r['AverageNs']) / 1e3:.2f} | {float(r['Percentage']):.2f} |")
+    L += ["", "## Dominant kernel: bench.py's HIP-event timing vs rocprof", "",
+          f"bench.py roofline: class `maxpy` ({rf['kernel']}), avg {rf['avg_launch_ms'] * 1e3:.1f} us/launch, "
+          f"{rf['bytes_per_launch'] / 1e9:.4f} GB algorithmic/launch -> {rf['achieved']:.0f} GB/s = "
+          f"{rf['frac']:.3f} of 8 TB/s.",
+          f"rocprof k_maxpy_chunk: avg {float(mx['AverageNs']) / 1e3:.1f} us over {mx['Calls']} calls "
+          "(the class also holds the BuildSoln accumulate launches).", "",
+          "## HBM traffic per launch (PMC) vs algorithmic bytes", "",
+          "| class | launches | HBM GB/launch | algorithmic GB/launch | ratio |", "|---|---|---|---|---|"]
+    for k, v in tr["classes"].items():
+        alg = v["alg_bytes_per_launch"]
+        ratio = v["hbm_over_alg"]
+        L.append(f"| {k} | {v['launches']} | {v['hbm_bytes_per_launch'] / 1e9:.4f} | "
+                 f"{(alg / 1e9) if alg else float('nan'):.4f} | {ratio if ratio else float('nan'):.4f} |")
+    L += ["", f"maxpy: 8n(k+2) algorithmic = {rf['bytes_per_launch'] / 1e9:.4f} GB/launch on average "
+          f"(bench.py's figure), PMC {tr['hbm_bytes_per_launch'] / 1e9:.4f}.",
+          "SpMV (scaled form: reads T, writes VV(it) and VV(it+1)): algorithmic 1.874 GB; PMC about 1.2x "
+          "(x gathers re-read across XCDs through the MALL).", "",
+          "Other directories: `smsm/` (SMSM-global), `convdiff/`, `async/` (transports and async drivers), "
+          "`configs/` (BASELINE configurations end to end), `spmv_ab/`, `skew_ab/`, earlier `*.json|csv` "
+          "(first correct path, tuning history in DESIGN.md)."]
+    open(os.path.join(ROOT, "profiles", a.tag, "README.md"), "w").write("\n".join(L) + "\n")
+
+
+if __name__ == "__main__":
+    main()
