@@ -12,6 +12,10 @@
  */
 #include "oracle.h"
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -20,6 +24,17 @@
 #define ORC_OK 0
 #define ORC_ERR_MEM 55
 #define ORC_ERR_ARG 62
+
+/* Threads for the CPU-baseline timing (orc_set_threads): element-wise loops run
+ * in parallel (each element's arithmetic is unchanged), and ORC_REDUCE_MT dots
+ * sum per-thread contiguous pieces, then the pieces in thread order -- PETSc's
+ * VecDot_MPI order (local ddot, then the Allreduce over ranks) with one rank per
+ * thread.  The tests use 1 thread and the SEQ / DBR orders. */
+static int orc_nthreads = 1;
+
+void orc_set_threads(int t) { orc_nthreads = t > 0 ? t : 1; }
+
+#define ORC_PAR _Pragma("omp parallel for schedule(static) num_threads(orc_nthreads) if (orc_nthreads > 1)")
 
 void orc_csr_free(orc_csr *A) {
   if (!A) return;
@@ -207,6 +222,7 @@ int orc_split(const orc_csr *Ab, int64_t c0, int64_t c1, orc_csr *Aii, orc_csr *
 
 /* MatMult_SeqAIJ [PETSc-ext]: sum = 0; sum += aa[k]*x[aj[k]] left to right. */
 void orc_spmv(const orc_csr *A, const double *x, double *y) {
+  ORC_PAR
   for (int32_t r = 0; r < A->nrows; ++r) {
     double s = 0.0;
     for (int32_t k = A->rowptr[r]; k < A->rowptr[r + 1]; ++k) s += A->val[k] * x[A->col[k]];
@@ -216,6 +232,7 @@ void orc_spmv(const orc_csr *A, const double *x, double *y) {
 
 /* MatResidual default [PETSc-ext]: MatMult(A,x,r); VecAYPX(r,-1,b) -> r = b - A x. */
 void orc_residual(const orc_csr *A, const double *b, const double *x, double *r) {
+  ORC_PAR
   for (int32_t row = 0; row < A->nrows; ++row) {
     double s = 0.0;
     for (int32_t k = A->rowptr[row]; k < A->rowptr[row + 1]; ++k) s += A->val[k] * x[A->col[k]];
@@ -277,7 +294,29 @@ static double seq_dot(int64_t n, const double *x, const double *y) {
   return s;
 }
 
+static double mt_dot(int64_t n, const double *x, const double *y) {
+  double part[1024];
+  int used = 1;
+#pragma omp parallel num_threads(orc_nthreads > 1024 ? 1024 : orc_nthreads)
+  {
+#ifdef _OPENMP
+    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+#else
+    const int t = 0, nt = 1;
+#endif
+    const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    double acc = 0.0;
+    for (int64_t i = lo; i < hi; ++i) acc += x[i] * y[i];
+    part[t] = acc;
+    if (t == 0) used = nt;
+  }
+  double s = 0.0;
+  for (int t = 0; t < used; ++t) s += part[t];
+  return s;
+}
+
 double orc_dot(int mode, int64_t n, const double *x, const double *y) {
+  if (mode == ORC_REDUCE_MT) return mt_dot(n, x, y);
   return mode == ORC_REDUCE_DBR ? dbr_dot(n, x, y) : seq_dot(n, x, y);
 }
 
@@ -294,6 +333,7 @@ void orc_mdot(int mode, int64_t n, int k, const double *w, const double *const *
  * evaluated left to right and then added to U. */
 void orc_maxpy(int64_t n, int k, const double *a, const double *const *V, double *w) {
   const int jrem = k & 3;
+  ORC_PAR
   for (int64_t i = 0; i < n; ++i) {
     double u = w[i];
     if (jrem == 3) u = u + ((a[0] * V[0][i] + a[1] * V[1][i]) + a[2] * V[2][i]);
@@ -379,6 +419,7 @@ static double gm_normalize(gm_t *g, double *v) {
   const double t = orc_norm2(g->o->reduce_mode, g->n, v);
   if (t != 0.0 && !is_bad(t)) {
     const double s = 1.0 / t;
+    ORC_PAR
     for (int64_t i = 0; i < g->n; ++i) v[i] = v[i] * s;
   }
   return t;
@@ -431,8 +472,10 @@ static void gm_build_soln(gm_t *g, int it) {
   }
   /* VecSet(TEMP,0); VecMAXPY(TEMP,it+1,nrs,VV); KSPUnwindPreconditioner (PCNONE: identity);
    * VecAXPY(x, 1.0, TEMP) */
+  ORC_PAR
   for (int64_t i = 0; i < g->n; ++i) g->tmp[i] = 0.0;
   orc_maxpy(g->n, it + 1, nrs, (const double *const *)g->VV, g->tmp);
+  ORC_PAR
   for (int64_t i = 0; i < g->n; ++i) g->x[i] = g->x[i] + 1.0 * g->tmp[i];
 }
 

@@ -46,7 +46,10 @@
 extern "C" {
 #endif
 
-enum { ORC_REDUCE_SEQ = 0, ORC_REDUCE_DBR = 1 };
+enum { ORC_REDUCE_SEQ = 0, ORC_REDUCE_DBR = 1, ORC_REDUCE_MT = 2 };
+/* CPU-baseline threads (default 1): see oracle.c; ORC_REDUCE_MT = PETSc's MPI dot
+ * order with one rank per thread. */
+void orc_set_threads(int threads);
 
 /* DBR geometry -- must match csrc/msplit_kernels.hip */
 #define ORC_DBR_THREADS 256

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(HERE, "liborc.so")
 
 REDUCE_SEQ = 0
 REDUCE_DBR = 1
+REDUCE_MT = 2      # PETSc's MPI dot order, one rank per thread (CPU-baseline timing)
 DBR_CHUNK = 256 * 2 * 8
 
 REASONS = {
@@ -118,6 +119,11 @@ def lib() -> C.CDLL:
                                      P(C.c_int), P(C.c_int), P(C.c_int), dp]
         _lib = L
     return _lib
+
+
+def set_threads(threads: int):
+    """OpenMP threads of the element-wise loops and of REDUCE_MT dots (CPU baseline)."""
+    lib().orc_set_threads(int(threads))
 
 
 def _dp(a: np.ndarray):
