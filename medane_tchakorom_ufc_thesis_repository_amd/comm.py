@@ -145,9 +145,29 @@ class TorchComm:
             return None
         transport = os.environ.get("MSPLIT_LSQR_TRANSPORT", "rccl" if self.backend == "nccl" else "host")
         if transport == "rccl":
-            obj = [Comm.unique_id() if self.rank == 0 else None]
+            obj = [None]
+            if self.rank == 0:
+                try:
+                    obj = [Comm.unique_id()]
+                except Exception as e:                   # no usable librccl: every rank takes the other path
+                    obj = [f"error: {e}"]
             self.dist.broadcast_object_list(obj, src=0, group=self.group)
-            return Comm.rccl(ctx, self.world, self.rank, obj[0])
+            ok = isinstance(obj[0], bytes)
+            comm = None
+            if ok:
+                try:
+                    comm = Comm.rccl(ctx, self.world, self.rank, obj[0])
+                except Exception as e:
+                    ok, obj = False, [f"error: {e}"]
+            # every rank must agree on the transport before the first all-gather
+            flags = self.allgather_scalar(1.0 if ok else 0.0)
+            if all(f == 1.0 for f in flags):
+                return comm
+            if comm is not None:
+                comm.destroy()
+            import sys
+            print(f"msplit: own RCCL communicator unavailable ({obj[0] if not ok else 'on another rank'}); "
+                  "LSQR partials go through the process group instead", file=sys.stderr)
         torch, dist, world, group = self.torch, self.dist, self.world, self.group
         dev = self.device if self.backend == "nccl" else torch.device("cpu")
 
