@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--s", type=int, default=20, help="SMSM: inner solves per minimization (-s)")
     p.add_argument("--inner-max-it", type=int, default=20)
     p.add_argument("--outer-max-it", type=int, default=70)
+    p.add_argument("--operator", default="csr", choices=["csr", "matfree"],
+                   help="gmres: the assembled CSR (the reference's MatMult, default) or the same operator applied "
+                        "matrix-free (bitwise the same products, no matrix traffic)")
     p.add_argument("--peclet", default=None,
                    help="Px,Py,Pz: the upwind convection-diffusion operator (configs[4]) instead of Poisson")
     a = p.parse_args()
@@ -153,7 +156,10 @@ def main():
 
     if variant == "gmres":
         # configs[1]: single-block GMRES(30) on 256^3 (gmres_solution.c:50-70 in 3D)
-        A = Mat.box_convdiff(ctx, 3, n, n, n, False, False, args.peclet or (0.0, 0.0, 0.0))
+        if args.operator == "matfree":
+            A = Mat.box_matfree(ctx, 3, n, n, n, False, False, args.peclet)
+        else:
+            A = Mat.box_convdiff(ctx, 3, n, n, n, False, False, args.peclet or (0.0, 0.0, 0.0))
         ones = Vec(ctx, rows)
         ones.set(1.0)
         b = Vec(ctx, rows)
@@ -169,6 +175,8 @@ def main():
             ksp.solve(b, x)                     # zero initial guess: x is reset by KSPSolve
             return ksp.get_iteration_number()
         workload = f"3D 7-pt Poisson {n}^3, single-block GMRES({args.restart}) on 1 MI355X (configs[1])"
+        if args.operator == "matfree":
+            workload += ", operator applied matrix-free (same arithmetic as the CSR; not the reference's MatMult)"
     elif variant == "sm":
         comm = TorchComm(device=torch.device("cuda", dev) if args.backend == "nccl" else torch.device("cpu"))
         L = block_layout(3, n, n, n * world, world, rank, args.peclet)

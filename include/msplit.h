@@ -123,6 +123,13 @@ int msp_mat_create_box_stencil(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, in
  * A_block_jacobi / A_block_jacobi_resdistributed rows, utils.c:30-121,
  * :247-293, :891-921).  plane = nx*ny (dim 3) or nx (dim 2).  This is the
  * operator of R = A S in the minimization variants (SMSM-global.c:326). */
+/* The same operator applied without storage (MATSHELL-like): MatMult / MatResidual
+ * and the GMRES SpMV compute exactly the assembled CSR's sums (ascending column
+ * order, same coefficients) from the stencil, so results are bitwise those of
+ * the assembled matrix while only the vectors cross HBM.  No MatMatMult /
+ * get_csr (MSP_ERR_SUP).  peclet may be NULL (Poisson). */
+int msp_mat_create_box_matfree(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo, int32_t hi,
+                               const double *peclet, msp_mat **A);
 int msp_mat_create_box_stencil_ext(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
                                    int32_t hi, msp_mat **A);
 /* The convection-diffusion operator of BASELINE configs[4] (build-defined; the

@@ -104,6 +104,8 @@ _SIGS = {
     "msp_ksp_get_residual_history": [_vp, _P(_dp), _i32p],
     "msp_mat_create_box_stencil_ext": [_vp, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                        _P(_vp)],
+    "msp_mat_create_box_matfree": [_vp, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _dp,
+                                   _P(_vp)],
     "msp_mat_create_box_convdiff": [_vp, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _dp,
                                     _P(_vp)],
     "msp_dense_create": [_vp, C.c_int64, C.c_int32, _P(_vp)],

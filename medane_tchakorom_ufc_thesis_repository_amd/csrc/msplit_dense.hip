@@ -428,6 +428,7 @@ extern "C" int msp_mat_matmult_dense(msp_mat* A, const msp_dense* S, msp_dense* 
          "MatMatMult sizes: A %d x %d, S %lld x %d, R %lld x %d", nr, ncol, (long long)S->nrows, S->ncols,
          (long long)R->nrows, R->ncols);
   const mspi_csr_view v = mspi_mat_csr(A);
+  ARGCHK(v.rowptr, MSP_ERR_SUP, "MatMatMult needs a stored CSR operator (not a matrix-free one)");
   ARGCHK(!v.compressed, MSP_ERR_SUP, "MatMatMult with a row-compressed matrix");
   msp_ctx* c = mspi_mat_ctx(A);
   if (nr == 0) return MSP_SUCCESS;

@@ -65,6 +65,10 @@ int msk_spmm(int32_t nrows, const int32_t* rowptr, const int32_t* col, const dou
 int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int32_t* rowptr, const int32_t* col,
                   const double* val, const double* x, const double* b, double* y, int resid, hipStream_t s);
 // lo/hi: extra coupling columns to the neighbour plane below/above (column space [lo | block | hi])
+// matrix-free y = A x / b - A x / scaled form for the box stencil (bitwise the CSR SpMV of its assembly)
+int msk_stencil_spmv(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi, const BoxCoef* cf,
+                     const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
+                     const int* stop, hipStream_t s);
 int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi, const BoxCoef* cf,
                     int32_t* rowptr, int32_t* col, double* val, hipStream_t s);
 int msk_blas1(int op, double* y, const double* x, const double* z, double alpha, int64_t n, hipStream_t s);

@@ -596,6 +596,90 @@ __global__ __launch_bounds__(kT) void k_box_stencil(int dim, int32_t nx, int32_t
   }
 }
 
+// ------------------------------------------------ matrix-free box stencil
+// y = A x for the operator k_box_stencil assembles, without storing it: row l
+// sums the same terms in the same (ascending column) order from 0.0, with the
+// same coefficients, so every result equals the CSR SpMV's bit for bit; only
+// x (its neighbours through L2/MALL) and y cross HBM.  MODE as k_spmv_lds8.
+// One workgroup per (x-segment, y, z) of the box: i, j and the slab plane come
+// from the grid, so no integer division per row.  V2 (nx even): each lane
+// takes two neighbouring rows, so x, y and the neighbour planes move as 16-byte
+// pairs; each row's sum is the same sequence either way.
+template <int MODE, bool V2>
+__global__ __launch_bounds__(kT) void k_stencil_spmv(int dim, int32_t nx, int32_t ny, int32_t nz, int lo, int hi,
+                                                     BoxCoef cf, const double* __restrict__ x,
+                                                     const double* __restrict__ b, double* __restrict__ y,
+                                                     const double* __restrict__ sdev, double* __restrict__ vout,
+                                                     const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  constexpr int R = V2 ? 2 : 1;
+  const int32_t i0 = ((int32_t)blockIdx.x * kT + (int32_t)threadIdx.x) * R;
+  if (i0 >= nx) return;
+  const int32_t j = (int32_t)blockIdx.y;       // y in 3D, the mesh line in 2D
+  const int32_t k = (int32_t)blockIdx.z;       // z in 3D (0 in 2D)
+  const int64_t P = dim == 3 ? (int64_t)nx * ny : (int64_t)nx;
+  const int64_t ns = dim == 3 ? nz : ny;
+  const int64_t sl = dim == 3 ? k : j;         // slab-plane index
+  const int64_t l0 = (dim == 3 ? (int64_t)k * P + (int64_t)j * nx : (int64_t)j * nx) + i0;
+  const int64_t e0 = l0 + (lo ? P : 0);
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  const bool has_lo = sl > 0 || lo, has_hi = sl < ns - 1 || hi;
+  const bool has_ym = dim == 3 && j > 0, has_yp = dim == 3 && j < ny - 1;
+  // the values each row reads: own pair, its x neighbours, the y and slab neighbours
+  double xc[R], xlo[R], xhi[R], xym[R], xyp[R];
+  double xm1, xpR;
+  if constexpr (V2) {
+    const double2 c = *reinterpret_cast<const double2*>(x + e0);
+    xc[0] = c.x;
+    xc[1] = c.y;
+    xm1 = i0 > 0 ? x[e0 - 1] : 0.0;
+    xpR = i0 + 2 < nx ? x[e0 + 2] : 0.0;
+    if (has_lo) { const double2 v = *reinterpret_cast<const double2*>(x + e0 - P); xlo[0] = v.x; xlo[1] = v.y; }
+    if (has_hi) { const double2 v = *reinterpret_cast<const double2*>(x + e0 + P); xhi[0] = v.x; xhi[1] = v.y; }
+    if (has_ym) { const double2 v = *reinterpret_cast<const double2*>(x + e0 - nx); xym[0] = v.x; xym[1] = v.y; }
+    if (has_yp) { const double2 v = *reinterpret_cast<const double2*>(x + e0 + nx); xyp[0] = v.x; xyp[1] = v.y; }
+  } else {
+    xc[0] = x[e0];
+    xm1 = i0 > 0 ? x[e0 - 1] : 0.0;
+    xpR = i0 + 1 < nx ? x[e0 + 1] : 0.0;
+    if (has_lo) xlo[0] = x[e0 - P];
+    if (has_hi) xhi[0] = x[e0 + P];
+    if (has_ym) xym[0] = x[e0 - nx];
+    if (has_yp) xyp[0] = x[e0 + nx];
+  }
+  auto S = [&](double v) { return MODE == MSK_SPMV_SCALED ? v * sc : v; };
+  double out[R], vo[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int32_t i = i0 + r;
+    const double left = r == 0 ? xm1 : xc[r - 1];
+    const double right = r == R - 1 ? xpR : xc[r + 1];
+    double s = 0.0;
+    if (has_lo) s = s + cf.c[0] * S(xlo[r]);
+    if (has_ym) s = s + cf.c[1] * S(xym[r]);
+    if (i > 0) s = s + cf.c[2] * S(left);
+    const double xd = S(xc[r]);
+    s = s + cf.c[3] * xd;
+    if (i < nx - 1) s = s + cf.c[4] * S(right);
+    if (has_yp) s = s + cf.c[5] * S(xyp[r]);
+    if (has_hi) s = s + cf.c[6] * S(xhi[r]);
+    out[r] = s;
+    vo[r] = xd;
+  }
+  if constexpr (V2) {
+    if (MODE == MSK_SPMV_RESID) {
+      const double2 bb = *reinterpret_cast<const double2*>(b + l0);
+      out[0] = bb.x - out[0];
+      out[1] = bb.y - out[1];
+    }
+    *reinterpret_cast<double2*>(y + l0) = make_double2(out[0], out[1]);
+    if (MODE == MSK_SPMV_SCALED) *reinterpret_cast<double2*>(vout + l0) = make_double2(vo[0], vo[1]);
+  } else {
+    y[l0] = MODE == MSK_SPMV_RESID ? b[l0] - out[0] : out[0];
+    if (MODE == MSK_SPMV_SCALED) vout[l0] = vo[0];
+  }
+}
+
 // --------------------------------------------------------------- BLAS-1
 template <int OP>
 __global__ __launch_bounds__(kT) void k_blas1(double* __restrict__ y, const double* __restrict__ x,
@@ -771,6 +855,24 @@ extern "C" int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int6
                                const BoxCoef* cf, int32_t* rowptr, int32_t* col, double* val, hipStream_t s) {
   const int g = grid_for(nrows + 1, 8192);
   k_box_stencil<<<dim3(g), dim3(kT), 0, s>>>(dim, nx, ny, nz, nrows, lo, hi, *cf, rowptr, col, val);
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_stencil_spmv(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi,
+                                const BoxCoef* cf, const double* x, const double* b, double* y, int mode,
+                                const double* sdev, double* vout, const int* stop, hipStream_t s) {
+  if (nrows <= 0) return 0;
+  // pairs need an even line length and 16-byte aligned vectors (x offset by a whole plane when lo)
+  const int64_t P = dim == 3 ? (int64_t)nx * ny : (int64_t)nx;
+  const bool v2 = nx % 2 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+                  (!b || ((uintptr_t)b & 15) == 0) && (!vout || ((uintptr_t)vout & 15) == 0) && (!lo || P % 2 == 0);
+  const int per = v2 ? 2 * kT : kT;
+  const dim3 g((unsigned)((nx + per - 1) / per), (unsigned)ny, (unsigned)(dim == 3 ? nz : 1));
+#define MSK_ST(M, V) k_stencil_spmv<M, V><<<g, dim3(kT), 0, s>>>(dim, nx, ny, nz, lo, hi, *cf, x, b, y, sdev, vout, stop)
+  if (mode == MSK_SPMV_RESID) { if (v2) MSK_ST(MSK_SPMV_RESID, true); else MSK_ST(MSK_SPMV_RESID, false); }
+  else if (mode == MSK_SPMV_SCALED) { if (v2) MSK_ST(MSK_SPMV_SCALED, true); else MSK_ST(MSK_SPMV_SCALED, false); }
+  else { if (v2) MSK_ST(MSK_SPMV_MULT, true); else MSK_ST(MSK_SPMV_MULT, false); }
+#undef MSK_ST
   return (int)hipGetLastError();
 }
 

@@ -368,6 +368,10 @@ struct msp_mat {
   int64_t plane = 0;          // rows per stencil plane (box-stencil operators), 0 otherwise
   int32_t nlisted = 0;
   int32_t* row_ids = nullptr;
+  bool matfree = false;       // box stencil applied without storage (msp_mat_create_box_matfree)
+  int dim = 0, lo = 0, hi = 0;
+  int32_t bx = 0, by = 0, bz = 0;
+  BoxCoef cf = {};
 };
 
 extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
@@ -548,6 +552,40 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
   return MSP_SUCCESS;
 }
 
+// The box operator applied without storage: same rows, same arithmetic as the
+// assembled CSR (k_stencil_spmv), none of its 12 bytes per entry in HBM.
+extern "C" int msp_mat_create_box_matfree(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
+                                          int32_t hi, const double* peclet, msp_mat** out) {
+  ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(dim == 2 || dim == 3, MSP_ERR_ARG_WRONG, "dim must be 2 or 3, got %d", dim);
+  if (dim == 2) nz = 1;
+  ARGCHK(nx > 0 && ny > 0 && nz > 0, MSP_ERR_ARG_SIZ, "box %d x %d x %d", nx, ny, nz);
+  const int64_t P = dim == 3 ? (int64_t)nx * ny : (int64_t)nx;
+  const int64_t nrows = P * (dim == 3 ? nz : ny);
+  ARGCHK(nrows + (lo ? P : 0) + (hi ? P : 0) < INT32_MAX, MSP_ERR_ARG_SIZ, "box too large for int32 rows");
+  ARGCHK(ny <= 65535 && nz <= 65535, MSP_ERR_ARG_SIZ, "matrix-free box: at most 65535 lines / planes (grid y, z)");
+  msp_mat* A = new msp_mat();
+  A->ctx = c;
+  A->matfree = true;
+  A->dim = dim;
+  A->bx = nx;
+  A->by = ny;
+  A->bz = nz;
+  A->lo = lo ? 1 : 0;
+  A->hi = hi ? 1 : 0;
+  A->nrows = (int32_t)nrows;
+  A->ncols = (int32_t)(nrows + (lo ? P : 0) + (hi ? P : 0));
+  A->plane = P;
+  A->cf = box_coefs(dim, peclet);
+  // entries the assembled operator would hold: 7 (5) per row less the missing neighbours on the faces
+  int64_t nnz = nrows * (dim == 3 ? 7 : 5);
+  nnz -= 2 * (dim == 3 ? (int64_t)ny * nz + (int64_t)nx * nz : (int64_t)ny);  // x and (3D) y faces
+  nnz -= (lo ? 0 : P) + (hi ? 0 : P);                                          // slow-direction faces
+  A->nnz = nnz;
+  *out = A;
+  return MSP_SUCCESS;
+}
+
 extern "C" int msp_mat_create_box_stencil_ext(msp_ctx* c, int dim, int32_t nx, int32_t ny, int32_t nz, int32_t lo,
                                               int32_t hi, msp_mat** out) {
   return msp_mat_create_box_convdiff(c, dim, nx, ny, nz, lo, hi, nullptr, out);
@@ -579,6 +617,7 @@ extern "C" int msp_mat_get_info(const msp_mat* A, int32_t* nrows, int32_t* ncols
 }
 
 extern "C" int msp_mat_get_csr(const msp_mat* A, int32_t* rowptr, int32_t* col, double* val) {
+  ARGCHK(A && !A->matfree, A ? MSP_ERR_SUP : MSP_ERR_ARG_NULL, "no stored CSR (matrix-free operator)");
   ARGCHK(A && rowptr, MSP_ERR_ARG_NULL, "NULL argument");
   ARGCHK(!A->compressed, MSP_ERR_SUP, "msp_mat_get_csr on a row-compressed matrix");
   hipStream_t s = A->ctx->stream;
@@ -600,6 +639,12 @@ static double spmv_bytes(const msp_mat* A, bool resid) {
 
 static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bool resid) {
   msp_ctx* c = A->ctx;
+  if (A->matfree) {  // x and y (and b) only
+    KTimer kt(c, MSP_KERNEL_SPMV, 8.0 * (double)A->ncols + 8.0 * A->nrows * (resid ? 2.0 : 1.0));
+    KCHK(msk_stencil_spmv(A->dim, A->bx, A->by, A->bz, A->nrows, A->lo, A->hi, &A->cf, x, b, y,
+                          resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
+    return MSP_SUCCESS;
+  }
   KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, resid));
   if (A->compressed) {
     // rows that hold no entries: y = 0 (MatMult) or r = b - 0 = b (MatResidual)
@@ -627,6 +672,12 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
   if (A->compressed || A->nrows != A->ncols) {
     mspi_set_error(MSP_ERR_SUP, "scaled MatMult needs a square, uncompressed operator");
     return MSP_ERR_SUP;
+  }
+  if (A->matfree) {
+    KTimer kt(c, MSP_KERNEL_SPMV, 8.0 * (double)A->ncols + 16.0 * (double)A->nrows);
+    KCHK(msk_stencil_spmv(A->dim, A->bx, A->by, A->bz, A->nrows, A->lo, A->hi, &A->cf, x, nullptr, y,
+                          MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
+    return MSP_SUCCESS;
   }
   KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, false) + 8.0 * (double)A->nrows);
   KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, nullptr, y, A->lds_cap, MSK_SPMV_SCALED, sdev, vout, stop,

@@ -305,6 +305,16 @@ class Mat:
              1 if hi else 0, _dp(pe), C.byref(h))
         return cls(ctx, h)
 
+    @classmethod
+    def box_matfree(cls, ctx: Context, dim: int, nx: int, ny: int, nz: int, lo: bool = False, hi: bool = False,
+                    peclet=None) -> "Mat":
+        """The box operator without storage (msp_mat_create_box_matfree): bitwise the assembled one's products."""
+        pe = np.ascontiguousarray(peclet if peclet is not None else (0.0, 0.0, 0.0), np.float64)
+        h = C.c_void_p()
+        call("msp_mat_create_box_matfree", ctx.h, int(dim), int(nx), int(ny), int(nz), 1 if lo else 0,
+             1 if hi else 0, _dp(pe), C.byref(h))
+        return cls(ctx, h)
+
     def mat_mult_dense(self, S: "DenseMat", R: "DenseMat"):        # MatMatMult(A, S, MAT_REUSE_MATRIX, &R)
         call("msp_mat_matmult_dense", self.h, S.h, R.h)
 
