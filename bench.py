@@ -63,8 +63,8 @@ def parse():
     p.add_argument("--inner-max-it", type=int, default=20)
     p.add_argument("--outer-max-it", type=int, default=70)
     p.add_argument("--operator", default="csr", choices=["csr", "matfree"],
-                   help="gmres: the assembled CSR (the reference's MatMult, default) or the same operator applied "
-                        "matrix-free (bitwise the same products, no matrix traffic)")
+                   help="the assembled CSR (the reference's MatMult, default) or the same operator applied "
+                        "matrix-free (bitwise the same products, no matrix traffic; gmres, and A_ii for smsm)")
     p.add_argument("--peclet", default=None,
                    help="Px,Py,Pz: the upwind convection-diffusion operator (configs[4]) instead of Poisson")
     a = p.parse_args()
@@ -210,7 +210,8 @@ def main():
                    f"-inner1_ksp_norm_type UNPRECONDITIONED "
                    f"-outer1_ksp_type lsqr -outer1_ksp_convergence_test default -outer1_ksp_lsqr_exact_mat_norm "
                    f"-outer1_ksp_atol 1e-100 -outer1_ksp_max_it {args.outer_max_it} -outer1_ksp_rtol 1e-15 "
-                   f"-outer1_pc_type none -outer1_ksp_norm_type UNPRECONDITIONED -s {args.s}")
+                   f"-outer1_pc_type none -outer1_ksp_norm_type UNPRECONDITIONED -s {args.s}"
+                   + (" -msplit_operator matfree" if args.operator == "matfree" else ""))
         o = Options(kspopts)
         L = block_layout(3, n, n, nz, world, rank, args.peclet)
         blk = GpuBlock(ctx, L, o, comm, prefix="inner1_")

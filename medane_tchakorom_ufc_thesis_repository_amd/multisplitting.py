@@ -38,7 +38,11 @@ class GpuBlock:
         n = layout.nrows
         dim, bx, by, bz = layout.box
         self.peclet = tuple(getattr(layout, "peclet", (0.0, 0.0, 0.0)))
-        self.A = Mat.box_convdiff(ctx, dim, bx, by, bz, False, False, self.peclet)
+        # -msplit_operator matfree: A_ii applied without storage (bitwise the assembled products)
+        if opts is not None and opts.get_string("msplit_operator", "csr") == "matfree":
+            self.A = Mat.box_matfree(ctx, dim, bx, by, bz, False, False, self.peclet)
+        else:
+            self.A = Mat.box_convdiff(ctx, dim, bx, by, bz, False, False, self.peclet)
         row_ids, rowptr, col, val = layout.coupling
         self.A_off = Mat.from_csr_rows(ctx, n, layout.halo_size, row_ids, rowptr, col, val)
         self.halo, self.halo_t = comm.alloc(ctx, layout.halo_size)
