@@ -21,7 +21,7 @@ import math
 import time
 from dataclasses import dataclass, field
 
-from .petsc import LSQR, Context, DenseMat, Mat, Options, Vec
+from .petsc import Context, DenseMat, Mat, Options, Vec
 from .utils import BlockLayout, block_layout, initializeKSP, initializeOuterKSP, inner_solver, updateLocalRHS
 
 

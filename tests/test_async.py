@@ -3,7 +3,6 @@ the C convergence detection against the independent twin (oracle/am_twin.py)
 step by step, the twin's AM replay, and multi-process AM runs of the product
 driver (asynchronous.am_solve) with CPU test-double blocks.  No GPU needed:
 amsg and the detection are host code."""
-import math
 import multiprocessing as mp
 import os
 import sys

@@ -26,7 +26,6 @@ class OracleBlock:
     """CPU test double of multisplitting.GpuBlock (same hooks, oracle arithmetic)."""
 
     def __init__(self, layout, po):
-        from medane_tchakorom_ufc_thesis_repository_amd import utils
         self.po = po
         self.layout = L = layout
         if L.dim == 3:

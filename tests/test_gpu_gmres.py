@@ -10,7 +10,6 @@ against the initial residual; see DESIGN.md "Parity").
 import numpy as np
 import pytest
 
-from medane_tchakorom_ufc_thesis_repository_amd import utils
 from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm
 from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import make_blocks, sm_solve
 from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Mat, Options, Vec

@@ -1,5 +1,4 @@
 """CPU tests of the boundary and the host logic (no compute calls)."""
-import ctypes
 import os
 import subprocess
 
