@@ -134,25 +134,29 @@ def _am_worker(rank, world, port, problem, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("problem", [("am", 3, 8, 8, 16, 0, 5, 1e-6), ("amam_global", 3, 8, 8, 16, 4, 5, 1e-6)])
-def test_am_two_processes_device_transport(problem):
+@pytest.mark.parametrize("world,problem,nbuf", [(2, ("am", 3, 8, 8, 16, 0, 5, 1e-6), "2"),
+                                                (2, ("amam_global", 3, 8, 8, 16, 4, 5, 1e-6), "2"),
+                                                (3, ("amam_global", 3, 8, 8, 18, 4, 5, 1e-6), "1")])
+def test_am_processes_device_transport(world, problem, nbuf, monkeypatch):
     """One process per block, truly asynchronous, planes (and for AMAM-global the
-    R rows) through HBM slots opened by IPC: the detection ends every block in
-    the same phase with one global final residual below the threshold."""
+    R rows, with two or one HBM buffers) through HBM slots opened by IPC: the
+    detection ends every block in the same phase with one global final residual
+    below the threshold."""
+    monkeypatch.setenv("MSPLIT_ABCAST_NBUF", nbuf)       # inherited by the spawned workers
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_am_worker, args=(r, 2, port, problem, q)) for r in range(2)]
+    procs = [ctx.Process(target=_am_worker, args=(r, world, port, problem, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = sorted([q.get(timeout=600) for _ in range(2)])
+    out = sorted([q.get(timeout=600) for _ in range(world)])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(o[5] == "device" for o in out)
-    assert out[0][3] == out[1][3] and out[0][4] == out[1][4]
+    assert all(o[3] == out[0][3] and o[4] == out[0][4] for o in out)
     assert out[0][4] <= 1e-4 * out[0][3]
-    assert out[0][2] == out[1][2]
+    assert all(o[2] == out[0][2] for o in out)
 
 
 def _comm_worker(rank, world, port, q):
