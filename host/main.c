@@ -1,0 +1,156 @@
+/*
+ * main.c -- the reference's multisplitting executables as a C host:
+ *
+ *   msplit_driver <program> -m M -n N [-s S] [-rtol R] [-atol A] [-dim 3 -p P]
+ *                 [-peclet px,py,pz] [-nb B] [-json] [-inner{b}_ksp_* ...] [-outer{b}_ksp_* ...]
+ *
+ * <program>: synchronous-multisplitting,
+ *            synchronous-multisplitting-synchronous-minimization-global,
+ *            asynchronous-multisplitting.
+ * Built with MPI (msplit_driver_mpi, MPICH): one block per rank, each rank on
+ * GPU (rank mod devices); the neighbour exchange, ordered sums and LSQR
+ * partials go through msp_comm -- RCCL (-msplit_transport rccl, the default)
+ * or MPI_Allgather (-msplit_transport host).  Without MPI: -nb blocks in one
+ * process, round-robin on GPU 0.  Output lines follow the reference
+ * (printElapsedTime, printFinalResidualNorm, computeError; utils.c:665-730).
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "msplit_drivers.h"
+
+#ifdef MSD_MPI
+#include <mpi.h>
+
+static void mpi_barrier(void *u) {
+  (void)u;
+  MPI_Barrier(MPI_COMM_WORLD);
+}
+
+static void mpi_bcast(void *u, void *buf, int bytes, int root) {
+  (void)u;
+  MPI_Bcast(buf, bytes, MPI_BYTE, root, MPI_COMM_WORLD);
+}
+
+static int mpi_allgather(void *u, const double *send, double *recv, int64_t count) {
+  (void)u;
+  return MPI_Allgather(send, (int)count, MPI_DOUBLE, recv, (int)count, MPI_DOUBLE, MPI_COMM_WORLD) != MPI_SUCCESS;
+}
+#endif
+
+static int usage(void) {
+  fprintf(stderr, "usage: msplit_driver <synchronous-multisplitting | "
+                  "synchronous-multisplitting-synchronous-minimization-global | asynchronous-multisplitting> "
+                  "-m M -n N [-s S] [-rtol R] [-dim 3 -p P] [-peclet px,py,pz] [-nb B] [-json] ...\n");
+  return 2;
+}
+
+int main(int argc, char **argv) {
+  int world = 1, rank = 0;
+#ifdef MSD_MPI
+  MPI_Init(&argc, &argv);
+  MPI_Comm_size(MPI_COMM_WORLD, &world);
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+#endif
+  if (argc < 2) return usage();
+  const char *prog = argv[1];
+  int kind;
+  if (!strcmp(prog, "synchronous-multisplitting")) kind = 0;
+  else if (!strcmp(prog, "synchronous-multisplitting-synchronous-minimization-global")) kind = 1;
+  else if (!strcmp(prog, "asynchronous-multisplitting")) kind = 2;
+  else return usage();
+  msd_options *o = msd_options_parse(argc - 1, argv + 1);
+  msd_problem p;
+  memset(&p, 0, sizeof(p));
+  p.dim = (int)msd_opt_int(o, NULL, "dim", 2);
+  p.nx = (int32_t)msd_opt_int(o, NULL, "m", 256);
+  p.ny = (int32_t)msd_opt_int(o, NULL, "n", 256);
+  p.nz = p.dim == 3 ? (int32_t)msd_opt_int(o, NULL, "p", p.ny) : 1;
+  p.s = (int)msd_opt_int(o, NULL, "s", 4);
+  p.rtol = msd_opt_real(o, NULL, "rtol", 1e-6);
+  p.atol = msd_opt_real(o, NULL, "atol", 1e-100);
+  p.max_outer = (int)msd_opt_int(o, NULL, "max_outer", 100000);
+  p.nb = world > 1 ? world : (int)msd_opt_int(o, NULL, "nb", 2);
+  p.matfree = !strcmp(msd_opt_str(o, NULL, "msplit_operator", "csr"), "matfree");
+  p.async_host = !strcmp(msd_opt_str(o, NULL, "msplit_async_transport", "device"), "host");
+  const char *pe = msd_opt_str(o, NULL, "peclet", NULL);
+  if (pe && sscanf(pe, "%lf,%lf,%lf", &p.peclet[0], &p.peclet[1], &p.peclet[2]) != 3) return usage();
+  if (msd_opt_int(o, NULL, "npb", 1) != 1) {
+    fprintf(stderr, "-npb must be 1: one GPU (one process) per block\n");
+    return 2;
+  }
+  int ndev = 1;
+  msp_get_device_count(&ndev);
+  msp_ctx *ctx;
+  if (msp_ctx_create(ndev > 0 ? rank % ndev : 0, NULL, &ctx)) {
+    fprintf(stderr, "msp_ctx_create: %s\n", msp_get_last_error());
+    return 1;
+  }
+  msd_transport t;
+  memset(&t, 0, sizeof(t));
+  t.world = world;
+  t.rank = rank;
+#ifdef MSD_MPI
+  t.barrier = mpi_barrier;
+  t.bcast = mpi_bcast;
+  if (world > 1) {
+    int ok = 0;
+    if (!strcmp(msd_opt_str(o, NULL, "msplit_transport", "rccl"), "rccl")) {
+      uint8_t id[MSP_COMM_ID_BYTES];
+      memset(id, 0, sizeof(id));
+      int have = rank == 0 ? msp_comm_get_unique_id(id) == 0 : 0;
+      MPI_Bcast(&have, 1, MPI_INT, 0, MPI_COMM_WORLD);
+      MPI_Bcast(id, MSP_COMM_ID_BYTES, MPI_BYTE, 0, MPI_COMM_WORLD);
+      ok = have && msp_comm_create_rccl(ctx, world, rank, id, &t.comm) == 0;
+      int all = 0;
+      MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+      if (!all) { /* every rank takes the MPI path (e.g. two ranks sharing one GPU) */
+        if (t.comm) msp_comm_destroy(&t.comm);
+        if (rank == 0) fprintf(stderr, "msplit: RCCL communicator unavailable, using MPI_Allgather\n");
+        ok = 0;
+      }
+    }
+    if (!ok && msp_comm_create_host(ctx, world, rank, mpi_allgather, NULL, &t.comm)) {
+      fprintf(stderr, "msp_comm_create_host: %s\n", msp_get_last_error());
+      return 1;
+    }
+  }
+#endif
+  msd_result r;
+  int rc = kind == 0 ? msd_sm_solve(ctx, &p, o, &t, &r)
+           : kind == 1 ? msd_smsm_global_solve(ctx, &p, o, &t, &r)
+                       : msd_am_solve(ctx, &p, o, &t, &r);
+  if (rc == MSP_ERR_ARG_OUTOFRANGE && kind == 2) rc = 0; /* stopped at -max_outer: still report */
+  if (!rc && rank == 0) {
+    if (msd_opt_has(o, NULL, "json")) {
+      printf("{\"program\": \"%s\", \"host\": \"c\", \"ranks\": %d, \"blocks\": %d, ", prog, world, p.nb);
+      if (kind == 2) {
+        printf("\"iterations\": [");
+        for (int i = 0; i < r.nlocal; ++i) printf("%s%d", i ? ", " : "", r.iterations[i]);
+        printf("], ");
+      } else {
+        printf("\"outer_its\": %d, ", r.outer_its);
+      }
+      printf("\"norm0\": %.17g, \"final_norm\": %.17g, \"error\": %.17g, \"elapsed\": %.6f}\n", r.norm0, r.final_norm,
+             r.error, r.elapsed);
+    } else {
+      printf("Elapsed time (iterations):   %f  seconds \n", r.elapsed);
+      if (kind == 2)
+        for (int i = 0; i < r.nlocal; ++i)
+          printf("[ Block rank %d ] Total number of iterations (outer_iterations) = %d \n", i, r.iterations[i]);
+      else
+        printf("Total number of iterations (outer_iterations) = %d \n", r.outer_its);
+      printf("Final residual norm 2 = %e \n", r.final_norm);
+      printf("Erreur  : %e  \n", r.error);
+    }
+  }
+  if (t.comm) msp_comm_destroy(&t.comm);
+  msp_ctx_destroy(&ctx);
+  msd_options_free(o);
+#ifdef MSD_MPI
+  MPI_Finalize();
+#endif
+  return rc ? 1 : 0;
+}

@@ -1,0 +1,80 @@
+"""The C host drivers (host/: the reference's executables in C over the C ABI)
+against the Python host and the oracle: same options, same outer iterations,
+the same final residual to the last bit; one process (-nb blocks) and one
+block per MPI rank (MPICH; both ranks share the one GPU, so the transport is
+MPI_Allgather through msp_comm's host path)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from medane_tchakorom_ufc_thesis_repository_amd import drivers
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST = os.path.join(ROOT, "host")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+
+@pytest.fixture(scope="module")
+def built():
+    subprocess.run(["make", "-s", "-C", HOST], check=True)
+    return HOST
+
+
+def _run(args, mpi=0):
+    exe = os.path.join(HOST, "msplit_driver_mpi" if mpi else "msplit_driver")
+    cmd = ([MPIEXEC, "-n", str(mpi)] if mpi else []) + [exe] + args + ["-json"]
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300).stdout
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+INNER2 = [a for b in (1, 2) for a in (f"-inner{b}_ksp_max_it", "20", f"-inner{b}_ksp_rtol", "1e-20")]
+OUTER2 = [a for b in (1, 2) for a in (f"-outer{b}_ksp_type", "lsqr", f"-outer{b}_ksp_convergence_test", "default",
+                                      f"-outer{b}_ksp_lsqr_exact_mat_norm", f"-outer{b}_ksp_max_it", "70",
+                                      f"-outer{b}_ksp_rtol", "1e-15", f"-outer{b}_ksp_atol", "1e-100")]
+
+
+@pytest.mark.parametrize("prog,args", [
+    ("synchronous-multisplitting", ["-m", "32", "-n", "32", "-rtol", "1e-6"] + INNER2),
+    ("synchronous-multisplitting", ["-dim", "3", "-m", "8", "-n", "8", "-p", "12", "-rtol", "1e-6",
+                                    "-peclet", "0.5,0.25,-0.3"] + INNER2),
+    ("synchronous-multisplitting-synchronous-minimization-global", ["-m", "32", "-n", "32", "-s", "4", "-rtol", "1e-6"]
+     + INNER2 + OUTER2),
+])
+def test_c_host_matches_python_host(ctx, built, prog, args):
+    c = _run([prog] + args)
+    py = drivers.run([prog] + args + ["-json"])
+    assert c["outer_its"] == py["outer_its"]
+    assert c["final_norm"] == py["final_norm"] and c["error"] == py["error"]
+
+
+def test_c_host_am_matches_python_host(ctx, built):
+    inner = [a for b in (1, 2) for a in (f"-inner{b}_ksp_max_it", "5", f"-inner{b}_ksp_rtol", "1e-20")]
+    args = ["asynchronous-multisplitting", "-dim", "3", "-m", "8", "-n", "8", "-p", "8", "-rtol", "1e-6"] + inner
+    c = _run(args)
+    py = drivers.run(args + ["-json"])
+    assert c["iterations"] == py["iterations"]
+    assert c["final_norm"] == py["final_norm"] and c["error"] == py["error"]
+
+
+@pytest.mark.parametrize("prog,args", [
+    ("synchronous-multisplitting", ["-m", "32", "-n", "32", "-rtol", "1e-6"] + INNER2),
+    ("synchronous-multisplitting-synchronous-minimization-global", ["-dim", "3", "-m", "8", "-n", "8", "-p", "8",
+                                                                    "-s", "4", "-rtol", "1e-6"] + INNER2 + OUTER2),
+])
+def test_c_host_mpi_two_ranks_equals_one_process(ctx, built, prog, args):
+    """One block per rank over MPI: bitwise the single-process run (ordered sums)."""
+    one = _run([prog] + args)
+    two = _run([prog] + args, mpi=2)
+    assert two["ranks"] == 2 and two["outer_its"] == one["outer_its"]
+    assert two["final_norm"] == one["final_norm"] and two["error"] == one["error"]
+
+
+def test_c_host_mpi_am_terminates(ctx, built):
+    inner = [a for b in (1, 2) for a in (f"-inner{b}_ksp_max_it", "5", f"-inner{b}_ksp_rtol", "1e-20")]
+    r = _run(["asynchronous-multisplitting", "-dim", "3", "-m", "8", "-n", "8", "-p", "16", "-rtol", "1e-6"] + inner,
+             mpi=2)
+    assert len(r["iterations"]) == 1 and r["final_norm"] < 1e-4 * r["norm0"]
