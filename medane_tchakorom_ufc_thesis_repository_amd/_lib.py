@@ -12,7 +12,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmsplit_hip.so")
+# MSPLIT_LIB: another build of the same library (same-box A/B of two builds, tools/ab_build.sh)
+LIB_PATH = os.environ.get("MSPLIT_LIB") or os.path.join(HERE, "libmsplit_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "msplit.h")
 
 KERNEL_CLASSES = {"spmv": 0, "mdot": 1, "maxpy": 2, "norm": 3, "scale": 4, "other": 5,

@@ -15,15 +15,21 @@
  * the state back once per cycle.  Iterations past a convergence are enqueued
  * speculatively and return at once on the device's stop flag.
  *
- * Per Arnoldi step (VV = basis, T = one work vector, all in HBM):
- *   SpMV      VV(it) = s*T ; VV(it+1) = A (s*T)      (VecNormalize of the
- *             previous vector fused into MatMult: s = 1/||T|| from the device)
- *   MDot      h(0..it) = VV(it+1) . VV(0..it)        (DBR order)
- *   MAXPY     T = VV(it+1) - sum h_j VV(j), and ||T||^2   (one pass)
- *   update    the Hessenberg column, Givens rotation, tests (one lane)
+ * Per Arnoldi step (VV = basis in HBM, sc = its scales on the device):
+ *   SpMV      W = A (sc[it]*VV(it))                  (VecNormalize of the
+ *             previous vector deferred: VV(it) stays as the MAXPY stored it and
+ *             every reader multiplies by sc[it] = 1/||VV(it)||, which rounds each
+ *             element exactly as VecScale would have stored it)
+ *   MDot      h(0..it) = W . sc.VV(0..it)            (DBR order)
+ *   MAXPY     VV(it+1) = W - sum h_j sc[j] VV(j), and ||VV(it+1)||^2   (one pass)
+ *   update    the Hessenberg column, Givens rotation, tests, sc[it+1] (one lane)
+ * W is PETSc's VEC_VV(it+1) before the orthogonalisation; keeping it in its own
+ * vector makes the MAXPY write a different vector than it reads (an in-place
+ * MAXPY measured 5 % slower, same box).
  *
  * Data layout: VV(0..m) are one allocation, (m+1) x stride doubles, stride =
- * n rounded up to 512 (4 KiB aligned); T is separate.
+ * n rounded up to 512 (4 KiB aligned); W is separate.  KSPInitialResidual
+ * writes VV(0).
  */
 #include <math.h>
 #include <stdlib.h>
@@ -38,8 +44,8 @@ struct msp_ksp {
   msp_ksp_opts o;
   int setup;
   int64_t n, stride;
-  double *basis;            /* device: (m+1) * stride */
-  double *tmp;              /* device: the work vector T */
+  double *basis;            /* device: (m+1) * stride, stored unnormalised (scales in g.sc) */
+  double *tmp;              /* device: W = A VV(it) before the orthogonalisation */
   mspi_gmres_dev g;         /* device-resident recurrence state and arrays */
   void *gblock;             /* the single device allocation behind g */
   mspi_gmres_state *hst;    /* pinned host mirror of *g.st */
@@ -162,8 +168,8 @@ int msp_ksp_set_up(msp_ksp *k) {
   if (env) skew = (atoll(env) + 511) / 512 * 512;
   k->stride = (k->n + 511) / 512 * 512 + skew;
   k->hist_cap = k->o.max_it + 2;
-  /* one device block for the recurrence: state, then hh, cc, ss, grs, h, hist */
-  const size_t nd = (size_t)((m + 2) * (m + 1) + 4 * (m + 2) + k->hist_cap);
+  /* one device block for the recurrence: state, then hh, cc, ss, grs, h, sc, hist */
+  const size_t nd = (size_t)((m + 2) * (m + 1) + 5 * (m + 2) + k->hist_cap);
   const size_t st_bytes = (sizeof(mspi_gmres_state) + 63) / 64 * 64;
   int rc = mspi_malloc(k->ctx, (void **)&k->basis, (size_t)(m + 1) * (size_t)k->stride * sizeof(double) + 4096);
   if (!rc) rc = mspi_malloc(k->ctx, (void **)&k->tmp, (size_t)k->stride * sizeof(double) + 4096);
@@ -190,6 +196,8 @@ int msp_ksp_set_up(msp_ksp *k) {
   d += m + 2;
   k->g.h = d;
   d += m + 2;
+  k->g.sc = d;
+  d += m + 2;
   k->g.hist = d;
   k->setup = 1;
   return MSP_SUCCESS;
@@ -197,27 +205,28 @@ int msp_ksp_set_up(msp_ksp *k) {
 
 static double *VV(const msp_ksp *k, int j) { return k->basis + (int64_t)j * k->stride; }
 
-/* One KSPGMRESCycle from its initial residual in T: VecNormalize, up to K
- * Arnoldi steps, BuildSoln(it-1) into x.  Enqueued, no host synchronisation. */
+/* One KSPGMRESCycle from its initial residual in VV(0): VecNormalize (deferred),
+ * up to K Arnoldi steps, BuildSoln(it-1) into x.  Enqueued, no host synchronisation. */
 static int enqueue_cycle(msp_ksp *k, double *x, int K) {
   msp_ctx *c = k->ctx;
   const int *stop = &k->g.st->stop;
+  const double *sc = k->g.sc;
   double *sumsq = &k->g.h[0];
-  int rc = mspi_norm2sq(c, k->tmp, k->n, sumsq);
+  int rc = mspi_norm2sq(c, VV(k, 0), k->n, sumsq);
   if (!rc) rc = mspi_gm_cycle_start(c, k->g, sumsq);
   for (int it = 0; it < K && !rc; ++it) {
-    /* VV(it) = s*T; VV(it+1) = A VV(it)  (KSP_PCApplyBAorAB with PCNONE) */
-    rc = mspi_spmv_scaled(k->A, k->tmp, &k->g.st->scale, VV(k, it), VV(k, it + 1), stop);
-    /* CGS: h = VecMDot(VV(it+1), VV(0..it)); T = VV(it+1) - sum h_j VV(j); ||T||^2 */
-    if (!rc) rc = mspi_mdot_basis(c, VV(k, it + 1), it + 1, k->basis, k->stride, k->n, k->g.h, stop);
-    /* then h(it+1) = ||T||^2 and the Hessenberg column update */
+    /* W = A (sc[it] VV(it))  (KSP_PCApplyBAorAB with PCNONE on the normalised VV(it)) */
+    rc = mspi_spmv_scaled(k->A, VV(k, it), sc + it, NULL, k->tmp, stop);
+    /* CGS: h = VecMDot(W, VV(0..it)); VV(it+1) = W - sum h_j VV(j); ||VV(it+1)||^2 */
+    if (!rc) rc = mspi_mdot_basis(c, k->tmp, it + 1, k->basis, k->stride, sc, k->n, k->g.h, stop);
+    /* then h(it+1) = ||VV(it+1)||^2, sc[it+1] and the Hessenberg column update */
     if (!rc)
-      rc = mspi_maxpy_norm_update(c, VV(k, it + 1), k->tmp, it + 1, k->basis, k->stride, k->n, k->g, it,
+      rc = mspi_maxpy_norm_update(c, k->tmp, VV(k, it + 1), it + 1, k->basis, k->stride, sc, k->n, k->g, it,
                                   k->o.restart, stop);
   }
   /* KSPGMRESBuildSoln: back-solve (one lane), then x += sum nrs_j VV(j) */
   if (!rc) rc = mspi_gm_build(c, k->g);
-  if (!rc) rc = mspi_maxpy_accum_basis(c, x, &k->g.st->nbuild, k->basis, k->stride, k->n, k->g.grs, K);
+  if (!rc) rc = mspi_maxpy_accum_basis(c, x, &k->g.st->nbuild, k->basis, k->stride, sc, k->n, k->g.grs, K);
   return rc;
 }
 
@@ -271,9 +280,9 @@ int msp_ksp_solve(msp_ksp *k, const msp_vec *b, msp_vec *x) {
 
   int cycle_zero_guess = guess_zero, itcount = 0, its = 0, reason = 0;
   while (!reason) {
-    /* KSPInitialResidual: T = b - A x (VecCopy + VecAXPY(-1)), or b for a zero guess */
-    if (!cycle_zero_guess) rc = mspi_residual(k->A, b->d, x->d, k->tmp);
-    else rc = mspi_copy(c, k->tmp, b->d, k->n);
+    /* KSPInitialResidual: VV(0) = b - A x (VecCopy + VecAXPY(-1)), or b for a zero guess */
+    if (!cycle_zero_guess) rc = mspi_residual(k->A, b->d, x->d, VV(k, 0));
+    else rc = mspi_copy(c, VV(k, 0), b->d, k->n);
     if (rc) return rc;
     int K = k->o.max_it - its;
     if (K > k->o.restart) K = k->o.restart;

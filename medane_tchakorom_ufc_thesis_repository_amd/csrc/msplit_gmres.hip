@@ -49,7 +49,8 @@ __device__ inline void converged(const mspi_gmres_dev& g, int n, double rnorm) {
   else if (rnorm >= st->divtol * st->rnorm0) st->reason = MSP_DIVERGED_DTOL;
 }
 
-// Start of KSPGMRESCycle, after VecNorm(VV(0)) (the scale is applied by the first SpMV).
+// Start of KSPGMRESCycle, after VecNorm(VV(0)).  VecNormalize is deferred: VV(0)
+// stays as stored and sc[0] = 1/||VV(0)|| multiplies every read of it.
 __global__ void k_cycle_start(mspi_gmres_dev g, const double* __restrict__ sumsq) {
   mspi_gmres_state* st = g.st;
   st->it = 0;
@@ -57,6 +58,7 @@ __global__ void k_cycle_start(mspi_gmres_dev g, const double* __restrict__ sumsq
   st->skip_build = 0;
   const double res = sqrt(*sumsq);
   st->scale = (res != 0.0 && !bad(res)) ? 1.0 / res : 1.0;
+  g.sc[0] = st->scale;
   if (bad(res)) {  // KSPCheckNorm: return
     st->reason = MSP_DIVERGED_NANORINF;
     st->stop = st->skip_build = 1;
@@ -130,7 +132,8 @@ __global__ void k_iter_update(mspi_gmres_dev g) {
       st->stop = st->skip_build = 1;
       return;
     }
-    st->scale = (tt != 0.0) ? 1.0 / tt : 1.0;  // VecNormalize of VV(it+1), applied by the next SpMV
+    st->scale = (tt != 0.0) ? 1.0 / tt : 1.0;  // VecNormalize of VV(it+1), deferred to its readers
+    g.sc[it + 1] = st->scale;
     HHD(it + 1, it) = tt;
     double hapbnd = fabs(tt / g.grs[it]);
     if (hapbnd > st->haptol) hapbnd = st->haptol;
@@ -226,7 +229,8 @@ __global__ __launch_bounds__(kUT) void k_norm_update(mspi_gmres_dev g, const dou
         ncol = it + 1;
         done = true;
       } else {
-        st->scale = (tt != 0.0) ? 1.0 / tt : 1.0;
+        st->scale = (tt != 0.0) ? 1.0 / tt : 1.0;  // VecNormalize of VV(it+1), deferred to its readers
+        g.sc[it + 1] = st->scale;
         hh[it + 1] = tt;
         double hapbnd = fabs(tt / g.grs[it]);
         if (hapbnd > st->haptol) hapbnd = st->haptol;

@@ -102,7 +102,7 @@ typedef struct {
   int32_t guess_zero;  /* the solve's original zero-guess flag (KSPConvergedDefault n == 0) */
   int32_t m, max_it, uirnorm, hist_cap;
   double res, rnorm, rnorm0, ttol, gm_rnorm0;
-  double scale;        /* VecNormalize factor still to apply to the newest vector (fused into SpMV) */
+  double scale;        /* VecNormalize factor of the newest vector (also kept in sc[it]) */
   double bnorm;        /* ||b|| for the n == 0 test with a nonzero guess and no UIRNorm */
   double rtol, abstol, divtol, haptol, breakdowntol;
 } mspi_gmres_state;
@@ -112,6 +112,7 @@ typedef struct {
   double *hh;           /* (m+2) x (m+1), HH(a,b) = hh[b*(m+2)+a] */
   double *cc, *ss, *grs; /* m+2 each */
   double *h;            /* m+2: MDot results h(0..it), then ||w||^2 at h(it+1) */
+  double *sc;           /* m+2: deferred VecNormalize, VV(j) = stored VV(j) * sc[j] */
   double *hist;         /* hist_cap */
 } mspi_gmres_dev;
 
@@ -123,15 +124,16 @@ int mspi_gm_build(msp_ctx *ctx, mspi_gmres_dev g);
 int mspi_gm_norm_update(msp_ctx *ctx, mspi_gmres_dev g, const double *partial, int64_t nchunks, int m);
 /* CGS VecMAXPY + ||w||^2 partials, then mspi_gm_norm_update (h(it+1) = ||w||^2) */
 int mspi_maxpy_norm_update(msp_ctx *ctx, const double *win, double *wout, int nv, const double *base, int64_t stride,
-                           int64_t n, mspi_gmres_dev g, int it, int m, const int *stop);
-/* data-path pieces with a stop flag; basis = VV(j) at base + j*stride */
+                           const double *scale, int64_t n, mspi_gmres_dev g, int it, int m, const int *stop);
+/* data-path pieces with a stop flag; basis = VV(j) at base + j*stride, its value
+   VV(j)[i] * scale[j] when scale (device) is not NULL */
 int mspi_spmv_scaled(msp_mat *A, const double *x, const double *sdev, double *vout, double *y, const int *stop);
-int mspi_mdot_basis(msp_ctx *ctx, const double *w, int nv, const double *base, int64_t stride, int64_t n,
-                    double *out_dev, const int *stop);
+int mspi_mdot_basis(msp_ctx *ctx, const double *w, int nv, const double *base, int64_t stride, const double *scale,
+                    int64_t n, double *out_dev, const int *stop);
 int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv, const double *base, int64_t stride,
-                          int64_t n, const double *alpha_dev, double *sumsq_dev, const int *stop);
-int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const double *base, int64_t stride, int64_t n,
-                           const double *coef_dev, int nv_expected);
+                          const double *scale, int64_t n, const double *alpha_dev, double *sumsq_dev, const int *stop);
+int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const double *base, int64_t stride,
+                           const double *scale, int64_t n, const double *coef_dev, int nv_expected);
 int mspi_h2d_async(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 /* ---- HBM mailboxes shared between processes (msplit_ipc.hip) ---- */

@@ -11,11 +11,14 @@
 enum { MSK_SET = 0, MSK_COPY, MSK_SCALE, MSK_AXPY, MSK_AYPX, MSK_WAXPY_P1, MSK_WAXPY_M1, MSK_WAXPY };
 
 // A set of vectors: an explicit table (up to 32), or a strided basis
-// V_j = base + j*stride (any count) when base != nullptr.
+// V_j = base + j*stride (any count) when base != nullptr.  scale != nullptr:
+// vector j is stored unnormalised and its value is V_j[i] * scale[j] (device
+// array), the rounding VecScale would have stored -- a deferred VecNormalize.
 struct Vecs {
   const double* p[MSK_MAX_GROUP];
   const double* base;
   int64_t stride;
+  const double* scale;
 };
 struct Coefs {
   double a[MSK_MAX_GROUP];
@@ -38,7 +41,8 @@ enum {
   MSK_TUNE_MAXPY_TEMPORAL_ST = 64,  // default-policy store of w in MAXPY
   MSK_TUNE_GM_UNFUSED = 128,        // separate ||w||^2 stage-2 and one-lane Hessenberg update launches
   MSK_TUNE_MAXPY_HALVES = 256,      // MAXPY: each chunk in two halves (fewer registers, more waves)
-  MSK_TUNE_SPMV_ZCHUNK = 512        // SpMV: XCD x takes the x-th eighth of the row blocks, in order
+  MSK_TUNE_SPMV_ZCHUNK = 512,       // SpMV: XCD x takes the x-th eighth of the row blocks, in order
+  MSK_TUNE_MDOT_SINGLE = 1024       // MDot: one vector's loads at a time (before grouped loads)
 };
 
 extern "C" {
@@ -54,7 +58,7 @@ int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, 
 int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, const int* nvdev, const Coefs* A,
                     const double* adev, int negate, int64_t n, int accum, double* partial, const int* stop,
                     hipStream_t s);
-// mode MULT: y = A x; RESID: y = b - A x; SCALED: sc = *sdev, vout = sc*x (own rows), y = A (sc*x).
+// mode MULT: y = A x; RESID: y = b - A x; SCALED: sc = *sdev, y = A (sc*x) and, when vout != null, vout = sc*x.
 // plane > 0: the operator is a stencil with this many rows per plane (XCD-aware schedule, MSK_TUNE_SPMV_XCD)
 int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
              const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,

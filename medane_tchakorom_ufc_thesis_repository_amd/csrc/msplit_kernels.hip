@@ -42,6 +42,9 @@ __device__ __forceinline__ int4 ld_nt(const int4* p) {
 __device__ __forceinline__ const double* vec_at(const Vecs& V, int j) {
   return V.base ? V.base + (int64_t)j * V.stride : V.p[j];
 }
+// deferred VecNormalize: element i of vector j is fl(V_j[i] * scale[j]); x * 1.0
+// is exact for every double, so unscaled sets multiply by 1.0 (wave-uniform load)
+__device__ __forceinline__ double vec_scale(const Vecs& V, int j) { return V.scale ? V.scale[j] : 1.0; }
 
 __device__ __forceinline__ double wave_butterfly(double v) {
   // v[l] <- v[l] + v[l ^ off], off = 32..1: every lane ends with the same sum.
@@ -60,6 +63,55 @@ __device__ __forceinline__ double wave_butterfly(double v) {
 // MALL, so caching it only evicts lines others still need; +8-16 % per kernel,
 // +7.7 % per GMRES step on 256^3, same-box A/B); bit 2 = non-temporal store
 // of w in MAXPY.  Results are identical.
+// G vectors of a full chunk at once: all G*8 loads are issued before the first
+// product (4 x 32 KiB in flight per workgroup instead of one vector's 32 KiB),
+// then G independent accumulations and butterflies.  Per vector the sum is the
+// same sequence as one at a time.
+template <int G, int VAR>
+__device__ __forceinline__ void dot_group_full(const double (&wr)[2 * kIters], const Vecs& V, int64_t base, int rev,
+                                               int nv, int g, double (*red)[4], int lane, int wv) {
+  double2 q[G][kIters];
+  double sv[G];
+  int vv[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    // load order only (each dot is independent): newest vector first when rev
+    vv[u] = rev ? nv - 1 - (g + u) : g + u;
+    const double* __restrict__ y = vec_at(V, vv[u]);
+    sv[u] = vec_scale(V, vv[u]);
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double2* pq = reinterpret_cast<const double2*>(y + base + j * (2 * kT));
+      q[u][j] = (VAR & 1) ? ld_nt(pq) : *pq;
+    }
+  }
+  double acc[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    acc[u] = 0.0;
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      acc[u] = acc[u] + wr[2 * j] * (q[u][j].x * sv[u]);
+      acc[u] = acc[u] + wr[2 * j + 1] * (q[u][j].y * sv[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    acc[u] = wave_butterfly(acc[u]);
+    if (lane == 0) red[vv[u]][wv] = acc[u];
+  }
+}
+
+// Stage 1: workgroup c reduces chunk c of every vector: lane t accumulates its
+// elements base + j*512 + 2t, +1 (j = 0..7) in order, wave butterfly, then
+// (w0 + w1) + (w2 + w3).  partial[v * nchunks + c].  w stays in registers and
+// each vector streams 32 KiB contiguous per workgroup.
+// VAR: bit 0 = non-temporal loads of the basis vectors (the default: each
+// vector streams through once per kernel and is far larger than the 256 MiB
+// MALL, so caching it only evicts lines others still need; +8-16 % per kernel,
+// +7.7 % per GMRES step on 256^3, same-box A/B); bit 2 = non-temporal store
+// of w in MAXPY; bit 4 = vectors one at a time in MDot (A/B of the grouped loads).
+// Results are identical.
 template <int NV, bool SELF, int VAR>
 __device__ __forceinline__ void dot_chunk(const double* __restrict__ w, const Vecs& V, int64_t n,
                                           double* __restrict__ partial, int64_t nchunks, int rev, int64_t c,
@@ -83,6 +135,15 @@ __device__ __forceinline__ void dot_chunk(const double* __restrict__ w, const Ve
       wr[2 * j + 1] = e + 1 < n ? w[e + 1] : 0.0;
     }
   }
+  if (!SELF && full && (VAR & 16) == 0) {
+    constexpr int G = NV >= 4 ? 4 : NV;
+    int g = 0;
+#pragma unroll 1
+    for (; g + G <= NV; g += G) dot_group_full<G, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
+    if constexpr (NV % G == 3) dot_group_full<3, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
+    if constexpr (NV % G == 2) dot_group_full<2, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
+    if constexpr (NV % G == 1) dot_group_full<1, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
+  } else {
 #pragma unroll
   for (int vi = 0; vi < NV; ++vi) {
     // load order only (each dot is independent): newest vector first when rev,
@@ -103,6 +164,7 @@ __device__ __forceinline__ void dot_chunk(const double* __restrict__ w, const Ve
       }
     } else {
       const double* __restrict__ y = vec_at(V, v);
+      const double sv = vec_scale(V, v);
       if (full) {
         double2 q[kIters];
 #pragma unroll
@@ -112,20 +174,21 @@ __device__ __forceinline__ void dot_chunk(const double* __restrict__ w, const Ve
         }
 #pragma unroll
         for (int j = 0; j < kIters; ++j) {
-          acc = acc + wr[2 * j] * q[j].x;
-          acc = acc + wr[2 * j + 1] * q[j].y;
+          acc = acc + wr[2 * j] * (q[j].x * sv);
+          acc = acc + wr[2 * j + 1] * (q[j].y * sv);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < kIters; ++j) {
           const int64_t e = base + j * (2 * kT);
-          if (e < n) acc = acc + wr[2 * j] * y[e];
-          if (e + 1 < n) acc = acc + wr[2 * j + 1] * y[e + 1];
+          if (e < n) acc = acc + wr[2 * j] * (y[e] * sv);
+          if (e + 1 < n) acc = acc + wr[2 * j + 1] * (y[e + 1] * sv);
         }
       }
     }
     acc = wave_butterfly(acc);
     if (lane == 0) red[v][wv] = acc;
+  }
   }
   __syncthreads();
   if (t < NV) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
@@ -189,13 +252,14 @@ template <int G, bool FULL, int VAR, int J0, int JN>
 __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs& V, const Coefs& A,
                                             const double* __restrict__ adev, int negate, int g, int64_t base,
                                             int64_t n) {
-  double a[G];
+  double a[G], sv[G];
   const double* vp[G];
 #pragma unroll
   for (int q = 0; q < G; ++q) {  // wave-uniform: scalar loads from the kernel arguments / adev
     const double aq = adev ? adev[g + q] : A.a[g + q];
     a[q] = negate ? -aq : aq;
     vp[q] = vec_at(V, g + q);
+    sv[q] = vec_scale(V, g + q);
   }
 #pragma unroll
   for (int j = J0; j < J0 + JN; ++j) {
@@ -206,11 +270,11 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs&
       if (FULL) {
         const double2* pv = reinterpret_cast<const double2*>(vp[q] + e);
         const double2 v = (VAR & 1) ? ld_nt(pv) : *pv;
-        p0[q] = v.x;
-        p1[q] = v.y;
+        p0[q] = v.x * sv[q];
+        p1[q] = v.y * sv[q];
       } else {
-        p0[q] = e < n ? vp[q][e] : 0.0;
-        p1[q] = e + 1 < n ? vp[q][e + 1] : 0.0;
+        p0[q] = e < n ? vp[q][e] * sv[q] : 0.0;
+        p1[q] = e + 1 < n ? vp[q][e + 1] * sv[q] : 0.0;
       }
     }
     const double s0 = group_sum<G>(a, p0), s1 = group_sum<G>(a, p1);
@@ -337,8 +401,9 @@ __global__ __launch_bounds__(kT) void k_maxpy_chunk(const double* win, double* w
 // each lane keeps 8 gathers in flight.
 //   MULT: y = A x    RESID: y = b - A x
 //   SCALED (VecNormalize fused into the next MatMult): sc = *sdev,
-//     vout[r] = x[r]*sc and y = A (sc*x), each product val*(x*sc) rounded
-//     exactly as VecScale followed by MatMult.
+//     y = A (sc*x), each product val*(x*sc) rounded exactly as VecScale
+//     followed by MatMult; vout[r] = x[r]*sc when vout != null (GMRES keeps
+//     its basis unnormalised with the scales beside it and passes null).
 // XCD-aware order (stencil operators whose plane is a multiple of 8 row
 // blocks): workgroups are dealt round-robin over the 8 XCDs, so XCD x runs
 // launches x, x+8, ...  Each plane's row blocks are cut into groups of gb
@@ -432,7 +497,7 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
     k0 = rowptr[r];
     k1 = rowptr[r + 1];
     if (MODE == MSK_SPMV_RESID) bb = b[r];
-    if (MODE == MSK_SPMV_SCALED) vout[r] = x[r] * sc;
+    if (MODE == MSK_SPMV_SCALED && vout) vout[r] = x[r] * sc;
   }
   stage_csr_block<NT, SU>(t, n2, n4, v2, c4, sval, scol);
   __syncthreads();
@@ -519,7 +584,7 @@ __global__ __launch_bounds__(kT) void k_spmv_direct(int32_t nrows, const int32_t
     if (MODE == MSK_SPMV_SCALED) xv = xv * sc;
     s = s + val[k] * xv;
   }
-  if (MODE == MSK_SPMV_SCALED) vout[r] = x[r] * sc;
+  if (MODE == MSK_SPMV_SCALED && vout) vout[r] = x[r] * sc;
   y[r] = MODE == MSK_SPMV_RESID ? b[r] - s : s;
 }
 
@@ -673,10 +738,10 @@ __global__ __launch_bounds__(kT) void k_stencil_spmv(int dim, int32_t nx, int32_
       out[1] = bb.y - out[1];
     }
     *reinterpret_cast<double2*>(y + l0) = make_double2(out[0], out[1]);
-    if (MODE == MSK_SPMV_SCALED) *reinterpret_cast<double2*>(vout + l0) = make_double2(vo[0], vo[1]);
+    if (MODE == MSK_SPMV_SCALED && vout) *reinterpret_cast<double2*>(vout + l0) = make_double2(vo[0], vo[1]);
   } else {
     y[l0] = MODE == MSK_SPMV_RESID ? b[l0] - out[0] : out[0];
-    if (MODE == MSK_SPMV_SCALED) vout[l0] = vo[0];
+    if (MODE == MSK_SPMV_SCALED && vout) vout[l0] = vo[0];
   }
 }
 
@@ -755,10 +820,12 @@ static void dot1_dispatch(int nv, const double* w, const Vecs& V, int64_t n, dou
 extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
                               int self, const int* stop, hipStream_t s) {
   if (nchunks <= 0) return 0;
-  const int var = vec_var();
+  const int var = vec_var() | ((g_tuning & MSK_TUNE_MDOT_SINGLE) ? 16 : 0);
   if (self)
     k_dot_stage1<1, true, 0><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, *V, n, partial, nchunks, stop, 0);
-  else if (var) dot1_dispatch<1, 1>(nv, w, *V, n, partial, nchunks, stop, s);
+  else if (var == 1) dot1_dispatch<1, 1>(nv, w, *V, n, partial, nchunks, stop, s);
+  else if (var == 17) dot1_dispatch<1, 17>(nv, w, *V, n, partial, nchunks, stop, s);
+  else if (var == 16) dot1_dispatch<1, 16>(nv, w, *V, n, partial, nchunks, stop, s);
   else dot1_dispatch<1, 0>(nv, w, *V, n, partial, nchunks, stop, s);
   return (int)hipGetLastError();
 }

@@ -258,8 +258,8 @@ extern "C" int mspi_host_unregister(void* p) {
   return MSP_SUCCESS;
 }
 
-extern "C" int mspi_mdot_basis(msp_ctx* c, const double* w, int nv, const double* base, int64_t stride, int64_t n,
-                               double* out_dev, const int* stop) {
+extern "C" int mspi_mdot_basis(msp_ctx* c, const double* w, int nv, const double* base, int64_t stride,
+                               const double* scale, int64_t n, double* out_dev, const int* stop) {
   if (nv <= 0) return MSP_SUCCESS;
   const int64_t nch = nchunks_of(n);
   if (nch == 0) {
@@ -272,6 +272,7 @@ extern "C" int mspi_mdot_basis(msp_ctx* c, const double* w, int nv, const double
     Vecs vg = {};
     vg.base = base + (int64_t)g0 * stride;
     vg.stride = stride;
+    vg.scale = scale ? scale + g0 : nullptr;
     KCHK(msk_dot_stage1(w, &vg, g, n, c->partial, nch, 0, stop, c->stream));
     KCHK(msk_dot_stage2(c->partial, nch, g, out_dev + g0, stop, c->stream));
   }
@@ -279,8 +280,8 @@ extern "C" int mspi_mdot_basis(msp_ctx* c, const double* w, int nv, const double
 }
 
 extern "C" int mspi_maxpy_norm_basis(msp_ctx* c, const double* win, double* wout, int nv, const double* base,
-                                     int64_t stride, int64_t n, const double* alpha_dev, double* sumsq_dev,
-                                     const int* stop) {
+                                     int64_t stride, const double* scale, int64_t n, const double* alpha_dev,
+                                     double* sumsq_dev, const int* stop) {
   const int64_t nch = nchunks_of(n);
   if (nch == 0 || nv <= 0) {
     mspi_set_error(MSP_ERR_ARG_SIZ, "maxpy_norm on an empty basis");
@@ -290,6 +291,7 @@ extern "C" int mspi_maxpy_norm_basis(msp_ctx* c, const double* win, double* wout
   Vecs vg = {};
   vg.base = base;
   vg.stride = stride;
+  vg.scale = scale;
   Coefs cf = {};
   KCHK(msk_maxpy_chunk(win, wout, &vg, nv, nullptr, &cf, alpha_dev, 1, n, 0, c->partial, stop, c->stream));
   KCHK(msk_dot_stage2(c->partial, nch, 1, sumsq_dev, stop, c->stream));
@@ -300,9 +302,10 @@ extern "C" int mspi_maxpy_norm_basis(msp_ctx* c, const double* win, double* wout
 // runs the Hessenberg update (k_norm_update).  MSK_TUNE_GM_UNFUSED: the separate
 // stage-2 and one-lane update launches (A/B).
 extern "C" int mspi_maxpy_norm_update(msp_ctx* c, const double* win, double* wout, int nv, const double* base,
-                                      int64_t stride, int64_t n, mspi_gmres_dev g, int it, int m, const int* stop) {
+                                      int64_t stride, const double* scale, int64_t n, mspi_gmres_dev g, int it, int m,
+                                      const int* stop) {
   if (msk_get_tuning() & MSK_TUNE_GM_UNFUSED) {
-    int rc = mspi_maxpy_norm_basis(c, win, wout, nv, base, stride, n, g.h, g.h + it + 1, stop);
+    int rc = mspi_maxpy_norm_basis(c, win, wout, nv, base, stride, scale, n, g.h, g.h + it + 1, stop);
     return rc ? rc : mspi_gm_iter_update(c, g);
   }
   const int64_t nch = nchunks_of(n);
@@ -315,6 +318,7 @@ extern "C" int mspi_maxpy_norm_update(msp_ctx* c, const double* win, double* wou
     Vecs vg = {};
     vg.base = base;
     vg.stride = stride;
+    vg.scale = scale;
     Coefs cf = {};
     KCHK(msk_maxpy_chunk(win, wout, &vg, nv, nullptr, &cf, g.h, 1, n, 0, c->partial, stop, c->stream));
   }
@@ -322,13 +326,14 @@ extern "C" int mspi_maxpy_norm_update(msp_ctx* c, const double* win, double* wou
 }
 
 extern "C" int mspi_maxpy_accum_basis(msp_ctx* c, double* x, const int* nvdev, const double* base, int64_t stride,
-                                      int64_t n, const double* coef_dev, int nv_expected) {
+                                      const double* scale, int64_t n, const double* coef_dev, int nv_expected) {
   if (n <= 0) return MSP_SUCCESS;
   // BuildSoln: the vector count lives on the device; bytes use the host's expectation
   KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n * (nv_expected + 2));
   Vecs vg = {};
   vg.base = base;
   vg.stride = stride;
+  vg.scale = scale;
   Coefs cf = {};
   KCHK(msk_maxpy_chunk(x, x, &vg, 0, nvdev, &cf, coef_dev, 0, n, 1, nullptr, nullptr, c->stream));
   return MSP_SUCCESS;
@@ -674,12 +679,12 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
     return MSP_ERR_SUP;
   }
   if (A->matfree) {
-    KTimer kt(c, MSP_KERNEL_SPMV, 8.0 * (double)A->ncols + 16.0 * (double)A->nrows);
+    KTimer kt(c, MSP_KERNEL_SPMV, 8.0 * (double)A->ncols + (vout ? 16.0 : 8.0) * (double)A->nrows);
     KCHK(msk_stencil_spmv(A->dim, A->bx, A->by, A->bz, A->nrows, A->lo, A->hi, &A->cf, x, nullptr, y,
                           MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
     return MSP_SUCCESS;
   }
-  KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, false) + 8.0 * (double)A->nrows);
+  KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, false) + (vout ? 8.0 * (double)A->nrows : 0.0));
   KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, nullptr, y, A->lds_cap, MSK_SPMV_SCALED, sdev, vout, stop,
                 A->plane, c->stream));
   return MSP_SUCCESS;
