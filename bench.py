@@ -37,7 +37,8 @@ KERNEL_NAMES = {"spmv": "k_spmv_lds (CSR MatMult/MatResidual)", "mdot": "k_dot_s
                 "maxpy": "k_maxpy (VecMAXPY, CGS update + BuildSoln)", "norm": "k_dot_stage1<1,self>+stage2 (VecNorm)",
                 "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy",
                 "spmm": "k_spmm (MatMatMult R = A S)", "dgemv": "k_dense_gemv (LSQR R v - alpha u + norm; S alpha)",
-                "dgemvt": "k_scaled_dot (LSQR scale + R^T u)"}
+                "dgemvt": "k_scaled_dot (LSQR scale + R^T u)",
+                "spmvdot": "k_spmv_mdot (GMRES MatMult fused with VecMDot stage 1)"}
 
 
 def parse():

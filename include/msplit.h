@@ -65,7 +65,8 @@ extern "C" {
 #define MSP_KERNEL_SPMM 6       /* MatMatMult(AIJ, DENSE): R = A S */
 #define MSP_KERNEL_DGEMV 7      /* dense MatMult (LSQR's R v - alpha u, and x = S alpha) */
 #define MSP_KERNEL_DGEMVT 8     /* dense MatMultTranspose (LSQR's R^T u), both DBR stages */
-#define MSP_KERNEL_NCLASSES 9
+#define MSP_KERNEL_SPMVDOT 9     /* GMRES MatMult fused with the VecMDot that follows (stage 1) */
+#define MSP_KERNEL_NCLASSES 10
 
 typedef struct msp_ctx msp_ctx;
 typedef struct msp_mat msp_mat;

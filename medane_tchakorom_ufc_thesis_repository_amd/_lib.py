@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("MSPLIT_LIB") or os.path.join(HERE, "libmsplit_hip.so"
 HEADER = os.path.join(os.path.dirname(HERE), "include", "msplit.h")
 
 KERNEL_CLASSES = {"spmv": 0, "mdot": 1, "maxpy": 2, "norm": 3, "scale": 4, "other": 5,
-                  "spmm": 6, "dgemv": 7, "dgemvt": 8}
+                  "spmm": 6, "dgemv": 7, "dgemvt": 8, "spmvdot": 9}
 
 REASONS = {
     0: "CONVERGED_ITERATING", 1: "CONVERGED_RTOL_NORMAL", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",

@@ -215,10 +215,14 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
   int rc = mspi_norm2sq(c, VV(k, 0), k->n, sumsq);
   if (!rc) rc = mspi_gm_cycle_start(c, k->g, sumsq);
   for (int it = 0; it < K && !rc; ++it) {
-    /* W = A (sc[it] VV(it))  (KSP_PCApplyBAorAB with PCNONE on the normalised VV(it)) */
-    rc = mspi_spmv_scaled(k->A, VV(k, it), sc + it, NULL, k->tmp, stop);
-    /* CGS: h = VecMDot(W, VV(0..it)); VV(it+1) = W - sum h_j VV(j); ||VV(it+1)||^2 */
-    if (!rc) rc = mspi_mdot_basis(c, k->tmp, it + 1, k->basis, k->stride, sc, k->n, k->g.h, stop);
+    /* W = A (sc[it] VV(it))  (KSP_PCApplyBAorAB with PCNONE on the normalised VV(it)),
+     * CGS: h = VecMDot(W, VV(0..it)) -- one fused launch where the operator allows */
+    rc = mspi_spmv_mdot(k->A, VV(k, it), sc + it, k->tmp, it + 1, k->basis, k->stride, sc, k->g.h, stop);
+    if (rc == MSP_ERR_SUP) {
+      rc = mspi_spmv_scaled(k->A, VV(k, it), sc + it, NULL, k->tmp, stop);
+      if (!rc) rc = mspi_mdot_basis(c, k->tmp, it + 1, k->basis, k->stride, sc, k->n, k->g.h, stop);
+    }
+    /* then VV(it+1) = W - sum h_j VV(j); ||VV(it+1)||^2 */
     /* then h(it+1) = ||VV(it+1)||^2, sc[it+1] and the Hessenberg column update */
     if (!rc)
       rc = mspi_maxpy_norm_update(c, k->tmp, VV(k, it + 1), it + 1, k->basis, k->stride, sc, k->n, k->g, it,

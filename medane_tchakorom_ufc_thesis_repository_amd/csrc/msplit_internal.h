@@ -128,6 +128,8 @@ int mspi_maxpy_norm_update(msp_ctx *ctx, const double *win, double *wout, int nv
 /* data-path pieces with a stop flag; basis = VV(j) at base + j*stride, its value
    VV(j)[i] * scale[j] when scale (device) is not NULL */
 int mspi_spmv_scaled(msp_mat *A, const double *x, const double *sdev, double *vout, double *y, const int *stop);
+int mspi_spmv_mdot(msp_mat *A, const double *x, const double *sdev, double *y, int nv, const double *base,
+                   int64_t stride, const double *scale, double *out_dev, const int *stop);
 int mspi_mdot_basis(msp_ctx *ctx, const double *w, int nv, const double *base, int64_t stride, const double *scale,
                     int64_t n, double *out_dev, const int *stop);
 int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv, const double *base, int64_t stride,

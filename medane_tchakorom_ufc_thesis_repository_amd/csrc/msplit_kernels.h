@@ -42,7 +42,9 @@ enum {
   MSK_TUNE_GM_UNFUSED = 128,        // separate ||w||^2 stage-2 and one-lane Hessenberg update launches
   MSK_TUNE_MAXPY_HALVES = 256,      // MAXPY: each chunk in two halves (fewer registers, more waves)
   MSK_TUNE_SPMV_ZCHUNK = 512,       // SpMV: XCD x takes the x-th eighth of the row blocks, in order
-  MSK_TUNE_MDOT_SINGLE = 1024       // MDot: one vector's loads at a time (before grouped loads)
+  MSK_TUNE_MDOT_SINGLE = 1024,      // MDot: one vector's loads at a time (before grouped loads)
+  MSK_TUNE_GM_SPMV_MDOT = 2048,     // GMRES: MatMult fused with the VecMDot that follows (k_spmv_mdot)
+  MSK_TUNE_SPMV_MDOT_G2 = 4096      // k_spmv_mdot: two basis vectors per load group instead of four
 };
 
 extern "C" {
@@ -63,6 +65,11 @@ int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, cons
 int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
              const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
              const int* stop, int64_t plane, hipStream_t s);
+// GMRES: y = A (sc*x), sc = *sdev, fused with the DBR stage 1 of y . V_v (v < nv <= 32) into partial;
+// lds_cap: LDS entries for the col/val slice of any 512-row sub-block (> 0)
+int msk_spmv_mdot(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
+                  const double* sdev, double* y, int32_t lds_cap, const Vecs* V, int nv, double* partial,
+                  int64_t nchunks, const int* stop, hipStream_t s);
 // R[:, 0:nc] = A S[:, 0:nc], column-major S (lds) and R (ldr); needs lds_cap > 0
 int msk_spmm(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* S,
              int64_t lds, int nc, double* R, int64_t ldr, int32_t lds_cap, hipStream_t s);

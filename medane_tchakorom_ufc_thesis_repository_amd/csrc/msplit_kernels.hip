@@ -521,6 +521,125 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
   }
 }
 
+// GMRES step, MatMult fused with the VecMDot that follows it:
+//   W = A (sc*X)  and  partial[v][c] = DBR chunk c of W . (scale_v V_v), v < nv.
+// Workgroup c owns DBR chunk c (rows [4096c, 4096c+4096)) and runs it as 8
+// sub-blocks of 512 rows; in sub-block j lane t computes rows j*512 + 2t and
+// 2t+1 -- exactly the elements the DBR order gives lane t -- so W never leaves
+// the registers between the two phases: MDot reads neither W nor (from HBM)
+// V(it) = X, which this workgroup has just gathered.  Each row is summed as in
+// k_spmv_lds8 (MatMult_SeqAIJ order, val*(x*sc)); each dot as in dot_chunk.
+// Needs every 512-row sub-block's col/val slice to fit lds_cap entries.
+template <int VAR>
+__device__ __forceinline__ void row_pair_sums(int32_t kA0, int32_t kA1, int32_t kB1, const double* sval,
+                                              const int32_t* scol, int32_t s2, int32_t s4,
+                                              const double* __restrict__ x, double sc, double& wa, double& wb) {
+  double sa = 0.0, sb = 0.0;
+  const int32_t la = kA1 - kA0, lb = kB1 - kA1;
+  const int32_t lmax = la > lb ? la : lb;
+  for (int32_t q0 = 0; q0 < lmax; q0 += 8) {
+    double av[8], xa[8], bv[8], xb[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // 16 gathers in flight, indices clamped to the row
+      // an empty row reads nothing (its slot of the slice may hold another block's indices)
+      const int32_t ka = kA0 + min(q0 + q, la - 1);
+      const int32_t kb = kA1 + min(q0 + q, lb - 1);
+      av[q] = la > 0 ? sval[ka - s2] : 0.0;
+      xa[q] = la > 0 ? x[scol[ka - s4]] : 0.0;
+      bv[q] = lb > 0 ? sval[kb - s2] : 0.0;
+      xb[q] = lb > 0 ? x[scol[kb - s4]] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (q0 + q < la) sa = sa + av[q] * (xa[q] * sc);
+      if (q0 + q < lb) sb = sb + bv[q] * (xb[q] * sc);
+    }
+  }
+  wa = sa;
+  wb = sb;
+}
+
+template <int VAR, int GF>
+__global__ __launch_bounds__(kT) void k_spmv_mdot(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                  const double* __restrict__ x, const double* __restrict__ sdev,
+                                                  double* __restrict__ y, int32_t lds_cap, Vecs V, int nv,
+                                                  double* __restrict__ partial, int64_t nchunks,
+                                                  const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sval = reinterpret_cast<double*>(smem);
+  int32_t* scol = reinterpret_cast<int32_t*>(smem + (size_t)lds_cap * 8);
+  __shared__ double red[MSK_MAX_GROUP][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t c = blockIdx.x;
+  const int64_t n = nrows;
+  const int64_t base = c * kChunk + 2 * t;
+  const bool full = (c + 1) * kChunk <= n;
+  const double sc = *sdev;
+  double wr[2 * kIters];
+#pragma unroll 1
+  for (int j = 0; j < kIters; ++j) {
+    const int32_t r0 = (int32_t)(c * kChunk + j * (2 * kT));
+    if (r0 >= nrows) {  // uniform: the chunk's tail past the last row
+      for (int jj = j; jj < kIters; ++jj) wr[2 * jj] = wr[2 * jj + 1] = 0.0;
+      break;
+    }
+    const int32_t r1 = min(r0 + 2 * kT, nrows);
+    const int32_t start = rowptr[r0], end = rowptr[r1];
+    const int32_t s2 = start & ~1, s4 = start & ~3;
+    const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
+    const int32_t ra = r0 + 2 * t;
+    int32_t kA0 = 0, kA1 = 0, kB1 = 0;
+    if (ra < r1) {
+      kA0 = rowptr[ra];
+      kA1 = rowptr[ra + 1];
+      kB1 = ra + 1 < r1 ? rowptr[ra + 2] : kA1;
+    }
+    if (j) __syncthreads();  // the previous sub-block's slice is no longer read
+    stage_csr_block<false, 8>(t, n2, n4, reinterpret_cast<const double2*>(val + s2),
+                              reinterpret_cast<const int4*>(col + s4), sval, scol);
+    __syncthreads();
+    double wa = 0.0, wb = 0.0;
+    if (ra < r1) {
+      row_pair_sums<VAR>(kA0, kA1, kB1, sval, scol, s2, s4, x, sc, wa, wb);
+      if (ra + 1 < r1) *reinterpret_cast<double2*>(y + ra) = make_double2(wa, wb);
+      else y[ra] = wa;
+    }
+    wr[2 * j] = wa;
+    wr[2 * j + 1] = wb;
+  }
+  // VecMDot of W against the nv basis vectors, this chunk (dot_chunk's order)
+  if (full) {
+    int g = 0;
+#pragma unroll 1
+    for (; g + GF <= nv; g += GF) dot_group_full<GF, VAR>(wr, V, base, 0, nv, g, red, lane, wv);
+    switch (nv - g) {
+      case 3: dot_group_full<3, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 2: dot_group_full<2, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 1: dot_group_full<1, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      default: break;
+    }
+  } else {
+#pragma unroll 1
+    for (int v = 0; v < nv; ++v) {
+      const double* __restrict__ yv = vec_at(V, v);
+      const double sv = vec_scale(V, v);
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < kIters; ++j) {
+        const int64_t e = base + j * (2 * kT);
+        if (e < n) acc = acc + wr[2 * j] * (yv[e] * sv);
+        if (e + 1 < n) acc = acc + wr[2 * j + 1] * (yv[e + 1] * sv);
+      }
+      acc = wave_butterfly(acc);
+      if (lane == 0) red[v][wv] = acc;
+    }
+  }
+  __syncthreads();
+  if (t < nv) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+}
+
 // R[:, 0:nc] = A S[:, 0:nc] (MatMatMult(AIJ, DENSE)): the row block's CSR slice
 // is staged once, then each column streams through it like one SpMV (per row:
 // entries in order, from 0), so A is read once for all nc columns.
@@ -896,6 +1015,22 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
     else
       k_spmv_direct<MSK_SPMV_MULT><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y, sdev, vout, stop);
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_spmv_mdot(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val,
+                             const double* x, const double* sdev, double* y, int32_t lds_cap, const Vecs* V, int nv,
+                             double* partial, int64_t nchunks, const int* stop, hipStream_t s) {
+  if (nrows <= 0 || nchunks <= 0) return 0;
+  if (lds_cap <= 0 || nv < 1 || nv > MSK_MAX_GROUP) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)lds_cap * 12;
+  const dim3 g((unsigned)nchunks), b(kT);
+#define MSK_SMD(VAR_, GF_) \
+  k_spmv_mdot<VAR_, GF_><<<g, b, lds, s>>>(nrows, rowptr, col, val, x, sdev, y, lds_cap, *V, nv, partial, nchunks, stop)
+  const bool g2 = (g_tuning & MSK_TUNE_SPMV_MDOT_G2) != 0;
+  if (vec_var()) { if (g2) MSK_SMD(1, 2); else MSK_SMD(1, 4); }
+  else { if (g2) MSK_SMD(0, 2); else MSK_SMD(0, 4); }
+#undef MSK_SMD
   return (int)hipGetLastError();
 }
 

@@ -369,6 +369,7 @@ struct msp_mat {
   int32_t* col = nullptr;     // nnz (+4 pad)
   double* val = nullptr;      // nnz (+2 pad)
   int32_t lds_cap = 0;        // LDS entries per 256-row block (0: direct kernel)
+  int32_t lds_cap512 = 0;     // LDS entries per 512-row block (0: no fused SpMV + MDot)
   bool compressed = false;
   int64_t plane = 0;          // rows per stencil plane (box-stencil operators), 0 otherwise
   int32_t nlisted = 0;
@@ -407,9 +408,9 @@ static int mat_alloc(msp_ctx* c, msp_mat* A, int64_t nptr, int64_t nnz) {
 }
 
 static int check_csr(int32_t nrows, int32_t ncols, const int32_t* rowptr, const int32_t* col, int64_t* nnz_out,
-                     int64_t* max_block) {
+                     int64_t* max_block, int64_t* max_block512) {
   ARGCHK(rowptr[0] == 0, MSP_ERR_ARG_WRONG, "rowptr[0] = %d, expected 0", rowptr[0]);
-  int64_t mb = 0;
+  int64_t mb = 0, mb2 = 0;
   for (int32_t r = 0; r < nrows; ++r) {
     ARGCHK(rowptr[r + 1] >= rowptr[r], MSP_ERR_ARG_WRONG, "rowptr not monotone at row %d", r);
     for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
@@ -422,9 +423,14 @@ static int check_csr(int32_t nrows, int32_t ncols, const int32_t* rowptr, const 
       const int32_t r1 = std::min(r + 256, nrows);
       mb = std::max<int64_t>(mb, (int64_t)rowptr[r1] - rowptr[r]);
     }
+    if ((r & 511) == 0) {
+      const int32_t r1 = std::min(r + 512, nrows);
+      mb2 = std::max<int64_t>(mb2, (int64_t)rowptr[r1] - rowptr[r]);
+    }
   }
   *nnz_out = rowptr[nrows];
   *max_block = mb;
+  *max_block512 = mb2;
   return MSP_SUCCESS;
 }
 
@@ -432,8 +438,8 @@ extern "C" int msp_mat_create_csr(msp_ctx* c, int32_t nrows, int32_t ncols, cons
                                   const double* val, msp_mat** out) {
   ARGCHK(c && out && rowptr, MSP_ERR_ARG_NULL, "NULL argument");
   ARGCHK(nrows >= 0 && ncols >= 0, MSP_ERR_ARG_SIZ, "negative size %d x %d", nrows, ncols);
-  int64_t nnz = 0, mb = 0;
-  int rc = check_csr(nrows, ncols, rowptr, col, &nnz, &mb);
+  int64_t nnz = 0, mb = 0, mb2 = 0;
+  int rc = check_csr(nrows, ncols, rowptr, col, &nnz, &mb, &mb2);
   if (rc) return rc;
   ARGCHK(nnz == 0 || (col && val), MSP_ERR_ARG_NULL, "col/val NULL with nnz=%lld", (long long)nnz);
   msp_mat* A = new msp_mat();
@@ -442,6 +448,7 @@ extern "C" int msp_mat_create_csr(msp_ctx* c, int32_t nrows, int32_t ncols, cons
   A->ncols = ncols;
   A->nnz = nnz;
   A->lds_cap = lds_cap_for(mb);
+  A->lds_cap512 = lds_cap_for(mb2);
   if ((rc = mat_alloc(c, A, (int64_t)nrows + 1, nnz))) {
     msp_mat_destroy(&A);
     return rc;
@@ -467,7 +474,8 @@ extern "C" int msp_mat_create_csr_rows(msp_ctx* c, int32_t nrows, int32_t ncols,
   }
   int64_t nnz = 0, mb = 0;
   int32_t zero = 0;
-  int rc = check_csr(nlisted, ncols, nlisted ? rowptr : &zero, col, &nnz, &mb);
+  int64_t mb2 = 0;
+  int rc = check_csr(nlisted, ncols, nlisted ? rowptr : &zero, col, &nnz, &mb, &mb2);
   if (rc) return rc;
   msp_mat* A = new msp_mat();
   A->ctx = c;
@@ -542,6 +550,7 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
   nnz += (lo + hi) * plane;
   A->nnz = nnz;
   A->lds_cap = lds_cap_for(deg * 256);
+  A->lds_cap512 = lds_cap_for(deg * 512);
   A->plane = dim == 3 ? plane : 0;
   int rc = mat_alloc(c, A, nrows + 1, nnz);
   if (rc) {
@@ -687,6 +696,33 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
   KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, false) + (vout ? 8.0 * (double)A->nrows : 0.0));
   KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, nullptr, y, A->lds_cap, MSK_SPMV_SCALED, sdev, vout, stop,
                 A->plane, c->stream));
+  return MSP_SUCCESS;
+}
+
+// GMRES: y = A (sc*x) fused with VecMDot(y, basis 0..nv-1) into out_dev (both DBR
+// stages); returns MSP_ERR_SUP when the operator cannot take the fused kernel (the
+// caller then runs mspi_spmv_scaled + mspi_mdot_basis, with identical results).
+extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, double* y, int nv, const double* base,
+                              int64_t stride, const double* scale, double* out_dev, const int* stop) {
+  msp_ctx* c = A->ctx;
+  const int64_t n = A->nrows;
+  const int64_t nch = nchunks_of(n);
+  if (A->matfree || A->compressed || A->nrows != A->ncols || A->lds_cap512 <= 0 || nv < 1 || nv > MSPI_MAX_GROUP ||
+      nch == 0 || !(msk_get_tuning() & MSK_TUNE_GM_SPMV_MDOT))
+    return MSP_ERR_SUP;
+  int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
+  if (rc) return rc;
+  {
+    // bytes: the SpMV's (x read, y written) plus MDot's nv basis vectors; W is not re-read
+    KTimer kt(c, MSP_KERNEL_SPMVDOT, spmv_bytes(A, false) + 8.0 * (double)n * nv);
+    Vecs vg = {};
+    vg.base = base;
+    vg.stride = stride;
+    vg.scale = scale;
+    KCHK(msk_spmv_mdot(A->nrows, A->rowptr, A->col, A->val, x, sdev, y, A->lds_cap512, &vg, nv, c->partial, nch,
+                       stop, c->stream));
+  }
+  KCHK(msk_dot_stage2(c->partial, nch, nv, out_dev, stop, c->stream));  // ~4 us, not in the class stats
   return MSP_SUCCESS;
 }
 
