@@ -6,7 +6,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-run}
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/gpu_tests.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread > $OUT/gpu_tests.log 2>&1 &&
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run -f csv -- python3 bench.py --steps 3 --no-cpu-baseline > $OUT/bench_trace.json 2> $OUT/trace.err &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -f csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-timing > $OUT/pmc_fetch.out 2>&1 &&

@@ -44,7 +44,9 @@ def main():
          "Summary written by `tools/profile_summary.py`.", "",
          f"bench.py (N=1, 256^3, GMRES(30), 300 iterations/step): **{b['value']:.4g} DOF-updates/s**, "
          f"{b['ms_per_step']:.1f} ms/step; under rocprof: {bt['value']:.4g}.",
-         f"cpu_baseline (oracle, 1 thread): {b['cpu_baseline']['value']:.3g} DOF-updates/s.", "",
+         f"cpu_baseline (oracle, {b['cpu_baseline']['cores']} host thread(s)): {b['cpu_baseline']['value']:.3g} DOF-updates/s"
+         + (f"; single core {b['cpu_baseline']['single_core']['value']:.3g}" if 'single_core' in b['cpu_baseline'] else "")
+         + ".", "",
          "## rocprofv3 --stats (4 solves = 1 warmup + 3 timed)", "",
          "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
     for r in rows:
