@@ -65,9 +65,13 @@ def parse():
     p.add_argument("--operator", default="csr", choices=["csr", "matfree"],
                    help="the assembled CSR (the reference's MatMult, default) or the same operator applied "
                         "matrix-free (bitwise the same products, no matrix traffic; gmres, and A_ii for smsm)")
+    p.add_argument("--storage", default="dv", choices=["dv", "csr"],
+                   help="entry storage of the assembled operator in HBM: dv (one byte per entry, the library's "
+                        "choice for any matrix that fits; default) or csr (rowptr/col/val); bitwise the same products")
     p.add_argument("--peclet", default=None,
                    help="Px,Py,Pz: the upwind convection-diffusion operator (configs[4]) instead of Poisson")
     a = p.parse_args()
+    os.environ["MSPLIT_MAT_STORAGE"] = a.storage  # read by the library at each matrix assembly
     a.peclet = tuple(float(v) for v in a.peclet.split(",")) if a.peclet else None
     if a.peclet is not None and len(a.peclet) != 3:
         raise SystemExit("--peclet takes three cell Peclet numbers Px,Py,Pz")
@@ -282,6 +286,7 @@ def main():
                "config": {"workload": workload, "variant": variant,
                           "mesh_per_gpu": [n, n, rows // (n * n)], "blocks": world,
                           "ksp": kspopts, "gmres_iterations_per_step_per_block": its_total / args.steps,
+                          "matrix_storage": "none (matrix-free)" if args.operator == "matfree" else args.storage,
                           "parallelism": f"{world} z-slab block(s), one per GPU"}}
         if variant == "smsm":
             out["config"]["lsqr_iterations_per_step"] = lsqr_its[-args.steps:]

@@ -144,6 +144,24 @@ int msp_mat_create_box_convdiff(msp_ctx *ctx, int dim, int32_t nx, int32_t ny, i
                                 const double *peclet, msp_mat **A);
 int msp_mat_destroy(msp_mat **A);
 int msp_mat_get_info(const msp_mat *A, int32_t *nrows, int32_t *ncols, int64_t *nnz);
+/* Storage of an assembled matrix in HBM (the values and the order of every
+ * product are the same in both; only the bytes a MatMult moves differ):
+ *   MSP_STORAGE_CSR  rowptr int32, col int32, val f64 -- 12 bytes per entry;
+ *   MSP_STORAGE_DV   one byte per entry naming a (col - row, value) pair of a
+ *                    per-matrix dictionary (<= 256 pairs) and one byte per row
+ *                    (its length, <= 255): ~1 byte per entry.  Every
+ *                    constant-coefficient stencil fits (7 pairs in 3D).
+ * A matrix that fits is given DV at assembly (MSPLIT_MAT_STORAGE=csr in the
+ * environment keeps CSR); the CSR stays resident for the kernels that need it
+ * (MatMatMult, get_csr).  This is MatSetType's choice of format inside one
+ * type, like PETSc's AIJ variants, invisible to the caller.  Setting DV on a
+ * matrix that does not fit: MSP_ERR_SUP.  get_storage reports
+ * MSP_STORAGE_NONE for a matrix-free operator; ndict may be NULL. */
+#define MSP_STORAGE_NONE (-1)
+#define MSP_STORAGE_CSR 0
+#define MSP_STORAGE_DV 1
+int msp_mat_set_storage(msp_mat *A, int storage);
+int msp_mat_get_storage(const msp_mat *A, int *storage, int *ndict);
 /* Download the CSR (host buffers of nrows+1 / nnz entries); synchronising. */
 int msp_mat_get_csr(const msp_mat *A, int32_t *rowptr, int32_t *col, double *val);
 /* MatMult y = A x (utils.c:626; KSP_PCApplyBAorAB inside KSPGMRESCycle). */

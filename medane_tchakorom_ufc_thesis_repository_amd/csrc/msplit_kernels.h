@@ -44,7 +44,10 @@ enum {
   MSK_TUNE_SPMV_ZCHUNK = 512,       // SpMV: XCD x takes the x-th eighth of the row blocks, in order
   MSK_TUNE_MDOT_SINGLE = 1024,      // MDot: one vector's loads at a time (before grouped loads)
   MSK_TUNE_GM_SPMV_MDOT = 2048,     // GMRES: MatMult fused with the VecMDot that follows (k_spmv_mdot)
-  MSK_TUNE_SPMV_MDOT_G2 = 4096      // k_spmv_mdot: two basis vectors per load group instead of four
+  MSK_TUNE_SPMV_MDOT_G2 = 4096,     // k_spmv_mdot: two basis vectors per load group instead of four
+  MSK_TUNE_DV_RPL1 = 8192,          // DV SpMV: one row per lane (256-row blocks)
+  MSK_TUNE_DV_RPL2 = 16384,         // DV SpMV: two rows per lane (512-row blocks); default four
+  MSK_TUNE_DV_NOELL = 32768         // DV storage: CSR-order codes even where the ELL layout fits (at assembly)
 };
 
 extern "C" {
@@ -65,6 +68,20 @@ int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, cons
 int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
              const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
              const int* stop, int64_t plane, hipStream_t s);
+// The same products over DV storage (len8: entries per row <= 255; code8: one byte per entry naming the
+// (col - row, value) pair ddelta/dval[code]; rowptr read only at block starts); max_block: most entries in
+// any 256-row block (sizes the LDS stage of the codes).  ell_w = 4, 8 or 16: ELL layout instead (row r's
+// codes at code8 + r*ell_w, padded with code 255; rowptr, len8 and max_block unused; ndict <= 255).
+int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const uint8_t* code8,
+                const int32_t* ddelta, const double* dval, int ndict, int32_t max_block, int ell_w,
+                const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
+                const int* stop, int64_t plane, hipStream_t s);
+int msk_ell_encode(int32_t nrows, int W, const int32_t* rowptr, const int32_t* col, const double* val, int ndict,
+                   const int32_t* ddelta, const double* dval, uint8_t* code8, int* fail, hipStream_t s);
+// DV codes of an assembled CSR against a dictionary; *fail (device) set when it does not fit
+int msk_dv_encode(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, int ndict,
+                  const int32_t* ddelta, const double* dval, uint8_t* len8, uint8_t* code8, int* fail,
+                  hipStream_t s);
 // GMRES: y = A (sc*x), sc = *sdev, fused with the DBR stage 1 of y . V_v (v < nv <= 32) into partial;
 // lds_cap: LDS entries for the col/val slice of any 512-row sub-block (> 0)
 int msk_spmv_mdot(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,

@@ -864,6 +864,358 @@ __global__ __launch_bounds__(kT) void k_stencil_spmv(int dim, int32_t nx, int32_
   }
 }
 
+// ------------------------------------------ DV storage (delta/value dictionary)
+// The same assembled matrix, its entries stored as one byte each: entry k of
+// row r is code[k], naming the pair (col - r, value) in a per-matrix
+// dictionary of at most 256 pairs, and row r holds len[r] <= 255 entries.  Row
+// starts come from the scan of len inside the workgroup, block starts from the
+// CSR rowptr at multiples of 256.  A 7-point operator needs 7 pairs, so an
+// entry moves 1 byte instead of 12 (col + val) and a row ~8 instead of ~88.
+// The entries keep the CSR order, so each row's sum is MatMult_SeqAIJ's
+// sequence term for term and results equal k_spmv_lds8's bit for bit.
+template <int MODE>
+__global__ __launch_bounds__(kT) void k_spmv_dv(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                                const uint8_t* __restrict__ len8, const uint8_t* __restrict__ code8,
+                                                const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
+                                                int ndict, const double* __restrict__ x, const double* __restrict__ b,
+                                                double* __restrict__ y, const double* __restrict__ sdev,
+                                                double* __restrict__ vout, const int* __restrict__ stop, XcdMap xm) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // the block's codes
+  __shared__ int32_t sdel[256];
+  __shared__ double sval[256];
+  __shared__ int32_t wtot[kT / 64];
+  const uint8_t* scode = reinterpret_cast<const uint8_t*>(smem);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int32_t r0 = row_block(xm) * kT;
+  const int32_t r1 = min(r0 + kT, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s16 = start & ~15;
+  const int32_t n16 = (end - s16 + 15) >> 4;
+  const int32_t r = r0 + t;
+  int32_t len = 0;
+  double bb = 0.0;
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  if (r < r1) {
+    len = len8[r];
+    if (MODE == MSK_SPMV_RESID) bb = b[r];
+    if (MODE == MSK_SPMV_SCALED && vout) vout[r] = x[r] * sc;
+  }
+  if (t < ndict) {
+    sdel[t] = ddelta[t];
+    sval[t] = dval[t];
+  }
+  const uint4* c16 = reinterpret_cast<const uint4*>(code8 + s16);
+  for (int32_t i = t; i < n16; i += kT) reinterpret_cast<uint4*>(smem)[i] = c16[i];
+  // exclusive scan of the row lengths: wave inclusive scan, then the waves before
+  int32_t inc = len;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t u = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += u;
+  }
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  int32_t k0 = (start - s16) + inc - len;
+#pragma unroll
+  for (int u = 0; u < kT / 64 - 1; ++u)
+    if (u < w) k0 += wtot[u];
+  if (r < r1) {
+    double s = 0.0;
+    for (int32_t q0 = 0; q0 < len; q0 += 8) {
+      double av[8], xv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {  // 8 gathers in flight, entries clamped to the row
+        const int c = scode[k0 + min(q0 + q, len - 1)];
+        av[q] = sval[c];
+        xv[q] = x[r + sdel[c]];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (MODE == MSK_SPMV_SCALED) xv[q] = xv[q] * sc;
+        if (q0 + q < len) s = s + av[q] * xv[q];
+      }
+    }
+    y[r] = MODE == MSK_SPMV_RESID ? bb - s : s;
+  }
+}
+
+// The same over blocks of RPL*256 rows: lane t takes rows t, t+256, ..
+// (each sub-block of 256 rows coalesced), all RPL rows' gathers issued before
+// the first product, so one block's chain of dependent loads (rowptr -> codes
+// -> x) covers RPL times the rows.  Row lengths arrive as RPL consecutive
+// bytes per lane; the scan runs over those and hands each row its code offset
+// through LDS.
+template <int MODE, int RPL>
+__global__ __launch_bounds__(kT) void k_spmv_dvb(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                                 const uint8_t* __restrict__ len8, const uint8_t* __restrict__ code8,
+                                                 const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
+                                                 int ndict, const double* __restrict__ x,
+                                                 const double* __restrict__ b, double* __restrict__ y,
+                                                 const double* __restrict__ sdev, double* __restrict__ vout,
+                                                 const int* __restrict__ stop) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
+  constexpr int RB = kT * RPL;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // the block's codes
+  __shared__ int32_t sdel[256];
+  __shared__ double sval[256];
+  __shared__ int32_t soff[RB];
+  __shared__ int32_t wtot[kT / 64];
+  const uint8_t* scode = reinterpret_cast<const uint8_t*>(smem);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int32_t r0 = (int32_t)blockIdx.x * RB;
+  const int32_t r1 = min(r0 + RB, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s16 = start & ~15;
+  const int32_t n16 = (end - s16 + 15) >> 4;
+  // lengths of rows r0 + RPL*t + j
+  int32_t l[RPL];
+  const int32_t rl = r0 + RPL * t;
+  if (rl + RPL <= r1) {
+    if constexpr (RPL == 4) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(len8 + rl);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) l[j] = (v >> (8 * j)) & 255;
+    } else if constexpr (RPL == 2) {
+      const uint16_t v = *reinterpret_cast<const uint16_t*>(len8 + rl);
+      l[0] = v & 255;
+      l[1] = v >> 8;
+    } else {
+      l[0] = len8[rl];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) l[j] = rl + j < r1 ? len8[rl + j] : 0;
+  }
+  if (t < ndict) {
+    sdel[t] = ddelta[t];
+    sval[t] = dval[t];
+  }
+  const uint4* c16 = reinterpret_cast<const uint4*>(code8 + s16);
+  for (int32_t i = t; i < n16; i += kT) reinterpret_cast<uint4*>(smem)[i] = c16[i];
+  int32_t tot = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) tot += l[j];
+  int32_t inc = tot;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t u = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += u;
+  }
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  int32_t k = (start - s16) + inc - tot;
+#pragma unroll
+  for (int u = 0; u < kT / 64 - 1; ++u)
+    if (u < w) k += wtot[u];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    soff[RPL * t + j] = (k << 8) | l[j];  // offset (< 2^23) and length packed
+    k += l[j];
+  }
+  __syncthreads();
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  int32_t k0[RPL], ln[RPL];
+  int32_t lmax = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    const int32_t pk = r < r1 ? soff[t + kT * j] : 0;
+    k0[j] = pk >> 8;
+    ln[j] = pk & 255;
+    lmax = max(lmax, ln[j]);
+  }
+  double s[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) s[j] = 0.0;
+  for (int32_t q0 = 0; q0 < lmax; q0 += 8) {
+    double av[RPL][8], xv[RPL][8];
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int32_t r = r0 + t + kT * j;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {  // every row's gathers in flight together, entries clamped to the row
+        if (ln[j] > 0) {
+          const int c = scode[k0[j] + min(q0 + q, ln[j] - 1)];
+          av[j][q] = sval[c];
+          xv[j][q] = x[r + sdel[c]];
+        } else {
+          av[j][q] = 0.0;
+          xv[j][q] = 0.0;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (MODE == MSK_SPMV_SCALED) xv[j][q] = xv[j][q] * sc;
+        if (q0 + q < ln[j]) s[j] = s[j] + av[j][q] * xv[j][q];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    if (r < r1) {
+      if (MODE == MSK_SPMV_SCALED && vout) vout[r] = x[r] * sc;
+      y[r] = MODE == MSK_SPMV_RESID ? b[r] - s[j] : s[j];
+    }
+  }
+}
+
+// DV storage in ELL layout, for matrices whose rows hold at most 16 entries:
+// row r's codes are the W bytes at r*W (W = 4, 8 or 16), its entries in CSR
+// order followed by code 255 (no entry).  A lane reads its row's codes with
+// one 4/8/16-byte load -- no row pointers, no scan, no LDS stage -- so the
+// chain of dependent loads per row is codes -> x -> y.  RPL rows per lane
+// (t, t+256, ..) keep RPL*W gathers in flight.  Each row's sum is the CSR
+// sequence term for term (code 255 entries are skipped, not added as zeros).
+template <int W>
+struct EllWord;
+template <>
+struct EllWord<4> {
+  typedef uint32_t T;
+  static __device__ __forceinline__ int byte(const T& v, int q) { return (v >> (8 * q)) & 255; }
+  static __device__ __forceinline__ T empty() { return 0xFFFFFFFFu; }
+};
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <>
+struct EllWord<8> {
+  typedef u32x2 T;
+  static __device__ __forceinline__ int byte(const T& v, int q) {
+    return ((q < 4 ? v.x : v.y) >> (8 * (q & 3))) & 255;
+  }
+  static __device__ __forceinline__ T empty() { return T{0xFFFFFFFFu, 0xFFFFFFFFu}; }
+};
+template <>
+struct EllWord<16> {
+  typedef u32x4 T;
+  static __device__ __forceinline__ int byte(const T& v, int q) {
+    const uint32_t w = q < 4 ? v.x : q < 8 ? v.y : q < 12 ? v.z : v.w;
+    return (w >> (8 * (q & 3))) & 255;
+  }
+  static __device__ __forceinline__ T empty() { return T{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}; }
+};
+
+template <int MODE, int W, int RPL>
+__global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* __restrict__ code8,
+                                                 const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
+                                                 int ndict, const double* __restrict__ x,
+                                                 const double* __restrict__ b, double* __restrict__ y,
+                                                 const double* __restrict__ sdev, double* __restrict__ vout,
+                                                 const int* __restrict__ stop) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
+  typedef EllWord<W> EW;
+  typedef typename EW::T CT;
+  __shared__ int32_t sdel[256];
+  __shared__ double sval[256];
+  const int t = threadIdx.x;
+  const int32_t r0 = (int32_t)blockIdx.x * (kT * RPL);
+  CT cw[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    cw[j] = r < nrows ? __builtin_nontemporal_load(reinterpret_cast<const CT*>(code8) + r) : EW::empty();
+  }
+  if (t < ndict) {
+    sdel[t] = ddelta[t];
+    sval[t] = dval[t];
+  }
+  __syncthreads();
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  double xv[RPL][W];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const int c = EW::byte(cw[j], q);
+      xv[j][q] = c != 255 ? x[r + sdel[c]] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const int c = EW::byte(cw[j], q);
+      if (c != 255) {
+        const double xx = MODE == MSK_SPMV_SCALED ? xv[j][q] * sc : xv[j][q];
+        s = s + sval[c] * xx;
+      }
+    }
+    if (r < nrows) {
+      if (MODE == MSK_SPMV_SCALED && vout) vout[r] = x[r] * sc;
+      y[r] = MODE == MSK_SPMV_RESID ? b[r] - s : s;
+    }
+  }
+}
+
+// ELL-layout encode: row r's W codes, then 255 padding; *fail when a row is
+// longer than W or an entry is not in the dictionary (ndict <= 255).
+__global__ __launch_bounds__(kT) void k_ell_encode(int32_t nrows, int W, const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                   int ndict, const int32_t* __restrict__ ddelta,
+                                                   const double* __restrict__ dval, uint8_t* __restrict__ code8,
+                                                   int* __restrict__ fail) {
+  const int64_t stride = (int64_t)gridDim.x * kT;
+  for (int64_t r = (int64_t)blockIdx.x * kT + threadIdx.x; r < nrows; r += stride) {
+    const int32_t k0 = rowptr[r], k1 = rowptr[r + 1];
+    if (k1 - k0 > W) {
+      atomicOr(fail, 1);
+      continue;
+    }
+    for (int q = 0; q < W; ++q) {
+      int j = 255;
+      if (k0 + q < k1) {
+        const int32_t k = k0 + q;
+        const int32_t d = col[k] - (int32_t)r;
+        const long long bits = __double_as_longlong(val[k]);
+        j = 0;
+        while (j < ndict && !(ddelta[j] == d && __double_as_longlong(dval[j]) == bits)) ++j;
+        if (j == ndict || j == 255) {
+          atomicOr(fail, 1);
+          j = 255;
+        }
+      }
+      code8[r * W + q] = (uint8_t)j;
+    }
+  }
+}
+
+// Encode an assembled CSR into DV storage against a given dictionary (one lane
+// per row); *fail is set when a row is longer than 255 or an entry's
+// (col - row, value bits) is not in the dictionary.
+__global__ __launch_bounds__(kT) void k_dv_encode(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ col, const double* __restrict__ val,
+                                                  int ndict, const int32_t* __restrict__ ddelta,
+                                                  const double* __restrict__ dval, uint8_t* __restrict__ len8,
+                                                  uint8_t* __restrict__ code8, int* __restrict__ fail) {
+  const int64_t stride = (int64_t)gridDim.x * kT;
+  for (int64_t r = (int64_t)blockIdx.x * kT + threadIdx.x; r < nrows; r += stride) {
+    const int32_t k0 = rowptr[r], k1 = rowptr[r + 1];
+    if (k1 - k0 > 255) {
+      atomicOr(fail, 1);
+      continue;
+    }
+    len8[r] = (uint8_t)(k1 - k0);
+    for (int32_t k = k0; k < k1; ++k) {
+      const int32_t d = col[k] - (int32_t)r;
+      const long long bits = __double_as_longlong(val[k]);
+      int j = 0;
+      while (j < ndict && !(ddelta[j] == d && __double_as_longlong(dval[j]) == bits)) ++j;
+      if (j == ndict) {
+        atomicOr(fail, 1);
+        break;
+      }
+      code8[k] = (uint8_t)j;
+    }
+  }
+}
+
 // --------------------------------------------------------------- BLAS-1
 template <int OP>
 __global__ __launch_bounds__(kT) void k_blas1(double* __restrict__ y, const double* __restrict__ x,
@@ -1015,6 +1367,86 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
     else
       k_spmv_direct<MSK_SPMV_MULT><<<dim3(g), dim3(kT), 0, s>>>(nrows, rowptr, col, val, x, b, y, sdev, vout, stop);
   }
+  return (int)hipGetLastError();
+}
+
+template <int W, int RPL>
+static void launch_ell(int mode, int32_t nrows, const uint8_t* code8, const int32_t* ddelta, const double* dval,
+                       int ndict, const double* x, const double* b, double* y, const double* sdev, double* vout,
+                       const int* stop, hipStream_t s) {
+  const unsigned g = (unsigned)((nrows + kT * RPL - 1) / (kT * RPL));
+  if (mode == MSK_SPMV_RESID)
+    k_spmv_ell<MSK_SPMV_RESID, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop);
+  else if (mode == MSK_SPMV_SCALED)
+    k_spmv_ell<MSK_SPMV_SCALED, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop);
+  else
+    k_spmv_ell<MSK_SPMV_MULT, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop);
+}
+
+extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const uint8_t* code8,
+                           const int32_t* ddelta, const double* dval, int ndict, int32_t max_block, int ell_w,
+                           const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
+                           const int* stop, int64_t plane, hipStream_t s) {
+  if (nrows <= 0) return 0;
+  if (max_block < 0 || ndict < 0 || ndict > 256) return (int)hipErrorInvalidValue;
+  if (ell_w) {
+    if (ndict > 255) return (int)hipErrorInvalidValue;
+    const int rpl = (g_tuning & MSK_TUNE_DV_RPL1) ? 1 : (g_tuning & MSK_TUNE_DV_RPL2) ? 2 : (ell_w == 16 ? 2 : 4);
+#define MSK_ELL(W_, R_) launch_ell<W_, R_>(mode, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, s)
+    if (ell_w == 4) { if (rpl == 1) MSK_ELL(4, 1); else if (rpl == 2) MSK_ELL(4, 2); else MSK_ELL(4, 4); }
+    else if (ell_w == 8) { if (rpl == 1) MSK_ELL(8, 1); else if (rpl == 2) MSK_ELL(8, 2); else MSK_ELL(8, 4); }
+    else if (ell_w == 16) { if (rpl == 1) MSK_ELL(16, 1); else MSK_ELL(16, 2); }
+    else return (int)hipErrorInvalidValue;
+#undef MSK_ELL
+    return (int)hipGetLastError();
+  }
+  const int rpl = (g_tuning & MSK_TUNE_DV_RPL1) ? 1 : (g_tuning & MSK_TUNE_DV_RPL2) ? 2 : 4;
+  // LDS for the codes of one block: its entries plus both 16-byte roundings
+  const size_t cap = ((size_t)rpl * max_block + 30 + 15) & ~(size_t)15;
+  if (rpl == 1) {
+    const unsigned g = (unsigned)((nrows + kT - 1) / kT);
+    const XcdMap xm = xcd_map(nrows, plane);
+#define MSK_DV(M) \
+  k_spmv_dv<M><<<dim3(g), dim3(kT), cap, s>>>(nrows, rowptr, len8, code8, ddelta, dval, ndict, x, b, y, sdev, vout, \
+                                              stop, xm)
+    if (mode == MSK_SPMV_RESID) MSK_DV(MSK_SPMV_RESID);
+    else if (mode == MSK_SPMV_SCALED) MSK_DV(MSK_SPMV_SCALED);
+    else MSK_DV(MSK_SPMV_MULT);
+#undef MSK_DV
+    return (int)hipGetLastError();
+  }
+  const unsigned g = (unsigned)((nrows + kT * rpl - 1) / (kT * rpl));
+#define MSK_DVB(M, R) \
+  k_spmv_dvb<M, R><<<dim3(g), dim3(kT), cap, s>>>(nrows, rowptr, len8, code8, ddelta, dval, ndict, x, b, y, sdev, \
+                                                  vout, stop)
+  if (rpl == 2) {
+    if (mode == MSK_SPMV_RESID) MSK_DVB(MSK_SPMV_RESID, 2);
+    else if (mode == MSK_SPMV_SCALED) MSK_DVB(MSK_SPMV_SCALED, 2);
+    else MSK_DVB(MSK_SPMV_MULT, 2);
+  } else {
+    if (mode == MSK_SPMV_RESID) MSK_DVB(MSK_SPMV_RESID, 4);
+    else if (mode == MSK_SPMV_SCALED) MSK_DVB(MSK_SPMV_SCALED, 4);
+    else MSK_DVB(MSK_SPMV_MULT, 4);
+  }
+#undef MSK_DVB
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_ell_encode(int32_t nrows, int W, const int32_t* rowptr, const int32_t* col, const double* val,
+                              int ndict, const int32_t* ddelta, const double* dval, uint8_t* code8, int* fail,
+                              hipStream_t s) {
+  if (nrows <= 0) return 0;
+  k_ell_encode<<<dim3(grid_for(nrows, 4096)), dim3(kT), 0, s>>>(nrows, W, rowptr, col, val, ndict, ddelta, dval,
+                                                                code8, fail);
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_dv_encode(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, int ndict,
+                             const int32_t* ddelta, const double* dval, uint8_t* len8, uint8_t* code8, int* fail,
+                             hipStream_t s) {
+  if (nrows <= 0) return 0;
+  k_dv_encode<<<dim3(grid_for(nrows, 4096)), dim3(kT), 0, s>>>(nrows, rowptr, col, val, ndict, ddelta, dval, len8,
+                                                               code8, fail);
   return (int)hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "msplit.h"
@@ -378,6 +379,15 @@ struct msp_mat {
   int dim = 0, lo = 0, hi = 0;
   int32_t bx = 0, by = 0, bz = 0;
   BoxCoef cf = {};
+  // DV storage (k_spmv_dv): one byte per entry naming a (col - row, value) pair
+  uint8_t* dv_len = nullptr;   // nrows (+16 pad)
+  uint8_t* dv_code = nullptr;  // nnz (+16 pad)
+  int32_t* dv_delta = nullptr; // ndict
+  double* dv_val = nullptr;    // ndict
+  int32_t ndict = 0;
+  int32_t dv_mb = 0;           // most entries in one 256-row block (sizes the LDS stage)
+  int32_t dv_w = 0;            // ELL layout: codes per row (4, 8, 16); 0: CSR-order codes + row lengths
+  bool dv_on = false;          // products read the DV storage
 };
 
 extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
@@ -392,10 +402,107 @@ extern "C" mspi_csr_view mspi_mat_csr(const msp_mat* A) {
 }
 
 static const int32_t kMaxLdsCap = 4096;  // 48 KiB of col+val per 256-row block
+static const int64_t kMaxDvBlock = 12288;  // DV codes per 256-row block (CSR-order layout)
 
 static int32_t lds_cap_for(int64_t max_block_nnz) {
   if (max_block_nnz + 8 > kMaxLdsCap) return 0;
   return (int32_t)((max_block_nnz + 8 + 3) & ~(int64_t)3);
+}
+
+// Storage chosen at assembly: DV whenever the matrix fits it, unless
+// MSPLIT_MAT_STORAGE=csr (then msp_mat_set_storage can still switch).
+static bool dv_default() {
+  const char* e = getenv("MSPLIT_MAT_STORAGE");
+  return !(e && strcmp(e, "csr") == 0);
+}
+
+static void dv_free(msp_mat* A) {
+  if (A->dv_len) (void)hipFree(A->dv_len);
+  if (A->dv_code) (void)hipFree(A->dv_code);
+  if (A->dv_delta) (void)hipFree(A->dv_delta);
+  if (A->dv_val) (void)hipFree(A->dv_val);
+  A->dv_len = A->dv_code = nullptr;
+  A->dv_delta = nullptr;
+  A->dv_val = nullptr;
+  A->ndict = 0;
+  A->dv_mb = 0;
+  A->dv_w = 0;
+  A->dv_on = false;
+}
+
+// Encode the device CSR of A against the dictionary (host arrays, nd <= 256).
+// Rows of at most 16 entries take the ELL layout (W codes per row, padded)
+// unless padding would add more than half the entries; other matrices take
+// CSR-order codes with a length byte per row.  A matrix the dictionary does
+// not cover keeps CSR storage only (returns 0).
+static int dv_build(msp_mat* A, int nd, const int32_t* delta, const double* val, int64_t max_block,
+                    int32_t max_len) {
+  msp_ctx* c = A->ctx;
+  if (A->compressed || A->matfree || A->nrows == 0 || nd < 1 || nd > 256) return MSP_SUCCESS;
+  const int W = max_len <= 4 ? 4 : max_len <= 8 ? 8 : max_len <= 16 ? 16 : 0;
+  const bool ell = W && nd <= 255 && !(msk_get_tuning() & MSK_TUNE_DV_NOELL) &&
+                   (double)W * A->nrows <= 1.5 * (double)A->nnz + 2.0 * A->nrows;
+  // CSR-order codes: one block's codes (up to 4 x 256 rows) are staged in LDS, at most 48 KiB
+  if (!ell && max_block > kMaxDvBlock) return MSP_SUCCESS;
+  A->dv_mb = (int32_t)max_block;
+  A->dv_w = ell ? W : 0;
+  if (!ell) HIPCHK(hipMalloc((void**)&A->dv_len, (size_t)A->nrows + 16));
+  const size_t ncode = ell ? (size_t)W * A->nrows : (size_t)A->nnz;
+  HIPCHK(hipMalloc((void**)&A->dv_code, ncode + 16));
+  HIPCHK(hipMalloc((void**)&A->dv_delta, 256 * sizeof(int32_t)));
+  HIPCHK(hipMalloc((void**)&A->dv_val, 256 * sizeof(double)));
+  HIPCHK(hipMemsetAsync(A->dv_code + ncode, 0, 16, c->stream));
+  HIPCHK(hipMemcpyAsync(A->dv_delta, delta, (size_t)nd * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(A->dv_val, val, (size_t)nd * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  int* fail = reinterpret_cast<int*>(mspi_dev_scratch(c));
+  HIPCHK(hipMemsetAsync(fail, 0, sizeof(int), c->stream));
+  if (ell)
+    KCHK(msk_ell_encode(A->nrows, W, A->rowptr, A->col, A->val, nd, A->dv_delta, A->dv_val, A->dv_code, fail,
+                        c->stream));
+  else
+    KCHK(msk_dv_encode(A->nrows, A->rowptr, A->col, A->val, nd, A->dv_delta, A->dv_val, A->dv_len, A->dv_code, fail,
+                       c->stream));
+  int hfail = 0;
+  HIPCHK(hipMemcpyAsync(&hfail, fail, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (hfail) {
+    dv_free(A);
+    return MSP_SUCCESS;
+  }
+  A->ndict = nd;
+  A->dv_on = dv_default();
+  return MSP_SUCCESS;
+}
+
+struct DvKey {
+  int32_t d;
+  uint64_t bits;
+  bool operator==(const DvKey& o) const { return d == o.d && bits == o.bits; }
+};
+struct DvKeyHash {
+  size_t operator()(const DvKey& k) const { return (size_t)(k.bits * 0x9E3779B97F4A7C15ull ^ (uint32_t)k.d); }
+};
+
+// The dictionary of a host CSR: its distinct (col - row, value bits) pairs in
+// order of first appearance; none (0) when there are more than 256 or a row
+// holds more than 255 entries.
+static int dv_dictionary(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val,
+                         std::vector<int32_t>& delta, std::vector<double>& dval) {
+  std::unordered_map<DvKey, int, DvKeyHash> seen;
+  for (int32_t r = 0; r < nrows; ++r) {
+    if (rowptr[r + 1] - rowptr[r] > 255) return 0;
+    for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+      DvKey key;
+      key.d = col[k] - r;
+      memcpy(&key.bits, &val[k], 8);
+      if (seen.count(key)) continue;
+      if (delta.size() == 256) return 0;
+      seen.emplace(key, (int)delta.size());
+      delta.push_back(key.d);
+      dval.push_back(val[k]);
+    }
+  }
+  return (int)delta.size();
 }
 
 static int mat_alloc(msp_ctx* c, msp_mat* A, int64_t nptr, int64_t nnz) {
@@ -459,6 +566,17 @@ extern "C" int msp_mat_create_csr(msp_ctx* c, int32_t nrows, int32_t ncols, cons
     HIPCHK(hipMemcpyAsync(A->val, val, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice, c->stream));
   }
   HIPCHK(hipStreamSynchronize(c->stream));  // host arrays stay the caller's
+  if (nnz) {
+    std::vector<int32_t> dd;
+    std::vector<double> dvv;
+    const int nd = dv_dictionary(nrows, rowptr, col, val, dd, dvv);
+    int32_t ml = 0;
+    for (int32_t r = 0; r < nrows; ++r) ml = std::max(ml, rowptr[r + 1] - rowptr[r]);
+    if (nd && (rc = dv_build(A, nd, dd.data(), dvv.data(), mb, ml))) {
+      msp_mat_destroy(&A);
+      return rc;
+    }
+  }
   *out = A;
   return MSP_SUCCESS;
 }
@@ -562,6 +680,21 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
   const BoxCoef cf = box_coefs(dim, peclet);
   KCHK(msk_box_stencil(dim, nx, ny, nz, nrows, lo, hi, &cf, A->rowptr, A->col, A->val, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  {  // the stencil's pairs: (slow-, y-, x-, diagonal, x+, y+, slow+) with the column shift of a lo plane
+    const int32_t off = lo ? (int32_t)plane : 0, P = (int32_t)plane;
+    std::vector<int32_t> dd;
+    std::vector<double> dvv;
+    const int32_t d3[7] = {off - P, off - nx, off - 1, off, off + 1, off + nx, off + P};
+    for (int q = 0; q < 7; ++q) {
+      if (dim == 2 && (q == 1 || q == 5)) continue;
+      dd.push_back(d3[q]);
+      dvv.push_back(cf.c[q]);
+    }
+    if ((rc = dv_build(A, (int)dd.size(), dd.data(), dvv.data(), deg * 256, (int32_t)deg))) {
+      msp_mat_destroy(&A);
+      return rc;
+    }
+  }
   *out = A;
   return MSP_SUCCESS;
 }
@@ -617,6 +750,7 @@ extern "C" int msp_mat_destroy(msp_mat** pA) {
   if (A->col) (void)hipFree(A->col);
   if (A->val) (void)hipFree(A->val);
   if (A->row_ids) (void)hipFree(A->row_ids);
+  dv_free(A);
   delete A;
   *pA = nullptr;
   return MSP_SUCCESS;
@@ -651,6 +785,32 @@ static double spmv_bytes(const msp_mat* A, bool resid) {
   return 12.0 * (double)A->nnz + 4.0 * (rows + 1) + 8.0 * xs + 8.0 * rows + (resid ? 8.0 * rows : 0.0);
 }
 
+// DV storage: 1 byte per entry and per row, the block starts, x read once, y written (b read, vout written)
+static double dv_bytes(const msp_mat* A, bool resid, bool vout) {
+  const double rows = (double)A->nrows;
+  const double codes = A->dv_w ? (double)A->dv_w * rows : (double)A->nnz + rows + 4.0 * (rows / 256.0 + 1.0);
+  return codes + 8.0 * (double)A->ncols + 8.0 * rows +
+         (resid ? 8.0 * rows : 0.0) + (vout ? 8.0 * rows : 0.0);
+}
+
+extern "C" int msp_mat_set_storage(msp_mat* A, int storage) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
+  ARGCHK(storage == MSP_STORAGE_CSR || storage == MSP_STORAGE_DV, MSP_ERR_ARG_OUTOFRANGE, "unknown storage %d",
+         storage);
+  if (storage == MSP_STORAGE_DV)
+    ARGCHK(A->ndict > 0, MSP_ERR_SUP, "matrix has no DV storage (more than 256 (col - row, value) pairs, a row "
+           "longer than 255, or not an assembled square-block CSR)");
+  A->dv_on = storage == MSP_STORAGE_DV;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_get_storage(const msp_mat* A, int* storage, int* ndict) {
+  ARGCHK(A && storage, MSP_ERR_ARG_NULL, "NULL argument");
+  *storage = A->matfree ? MSP_STORAGE_NONE : (A->dv_on ? MSP_STORAGE_DV : MSP_STORAGE_CSR);
+  if (ndict) *ndict = A->ndict;
+  return MSP_SUCCESS;
+}
+
 static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bool resid) {
   msp_ctx* c = A->ctx;
   if (A->matfree) {  // x and y (and b) only
@@ -659,8 +819,8 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
                           resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
     return MSP_SUCCESS;
   }
-  KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, resid));
   if (A->compressed) {
+    KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, resid));
     // rows that hold no entries: y = 0 (MatMult) or r = b - 0 = b (MatResidual)
     if (resid) {
       if (y != b) HIPCHK(hipMemcpyAsync(y, b, (size_t)A->nrows * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
@@ -670,6 +830,13 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
     KCHK(msk_spmv_rows(A->nlisted, A->row_ids, A->rowptr, A->col, A->val, x, b, y, resid ? 1 : 0, c->stream));
     return MSP_SUCCESS;
   }
+  if (A->dv_on) {
+    KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, resid, false));
+    KCHK(msk_spmv_dv(A->nrows, A->rowptr, A->dv_len, A->dv_code, A->dv_delta, A->dv_val, A->ndict, A->dv_mb, A->dv_w, x, b,
+                     y, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, A->plane, c->stream));
+    return MSP_SUCCESS;
+  }
+  KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, resid));
   KCHK(msk_spmv(A->nrows, A->rowptr, A->col, A->val, x, b, y, A->lds_cap, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT,
                 nullptr, nullptr, nullptr, A->plane, c->stream));
   return MSP_SUCCESS;
@@ -691,6 +858,12 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
     KTimer kt(c, MSP_KERNEL_SPMV, 8.0 * (double)A->ncols + (vout ? 16.0 : 8.0) * (double)A->nrows);
     KCHK(msk_stencil_spmv(A->dim, A->bx, A->by, A->bz, A->nrows, A->lo, A->hi, &A->cf, x, nullptr, y,
                           MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
+    return MSP_SUCCESS;
+  }
+  if (A->dv_on) {
+    KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, false, vout != nullptr));
+    KCHK(msk_spmv_dv(A->nrows, A->rowptr, A->dv_len, A->dv_code, A->dv_delta, A->dv_val, A->ndict, A->dv_mb, A->dv_w, x,
+                     nullptr, y, MSK_SPMV_SCALED, sdev, vout, stop, A->plane, c->stream));
     return MSP_SUCCESS;
   }
   KTimer kt(c, MSP_KERNEL_SPMV, spmv_bytes(A, false) + (vout ? 8.0 * (double)A->nrows : 0.0));

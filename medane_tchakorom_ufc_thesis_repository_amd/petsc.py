@@ -325,6 +325,18 @@ class Mat:
         call("msp_mat_get_csr", self.h, _ip(rp), _ip(cl), _dp(vl))
         return rp, cl[: self.nnz], vl[: self.nnz]
 
+    STORAGE = {"none": -1, "csr": 0, "dv": 1}
+
+    def set_storage(self, storage: str):
+        """Entry storage in HBM (msp_mat_set_storage): 'csr' or 'dv' (one byte per entry); same products."""
+        call("msp_mat_set_storage", self.h, self.STORAGE[storage])
+
+    def get_storage(self) -> str:
+        st = C.c_int32()
+        nd = C.c_int32()
+        call("msp_mat_get_storage", self.h, C.byref(st), C.byref(nd))
+        return {v: k for k, v in self.STORAGE.items()}[st.value]
+
     def create_vecs(self):                                          # MatCreateVecs
         return Vec(self.ctx, self.shape[1]), Vec(self.ctx, self.shape[0])
 

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--tunings", default="0")
     ap.add_argument("--groups", default="0", help="SpMV XCD group sizes to sweep (0 = auto)")
     ap.add_argument("--kernels", default="spmv,mdot,maxpy")
+    ap.add_argument("--storage", default="csr", choices=["csr", "dv"], help="SpMV entry storage")
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401
@@ -47,6 +48,7 @@ def main():
     N = n * n * nz
     ctx = Context(0)
     A = Mat.box_stencil(ctx, 3, n, n, nz)
+    A.set_storage(args.storage)
     rng = np.random.default_rng(1)
     w = Vec.from_array(ctx, rng.uniform(-1, 1, N))
     y = Vec(ctx, N)
