@@ -68,6 +68,8 @@ def parse():
     p.add_argument("--storage", default="dv", choices=["dv", "csr"],
                    help="entry storage of the assembled operator in HBM: dv (one byte per entry, the library's "
                         "choice for any matrix that fits; default) or csr (rowptr/col/val); bitwise the same products")
+    p.add_argument("--no-csr-compare", action="store_true",
+                   help="skip the untimed-in-value CSR-storage rerun that N=1 GMRES reports beside the DV figure")
     p.add_argument("--peclet", default=None,
                    help="Px,Py,Pz: the upwind convection-diffusion operator (configs[4]) instead of Poisson")
     a = p.parse_args()
@@ -266,6 +268,21 @@ def main():
     ctx.set_timing(False)
     stats = ctx.kernel_stats() if timing else {}
 
+    csr_same_run = None
+    if (variant == "gmres" and world == 1 and args.operator == "csr" and args.storage == "dv"
+            and not args.no_csr_compare):
+        # the same workload with the matrix in CSR storage, same process, after the timed region
+        A.set_storage("csr")
+        step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        its_c = sum(step() for _ in range(args.steps))
+        torch.cuda.synchronize()
+        el_c = time.perf_counter() - t1
+        A.set_storage("dv")
+        csr_same_run = {"matrix_storage": "csr", "value": float(rows) * its_c / el_c,
+                        "ms_per_step": 1e3 * el_c / args.steps}
+
     my_updates = float(rows) * its_total
     if world > 1:
         t = torch.tensor([elapsed, my_updates], dtype=torch.float64,
@@ -290,6 +307,8 @@ def main():
                           "parallelism": f"{world} z-slab block(s), one per GPU"}}
         if variant == "smsm":
             out["config"]["lsqr_iterations_per_step"] = lsqr_its[-args.steps:]
+        if csr_same_run:
+            out["same_run_csr_storage"] = csr_same_run
         if stats:
             total_ms = sum(s["ms"] for s in stats.values())
             dom = max(stats, key=lambda k: stats[k]["ms"])

@@ -39,6 +39,23 @@ def nv_of(name: str):
     return int(m.group(1)) if m else None
 
 
+def spmv_alg(name: str, n: int):
+    """Algorithmic bytes of one SpMV launch on the n^3 7-point operator, by kernel and mode:
+    DV-ELL W codes per row, CSR 12 per entry + rowptr; x read once, y written, b read in MatResidual."""
+    nm = name.replace(" ", "")
+    N = float(n) ** 3
+    nnz = 7.0 * N - 6.0 * n * n
+    m = re.search(r"k_spmv_ell<(\d+),(\d+),", nm)
+    if m:
+        mode, w = int(m.group(1)), int(m.group(2))
+        return w * N + 16.0 * N + (8.0 * N if mode == 1 else 0.0)
+    m = re.search(r"k_spmv_lds8<(\d+),", nm)
+    if m:
+        mode = int(m.group(1))
+        return 12.0 * nnz + 4.0 * (N + 1) + 16.0 * N + (8.0 * N if mode == 1 else 0.0)
+    return None
+
+
 def load(d, counter):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
@@ -85,6 +102,10 @@ def main():
                 alg = sum(8.0 * N * (nv + k) for nv in nvs) / m
         elif cls == "norm":
             alg = 8.0 * N
+        elif cls == "spmv":
+            als = [spmv_alg(nm, a.n) for nm, _ in F[:m]]
+            if all(als):
+                alg = sum(als) / m
         out["classes"][cls] = {"launches": m, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                                "hbm_bytes_per_launch": rd + wr, "alg_bytes_per_launch": alg,
                                "hbm_over_alg": (rd + wr) / alg if alg else None}

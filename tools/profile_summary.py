@@ -67,8 +67,10 @@ def main():
                  f"{(alg / 1e9) if alg else float('nan'):.4f} | {ratio if ratio else float('nan'):.4f} |")
     L += ["", f"maxpy: 8n(k+2) algorithmic = {rf['bytes_per_launch'] / 1e9:.4f} GB/launch on average "
           f"(bench.py's figure), PMC {tr['hbm_bytes_per_launch'] / 1e9:.4f}.",
-          "SpMV (scaled form: reads T, writes VV(it) and VV(it+1)): algorithmic 1.874 GB; PMC about 1.2x "
-          "(x gathers re-read across XCDs through the MALL).", "",
+          (f"SpMV ({b['config'].get('matrix_storage', 'csr')} storage; GMRES's scaled form reads T once and writes "
+           f"VV(it+1)): algorithmic {tr['classes']['spmv']['alg_bytes_per_launch'] / 1e9:.4f} GB/launch, PMC "
+           f"{tr['classes']['spmv']['hbm_over_alg']:.2f}x (x gathers re-read through the MALL)."
+           if tr['classes'].get('spmv', {}).get('alg_bytes_per_launch') else ""), "",
           "Other directories: `smsm/` (SMSM-global), `convdiff/`, `async/` (transports and async drivers), "
           "`configs/` (BASELINE configurations end to end), `spmv_ab/`, `skew_ab/`, earlier `*.json|csv` "
           "(first correct path, tuning history in DESIGN.md)."]
