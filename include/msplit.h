@@ -162,6 +162,13 @@ int msp_mat_get_info(const msp_mat *A, int32_t *nrows, int32_t *ncols, int64_t *
 #define MSP_STORAGE_DV 1
 int msp_mat_set_storage(msp_mat *A, int storage);
 int msp_mat_get_storage(const msp_mat *A, int *storage, int *ndict);
+/* Free the CSR arrays of a matrix in DV storage (col/val; rowptr too in the
+ * ELL layout): 12 bytes per entry of HBM back, e.g. 11.7 GB per GPU for a
+ * 1024^3 / 8 block.  MatMult, MatResidual, the GMRES products and, in the ELL
+ * layout, MatMatMult keep working on the DV storage; msp_mat_get_csr and
+ * msp_mat_set_storage(.., MSP_STORAGE_CSR) then return MSP_ERR_SUP.
+ * MSP_ERR_SUP on a matrix not in DV storage. */
+int msp_mat_release_csr(msp_mat *A);
 /* Download the CSR (host buffers of nrows+1 / nnz entries); synchronising. */
 int msp_mat_get_csr(const msp_mat *A, int32_t *rowptr, int32_t *col, double *val);
 /* MatMult y = A x (utils.c:626; KSP_PCApplyBAorAB inside KSPGMRESCycle). */

@@ -428,10 +428,17 @@ extern "C" int msp_mat_matmult_dense(msp_mat* A, const msp_dense* S, msp_dense* 
          "MatMatMult sizes: A %d x %d, S %lld x %d, R %lld x %d", nr, ncol, (long long)S->nrows, S->ncols,
          (long long)R->nrows, R->ncols);
   const mspi_csr_view v = mspi_mat_csr(A);
-  ARGCHK(v.rowptr, MSP_ERR_SUP, "MatMatMult needs a stored CSR operator (not a matrix-free one)");
-  ARGCHK(!v.compressed, MSP_ERR_SUP, "MatMatMult with a row-compressed matrix");
   msp_ctx* c = mspi_mat_ctx(A);
   if (nr == 0) return MSP_SUCCESS;
+  {  // DV storage (ELL): one byte per entry instead of 12
+    int st = 0;
+    msp_mat_get_storage(A, &st, nullptr);
+    if (st == MSP_STORAGE_DV && mspi_mat_spmm_dv(A, S->d, S->lda, S->ncols, S->nrows, R->d, R->lda) == MSP_SUCCESS)
+      return MSP_SUCCESS;
+  }
+  ARGCHK(v.rowptr && v.col, MSP_ERR_SUP, "MatMatMult needs a stored operator (not a matrix-free one, nor one whose "
+         "CSR was released without an ELL-layout DV storage)");
+  ARGCHK(!v.compressed, MSP_ERR_SUP, "MatMatMult with a row-compressed matrix");
   KTimer kt(c, MSP_KERNEL_SPMM,
             12.0 * (double)v.nnz + 4.0 * (nr + 1.0) + 8.0 * (double)S->ncols * ((double)S->nrows + (double)nr));
   if (v.lds_cap > 0) {  // CSR slice staged once per row block, columns streamed through it

@@ -50,6 +50,8 @@ typedef struct {
   int32_t lds_cap; /* LDS entries per 256-row block for the staged kernels (0: rows too long) */
 } mspi_csr_view;
 mspi_csr_view mspi_mat_csr(const msp_mat *A);
+/* R = A S over DV storage (ELL layout); MSP_ERR_SUP when A is not in it */
+int mspi_mat_spmm_dv(msp_mat *A, const double *S, int64_t lds, int nc, int64_t srows, double *R, int64_t ldr);
 
 /* dense row block, column-major, lda a multiple of 512 */
 struct msp_dense {

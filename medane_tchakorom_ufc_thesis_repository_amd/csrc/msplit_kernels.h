@@ -76,6 +76,9 @@ int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const
                 const int32_t* ddelta, const double* dval, int ndict, int32_t max_block, int ell_w,
                 const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
                 const int* stop, int64_t plane, hipStream_t s);
+// R[:, 0:nc] = A S[:, 0:nc] over DV storage in the ELL layout (W codes per row)
+int msk_spmm_ell(int32_t nrows, int W, const uint8_t* code8, const int32_t* ddelta, const double* dval, int ndict,
+                 const double* S, int64_t lds, int nc, double* R, int64_t ldr, hipStream_t s);
 int msk_ell_encode(int32_t nrows, int W, const int32_t* rowptr, const int32_t* col, const double* val, int ndict,
                    const int32_t* ddelta, const double* dval, uint8_t* code8, int* fail, hipStream_t s);
 // DV codes of an assembled CSR against a dictionary; *fail (device) set when it does not fit

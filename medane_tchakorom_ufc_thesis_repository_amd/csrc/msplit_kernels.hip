@@ -1154,6 +1154,51 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
   }
 }
 
+// MatMatMult R = A S over DV storage (ELL layout): lane per row, its codes
+// decoded once into (delta, value) registers, then every column of S streamed
+// past them; each R(r, q) is the CSR row sum of k_spmm_lds8 term for term.
+template <int W>
+__global__ __launch_bounds__(kT) void k_spmm_ell(int32_t nrows, const uint8_t* __restrict__ code8,
+                                                 const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
+                                                 int ndict, const double* __restrict__ S, int64_t lds, int nc,
+                                                 double* __restrict__ R, int64_t ldr) {
+  typedef EllWord<W> EW;
+  typedef typename EW::T CT;
+  __shared__ int32_t sdel[256];
+  __shared__ double sval[256];
+  const int t = threadIdx.x;
+  const int32_t r = (int32_t)blockIdx.x * kT + t;
+  const CT cw = r < nrows ? reinterpret_cast<const CT*>(code8)[r] : EW::empty();
+  if (t < ndict) {
+    sdel[t] = ddelta[t];
+    sval[t] = dval[t];
+  }
+  __syncthreads();
+  if (r >= nrows) return;
+  int32_t dl[W];
+  double av[W];
+  bool ok[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    const int c = EW::byte(cw, q);
+    ok[q] = c != 255;
+    dl[q] = ok[q] ? sdel[c] : 0;
+    av[q] = ok[q] ? sval[c] : 0.0;
+  }
+#pragma unroll 1
+  for (int j = 0; j < nc; ++j) {
+    const double* __restrict__ x = S + (int64_t)j * lds;
+    double xv[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) xv[q] = ok[q] ? x[r + dl[q]] : 0.0;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < W; ++q)
+      if (ok[q]) s = s + av[q] * xv[q];
+    R[r + (int64_t)j * ldr] = s;
+  }
+}
+
 // ELL-layout encode: row r's W codes, then 255 padding; *fail when a row is
 // longer than W or an entry is not in the dictionary (ndict <= 255).
 __global__ __launch_bounds__(kT) void k_ell_encode(int32_t nrows, int W, const int32_t* __restrict__ rowptr,
@@ -1429,6 +1474,17 @@ extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* 
     else MSK_DVB(MSK_SPMV_MULT, 4);
   }
 #undef MSK_DVB
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_spmm_ell(int32_t nrows, int W, const uint8_t* code8, const int32_t* ddelta, const double* dval,
+                            int ndict, const double* S, int64_t lds, int nc, double* R, int64_t ldr, hipStream_t s) {
+  if (nrows <= 0 || nc <= 0) return 0;
+  const unsigned g = (unsigned)((nrows + kT - 1) / kT);
+  if (W == 4) k_spmm_ell<4><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, S, lds, nc, R, ldr);
+  else if (W == 8) k_spmm_ell<8><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, S, lds, nc, R, ldr);
+  else if (W == 16) k_spmm_ell<16><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, S, lds, nc, R, ldr);
+  else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

@@ -388,6 +388,7 @@ struct msp_mat {
   int32_t dv_mb = 0;           // most entries in one 256-row block (sizes the LDS stage)
   int32_t dv_w = 0;            // ELL layout: codes per row (4, 8, 16); 0: CSR-order codes + row lengths
   bool dv_on = false;          // products read the DV storage
+  bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
 };
 
 extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
@@ -768,6 +769,7 @@ extern "C" int msp_mat_get_csr(const msp_mat* A, int32_t* rowptr, int32_t* col, 
   ARGCHK(A && !A->matfree, A ? MSP_ERR_SUP : MSP_ERR_ARG_NULL, "no stored CSR (matrix-free operator)");
   ARGCHK(A && rowptr, MSP_ERR_ARG_NULL, "NULL argument");
   ARGCHK(!A->compressed, MSP_ERR_SUP, "msp_mat_get_csr on a row-compressed matrix");
+  ARGCHK(!A->csr_released, MSP_ERR_SUP, "CSR storage released (msp_mat_release_csr)");
   hipStream_t s = A->ctx->stream;
   HIPCHK(hipMemcpyAsync(rowptr, A->rowptr, ((size_t)A->nrows + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   if (A->nnz) {
@@ -797,10 +799,39 @@ extern "C" int msp_mat_set_storage(msp_mat* A, int storage) {
   ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
   ARGCHK(storage == MSP_STORAGE_CSR || storage == MSP_STORAGE_DV, MSP_ERR_ARG_OUTOFRANGE, "unknown storage %d",
          storage);
+  ARGCHK(!(A->csr_released && storage == MSP_STORAGE_CSR), MSP_ERR_SUP, "CSR storage released (msp_mat_release_csr)");
   if (storage == MSP_STORAGE_DV)
     ARGCHK(A->ndict > 0, MSP_ERR_SUP, "matrix has no DV storage (more than 256 (col - row, value) pairs, a row "
            "longer than 255, or not an assembled square-block CSR)");
   A->dv_on = storage == MSP_STORAGE_DV;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_release_csr(msp_mat* A) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
+  if (A->csr_released) return MSP_SUCCESS;
+  ARGCHK(A->ndict > 0 && A->dv_on, MSP_ERR_SUP, "release_csr needs the matrix in DV storage");
+  HIPCHK(hipStreamSynchronize(A->ctx->stream));
+  if (A->col) HIPCHK(hipFree(A->col));
+  if (A->val) HIPCHK(hipFree(A->val));
+  A->col = nullptr;
+  A->val = nullptr;
+  if (A->dv_w) {  // the ELL layout reads no row pointers
+    if (A->rowptr) HIPCHK(hipFree(A->rowptr));
+    A->rowptr = nullptr;
+  }
+  A->lds_cap = A->lds_cap512 = 0;
+  A->csr_released = true;
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_mat_spmm_dv(msp_mat* A, const double* S, int64_t lds, int nc, int64_t srows, double* R,
+                                int64_t ldr) {
+  if (!A->dv_on || !A->dv_w) return MSP_ERR_SUP;
+  // codes once, S's columns read once, R written
+  KTimer kt(A->ctx, MSP_KERNEL_SPMM, (double)A->dv_w * A->nrows + 8.0 * nc * ((double)srows + A->nrows));
+  KCHK(msk_spmm_ell(A->nrows, A->dv_w, A->dv_code, A->dv_delta, A->dv_val, A->ndict, S, lds, nc, R, ldr,
+                    A->ctx->stream));
   return MSP_SUCCESS;
 }
 
@@ -880,7 +911,8 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
   msp_ctx* c = A->ctx;
   const int64_t n = A->nrows;
   const int64_t nch = nchunks_of(n);
-  if (A->matfree || A->compressed || A->nrows != A->ncols || A->lds_cap512 <= 0 || nv < 1 || nv > MSPI_MAX_GROUP ||
+  if (A->matfree || A->compressed || A->csr_released || A->nrows != A->ncols || A->lds_cap512 <= 0 || nv < 1 ||
+      nv > MSPI_MAX_GROUP ||
       nch == 0 || !(msk_get_tuning() & MSK_TUNE_GM_SPMV_MDOT))
     return MSP_ERR_SUP;
   int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);

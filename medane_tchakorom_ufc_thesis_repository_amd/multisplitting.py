@@ -43,6 +43,9 @@ class GpuBlock:
             self.A = Mat.box_matfree(ctx, dim, bx, by, bz, False, False, self.peclet)
         else:
             self.A = Mat.box_convdiff(ctx, dim, bx, by, bz, False, False, self.peclet)
+        # DV storage holds the operator in ~1 byte per entry; its CSR copy is freed unless -msplit_keep_csr
+        self._release_csr = not (opts is not None and opts.get_bool("msplit_keep_csr", False))
+        self._maybe_release_csr(self.A)
         row_ids, rowptr, col, val = layout.coupling
         self.A_off = Mat.from_csr_rows(ctx, n, layout.halo_size, row_ids, rowptr, col, val)
         self.halo, self.halo_t = comm.alloc(ctx, layout.halo_size)
@@ -136,6 +139,11 @@ class GpuBlock:
         dim, bx, by, bz = L.box
         self.A_ext = Mat.box_convdiff(self.ctx, dim, bx, by, bz, self.lo_rows > 0, self.hi_rows > 0,
                                       getattr(self, "peclet", (0.0, 0.0, 0.0)))
+        self._maybe_release_csr(self.A_ext)
+
+    def _maybe_release_csr(self, M):
+        if getattr(self, "_release_csr", False) and M.get_storage() == "dv":
+            M.release_csr()
 
     # -- local minimization (SMSM-local, AMAM-local) hooks
     def setup_local_minimization(self, s: int, opts: Options | None, prefix: str | None = None):

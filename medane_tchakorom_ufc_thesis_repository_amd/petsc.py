@@ -337,6 +337,10 @@ class Mat:
         call("msp_mat_get_storage", self.h, C.byref(st), C.byref(nd))
         return {v: k for k, v in self.STORAGE.items()}[st.value]
 
+    def release_csr(self):
+        """Free the CSR arrays of a matrix in DV storage (msp_mat_release_csr); products keep working."""
+        call("msp_mat_release_csr", self.h)
+
     def create_vecs(self):                                          # MatCreateVecs
         return Vec(self.ctx, self.shape[1]), Vec(self.ctx, self.shape[0])
 

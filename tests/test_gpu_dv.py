@@ -201,3 +201,67 @@ def test_layout_and_rows_per_lane_variants_bitwise(ctx, oracle, assembly, produc
         _products(ctx, A, O, r)
     finally:
         L.msk_set_tuning(0)
+
+
+@pytest.mark.parametrize("s", [1, 7, 20, 33])
+@pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 1.0)])
+def test_matmult_dense_on_dv_equals_csr_and_oracle(ctx, oracle, s, peclet):
+    """MatMatMult R = A_ext S (SMSM's R, SMSM-global.c:325-327) on DV storage: the CSR kernel's and the
+    oracle's row sums bit for bit."""
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import DenseMat
+    A = Mat.box_convdiff(ctx, 3, 12, 9, 7, True, True, peclet or (0.0, 0.0, 0.0))
+    rp, col, val = A.get_csr()
+    nr, nc = A.shape
+    S = np.random.default_rng(SEED + s).standard_normal((nc, s))
+    out = {}
+    for st in ("dv", "csr"):
+        A.set_storage(st)
+        Rd = DenseMat(ctx, nr, s)
+        A.mat_mult_dense(DenseMat.from_array(ctx, S), Rd)
+        out[st] = Rd.get_values()
+    O = oracle.Mat.from_arrays(nr, nc, rp, col, val)
+    ref = np.stack([O.mult(S[:, j]) for j in range(s)], axis=1)
+    assert np.array_equal(out["dv"], ref)
+    assert np.array_equal(out["csr"], ref)
+
+
+def test_release_csr(ctx, oracle):
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import DenseMat
+    A = Mat.box_stencil_ext(ctx, 3, 16, 12, 10, True, False)
+    rp, col, val = A.get_csr()
+    O = oracle.Mat.from_arrays(A.shape[0], A.shape[1], rp, col, val)
+    A.release_csr()
+    A.release_csr()                          # idempotent
+    assert A.get_storage() == "dv"
+    with pytest.raises(Exception):
+        A.get_csr()
+    with pytest.raises(Exception):
+        A.set_storage("csr")
+    _products(ctx, A, O, np.random.default_rng(SEED))
+    S = np.random.default_rng(SEED).standard_normal((A.shape[1], 5))
+    Rd = DenseMat(ctx, A.shape[0], 5)
+    A.mat_mult_dense(DenseMat.from_array(ctx, S), Rd)
+    assert np.array_equal(Rd.get_values(), np.stack([O.mult(S[:, j]) for j in range(5)], axis=1))
+    # a matrix in CSR storage cannot drop its CSR
+    B = Mat.box_stencil(ctx, 3, 8, 8, 8)
+    B.set_storage("csr")
+    with pytest.raises(Exception):
+        B.release_csr()
+
+
+def test_gmres_after_release_csr(ctx, oracle):
+    A = Mat.box_stencil(ctx, 3, 20, 16, 12)
+    A.release_csr()
+    n = A.shape[0]
+    ones, b, x = Vec(ctx, n), Vec(ctx, n), Vec(ctx, n)
+    ones.set(1.0)
+    A.mult(ones, b)
+    ksp = KSP(ctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options("-ksp_gmres_restart 30 -ksp_max_it 70 -ksp_rtol 1e-12 -pc_type none"))
+    ksp.solve(b, x)
+    Ao = oracle.poisson3d_rows(20, 16, 12, 0, 12)
+    xo, ro = oracle.gmres(Ao, b.get_array(), restart=30, max_it=70, rtol=1e-12, reduce_mode=oracle.REDUCE_DBR)
+    assert ksp.get_iteration_number() == ro["its"]
+    assert np.array_equal(ksp.get_residual_history(), ro["hist"])
+    assert np.array_equal(x.get_array(), xo)
