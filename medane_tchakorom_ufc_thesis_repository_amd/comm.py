@@ -85,6 +85,8 @@ class TorchComm:
         from .petsc import Vec
         if self.device_buffers:
             t = self.torch.zeros(max(int(n), 2), dtype=self.torch.float64, device=self.device)
+            # the zero fill runs on torch's stream; the library writes the buffer on its own
+            self.torch.cuda.current_stream(self.device).synchronize()
             return Vec(ctx, n, device_ptr=t.data_ptr()), t
         return Vec(ctx, n), self.torch.zeros(max(int(n), 2), dtype=self.torch.float64)
 
