@@ -38,8 +38,24 @@
 #include "msplit.h"
 #include "msplit_internal.h"
 
+/* Captured restart cycles (HIP graphs), keyed by everything the capture baked
+ * in: the operator and the kernels its products launch, x, the cycle length
+ * K and the tuning flags.  The basis, W and the device state are fixed
+ * between ksp_free_work calls, which drop the cache. */
+#define KSP_NGRAPH 4
+typedef struct {
+  void *exec;
+  const msp_mat *A;
+  uint64_t aver;
+  const double *x;
+  int K, tuning;
+} ksp_graph;
+
 struct msp_ksp {
   msp_ctx *ctx;
+  ksp_graph graphs[KSP_NGRAPH];
+  int gnext;
+  int graphs_off; /* a capture failed on this KSP's stream (e.g. the legacy null stream): eager from then on */
   msp_mat *A;
   msp_ksp_opts o;
   int setup;
@@ -88,7 +104,16 @@ int msp_ksp_create(msp_ctx *ctx, msp_ksp **out) {
   return MSP_SUCCESS;
 }
 
+static void ksp_drop_graphs(msp_ksp *k) {
+  for (int i = 0; i < KSP_NGRAPH; ++i) {
+    mspi_graph_destroy(k->graphs[i].exec);
+    memset(&k->graphs[i], 0, sizeof(k->graphs[i]));
+  }
+  k->gnext = 0;
+}
+
 static void ksp_free_work(msp_ksp *k) {
+  ksp_drop_graphs(k);
   if (k->basis) mspi_free(k->ctx, k->basis);
   if (k->tmp) mspi_free(k->ctx, k->tmp);
   if (k->gblock) mspi_free(k->ctx, k->gblock);
@@ -128,6 +153,7 @@ int msp_ksp_set_operators(msp_ksp *k, msp_mat *A) {
     return MSP_ERR_ARG_WRONG;
   }
   if (k->A && k->n != nr) ksp_free_work(k);
+  if (k->A != A) ksp_drop_graphs(k);
   k->A = A;
   k->n = nr;
   return MSP_SUCCESS;
@@ -234,6 +260,46 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
   return rc;
 }
 
+/* A cycle from the graph cache: captured the first time its key is seen, then
+ * replayed with one hipGraphLaunch (the host enqueues ~5 launches per Arnoldi
+ * step otherwise, which small systems feel).  Same kernels, same arguments,
+ * same order: results are those of the eager enqueue. */
+static int run_cycle(msp_ksp *k, double *x, int K) {
+  msp_ctx *c = k->ctx;
+  if (k->graphs_off || !mspi_graphs_enabled(c)) return enqueue_cycle(k, x, K);
+  const uint64_t aver = mspi_mat_version(k->A);
+  const int tuning = msk_get_tuning();
+  for (int i = 0; i < KSP_NGRAPH; ++i) {
+    const ksp_graph *g = &k->graphs[i];
+    if (g->exec && g->A == k->A && g->aver == aver && g->x == x && g->K == K && g->tuning == tuning)
+      return mspi_graph_launch(c, g->exec);
+  }
+  int rc = mspi_reserve_partial(c, k->n);
+  if (rc) return rc;
+  if (mspi_capture_begin(c)) { /* stream cannot be captured: run it eagerly */
+    k->graphs_off = 1;
+    return enqueue_cycle(k, x, K);
+  }
+  rc = enqueue_cycle(k, x, K);
+  void *exec = NULL;
+  const int rc2 = mspi_capture_end(c, rc == 0, &exec);
+  if (rc) return rc;
+  if (rc2 || !exec) { /* nothing ran: the capture only recorded the cycle */
+    k->graphs_off = 1;
+    return enqueue_cycle(k, x, K);
+  }
+  ksp_graph *g = &k->graphs[k->gnext];
+  k->gnext = (k->gnext + 1) % KSP_NGRAPH;
+  mspi_graph_destroy(g->exec);
+  g->exec = exec;
+  g->A = k->A;
+  g->aver = aver;
+  g->x = x;
+  g->K = K;
+  g->tuning = tuning;
+  return mspi_graph_launch(c, exec);
+}
+
 int msp_ksp_solve(msp_ksp *k, const msp_vec *b, msp_vec *x) {
   if (!k || !b || !x) {
     mspi_set_error(MSP_ERR_ARG_NULL, "NULL argument");
@@ -291,7 +357,7 @@ int msp_ksp_solve(msp_ksp *k, const msp_vec *b, msp_vec *x) {
     int K = k->o.max_it - its;
     if (K > k->o.restart) K = k->o.restart;
     if (K < 0) K = 0;
-    if ((rc = enqueue_cycle(k, x->d, K))) return rc;
+    if ((rc = run_cycle(k, x->d, K))) return rc;
     if ((rc = mspi_d2h_sync(c, h, k->g.st, sizeof(*h)))) return rc; /* the one sync per cycle */
     its = h->its;
     reason = h->reason;

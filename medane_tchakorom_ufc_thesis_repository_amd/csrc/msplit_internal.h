@@ -139,6 +139,19 @@ int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv,
 int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const double *base, int64_t stride,
                            const double *scale, int64_t n, const double *coef_dev, int nv_expected);
 int mspi_h2d_async(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
+/* ---- HIP graphs of enqueued work (a GMRES restart cycle is replayed as one graph launch) ---- */
+/* 1 unless MSPLIT_GRAPHS=0 or per-kernel timing is on (its events need eager launches) */
+int mspi_graphs_enabled(msp_ctx *ctx);
+/* the DBR partial buffer sized for n-element work, so nothing allocates during a capture */
+int mspi_reserve_partial(msp_ctx *ctx, int64_t n);
+int mspi_capture_begin(msp_ctx *ctx);
+/* ok = 0: the enqueue failed, end and drop the capture; *exec receives the instantiated graph otherwise */
+int mspi_capture_end(msp_ctx *ctx, int ok, void **exec);
+int mspi_graph_launch(msp_ctx *ctx, void *exec);
+void mspi_graph_destroy(void *exec);
+/* changes whenever the kernels a product of A launches change (storage switch, CSR release) */
+uint64_t mspi_mat_version(const msp_mat *A);
+int msk_get_tuning(void);
 int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 /* ---- HBM mailboxes shared between processes (msplit_ipc.hip) ---- */
 #define MSPI_IPC_HANDLE_BYTES 64

@@ -389,6 +389,7 @@ struct msp_mat {
   int32_t dv_w = 0;            // ELL layout: codes per row (4, 8, 16); 0: CSR-order codes + row lengths
   bool dv_on = false;          // products read the DV storage
   bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
+  uint64_t version = 0;        // bumped when the kernels its products launch change (captured graphs)
 };
 
 extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
@@ -804,6 +805,7 @@ extern "C" int msp_mat_set_storage(msp_mat* A, int storage) {
     ARGCHK(A->ndict > 0, MSP_ERR_SUP, "matrix has no DV storage (more than 256 (col - row, value) pairs, a row "
            "longer than 255, or not an assembled square-block CSR)");
   A->dv_on = storage == MSP_STORAGE_DV;
+  A->version++;
   return MSP_SUCCESS;
 }
 
@@ -822,7 +824,51 @@ extern "C" int msp_mat_release_csr(msp_mat* A) {
   }
   A->lds_cap = A->lds_cap512 = 0;
   A->csr_released = true;
+  A->version++;
   return MSP_SUCCESS;
+}
+
+extern "C" uint64_t mspi_mat_version(const msp_mat* A) { return A->version; }
+
+extern "C" int mspi_graphs_enabled(msp_ctx* c) {
+  if (c->timing) return 0;
+  const char* e = getenv("MSPLIT_GRAPHS");
+  return !(e && e[0] == '0');
+}
+
+extern "C" int mspi_reserve_partial(msp_ctx* c, int64_t n) {
+  return ensure_partial(c, std::max<int64_t>(nchunks_of(n), 1) * MSPI_MAX_GROUP);
+}
+
+extern "C" int mspi_capture_begin(msp_ctx* c) {
+  HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_capture_end(msp_ctx* c, int ok, void** exec) {
+  hipGraph_t g = nullptr;
+  *exec = nullptr;
+  const hipError_t e = hipStreamEndCapture(c->stream, &g);
+  if (!ok) {
+    if (g) (void)hipGraphDestroy(g);
+    return MSP_SUCCESS;
+  }
+  HIPCHK(e);
+  hipGraphExec_t x = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  HIPCHK(ei);
+  *exec = (void*)x;
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_graph_launch(msp_ctx* c, void* exec) {
+  HIPCHK(hipGraphLaunch((hipGraphExec_t)exec, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" void mspi_graph_destroy(void* exec) {
+  if (exec) (void)hipGraphExecDestroy((hipGraphExec_t)exec);
 }
 
 extern "C" int mspi_mat_spmm_dv(msp_mat* A, const double* S, int64_t lds, int nc, int64_t srows, double* R,
