@@ -39,14 +39,14 @@
 #include "msplit_internal.h"
 
 /* Captured restart cycles (HIP graphs), keyed by everything the capture baked
- * in: the operator and the kernels its products launch, x, the cycle length
- * K and the tuning flags.  The basis, W and the device state are fixed
+ * in: the operator and the kernels its products launch, the context's DBR
+ * partial buffer (its epoch), x, the cycle length K and the tuning flags.  The basis, W and the device state are fixed
  * between ksp_free_work calls, which drop the cache. */
 #define KSP_NGRAPH 4
 typedef struct {
   void *exec;
   const msp_mat *A;
-  uint64_t aver;
+  uint64_t aver, epoch;
   const double *x;
   int K, tuning;
 } ksp_graph;
@@ -240,7 +240,16 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
   double *sumsq = &k->g.h[0];
   int rc = mspi_norm2sq(c, VV(k, 0), k->n, sumsq);
   if (!rc) rc = mspi_gm_cycle_start(c, k->g, sumsq);
-  for (int it = 0; it < K && !rc; ++it) {
+  const int opfuse = mspi_op_fusable(k->A) && k->o.restart + 1 <= MSPI_MAX_GROUP;
+  for (int it = 0; it < K && !rc && opfuse; ++it) {
+    /* W = A (sc[it] VV(it)) never reaches HBM: MDot and MAXPY each compute their rows of it from the operator's
+     * one-byte codes and VV(it) (which both stream anyway), bitwise the separate MatMult's W */
+    rc = mspi_mdot_op(k->A, VV(k, it), sc + it, it + 1, k->basis, k->stride, sc, k->g.h, stop);
+    if (!rc)
+      rc = mspi_maxpy_norm_update_op(k->A, VV(k, it), sc + it, VV(k, it + 1), it + 1, k->basis, k->stride, sc, k->g,
+                                     k->o.restart, stop);
+  }
+  for (int it = 0; it < K && !rc && !opfuse; ++it) {
     /* W = A (sc[it] VV(it))  (KSP_PCApplyBAorAB with PCNONE on the normalised VV(it)),
      * CGS: h = VecMDot(W, VV(0..it)) -- one fused launch where the operator allows */
     rc = mspi_spmv_mdot(k->A, VV(k, it), sc + it, k->tmp, it + 1, k->basis, k->stride, sc, k->g.h, stop);
@@ -267,15 +276,16 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
 static int run_cycle(msp_ksp *k, double *x, int K) {
   msp_ctx *c = k->ctx;
   if (k->graphs_off || !mspi_graphs_enabled(c)) return enqueue_cycle(k, x, K);
-  const uint64_t aver = mspi_mat_version(k->A);
+  int rc = mspi_reserve_partial(c, k->n); /* before the lookup: it may reallocate (a new epoch) */
+  if (rc) return rc;
+  const uint64_t aver = mspi_mat_version(k->A), epoch = mspi_ctx_epoch(c);
   const int tuning = msk_get_tuning();
   for (int i = 0; i < KSP_NGRAPH; ++i) {
     const ksp_graph *g = &k->graphs[i];
-    if (g->exec && g->A == k->A && g->aver == aver && g->x == x && g->K == K && g->tuning == tuning)
+    if (g->exec && g->A == k->A && g->aver == aver && g->epoch == epoch && g->x == x && g->K == K &&
+        g->tuning == tuning)
       return mspi_graph_launch(c, g->exec);
   }
-  int rc = mspi_reserve_partial(c, k->n);
-  if (rc) return rc;
   if (mspi_capture_begin(c)) { /* stream cannot be captured: run it eagerly */
     k->graphs_off = 1;
     return enqueue_cycle(k, x, K);
@@ -294,6 +304,7 @@ static int run_cycle(msp_ksp *k, double *x, int K) {
   g->exec = exec;
   g->A = k->A;
   g->aver = aver;
+  g->epoch = epoch;
   g->x = x;
   g->K = K;
   g->tuning = tuning;

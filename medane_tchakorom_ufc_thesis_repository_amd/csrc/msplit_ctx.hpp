@@ -54,6 +54,7 @@ struct msp_ctx {
   double* hscratch = nullptr;  // pinned host scalars
   double* partial = nullptr;   // DBR stage-1 partials
   int64_t partial_cap = 0;     // doubles
+  uint64_t epoch = 0;          // bumped when a buffer captured graphs point at is reallocated
   bool timing = false;
   std::vector<hipEvent_t> pool;
   size_t pool_used = 0;
@@ -94,6 +95,7 @@ static inline int ensure_partial(msp_ctx* c, int64_t need) {
   c->partial_cap = 0;
   HIPCHK(hipMalloc((void**)&c->partial, (size_t)need * sizeof(double)));
   c->partial_cap = need;
+  c->epoch++;
   return MSP_SUCCESS;
 }
 

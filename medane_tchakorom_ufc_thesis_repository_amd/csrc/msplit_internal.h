@@ -139,6 +139,15 @@ int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv,
 int mspi_maxpy_accum_basis(msp_ctx *ctx, double *x, const int *nvdev, const double *base, int64_t stride,
                            const double *scale, int64_t n, const double *coef_dev, int nv_expected);
 int mspi_h2d_async(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
+/* ---- the GMRES step's MatMult inside the CGS kernels (A in DV storage, 8-code ELL layout) ---- */
+int mspi_op_fusable(const msp_mat *A);
+/* h(0..nv-1) = (A (sdev[0] x)) . scale_j VV(j): stage 1 computes each row of A(sc x) in registers */
+int mspi_mdot_op(msp_mat *A, const double *x, const double *sdev, int nv, const double *base, int64_t stride,
+                 const double *scale, double *out_dev, const int *stop);
+/* VV(it+1) = A (sdev[0] x) - sum_j h_j scale_j VV(j), ||VV(it+1)||^2, then the Hessenberg update */
+int mspi_maxpy_norm_update_op(msp_mat *A, const double *x, const double *sdev, double *wout, int nv,
+                              const double *base, int64_t stride, const double *scale, mspi_gmres_dev g, int m,
+                              const int *stop);
 /* ---- HIP graphs of enqueued work (a GMRES restart cycle is replayed as one graph launch) ---- */
 /* 1 unless MSPLIT_GRAPHS=0 or per-kernel timing is on (its events need eager launches) */
 int mspi_graphs_enabled(msp_ctx *ctx);
@@ -151,6 +160,8 @@ int mspi_graph_launch(msp_ctx *ctx, void *exec);
 void mspi_graph_destroy(void *exec);
 /* changes whenever the kernels a product of A launches change (storage switch, CSR release) */
 uint64_t mspi_mat_version(const msp_mat *A);
+/* changes whenever a context buffer that enqueued work points at (the DBR partials) is reallocated */
+uint64_t mspi_ctx_epoch(const msp_ctx *ctx);
 int msk_get_tuning(void);
 int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 /* ---- HBM mailboxes shared between processes (msplit_ipc.hip) ---- */

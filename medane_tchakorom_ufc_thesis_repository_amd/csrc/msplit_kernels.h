@@ -23,6 +23,16 @@ struct Vecs {
 struct Coefs {
   double a[MSK_MAX_GROUP];
 };
+// W = A (sc * x) computed where it is consumed (the GMRES step's MatMult fused
+// into the CGS kernels): A in DV storage, ELL layout with 8 codes per row.
+struct EllOp {
+  const uint8_t* code8;   // nrows * 8 codes (+16 pad)
+  const int32_t* ddelta;  // dictionary: col - row
+  const double* dval;     //             value
+  int ndict;              // <= 255
+  const double* x;        // VV(it), stored unnormalised
+  const double* sdev;     // its scale sc[it] (device)
+};
 // constant 7-point stencil values: slow-, y-, x-, diagonal, x+, y+, slow+
 struct BoxCoef {
   double c[7];
@@ -47,13 +57,20 @@ enum {
   MSK_TUNE_SPMV_MDOT_G2 = 4096,     // k_spmv_mdot: two basis vectors per load group instead of four
   MSK_TUNE_DV_RPL1 = 8192,          // DV SpMV: one row per lane (256-row blocks)
   MSK_TUNE_DV_RPL2 = 16384,         // DV SpMV: two rows per lane (512-row blocks); default four
-  MSK_TUNE_DV_NOELL = 32768         // DV storage: CSR-order codes even where the ELL layout fits (at assembly)
+  MSK_TUNE_DV_NOELL = 32768,        // DV storage: CSR-order codes even where the ELL layout fits (at assembly)
+  MSK_TUNE_GM_OPFUSE = 65536        // GMRES: W = A (sc x) computed inside MDot and MAXPY instead of a MatMult kernel
 };
 
 extern "C" {
 void msk_set_tuning(int flags);
 int msk_get_tuning(void);
 void msk_set_spmv_group(int gb);
+// The CGS block with W = A (sc x) computed in the kernel (op) instead of read from w: stage 1 of
+// W . V_v (v < nv <= 32), and the MAXPY wout = W - sum_j adev_j V_j with the ||wout||^2 partials.
+int msk_dot_stage1_op(const EllOp* op, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
+                      const int* stop, hipStream_t s);
+int msk_maxpy_op(const EllOp* op, double* wout, const Vecs* V, int nv, const double* adev, int64_t n,
+                 double* partial, const int* stop, hipStream_t s);
 // DBR stage 1 over nv <= 32 vectors (self: ||w||^2).  stop: device flag, skip when set (may be null).
 int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks, int self,
                    const int* stop, hipStream_t s);

@@ -46,6 +46,64 @@ __device__ __forceinline__ const double* vec_at(const Vecs& V, int j) {
 // is exact for every double, so unscaled sets multiply by 1.0 (wave-uniform load)
 __device__ __forceinline__ double vec_scale(const Vecs& V, int j) { return V.scale ? V.scale[j] : 1.0; }
 
+// ---------------------------------------------- W = A (sc x) in the CGS kernels
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+// Stage the DV dictionary in LDS (the caller synchronises before use).
+__device__ __forceinline__ void ell_dict_stage(const EllOp& op, int32_t* sdel, double* sval) {
+  const int t = threadIdx.x;
+  if (t < op.ndict) {
+    sdel[t] = op.ddelta[t];
+    sval[t] = op.dval[t];
+  } else {
+    sdel[t] = 0;  // code 255 (no entry) and unused codes: delta 0, never added
+    sval[t] = 0.0;
+  }
+}
+
+// The lane's W values at its DBR positions base + j*512 + {0,1}, j in [J0, J0+JN):
+// rows e, e+1 read their 2 x 8 codes with one 16-byte load, then every gather
+// of the pair is issued before the first product (padding entries gather x[0]
+// and are masked out).  Each row sums val * (x * sc) over its entries in CSR
+// order from 0.0 -- k_spmv_ell's SCALED sum, term for term.  Rows >= n: 0.
+template <int J0, int JN>
+__device__ __forceinline__ void ell_rows(const EllOp& op, const int32_t* sdel, const double* sval, double sc,
+                                         int64_t base, int64_t n, double (&wr)[2 * kIters]) {
+#pragma unroll
+  for (int j = J0; j < J0 + JN; ++j) {
+    const int64_t e = base + j * (2 * kT);
+    u32x4v cw = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (e + 1 < n) {
+      cw = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(op.code8 + e * 8));
+    } else if (e < n) {
+      cw.x = reinterpret_cast<const uint32_t*>(op.code8 + e * 8)[0];
+      cw.y = reinterpret_cast<const uint32_t*>(op.code8 + e * 8)[1];
+    }
+    int32_t ix[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t w4 = q < 4 ? cw.x : q < 8 ? cw.y : q < 12 ? cw.z : cw.w;
+      const int c = (w4 >> (8 * (q & 3))) & 255;
+      ix[q] = c != 255 ? (int32_t)(e + (q >> 3)) + sdel[c] : 0;
+    }
+    double xv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) xv[q] = op.x[ix[q]];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 8 * h; q < 8 * h + 8; ++q) {
+        const uint32_t w4 = q < 4 ? cw.x : q < 8 ? cw.y : q < 12 ? cw.z : cw.w;
+        const int c = (w4 >> (8 * (q & 3))) & 255;
+        const double sn = acc + sval[c] * (xv[q] * sc);
+        acc = c != 255 ? sn : acc;
+      }
+      wr[2 * j + h] = acc;
+    }
+  }
+}
+
 __device__ __forceinline__ double wave_butterfly(double v) {
   // v[l] <- v[l] + v[l ^ off], off = 32..1: every lane ends with the same sum.
 #pragma unroll
@@ -112,15 +170,18 @@ __device__ __forceinline__ void dot_group_full(const double (&wr)[2 * kIters], c
 // +7.7 % per GMRES step on 256^3, same-box A/B); bit 2 = non-temporal store
 // of w in MAXPY; bit 4 = vectors one at a time in MDot (A/B of the grouped loads).
 // Results are identical.
-template <int NV, bool SELF, int VAR>
+template <int NV, bool SELF, int VAR, bool OPW = false>
 __device__ __forceinline__ void dot_chunk(const double* __restrict__ w, const Vecs& V, int64_t n,
                                           double* __restrict__ partial, int64_t nchunks, int rev, int64_t c,
-                                          double (&red)[NV][4]) {
+                                          double (&red)[NV][4], const EllOp* op = nullptr,
+                                          const int32_t* sdel = nullptr, const double* sval = nullptr) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t base = c * kChunk + 2 * t;
   const bool full = (c + 1) * kChunk <= n;
   double wr[2 * kIters];
-  if (full) {
+  if constexpr (OPW) {
+    ell_rows<0, kIters>(*op, sdel, sval, *op->sdev, base, n, wr);
+  } else if (full) {
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
       const double2 q = *reinterpret_cast<const double2*>(w + base + j * (2 * kT));
@@ -201,6 +262,19 @@ __global__ __launch_bounds__(kT) void k_dot_stage1(const double* __restrict__ w,
   if (stopped(stop)) return;
   __shared__ double red[NV][4];
   dot_chunk<NV, SELF, VAR>(w, V, n, partial, nchunks, rev, blockIdx.x, red);
+}
+
+// Stage 1 with W = A (sc x) computed in the kernel (no W vector in HBM).
+template <int NV, int VAR>
+__global__ __launch_bounds__(kT) void k_dot_stage1_op(EllOp op, Vecs V, int64_t n, double* __restrict__ partial,
+                                                      int64_t nchunks, const int* __restrict__ stop) {
+  __shared__ double red[NV][4];
+  __shared__ int32_t sdel[kT];
+  __shared__ double sval[kT];
+  ell_dict_stage(op, sdel, sval);
+  if (stopped(stop)) return;  // uniform: every lane reads the same flag
+  __syncthreads();
+  dot_chunk<NV, false, VAR, true>(nullptr, V, n, partial, nchunks, 0, blockIdx.x, red, &op, sdel, sval);
 }
 
 // Stage 2: workgroup v folds the nchunks partials of vector v the same way.
@@ -292,24 +366,30 @@ __device__ __forceinline__ void chunk_group(double (&u)[2 * kIters], const Vecs&
 // vector group over it, store and add its squares to acc in j order.  The
 // chunk is one slice (VAR bit 3 clear) or two halves one after the other (set:
 // half the registers, twice the waves per SIMD); per element nothing changes.
-template <bool ACCUM, bool NORM, bool FULL, int VAR, int J0, int JN>
+template <bool ACCUM, bool NORM, bool FULL, int VAR, int J0, int JN, bool OPW = false>
 __device__ __forceinline__ void maxpy_slice(const double* __restrict__ win, double* __restrict__ wout,
                                             const Vecs& V, const Coefs& A, const double* __restrict__ adev,
-                                            int negate, int nv, int64_t base, int64_t n, double& acc) {
+                                            int negate, int nv, int64_t base, int64_t n, double& acc,
+                                            const EllOp* op = nullptr, const int32_t* sdel = nullptr,
+                                            const double* sval = nullptr) {
   double u[2 * kIters];
+  if constexpr (OPW) {
+    ell_rows<J0, JN>(*op, sdel, sval, *op->sdev, base, n, u);
+  } else {
 #pragma unroll
-  for (int j = J0; j < J0 + JN; ++j) {
-    const int64_t e = base + j * (2 * kT);
-    if (ACCUM) {
-      u[2 * j] = 0.0;
-      u[2 * j + 1] = 0.0;
-    } else if (FULL) {
-      const double2 q = *reinterpret_cast<const double2*>(win + e);
-      u[2 * j] = q.x;
-      u[2 * j + 1] = q.y;
-    } else {
-      u[2 * j] = e < n ? win[e] : 0.0;
-      u[2 * j + 1] = e + 1 < n ? win[e + 1] : 0.0;
+    for (int j = J0; j < J0 + JN; ++j) {
+      const int64_t e = base + j * (2 * kT);
+      if (ACCUM) {
+        u[2 * j] = 0.0;
+        u[2 * j + 1] = 0.0;
+      } else if (FULL) {
+        const double2 q = *reinterpret_cast<const double2*>(win + e);
+        u[2 * j] = q.x;
+        u[2 * j + 1] = q.y;
+      } else {
+        u[2 * j] = e < n ? win[e] : 0.0;
+        u[2 * j + 1] = e + 1 < n ? win[e + 1] : 0.0;
+      }
     }
   }
   const int jrem = nv & 3;
@@ -355,16 +435,21 @@ __device__ __forceinline__ void maxpy_slice(const double* __restrict__ win, doub
   }
 }
 
-template <bool ACCUM, bool NORM, bool FULL, int VAR>
+template <bool ACCUM, bool NORM, bool FULL, int VAR, bool OPW = false>
 __device__ __forceinline__ void maxpy_chunk_body(const double* __restrict__ win, double* __restrict__ wout,
                                                  const Vecs& V, const Coefs& A, const double* __restrict__ adev,
-                                                 int negate, int nv, int64_t base, int64_t n, double& sq) {
+                                                 int negate, int nv, int64_t base, int64_t n, double& sq,
+                                                 const EllOp* op = nullptr, const int32_t* sdel = nullptr,
+                                                 const double* sval = nullptr) {
   double acc = 0.0;
   if constexpr ((VAR & 8) != 0) {
-    maxpy_slice<ACCUM, NORM, FULL, VAR, 0, kIters / 2>(win, wout, V, A, adev, negate, nv, base, n, acc);
-    maxpy_slice<ACCUM, NORM, FULL, VAR, kIters / 2, kIters / 2>(win, wout, V, A, adev, negate, nv, base, n, acc);
+    maxpy_slice<ACCUM, NORM, FULL, VAR, 0, kIters / 2, OPW>(win, wout, V, A, adev, negate, nv, base, n, acc, op,
+                                                            sdel, sval);
+    maxpy_slice<ACCUM, NORM, FULL, VAR, kIters / 2, kIters / 2, OPW>(win, wout, V, A, adev, negate, nv, base, n,
+                                                                     acc, op, sdel, sval);
   } else {
-    maxpy_slice<ACCUM, NORM, FULL, VAR, 0, kIters>(win, wout, V, A, adev, negate, nv, base, n, acc);
+    maxpy_slice<ACCUM, NORM, FULL, VAR, 0, kIters, OPW>(win, wout, V, A, adev, negate, nv, base, n, acc, op, sdel,
+                                                        sval);
   }
   sq = acc;
 }
@@ -390,6 +475,32 @@ __global__ __launch_bounds__(kT) void k_maxpy_chunk(const double* win, double* w
     __syncthreads();
     if (t == 0) partial[c] = (red[0] + red[1]) + (red[2] + red[3]);
   }
+}
+
+// CGS VecMAXPY with W = A (sc x) computed in the kernel, and the ||w||^2 partials.
+template <int VAR>
+__global__ __launch_bounds__(kT) void k_maxpy_op(EllOp op, double* wout, Vecs V, const double* __restrict__ adev,
+                                                 int nv, int64_t n, double* __restrict__ partial,
+                                                 const int* __restrict__ stop) {
+  __shared__ int32_t sdel[kT];
+  __shared__ double sval[kT];
+  __shared__ double red[4];
+  ell_dict_stage(op, sdel, sval);
+  if (stopped(stop)) return;  // uniform
+  __syncthreads();
+  const int t = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const int64_t base = c * kChunk + 2 * t;
+  const Coefs A = {};
+  double sq = 0.0;
+  if ((c + 1) * kChunk <= n)
+    maxpy_chunk_body<false, true, true, VAR, true>(nullptr, wout, V, A, adev, 1, nv, base, n, sq, &op, sdel, sval);
+  else
+    maxpy_chunk_body<false, true, false, VAR, true>(nullptr, wout, V, A, adev, 1, nv, base, n, sq, &op, sdel, sval);
+  sq = wave_butterfly(sq);
+  if ((t & 63) == 0) red[t >> 6] = sq;
+  __syncthreads();
+  if (t == 0) partial[c] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ------------------------------------------------------------------- SpMV
@@ -1343,6 +1454,38 @@ extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n,
   else if (var == 17) dot1_dispatch<1, 17>(nv, w, *V, n, partial, nchunks, stop, s);
   else if (var == 16) dot1_dispatch<1, 16>(nv, w, *V, n, partial, nchunks, stop, s);
   else dot1_dispatch<1, 0>(nv, w, *V, n, partial, nchunks, stop, s);
+  return (int)hipGetLastError();
+}
+
+template <int NV, int VAR>
+static void dot1_op_dispatch(int nv, const EllOp& op, const Vecs& V, int64_t n, double* partial, int64_t nchunks,
+                             const int* stop, hipStream_t s) {
+  if (nv == NV) {
+    k_dot_stage1_op<NV, VAR><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(op, V, n, partial, nchunks, stop);
+  } else if constexpr (NV < MSK_MAX_GROUP) {
+    dot1_op_dispatch<NV + 1, VAR>(nv, op, V, n, partial, nchunks, stop, s);
+  }
+}
+
+extern "C" int msk_dot_stage1_op(const EllOp* op, const Vecs* V, int nv, int64_t n, double* partial,
+                                 int64_t nchunks, const int* stop, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  if (nv < 1 || nv > MSK_MAX_GROUP || op->ndict > 255) return (int)hipErrorInvalidValue;
+  if (vec_var()) dot1_op_dispatch<1, 1>(nv, *op, *V, n, partial, nchunks, stop, s);
+  else dot1_op_dispatch<1, 0>(nv, *op, *V, n, partial, nchunks, stop, s);
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_maxpy_op(const EllOp* op, double* wout, const Vecs* V, int nv, const double* adev, int64_t n,
+                            double* partial, const int* stop, hipStream_t s) {
+  if (n <= 0 || nv <= 0) return 0;
+  if (op->ndict > 255) return (int)hipErrorInvalidValue;
+  const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
+  const int var = vec_var() | ((g_tuning & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4);
+  if (var == 5) k_maxpy_op<5><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
+  else if (var == 4) k_maxpy_op<4><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
+  else if (var == 1) k_maxpy_op<1><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
+  else k_maxpy_op<0><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
   return (int)hipGetLastError();
 }
 

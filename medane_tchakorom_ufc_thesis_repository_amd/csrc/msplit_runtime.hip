@@ -829,6 +829,71 @@ extern "C" int msp_mat_release_csr(msp_mat* A) {
 }
 
 extern "C" uint64_t mspi_mat_version(const msp_mat* A) { return A->version; }
+extern "C" uint64_t mspi_ctx_epoch(const msp_ctx* c) { return c->epoch; }
+
+// The GMRES step's MatMult folded into the CGS kernels (MSK_TUNE_GM_OPFUSE): A
+// square, in DV storage with the 8-code ELL layout.  Bitwise the separate
+// MatMult, and it saves W's 24 bytes per row, but measured 26 % slower per
+// GMRES step (MDot 6.7 -> 4.3 TB/s): at the 2-3 waves per SIMD the CGS kernels
+// run at, the far (+-plane) gathers of each row pair are 8 exposed round trips
+// per workgroup, which the standalone SpMV hides with 6-8 waves.
+extern "C" int mspi_op_fusable(const msp_mat* A) {
+  return A && A->dv_on && A->dv_w == 8 && A->ndict <= 255 && A->nrows == A->ncols && A->nrows > 0 &&
+         (msk_get_tuning() & MSK_TUNE_GM_OPFUSE);
+}
+
+static EllOp ell_op(const msp_mat* A, const double* x, const double* sdev) {
+  EllOp op;
+  op.code8 = A->dv_code;
+  op.ddelta = A->dv_delta;
+  op.dval = A->dv_val;
+  op.ndict = A->ndict;
+  op.x = x;
+  op.sdev = sdev;
+  return op;
+}
+
+extern "C" int mspi_mdot_op(msp_mat* A, const double* x, const double* sdev, int nv, const double* base,
+                            int64_t stride, const double* scale, double* out_dev, const int* stop) {
+  if (!mspi_op_fusable(A) || nv < 1 || nv > MSPI_MAX_GROUP) return MSP_ERR_SUP;
+  msp_ctx* c = A->ctx;
+  const int64_t n = A->nrows, nch = nchunks_of(n);
+  int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
+  if (rc) return rc;
+  {
+    // codes once, the nv basis vectors (VV(it), the operator's x, among them)
+    KTimer kt(c, MSP_KERNEL_MDOT, 8.0 * (double)n + 8.0 * (double)n * nv);
+    const EllOp op = ell_op(A, x, sdev);
+    Vecs vg = {};
+    vg.base = base;
+    vg.stride = stride;
+    vg.scale = scale;
+    KCHK(msk_dot_stage1_op(&op, &vg, nv, n, c->partial, nch, stop, c->stream));
+  }
+  KCHK(msk_dot_stage2(c->partial, nch, nv, out_dev, stop, c->stream));
+  return MSP_SUCCESS;
+}
+
+extern "C" int mspi_maxpy_norm_update_op(msp_mat* A, const double* x, const double* sdev, double* wout, int nv,
+                                         const double* base, int64_t stride, const double* scale, mspi_gmres_dev g,
+                                         int m, const int* stop) {
+  if (!mspi_op_fusable(A) || nv < 1) return MSP_ERR_SUP;
+  msp_ctx* c = A->ctx;
+  const int64_t n = A->nrows, nch = nchunks_of(n);
+  int rc = ensure_partial(c, nch);
+  if (rc) return rc;
+  {
+    // codes, the nv basis vectors read, VV(it+1) written
+    KTimer kt(c, MSP_KERNEL_MAXPY, 8.0 * (double)n + 8.0 * (double)n * (nv + 1));
+    const EllOp op = ell_op(A, x, sdev);
+    Vecs vg = {};
+    vg.base = base;
+    vg.stride = stride;
+    vg.scale = scale;
+    KCHK(msk_maxpy_op(&op, wout, &vg, nv, g.h, n, c->partial, stop, c->stream));
+  }
+  return mspi_gm_norm_update(c, g, c->partial, nch, m);
+}
 
 extern "C" int mspi_graphs_enabled(msp_ctx* c) {
   if (c->timing) return 0;

@@ -81,4 +81,56 @@ def test_graphs_off_under_timing(ctx):
     finally:
         ctx.set_timing(False)
     assert ksp.get_iteration_number() == 20
-    assert st["spmv"]["launches"] >= 20
+    assert st["mdot"]["launches"] >= 20 and st["maxpy"]["launches"] >= 20
+
+
+def test_graph_recaptured_after_partial_buffer_grows(ctx):
+    """A captured cycle points at the context's DBR partial buffer; work on a larger vector reallocates it,
+    and the next solve must capture again (not replay into the freed buffer)."""
+    def solve_twice(graphs):
+        os.environ["MSPLIT_GRAPHS"] = "1" if graphs else "0"
+        try:
+            A = Mat.box_stencil(ctx, 3, 16, 16, 16)
+            n = A.shape[0]
+            ones, b, x = Vec(ctx, n), Vec(ctx, n), Vec(ctx, n)
+            ones.set(1.0)
+            A.mult(ones, b)
+            ksp = _solve(ctx, A, b, x, "-ksp_gmres_restart 20 -ksp_max_it 40 -ksp_rtol 1e-30")
+            big = Vec(ctx, 64 * n)                  # its norm needs a larger partial buffer
+            big.set(0.5)
+            big.norm()
+            ksp.solve(b, x)
+            return ksp.get_residual_history().copy(), x.get_array()
+        finally:
+            os.environ.pop("MSPLIT_GRAPHS", None)
+    he, xe = solve_twice(False)
+    hg, xg = solve_twice(True)
+    assert np.array_equal(he, hg) and np.array_equal(xe, xg)
+
+
+@pytest.mark.parametrize("restart,max_it", [(30, 75), (7, 40)])
+def test_gmres_with_matmult_in_cgs_kernels_bitwise(ctx, oracle, restart, max_it):
+    """MSK_TUNE_GM_OPFUSE (65536): W = A (sc VV(it)) computed inside MDot and MAXPY from the DV codes
+    instead of a MatMult kernel writing it: the oracle's histories and solution, bit for bit."""
+    import ctypes
+    from medane_tchakorom_ufc_thesis_repository_amd import _lib
+    L = _lib.load()
+    L.msk_set_tuning.argtypes = [ctypes.c_int]
+    L.msk_set_tuning.restype = None
+    A = Mat.box_convdiff(ctx, 3, 20, 17, 13, False, False, (0.3, -0.2, 0.1))
+    rp, col, val = A.get_csr()
+    n = A.shape[0]
+    ones, b, x = Vec(ctx, n), Vec(ctx, n), Vec(ctx, n)
+    ones.set(1.0)
+    A.mult(ones, b)
+    try:
+        L.msk_set_tuning(65536)
+        ksp = _solve(ctx, A, b, x, f"-ksp_gmres_restart {restart} -ksp_max_it {max_it} -ksp_rtol 1e-13")
+    finally:
+        L.msk_set_tuning(0)
+    Ao = oracle.Mat.from_arrays(n, n, rp, col, val)
+    xo, ro = oracle.gmres(Ao, b.get_array(), restart=restart, max_it=max_it, rtol=1e-13,
+                          reduce_mode=oracle.REDUCE_DBR)
+    assert ksp.get_iteration_number() == ro["its"]
+    assert np.array_equal(ksp.get_residual_history(), ro["hist"])
+    assert np.array_equal(x.get_array(), xo)
