@@ -153,7 +153,7 @@ int msp_ksp_set_operators(msp_ksp *k, msp_mat *A) {
     return MSP_ERR_ARG_WRONG;
   }
   if (k->A && k->n != nr) ksp_free_work(k);
-  if (k->A != A) ksp_drop_graphs(k);
+  ksp_drop_graphs(k); /* even for the same handle: a new matrix can reuse a destroyed one's address */
   k->A = A;
   k->n = nr;
   return MSP_SUCCESS;

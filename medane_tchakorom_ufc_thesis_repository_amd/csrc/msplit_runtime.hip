@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -362,6 +363,11 @@ extern "C" int mspi_set(msp_ctx* c, double* x, int64_t n, double alpha) {
 }
 
 // -------------------------------------------------------------------- Mat
+static uint64_t next_version() {
+  static std::atomic<uint64_t> v{1};
+  return v.fetch_add(1 << 20);  // objects 2^20 apart: a million storage switches before two could meet
+}
+
 struct msp_mat {
   msp_ctx* ctx = nullptr;
   int32_t nrows = 0, ncols = 0;
@@ -389,7 +395,7 @@ struct msp_mat {
   int32_t dv_w = 0;            // ELL layout: codes per row (4, 8, 16); 0: CSR-order codes + row lengths
   bool dv_on = false;          // products read the DV storage
   bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
-  uint64_t version = 0;        // bumped when the kernels its products launch change (captured graphs)
+  uint64_t version = next_version();  // unique per object and bumped when its products' kernels change
 };
 
 extern "C" int mspi_mat_dims(const msp_mat* A, int32_t* nr, int32_t* nc) {
