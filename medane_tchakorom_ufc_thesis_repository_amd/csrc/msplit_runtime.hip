@@ -912,7 +912,11 @@ extern "C" int mspi_reserve_partial(msp_ctx* c, int64_t n) {
 }
 
 extern "C" int mspi_capture_begin(msp_ctx* c) {
-  HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+  if (!c->stream) return MSP_ERR_SUP;  // the legacy null stream cannot be captured
+  if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
+    (void)hipGetLastError();  // the caller falls back to eager launches: leave no sticky error behind
+    return MSP_ERR_SUP;
+  }
   return MSP_SUCCESS;
 }
 
@@ -920,15 +924,18 @@ extern "C" int mspi_capture_end(msp_ctx* c, int ok, void** exec) {
   hipGraph_t g = nullptr;
   *exec = nullptr;
   const hipError_t e = hipStreamEndCapture(c->stream, &g);
-  if (!ok) {
+  if (!ok || e != hipSuccess) {
     if (g) (void)hipGraphDestroy(g);
-    return MSP_SUCCESS;
+    (void)hipGetLastError();
+    return ok ? MSP_ERR_SUP : MSP_SUCCESS;
   }
-  HIPCHK(e);
   hipGraphExec_t x = nullptr;
   const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
-  HIPCHK(ei);
+  if (ei != hipSuccess) {
+    (void)hipGetLastError();
+    return MSP_ERR_SUP;
+  }
   *exec = (void*)x;
   return MSP_SUCCESS;
 }
