@@ -496,6 +496,8 @@ struct DvKeyHash {
 // holds more than 255 entries.
 static int dv_dictionary(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val,
                          std::vector<int32_t>& delta, std::vector<double>& dval) {
+  // a stencil has a handful of pairs: a linear scan of the dictionary beats hashing until it grows
+  std::vector<DvKey> keys;
   std::unordered_map<DvKey, int, DvKeyHash> seen;
   for (int32_t r = 0; r < nrows; ++r) {
     if (rowptr[r + 1] - rowptr[r] > 255) return 0;
@@ -503,8 +505,19 @@ static int dv_dictionary(int32_t nrows, const int32_t* rowptr, const int32_t* co
       DvKey key;
       key.d = col[k] - r;
       memcpy(&key.bits, &val[k], 8);
-      if (seen.count(key)) continue;
-      if (delta.size() == 256) return 0;
+      bool found = false;
+      if (keys.size() <= 16) {
+        for (const DvKey& e : keys)
+          if (e == key) {
+            found = true;
+            break;
+          }
+      } else {
+        found = seen.count(key) != 0;
+      }
+      if (found) continue;
+      if (keys.size() == 256) return 0;
+      keys.push_back(key);
       seen.emplace(key, (int)delta.size());
       delta.push_back(key.d);
       dval.push_back(val[k]);
