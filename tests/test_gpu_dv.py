@@ -265,3 +265,19 @@ def test_gmres_after_release_csr(ctx, oracle):
     assert ksp.get_iteration_number() == ro["its"]
     assert np.array_equal(ksp.get_residual_history(), ro["hist"])
     assert np.array_equal(x.get_array(), xo)
+
+
+def test_tall_matrix_dv(ctx, oracle):
+    """More rows than columns (each row reads x at row - offset inside [0, ncols))."""
+    r = np.random.default_rng(SEED)
+    nr, nc = 3000, 1100
+    rows_c, rows_v, rp = [], [], [0]
+    for i in range(nr):
+        cs = sorted({c for c in (i - 1900, i - 1000, i - 7) if 0 <= c < nc and r.random() > 0.2})
+        rows_c += cs
+        rows_v += list(r.choice([2.0, -1.5], size=len(cs)))
+        rp.append(len(rows_c))
+    rp, col, val = np.array(rp, np.int32), np.array(rows_c, np.int32), np.array(rows_v)
+    A = Mat.from_csr(ctx, nr, nc, rp, col, val)
+    O = oracle.Mat.from_arrays(nr, nc, rp, col, val)
+    _both_storages(ctx, A, O)
