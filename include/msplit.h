@@ -90,7 +90,10 @@ int msp_ctx_destroy(msp_ctx **ctx);
 int msp_ctx_synchronize(msp_ctx *ctx);
 int msp_get_device_count(int *count);
 const char *msp_get_last_error(void);
-/* Per-kernel-class HIP-event timing (used by bench.py; off by default). */
+/* Per-kernel-class HIP-event timing (used by bench.py; off by default).
+ * enable = 0: off; 1: every logical kernel; N > 1: one in N of each class
+ * (the event records between kernels cost ~2 % of a GMRES step when every
+ * launch is bracketed; statistics then cover the sampled launches). */
 int msp_ctx_set_timing(msp_ctx *ctx, int enable);
 int msp_ctx_reset_kernel_stats(msp_ctx *ctx);
 /* launches, summed kernel time (ms) and summed algorithmic bytes for one class;

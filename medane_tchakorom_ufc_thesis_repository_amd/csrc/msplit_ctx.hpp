@@ -56,6 +56,8 @@ struct msp_ctx {
   int64_t partial_cap = 0;     // doubles
   uint64_t epoch = 0;          // bumped when a buffer captured graphs point at is reallocated
   bool timing = false;
+  int timing_every = 1;         // time one logical kernel in timing_every per class
+  int64_t timing_seen[16] = {};  // per-class launch counters (MSP_KERNEL_NCLASSES <= 16)
   std::vector<hipEvent_t> pool;
   size_t pool_used = 0;
   std::vector<TimedRec> recs;
@@ -69,6 +71,7 @@ struct KTimer {
   int ev = -1;
   KTimer(msp_ctx* ctx, int cls, double bytes) : c(ctx) {
     if (!c->timing) return;
+    if (c->timing_every > 1 && (c->timing_seen[cls & 15]++ % c->timing_every) != 0) return;
     if (c->pool_used + 2 > c->pool.size()) {
       for (int i = 0; i < 256; ++i) {
         hipEvent_t e;

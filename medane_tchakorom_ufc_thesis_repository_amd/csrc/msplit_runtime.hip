@@ -98,7 +98,11 @@ extern "C" int msp_ctx_synchronize(msp_ctx* c) {
 
 extern "C" int msp_ctx_set_timing(msp_ctx* c, int enable) {
   ARGCHK(c, MSP_ERR_ARG_NULL, "ctx is NULL");
+  ARGCHK(enable >= 0, MSP_ERR_ARG_OUTOFRANGE, "timing %d", enable);
+  static_assert(MSP_KERNEL_NCLASSES <= 16, "per-class counters");
   c->timing = enable != 0;
+  c->timing_every = enable > 1 ? enable : 1;
+  for (auto& v : c->timing_seen) v = 0;
   return MSP_SUCCESS;
 }
 

@@ -111,8 +111,9 @@ class Context:
     def synchronize(self):
         call("msp_ctx_synchronize", self.h)
 
-    def set_timing(self, on: bool):
-        call("msp_ctx_set_timing", self.h, 1 if on else 0)
+    def set_timing(self, on: bool, every: int = 1):
+        """HIP-event timing of each kernel class; every > 1 brackets one launch in `every` per class."""
+        call("msp_ctx_set_timing", self.h, max(1, int(every)) if on else 0)
 
     def reset_kernel_stats(self):
         call("msp_ctx_reset_kernel_stats", self.h)

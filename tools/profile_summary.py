@@ -53,7 +53,8 @@ def main():
         L.append(f"| {r['Name']} | {r['Calls']} | {int(r['TotalDurationNs']) / 1e6:.2f} | "
                  f"{float(r['AverageNs']) / 1e3:.2f} | {float(r['Percentage']):.2f} |")
     L += ["", "## Dominant kernel: bench.py's HIP-event timing vs rocprof", "",
-          f"bench.py roofline: class `maxpy` ({rf['kernel']}), avg {rf['avg_launch_ms'] * 1e3:.1f} us/launch, "
+          f"bench.py roofline (HIP events on {rf.get('timed_launches', 'every launch')}): class `maxpy` "
+          f"({rf['kernel']}), avg {rf['avg_launch_ms'] * 1e3:.1f} us/launch, "
           f"{rf['bytes_per_launch'] / 1e9:.4f} GB algorithmic/launch -> {rf['achieved']:.0f} GB/s = "
           f"{rf['frac']:.3f} of 8 TB/s.",
           f"rocprof k_maxpy_chunk: avg {float(mx['AverageNs']) / 1e3:.1f} us over {mx['Calls']} calls "
@@ -74,6 +75,16 @@ def main():
           "Other directories: `smsm/` (SMSM-global), `convdiff/`, `async/` (transports and async drivers), "
           "`configs/` (BASELINE configurations end to end), `spmv_ab/`, `skew_ab/`, earlier `*.json|csv` "
           "(first correct path, tuning history in DESIGN.md)."]
+    mb = []
+    for st in ("csr", "dv"):
+        f = os.path.join(run, f"spmv512_{st}.json")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(D, f"spmv512_{st}.json"))
+            d = json.load(open(f))["spmv/t0/g0"]
+            mb.append(f"| {st} | {d['us_median']:.1f} | {d['GBps_median']:.0f} | {d['GBps_median'] / 8000:.3f} |")
+    if mb:
+        L += ["", "## MatMult on the 512^3 7-point matrix (tools/microbench.py, y = A x, median of 3 x 10)", "",
+              "| storage | us | algorithmic GB/s | of 8 TB/s |", "|---|---|---|---|"] + mb
     open(os.path.join(ROOT, "profiles", a.tag, "README.md"), "w").write("\n".join(L) + "\n")
 
 
