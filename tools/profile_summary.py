@@ -73,7 +73,8 @@ def main():
            f"{tr['classes']['spmv']['hbm_over_alg']:.2f}x (x gathers re-read through the MALL)."
            if tr['classes'].get('spmv', {}).get('alg_bytes_per_launch') else ""), "",
           "Other directories: `smsm/` (SMSM-global), `convdiff/`, `async/` (transports and async drivers), "
-          "`configs/` (BASELINE configurations end to end), `spmv_ab/`, `skew_ab/`, earlier `*.json|csv` "
+          "`configs/` (BASELINE configurations end to end), `spmv_ab/`, `skew_ab/`, `dv/`, `opfuse/`, `graphs/`, "
+          "`matfree/`, A/Bs not adopted (`maxpy_pipe/`, `store_ab/`, `chunk_order/`, `dv/tried/`), earlier `*.json|csv` "
           "(first correct path, tuning history in DESIGN.md)."]
     mb = []
     for st in ("csr", "dv"):
