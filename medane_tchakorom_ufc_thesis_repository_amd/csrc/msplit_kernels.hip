@@ -396,8 +396,13 @@ __device__ __forceinline__ void maxpy_slice(const double* __restrict__ win, doub
   if (jrem == 3) chunk_group<3, FULL, VAR, J0, JN>(u, V, A, adev, negate, 0, base, n);
   else if (jrem == 2) chunk_group<2, FULL, VAR, J0, JN>(u, V, A, adev, negate, 0, base, n);
   else if (jrem == 1) chunk_group<1, FULL, VAR, J0, JN>(u, V, A, adev, negate, 0, base, n);
+  if constexpr ((VAR & 32) != 0) {  // two groups per iteration: the compiler issues 8 vectors' loads at once
+#pragma unroll 2
+    for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL, VAR, J0, JN>(u, V, A, adev, negate, g, base, n);
+  } else {
 #pragma unroll 1
-  for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL, VAR, J0, JN>(u, V, A, adev, negate, g, base, n);
+    for (int g = jrem; g < nv; g += 4) chunk_group<4, FULL, VAR, J0, JN>(u, V, A, adev, negate, g, base, n);
+  }
 #pragma unroll
   for (int j = J0; j < J0 + JN; ++j) {
     const int64_t e = base + j * (2 * kT);
@@ -1499,9 +1504,10 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
                                const Coefs* A, const double* adev, int negate, int64_t n, int accum, double* partial,
                                const int* stop, hipStream_t s) {
   if (n <= 0 || (nv <= 0 && !nvdev)) return 0;
-  // non-temporal store of w too unless MSK_TUNE_MAXPY_TEMPORAL_ST (+0.4 % per step)
+  // non-temporal store of w too unless MSK_TUNE_MAXPY_TEMPORAL_ST (+0.4 % per step); the group loop
+  // unrolled by two unless MSK_TUNE_MAXPY_UNROLL1 (+1.7 % per step: 64-load bursts at one wave per SIMD)
   const int var = vec_var() | ((g_tuning & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4) |
-                  ((g_tuning & MSK_TUNE_MAXPY_HALVES) ? 8 : 0);
+                  ((g_tuning & MSK_TUNE_MAXPY_HALVES) ? 8 : 0) | ((g_tuning & MSK_TUNE_MAXPY_UNROLL1) ? 0 : 32);
   const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
 #define MSK_MAXPY_LAUNCH(V_)                                                                                     \
   if (partial)                                                                                                  \
@@ -1519,7 +1525,12 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
     case 4: MSK_MAXPY_LAUNCH(4) break;
     case 5: MSK_MAXPY_LAUNCH(5) break;
     case 13: MSK_MAXPY_LAUNCH(13) break;
-    default: MSK_MAXPY_LAUNCH(5) break;
+    case 32: MSK_MAXPY_LAUNCH(32) break;
+    case 33: MSK_MAXPY_LAUNCH(33) break;
+    case 36: MSK_MAXPY_LAUNCH(36) break;
+    case 37: MSK_MAXPY_LAUNCH(37) break;
+    case 45: MSK_MAXPY_LAUNCH(45) break;
+    default: MSK_MAXPY_LAUNCH(37) break;
   }
 #undef MSK_MAXPY_LAUNCH
   return (int)hipGetLastError();
