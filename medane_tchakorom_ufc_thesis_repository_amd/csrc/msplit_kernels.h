@@ -59,7 +59,8 @@ enum {
   MSK_TUNE_DV_RPL2 = 16384,         // DV SpMV: two rows per lane (512-row blocks); default four
   MSK_TUNE_DV_NOELL = 32768,        // DV storage: CSR-order codes even where the ELL layout fits (at assembly)
   MSK_TUNE_GM_OPFUSE = 65536,       // GMRES: W = A (sc x) computed inside MDot and MAXPY instead of a MatMult kernel
-  MSK_TUNE_MAXPY_UNROLL1 = 131072   // MAXPY: one group of four per loop iteration (default: two, unrolled)
+  MSK_TUNE_MAXPY_UNROLL1 = 131072,  // MAXPY: one group of four per loop iteration (default: two, unrolled)
+  MSK_TUNE_MDOT_UNROLL2 = 262144    // MDot: two groups of four per loop iteration
 };
 
 extern "C" {

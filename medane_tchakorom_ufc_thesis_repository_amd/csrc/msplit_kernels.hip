@@ -199,8 +199,13 @@ __device__ __forceinline__ void dot_chunk(const double* __restrict__ w, const Ve
   if (!SELF && full && (VAR & 16) == 0) {
     constexpr int G = NV >= 4 ? 4 : NV;
     int g = 0;
+    if constexpr ((VAR & 32) != 0) {  // two groups per iteration (MSK_TUNE_MDOT_UNROLL2)
+#pragma unroll 2
+      for (; g + G <= NV; g += G) dot_group_full<G, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
+    } else {
 #pragma unroll 1
-    for (; g + G <= NV; g += G) dot_group_full<G, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
+      for (; g + G <= NV; g += G) dot_group_full<G, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
+    }
     if constexpr (NV % G == 3) dot_group_full<3, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
     if constexpr (NV % G == 2) dot_group_full<2, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
     if constexpr (NV % G == 1) dot_group_full<1, VAR>(wr, V, base, rev, NV, g, red, lane, wv);
@@ -1452,10 +1457,12 @@ static void dot1_dispatch(int nv, const double* w, const Vecs& V, int64_t n, dou
 extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
                               int self, const int* stop, hipStream_t s) {
   if (nchunks <= 0) return 0;
-  const int var = vec_var() | ((g_tuning & MSK_TUNE_MDOT_SINGLE) ? 16 : 0);
+  const int var = vec_var() | ((g_tuning & MSK_TUNE_MDOT_SINGLE) ? 16 : 0) |
+                  ((g_tuning & MSK_TUNE_MDOT_UNROLL2) ? 32 : 0);
   if (self)
     k_dot_stage1<1, true, 0><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, *V, n, partial, nchunks, stop, 0);
   else if (var == 1) dot1_dispatch<1, 1>(nv, w, *V, n, partial, nchunks, stop, s);
+  else if (var == 33) dot1_dispatch<1, 33>(nv, w, *V, n, partial, nchunks, stop, s);
   else if (var == 17) dot1_dispatch<1, 17>(nv, w, *V, n, partial, nchunks, stop, s);
   else if (var == 16) dot1_dispatch<1, 16>(nv, w, *V, n, partial, nchunks, stop, s);
   else dot1_dispatch<1, 0>(nv, w, *V, n, partial, nchunks, stop, s);
