@@ -100,6 +100,22 @@ int msp_ctx_reset_kernel_stats(msp_ctx *ctx);
  * synchronises the stream. */
 int msp_ctx_get_kernel_stats(msp_ctx *ctx, int kernel_class, int64_t *launches, double *total_ms,
                              double *total_bytes);
+/* Reduction order of every dot, norm, MDot and dense column sum on this context.
+ * MSP_REDUCE_DBR (default): the deterministic blocked reduction (4096-element
+ * chunks, wave butterflies; bitwise reproducible, full HBM bandwidth).
+ * MSP_REDUCE_SEQ: PETSc's Seq order -- one running sum per result, elements in
+ * index order (VecDot_Seq / VecNorm_Seq through f2cblaslapack ddot, VecMDot_Seq
+ * per vector, MatMultTranspose_SeqDense's dgemv 'T' per column, MatNorm_SeqDense
+ * NORM_FROBENIUS over the column-major array), and for an LSQR over several row
+ * blocks of one process one running sum across the blocks in block order (the
+ * reference's replicated R on one rank, SMSM-global.c:136).  A parity mode: one
+ * lane per result, orders of magnitude slower; LSQR over more than one rank
+ * returns MSP_ERR_SUP in it.  The environment variable MSPLIT_REDUCTION=seq
+ * selects it at msp_ctx_create. */
+#define MSP_REDUCE_DBR 0
+#define MSP_REDUCE_SEQ 1
+int msp_ctx_set_reduction(msp_ctx *ctx, int mode);
+int msp_ctx_get_reduction(const msp_ctx *ctx, int *mode);
 
 /* -------------------------------------------------------------------- Mat */
 /* MATSEQAIJ from host CSR arrays (ascending columns per row), copied to HBM.

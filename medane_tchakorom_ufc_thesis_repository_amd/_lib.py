@@ -62,6 +62,8 @@ _SIGS = {
     "msp_ctx_synchronize": [_vp],
     "msp_get_device_count": [_P(C.c_int)],
     "msp_ctx_set_timing": [_vp, C.c_int],
+    "msp_ctx_set_reduction": [_vp, C.c_int],
+    "msp_ctx_get_reduction": [_vp, _P(C.c_int)],
     "msp_ctx_reset_kernel_stats": [_vp],
     "msp_ctx_get_kernel_stats": [_vp, C.c_int, _P(C.c_int64), _dp, _dp],
     "msp_mat_create_csr": [_vp, C.c_int32, C.c_int32, _i32p, _i32p, _dp, _P(_vp)],

@@ -203,6 +203,25 @@ fail:
   return rc;
 }
 
+/* MSP_REDUCE_SEQ: overwrite the nloc block partials in loc (m per block, ncol used) with
+ * one sequential sum chained across the blocks (the reference's LSQR runs on one rank
+ * over all of R, SMSM-global.c:136), carried by the last block's slot.  x[k] + j*ldx
+ * is column j of block k (ldx = 0 with ncol = 1: a vector); y[k] the vector it is
+ * dotted with (y = x: a squared norm); frob: every column's squares in one sum. */
+static int seq_chain(msp_lsqr *l, double *const *x, int64_t ldx_R, double *const *y, int ncol, int frob,
+                     double *loc, int m) {
+  mspi_seq_segs sg;
+  memset(&sg, 0, sizeof(sg));
+  sg.nseg = l->nloc;
+  for (int k = 0; k < l->nloc; ++k) {
+    sg.x[k] = x ? x[k] : l->R[k]->d;
+    sg.ldx[k] = ldx_R ? l->R[k]->lda : 0;
+    sg.y[k] = y ? y[k] : (x ? x[k] : NULL);
+    sg.n[k] = l->R[k]->nrows;
+  }
+  return mspi_seq_chain(l->ctx, &sg, ncol, frob, loc, m, &l->d.st->stop);
+}
+
 /* all-gather nloc*m local partials into gall (block order over ranks) */
 static int gather(msp_lsqr *l, const double *loc, double *all, int m) {
   if (!l->comm) return MSP_SUCCESS;
@@ -220,6 +239,11 @@ int msp_lsqr_solve(msp_lsqr *l, msp_vec *const *b, msp_vec *x) {
   int rc;
   if ((rc = mspi_set_device(l->ctx)) || (rc = lsqr_setup(l))) return rc;
   msp_ctx *c = l->ctx;
+  const int seq = mspi_reduce_seq(c);
+  if (seq && (l->nranks > 1 || l->nloc > MSPI_SEQ_MAXSEG))
+    return err(MSP_ERR_SUP, "MSP_REDUCE_SEQ chains the LSQR sums across the row blocks of one process only");
+  double *bd[MSPI_SEQ_MAXSEG];
+  for (int k = 0; k < l->nloc && seq; ++k) bd[k] = b[k]->d;
   const int s = l->s, nloc = l->nloc;
   const int *stop = &l->d.st->stop;
   mspi_lsqr_dev d = l->d;
@@ -241,17 +265,20 @@ int msp_lsqr_solve(msp_lsqr *l, msp_vec *const *b, msp_vec *x) {
   /* u <- b; rnorm = ||u|| (n = 0 test); u *= 1/beta; V = R^T u */
   for (int k = 0; k < nloc; ++k)
     if ((rc = mspi_norm2sq(c, b[k]->d, b[k]->n, l->gloc + k))) return rc;
+  if (seq && (rc = seq_chain(l, bd, 0, NULL, 1, 0, l->gloc, 1))) return rc;
   if ((rc = gather(l, l->gloc, l->gall, 1)) || (rc = mspi_ls_start(c, d))) return rc;
   if (l->o.exact_norm) {
     for (int k = 0; k < nloc; ++k)
       if ((rc = mspi_dense_colsumsq(c, l->R[k]->d, l->R[k]->lda, s, l->R[k]->nrows, l->partial, l->floc + k * s)))
         return rc;
+    if (seq && (rc = seq_chain(l, NULL, 1, NULL, s, 1, l->floc, s))) return rc;
     if ((rc = gather(l, l->floc, l->fall, s))) return rc;
   }
   for (int k = 0; k < nloc; ++k)
     if ((rc = mspi_dense_scaled_dots(c, b[k]->d, l->U[k], &d.st->uscale, l->R[k]->d, l->R[k]->lda, s,
                                      l->R[k]->nrows, l->partial, l->gloc + k * s, stop)))
       return rc;
+  if (seq && (rc = seq_chain(l, NULL, 1, l->U, s, 0, l->gloc, s))) return rc;
   if ((rc = gather(l, l->gloc, l->gall, s)) || (rc = mspi_ls_first(c, d, l->o.exact_norm ? l->fall : NULL)))
     return rc;
 
@@ -263,11 +290,13 @@ int msp_lsqr_solve(msp_lsqr *l, msp_vec *const *b, msp_vec *x) {
       if ((rc = mspi_dense_gemv(c, l->R[k]->d, l->R[k]->lda, s, l->R[k]->nrows, d.V, &d.st->nalpha, U[k], U1[k],
                                 l->partial, l->gloc + k, stop)))
         return rc;
+    if (seq && (rc = seq_chain(l, U1, 0, NULL, 1, 0, l->gloc, 1))) return rc;
     if ((rc = gather(l, l->gloc, l->gall, 1)) || (rc = mspi_ls_beta(c, d))) return rc;
     for (int k = 0; k < nloc; ++k)
       if ((rc = mspi_dense_scaled_dots(c, U1[k], U1[k], &d.st->uscale, l->R[k]->d, l->R[k]->lda, s,
                                        l->R[k]->nrows, l->partial, l->gloc + k * s, stop)))
         return rc;
+    if (seq && (rc = seq_chain(l, NULL, 1, U1, s, 0, l->gloc, s))) return rc;
     if ((rc = gather(l, l->gloc, l->gall, s)) || (rc = mspi_ls_step(c, d))) return rc;
     if ((i + 1) % LSQR_CHUNK == 0 || i + 1 == nsteps) {
       if ((rc = mspi_d2h_sync(c, h, d.st, sizeof(*h)))) return rc;

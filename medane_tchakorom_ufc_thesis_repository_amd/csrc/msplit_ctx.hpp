@@ -55,6 +55,7 @@ struct msp_ctx {
   double* partial = nullptr;   // DBR stage-1 partials
   int64_t partial_cap = 0;     // doubles
   uint64_t epoch = 0;          // bumped when a buffer captured graphs point at is reallocated
+  int reduce = MSP_REDUCE_DBR;  // MSP_REDUCE_SEQ: PETSc's sequential order (msplit_seq.hip)
   bool timing = false;
   int timing_every = 1;         // time one logical kernel in timing_every per class
   int64_t timing_seen[16] = {};  // per-class launch counters (MSP_KERNEL_NCLASSES <= 16)

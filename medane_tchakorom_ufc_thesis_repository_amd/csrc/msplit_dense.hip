@@ -255,6 +255,10 @@ extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc,
 #undef GEMV3
 #undef GEMV
   KCHK((int)hipGetLastError());
+  if (norm && mspi_reduce_seq(c)) {  // ||y||^2 in PETSc's order (msplit_seq.hip)
+    Vecs v = {};
+    KCHK(msk_seq_stage1(y, &v, 1, n, 1, partial, nch, stop, c->stream));
+  }
   if (norm) KCHK(msk_dot_stage2(partial, nch, 1, sumsq_dev, stop, c->stream));
   return MSP_SUCCESS;
 }
@@ -289,6 +293,12 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
     }
 #undef SDOT
     KCHK((int)hipGetLastError());
+    if (mspi_reduce_seq(c)) {  // dgemv 'T' order: each column . w in sequence (msplit_seq.hip)
+      Vecs v = {};
+      v.base = Ag;
+      v.stride = lda;
+      KCHK(msk_seq_stage1(sc_dev ? wout : win, &v, g, n, 0, partial, nch, stop, c->stream));
+    }
     KCHK(msk_dot_stage2(partial, nch, g, out_dev + g0, stop, c->stream));
   }
   return MSP_SUCCESS;
@@ -307,7 +317,8 @@ extern "C" int mspi_dense_colsumsq(msp_ctx* c, const double* A, int64_t lda, int
   for (int j = 0; j < nc; ++j) {
     Vecs v = {};
     v.p[0] = A + (int64_t)j * lda;
-    KCHK(msk_dot_stage1(v.p[0], &v, 1, n, partial, nch, 1, nullptr, c->stream));
+    if (mspi_reduce_seq(c)) KCHK(msk_seq_stage1(v.p[0], &v, 1, n, 1, partial, nch, nullptr, c->stream));
+    else KCHK(msk_dot_stage1(v.p[0], &v, 1, n, partial, nch, 1, nullptr, c->stream));
     KCHK(msk_dot_stage2(partial, nch, 1, out_dev + j, nullptr, c->stream));
   }
   return MSP_SUCCESS;

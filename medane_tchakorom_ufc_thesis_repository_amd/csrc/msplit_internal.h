@@ -205,6 +205,22 @@ typedef struct {
   double *hist;         /* hist_cap */
 } mspi_lsqr_dev;
 
+/* ---- MSP_REDUCE_SEQ (msplit_seq.hip) ---- */
+int mspi_reduce_seq(const msp_ctx *ctx);
+#define MSPI_SEQ_MAXSEG 16
+typedef struct {
+  int32_t nseg;
+  const double *x[MSPI_SEQ_MAXSEG]; /* segment k: column j at x[k] + j*ldx[k] */
+  int64_t ldx[MSPI_SEQ_MAXSEG];
+  const double *y[MSPI_SEQ_MAXSEG]; /* the vector each column is dotted with (unused by frob) */
+  int64_t n[MSPI_SEQ_MAXSEG];
+} mspi_seq_segs;
+/* One sequential sum per column j < ncol of column_j . y chained over the segments in order
+ * (frob != 0: one sum of the squares of every column, columns outer, segments inner).  out[k*m + j]
+ * of the last segment k holds the sum (frob: the last segment's column ncol-1), every other slot
+ * of the first ncol columns +0.0, so a block-order sum of the slots is the chained sum. */
+int mspi_seq_chain(msp_ctx *ctx, const mspi_seq_segs *sg, int ncol, int frob, double *out, int m, const int *stop);
+
 /* one-lane kernels of the LSQR recurrence (g holds nblk values / nblk*s values) */
 int mspi_ls_start(msp_ctx *ctx, mspi_lsqr_dev d);
 int mspi_ls_first(msp_ctx *ctx, mspi_lsqr_dev d, const double *gfrob);

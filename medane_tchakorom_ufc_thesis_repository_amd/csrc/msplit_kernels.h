@@ -77,6 +77,10 @@ int msk_maxpy_op(const EllOp* op, double* wout, const Vecs* V, int nv, const dou
 int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks, int self,
                    const int* stop, hipStream_t s);
 int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, const int* stop, hipStream_t s);
+// MSP_REDUCE_SEQ stage 1 (msplit_seq.hip): w . V_v (self: w . w) as one sequential sum per vector, written in
+// the DBR partial layout (chunk 0 holds the sum, the others +0.0) so stage 2 folds it unchanged.
+int msk_seq_stage1(const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial, int64_t nchunks,
+                   const int* stop, hipStream_t s);
 // wout = win + sum_j a_j V_j (PETSc grouping), a_j = (negate ? -1 : 1) * (adev ? adev[j] : A->a[j]);
 // nv = *nvdev when nvdev != null; accum: wout = win + (0 + sum); partial != null: DBR partial of ||wout||^2.
 int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, const int* nvdev, const Coefs* A,

@@ -56,6 +56,7 @@ extern "C" int msp_ctx_create(int device, void* stream, msp_ctx** out) {
   if (const char* e = getenv("MSPLIT_TUNING")) msk_set_tuning(atoi(e));
   msp_ctx* c = new msp_ctx();
   c->device = device;
+  if (const char* e = getenv("MSPLIT_REDUCTION")) c->reduce = (e[0] == 's' || e[0] == 'S') ? MSP_REDUCE_SEQ : MSP_REDUCE_DBR;
   if (stream) {
     c->stream = (hipStream_t)stream;
   } else {
@@ -103,6 +104,19 @@ extern "C" int msp_ctx_set_timing(msp_ctx* c, int enable) {
   c->timing = enable != 0;
   c->timing_every = enable > 1 ? enable : 1;
   for (auto& v : c->timing_seen) v = 0;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_set_reduction(msp_ctx* c, int mode) {
+  ARGCHK(c, MSP_ERR_ARG_NULL, "ctx is NULL");
+  ARGCHK(mode == MSP_REDUCE_DBR || mode == MSP_REDUCE_SEQ, MSP_ERR_ARG_OUTOFRANGE, "reduction mode %d", mode);
+  c->reduce = mode;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_ctx_get_reduction(const msp_ctx* c, int* mode) {
+  ARGCHK(c && mode, MSP_ERR_ARG_NULL, "NULL argument");
+  *mode = c->reduce;
   return MSP_SUCCESS;
 }
 
@@ -179,6 +193,14 @@ extern "C" int mspi_d2h_sync(msp_ctx* c, void* host, const void* dev, size_t byt
 }
 
 // --------------------------------------------------------------- internal ops
+// Stage 1 of a reduction in the context's order (DBR, or MSP_REDUCE_SEQ's sequential sums
+// written in the DBR partial layout).
+static int stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, int64_t nch,
+                  const int* stop) {
+  if (c->reduce == MSP_REDUCE_SEQ) return msk_seq_stage1(w, V, nv, n, self, c->partial, nch, stop, c->stream);
+  return msk_dot_stage1(w, V, nv, n, c->partial, nch, self, stop, c->stream);
+}
+
 extern "C" int mspi_mdot(msp_ctx* c, const double* w, int nv, const double* const* V, int64_t n, double* out_dev) {
   if (nv <= 0) return MSP_SUCCESS;
   const int64_t nch = nchunks_of(n);
@@ -193,7 +215,7 @@ extern "C" int mspi_mdot(msp_ctx* c, const double* w, int nv, const double* cons
     const int g = std::min(MSPI_MAX_GROUP, nv - g0);
     Vecs vg = {};
     for (int j = 0; j < g; ++j) vg.p[j] = V[g0 + j];
-    KCHK(msk_dot_stage1(w, &vg, g, n, c->partial, nch, 0, nullptr, c->stream));
+    KCHK(stage1(c, w, &vg, g, n, 0, nch, nullptr));
     KCHK(msk_dot_stage2(c->partial, nch, g, out_dev + g0, nullptr, c->stream));
   }
   return MSP_SUCCESS;
@@ -210,7 +232,7 @@ extern "C" int mspi_norm2sq(msp_ctx* c, const double* x, int64_t n, double* out_
   KTimer kt(c, MSP_KERNEL_NORM, 8.0 * (double)n);
   Vecs vg = {};
   vg.p[0] = x;
-  KCHK(msk_dot_stage1(x, &vg, 1, n, c->partial, nch, 1, nullptr, c->stream));
+  KCHK(stage1(c, x, &vg, 1, n, 1, nch, nullptr));
   KCHK(msk_dot_stage2(c->partial, nch, 1, out_dev, nullptr, c->stream));
   return MSP_SUCCESS;
 }
@@ -279,7 +301,7 @@ extern "C" int mspi_mdot_basis(msp_ctx* c, const double* w, int nv, const double
     vg.base = base + (int64_t)g0 * stride;
     vg.stride = stride;
     vg.scale = scale ? scale + g0 : nullptr;
-    KCHK(msk_dot_stage1(w, &vg, g, n, c->partial, nch, 0, stop, c->stream));
+    KCHK(stage1(c, w, &vg, g, n, 0, nch, stop));
     KCHK(msk_dot_stage2(c->partial, nch, g, out_dev + g0, stop, c->stream));
   }
   return MSP_SUCCESS;
@@ -300,6 +322,7 @@ extern "C" int mspi_maxpy_norm_basis(msp_ctx* c, const double* win, double* wout
   vg.scale = scale;
   Coefs cf = {};
   KCHK(msk_maxpy_chunk(win, wout, &vg, nv, nullptr, &cf, alpha_dev, 1, n, 0, c->partial, stop, c->stream));
+  if (c->reduce == MSP_REDUCE_SEQ) KCHK(stage1(c, wout, &vg, 1, n, 1, nch, stop));  // ||wout||^2 in order
   KCHK(msk_dot_stage2(c->partial, nch, 1, sumsq_dev, stop, c->stream));
   return MSP_SUCCESS;
 }
@@ -327,6 +350,7 @@ extern "C" int mspi_maxpy_norm_update(msp_ctx* c, const double* win, double* wou
     vg.scale = scale;
     Coefs cf = {};
     KCHK(msk_maxpy_chunk(win, wout, &vg, nv, nullptr, &cf, g.h, 1, n, 0, c->partial, stop, c->stream));
+    if (c->reduce == MSP_REDUCE_SEQ) KCHK(stage1(c, wout, &vg, 1, n, 1, nch, stop));  // ||wout||^2 in order
   }
   return mspi_gm_norm_update(c, g, c->partial, nch, m);
 }
@@ -861,7 +885,8 @@ extern "C" uint64_t mspi_ctx_epoch(const msp_ctx* c) { return c->epoch; }
 // run at, the far (+-plane) gathers of each row pair are 8 exposed round trips
 // per workgroup, which the standalone SpMV hides with 6-8 waves.
 extern "C" int mspi_op_fusable(const msp_mat* A) {
-  return A && A->dv_on && A->dv_w == 8 && A->ndict <= 255 && A->nrows == A->ncols && A->nrows > 0 &&
+  return A && A->ctx->reduce == MSP_REDUCE_DBR && A->dv_on && A->dv_w == 8 && A->ndict <= 255 &&
+         A->nrows == A->ncols && A->nrows > 0 &&
          (msk_get_tuning() & MSK_TUNE_GM_OPFUSE);
 }
 
@@ -919,7 +944,7 @@ extern "C" int mspi_maxpy_norm_update_op(msp_mat* A, const double* x, const doub
 }
 
 extern "C" int mspi_graphs_enabled(msp_ctx* c) {
-  if (c->timing) return 0;
+  if (c->timing || c->reduce == MSP_REDUCE_SEQ) return 0;
   const char* e = getenv("MSPLIT_GRAPHS");
   return !(e && e[0] == '0');
 }
@@ -1052,7 +1077,8 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
   msp_ctx* c = A->ctx;
   const int64_t n = A->nrows;
   const int64_t nch = nchunks_of(n);
-  if (A->matfree || A->compressed || A->csr_released || A->nrows != A->ncols || A->lds_cap512 <= 0 || nv < 1 ||
+  if (c->reduce == MSP_REDUCE_SEQ || A->matfree || A->compressed || A->csr_released || A->nrows != A->ncols ||
+      A->lds_cap512 <= 0 || nv < 1 ||
       nv > MSPI_MAX_GROUP ||
       nch == 0 || !(msk_get_tuning() & MSK_TUNE_GM_SPMV_MDOT))
     return MSP_ERR_SUP;

@@ -111,6 +111,19 @@ class Context:
     def synchronize(self):
         call("msp_ctx_synchronize", self.h)
 
+    REDUCTIONS = {"dbr": 0, "seq": 1}
+
+    def set_reduction(self, mode: str):
+        """Reduction order of every dot/norm/MDot on this context: "dbr" (default, the
+        deterministic blocked reduction) or "seq" (PETSc's sequential order, a parity mode;
+        include/msplit.h MSP_REDUCE_SEQ)."""
+        call("msp_ctx_set_reduction", self.h, self.REDUCTIONS[mode])
+
+    def get_reduction(self) -> str:
+        m = C.c_int()
+        call("msp_ctx_get_reduction", self.h, C.byref(m))
+        return {v: k for k, v in self.REDUCTIONS.items()}[m.value]
+
     def set_timing(self, on: bool, every: int = 1):
         """HIP-event timing of each kernel class; every > 1 brackets one launch in `every` per class."""
         call("msp_ctx_set_timing", self.h, max(1, int(every)) if on else 0)

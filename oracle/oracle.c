@@ -264,8 +264,11 @@ static double dbr_dot(int64_t n, const double *x, const double *y) {
   const int64_t nchunks = (n + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
   double *part = (double *)malloc((size_t)(nchunks > 0 ? nchunks : 1) * sizeof(double));
   double lanes[ORC_DBR_THREADS];
+  /* chunks are independent: threads split them, each chunk's arithmetic unchanged */
+  ORC_PAR
   for (int64_t c = 0; c < nchunks; ++c) {
     const int64_t base = c * ORC_DBR_CHUNK;
+    double lanes[ORC_DBR_THREADS];
     for (int t = 0; t < ORC_DBR_THREADS; ++t) {
       double acc = 0.0;
       for (int j = 0; j < ORC_DBR_ITERS; ++j) {

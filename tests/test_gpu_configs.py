@@ -1,0 +1,218 @@
+"""Every BASELINE.json configuration at full size in the -m gpu suite.
+
+  configs[0]  2D 256^2 SMSM-global, 2 blocks         tests/test_gpu_seq.py::test_configs0_*
+              (bitwise vs the DBR oracle, and in PETSc's order vs the PETSc-order oracle)
+  configs[1]  3D 256^3 GMRES(30), max_it 300          bitwise vs the DBR oracle (OpenMP oracle)
+  configs[2]  3D 512^3 SMSM-global, 2 blocks          both blocks on this GPU: converges in the
+              outer count tools/configs_run.py measured, ||r|| <= rtol ||b||, rerun bitwise
+  configs[3]  3D 1024^3 in 8 blocks                   one interior block (1024x1024x128) assembled
+              on the device: A_ii and A_ext nnz, A.1 and A.(column index) against closed forms
+              (exact integer arithmetic, so order-independent), DV = CSR products, GMRES steps
+  configs[4]  3D convection-diffusion 512^3, 8 blocks one interior block (512x512x64) of the upwind
+              operator: the same checks with dyadic Peclet numbers (every product and sum exact)
+
+The 1024^3 and 512^3 per-GPU blocks cannot be held by the CPU oracle in a test's
+time, so they are pinned by properties that hold bit for bit.  configs[3]'s A_ii has
+936,902,656 entries: int32 rowptr (PetscInt = int32) at 0.44 of its range.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm
+from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import make_smsm, smsm_solve
+from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Mat, Options, Vec
+
+pytestmark = pytest.mark.gpu
+
+
+def _threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+
+
+def test_configs1_256cube_gmres_bitwise(ctx, oracle):
+    """configs[1]: 3D 7-pt Poisson 256^3, GMRES(30), pc none, rtol 1e-4 with the bench's
+    fixed max_it 300 (10 full cycles): 300 iterations, history and x bitwise the DBR oracle."""
+    n = 256
+    A = Mat.box_stencil(ctx, 3, n, n, n)
+    N = A.shape[0]
+    ones = Vec(ctx, N)
+    ones.set(1.0)
+    b = Vec(ctx, N)
+    A.mult(ones, b)
+    x = Vec(ctx, N)
+    ksp = KSP(ctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options("-ksp_gmres_restart 30 -ksp_max_it 300 -ksp_rtol 1e-30 -pc_type none "
+                                 "-ksp_norm_type unpreconditioned"))
+    ksp.solve(b, x)
+    hist = ksp.get_residual_history()
+    assert ksp.get_iteration_number() == 300 and len(hist) == 301
+    oracle.set_threads(_threads())
+    try:
+        O = oracle.poisson3d_rows(n, n, n, 0, n)
+        bo = O.mult(np.ones(N))
+        assert np.array_equal(bo, b.get_array())
+        xo, ro = oracle.gmres(O, bo, restart=30, max_it=300, rtol=1e-30, reduce_mode=oracle.REDUCE_DBR)
+    finally:
+        oracle.set_threads(1)
+    assert (ksp.get_iteration_number(), ksp.get_converged_reason()) == (ro["its"], ro["reason"])
+    assert np.array_equal(hist, ro["hist"])
+    assert np.array_equal(x.get_array(), xo)
+
+
+def _smsm_opts(nb, s):
+    inner = " ".join(f"-inner{b + 1}_ksp_gmres_restart 30 -inner{b + 1}_ksp_max_it 20 -inner{b + 1}_ksp_rtol 1e-20 "
+                     f"-inner{b + 1}_pc_type none -inner{b + 1}_ksp_norm_type unpreconditioned" for b in range(nb))
+    outer = " ".join(f"-outer{b + 1}_ksp_type lsqr -outer{b + 1}_ksp_convergence_test default "
+                     f"-outer{b + 1}_ksp_lsqr_exact_mat_norm -outer{b + 1}_ksp_atol 1e-100 "
+                     f"-outer{b + 1}_ksp_max_it 70 -outer{b + 1}_ksp_rtol 1e-15 -outer{b + 1}_pc_type none"
+                     for b in range(nb))
+    return Options(f"{inner} {outer} -s {s}")
+
+
+C3_OUTER_ITS = 5   # tools/configs_run.py c3 (profiles/r01/configs/), the DBR order
+
+
+def _c3_run(ctx):
+    comm = LocalComm()
+    blocks, mini = make_smsm(ctx, 3, 512, 512, 512, 2, range(2), 20, _smsm_opts(2, 20), comm)
+    res = smsm_solve(blocks, comm, 20, mini, rtol=1e-4, max_outer=12)
+    x = np.concatenate([blk.x.get_array() for blk in blocks])
+    mini.close()
+    return res, x
+
+
+def test_configs2_512cube_smsm_two_blocks(ctx):
+    """configs[2]: 3D 512^3, SMSM-global, 2 blocks (both on this GPU), s 20, inner max_it 20
+    rtol 1e-20, outer LSQR max_it 70 rtol 1e-15 exact norm, -rtol 1e-4."""
+    res, x = _c3_run(ctx)
+    assert res.outer_its == C3_OUTER_ITS
+    assert res.hist[-1] <= 1e-4 * res.norm0 < res.hist[-2]
+    assert res.final_norm <= 1e-4 * res.norm0 * 1.0001
+    assert all(r != 0 for r in res.lsqr_reason)
+    res2, x2 = _c3_run(ctx)   # deterministic: the rerun is bitwise the first run
+    assert res2.hist == res.hist and res2.lsqr_its == res.lsqr_its
+    assert np.array_equal(x2, x)
+
+
+# ----------------------------------------------------- configs[3] / configs[4] blocks
+def _grid(nx, ny, nz):
+    r = np.arange(nx * ny * nz, dtype=np.int64)
+    i = r % nx
+    j = (r // nx) % ny
+    k = r // (nx * ny)
+    return r, i, j, k
+
+
+def _expected(nx, ny, nz, ext, coef):
+    """A.1 and A.g (g = the column index, in the matrix's own column space) for one box block:
+    coef = (lz, ly, lx, d, ux, uy, uz); ext: the z neighbours live in the halo columns."""
+    lz, ly, lx, d, ux, uy, uz = coef
+    nxny = nx * ny
+    r, i, j, k = _grid(nx, ny, nz)
+    c = r + (nxny if ext else 0)
+    ones = np.full(r.size, d)
+    g = d * c.astype(np.float64)
+    del r
+    for present, cf, off in ((i > 0, lx, -1), (i < nx - 1, ux, 1), (j > 0, ly, -nx), (j < ny - 1, uy, nx),
+                             ((k > 0) | ext, lz, -nxny), ((k < nz - 1) | ext, uz, nxny)):
+        ones += np.where(present, cf, 0.0)
+        g += np.where(present, cf * (c + off).astype(np.float64), 0.0)
+    return ones, g
+
+
+def _check_block(ctx, A, nx, ny, nz, ext, coef):
+    N = nx * ny * nz
+    ncol = N + (2 * nx * ny if ext else 0)
+    assert A.shape == (N, ncol)
+    faces = 2 * ny * nz + 2 * nx * nz + (0 if ext else 2 * nx * ny)
+    assert A.nnz == 7 * N - faces
+    e1, eg = _expected(nx, ny, nz, ext, coef)
+    x = Vec(ctx, ncol)
+    y = Vec(ctx, N)
+    x.set(1.0)
+    A.mult(x, y)
+    assert np.array_equal(y.get_array(), e1)
+    del e1
+    x.set_values(np.arange(ncol, dtype=np.float64))
+    A.mult(x, y)
+    assert np.array_equal(y.get_array(), eg)
+    del eg
+    # the one-byte (DV) storage and the CSR storage give the same products at this size
+    rng = np.random.default_rng(5)
+    x.set_values(rng.uniform(-1, 1, ncol))
+    A.set_storage("dv")
+    A.mult(x, y)
+    ydv = y.get_array()
+    A.set_storage("csr")
+    A.mult(x, y)
+    assert np.array_equal(y.get_array(), ydv)
+
+
+def _gmres_steps(ctx, A, its=10):
+    """A few GMRES(30) iterations on the block: the history never increases (GMRES minimises the
+    residual over a growing space) and its last entry is the true residual ||b - A x||."""
+    N = A.shape[0]
+    ones = Vec(ctx, N)
+    ones.set(1.0)
+    b = Vec(ctx, N)
+    A.mult(ones, b)
+    x = Vec(ctx, N)
+    ksp = KSP(ctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options(f"-ksp_gmres_restart 30 -ksp_max_it {its} -ksp_rtol 1e-30 -pc_type none"))
+    ksp.solve(b, x)
+    h = ksp.get_residual_history()
+    assert ksp.get_iteration_number() == its and len(h) == its + 1
+    assert np.all(np.diff(h) <= 0)
+    r = Vec(ctx, N)
+    A.residual(b, x, r)
+    assert r.norm() == pytest.approx(h[-1], rel=1e-8)
+
+
+POISSON = (-1.0, -1.0, -1.0, 6.0, -1.0, -1.0, -1.0)
+
+
+def test_configs3_1024cube_block_assembly(ctx):
+    """configs[3]: one interior block of 1024^3 in 8 z-slabs (1024 x 1024 x 128 rows)."""
+    nx = ny = 1024
+    nz = 128
+    A = Mat.box_stencil(ctx, 3, nx, ny, nz)            # A_ii, the inner solve's operator
+    assert A.nnz == 936_902_656
+    _check_block(ctx, A, nx, ny, nz, False, POISSON)
+    _gmres_steps(ctx, A)
+    A.destroy()
+    E = Mat.box_stencil_ext(ctx, 3, nx, ny, nz, True, True)   # A_ext: R = A S's operator (both halos)
+    _check_block(ctx, E, nx, ny, nz, True, POISSON)
+    E.destroy()
+
+
+def _convdiff_coef(P):
+    px, py, pz = P
+    lo = [-1.0 - 2.0 * max(p, 0.0) for p in (px, py, pz)]
+    up = [-1.0 + 2.0 * min(p, 0.0) for p in (px, py, pz)]
+    d = 6.0 + 2.0 * abs(px) + 2.0 * abs(py) + 2.0 * abs(pz)
+    return (lo[2], lo[1], lo[0], d, up[0], up[1], up[2])
+
+
+def test_configs4_convdiff_512cube_block_assembly(ctx):
+    """configs[4]: one interior block of the 512^3 convection-diffusion operator in 8 z-slabs
+    (512 x 512 x 64), cell Peclet (0.5, 0.25, -0.375): dyadic, so every entry, product
+    and row sum below is exact in double."""
+    nx = ny = 512
+    nz = 64
+    P = (0.5, 0.25, -0.375)
+    coef = _convdiff_coef(P)
+    A = Mat.box_convdiff(ctx, 3, nx, ny, nz, False, False, P)
+    _check_block(ctx, A, nx, ny, nz, False, coef)
+    _gmres_steps(ctx, A)
+    A.destroy()
+    E = Mat.box_convdiff(ctx, 3, nx, ny, nz, True, True, P)
+    _check_block(ctx, E, nx, ny, nz, True, coef)
+    E.destroy()
