@@ -5,16 +5,30 @@ N = 1 : configs[1] -- 3D 7-pt Poisson 256^3, single-block GMRES(30), pc none,
         one step = one KSPSolve from x0 = 0 with the canonical options
         (running_bulk_test_g5k:64-70: rtol 1e-4, unpreconditioned norm) and a
         fixed max_it = 300 (10 restart cycles).
+        The same JSON line also carries, each measured in this run:
+          smsm_per_gpu  the N > 1 workload below on one GPU (one 512x512x256
+                        block), so that N -> 8 compares SMSM with SMSM;
+          spmv_512_csr  the north star's "CSR SpMV on the 512^3 7-point
+                        matrix": MatMult with the matrix in CSR storage
+                        (k_spmv_lds8), HIP-event time per launch and fraction
+                        of the 8 TB/s HBM peak.
 N > 1 : SMSM with global minimization (configs[2], BASELINE "SMSM 2 blocks on
         2 MI355X"), weak scaling: one 512 x 512 x 256 z-slab block per GPU
         (global 512 x 512 x 256N; N = 2 is the 512^3 two-block case).  One
         step = one outer iteration of SMSM-global.c:288-363 with the campaign
         options of running_bulk_test_g5k:230-248: s = 20 inner solves
-        (GMRES(30), max_it 20, rtol 1e-20, warm started, RCCL boundary-plane
+        (GMRES(30), max_it 20, rtol 1e-20, warm started, boundary-plane
         exchange after each), S(:,k) = x, R = A S, LSQR (max_it 70,
-        rtol 1e-15, exact Frobenius norm; block partials all-gathered over
-        RCCL) and x = S alpha.  (--variant sm: plain synchronous
-        multisplitting instead; --variant smsm also runs on one GPU.)
+        rtol 1e-15, exact Frobenius norm) and x = S alpha.  Exchange, residual
+        sums and LSQR partials go over ONE library RCCL communicator on the
+        context's stream (comm.LibComm; comm.c:126-141's replacement).
+--variant sm    plain synchronous multisplitting (one z-slab block per GPU);
+--variant amam  AMAM-global (asynchronous-multisplitting-asynchronous-
+        minimization-global_prime.c:371-481): configs[3]'s per-GPU block of
+        1024^3/8 = 1024x1024x128 (Poisson); with --peclet, configs[4]'s
+        512^3/8 = 512x512x64 block of the convection-diffusion operator.  One
+        step = one asynchronous solve of --amam-its outer iterations per block
+        (HBM mailboxes, newest-value R broadcast, convergence detection).
 value = sum over blocks of (rows x inner GMRES iterations) / max-over-ranks time.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]   (N > 1 under
@@ -33,12 +47,16 @@ sys.path.insert(0, ROOT)
 
 METRIC = "DOF-updates/s on 3D 7-pt Poisson GMRES; achieved HBM GB/s vs peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-KERNEL_NAMES = {"spmv": "k_spmv_lds (CSR MatMult/MatResidual)", "mdot": "k_dot_stage1+2 (VecMDot, DBR)",
-                "maxpy": "k_maxpy (VecMAXPY, CGS update + BuildSoln)", "norm": "k_dot_stage1<1,self>+stage2 (VecNorm)",
+KERNEL_NAMES = {"mdot": "k_dot_stage1+2 (VecMDot, DBR)",
+                "maxpy": "k_maxpy_chunk (VecMAXPY, CGS update + fused ||w||^2, and BuildSoln)",
+                "norm": "k_dot_stage1<1,self>+stage2 (VecNorm)",
                 "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy",
                 "spmm": "k_spmm (MatMatMult R = A S)", "dgemv": "k_dense_gemv (LSQR R v - alpha u + norm; S alpha)",
                 "dgemvt": "k_scaled_dot (LSQR scale + R^T u)",
                 "spmvdot": "k_spmv_mdot (GMRES MatMult fused with VecMDot stage 1)"}
+SPMV_NAMES = {"dv": "k_spmv_ell (MatMult/MatResidual, DV storage: one byte per entry)",
+              "csr": "k_spmv_lds8 (MatMult/MatResidual, CSR storage)",
+              "matfree": "k_stencil_spmv (MatMult/MatResidual, matrix-free)"}
 
 
 def parse():
@@ -58,22 +76,30 @@ def parse():
                         "which costs ~2%% of the step in event records; 7 is co-prime with the restart 30, so the "
                         "samples cycle through every Krylov dimension)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                   help="N>1 exchange backend: nccl (= RCCL, the product) or gloo (single-GPU rehearsal)")
-    p.add_argument("--variant", default=None, choices=["gmres", "sm", "smsm"],
-                   help="gmres (N=1 default), smsm (N>1 default), sm")
+                   help="N>1 process group: nccl (= RCCL, the product) or gloo (single-GPU rehearsal: the library "
+                        "communicator then uses its host transport over gloo)")
+    p.add_argument("--variant", default=None, choices=["gmres", "sm", "smsm", "amam"],
+                   help="gmres (N=1 default), smsm (N>1 default), sm, amam")
     p.add_argument("--smsm-mesh", type=int, default=512, help="SMSM: nx = ny")
     p.add_argument("--smsm-planes", type=int, default=256, help="SMSM: z-planes per GPU block")
-    p.add_argument("--s", type=int, default=20, help="SMSM: inner solves per minimization (-s)")
+    p.add_argument("--s", type=int, default=20, help="SMSM / AMAM: inner solves per minimization (-s)")
     p.add_argument("--inner-max-it", type=int, default=20)
     p.add_argument("--outer-max-it", type=int, default=70)
+    p.add_argument("--amam-mesh", type=int, default=None, help="AMAM: nx = ny (1024; 512 with --peclet)")
+    p.add_argument("--amam-planes", type=int, default=None, help="AMAM: z-planes per GPU (128; 64 with --peclet)")
+    p.add_argument("--amam-its", type=int, default=2, help="AMAM: outer iterations per block per step")
     p.add_argument("--operator", default="csr", choices=["csr", "matfree"],
-                   help="the assembled CSR (the reference's MatMult, default) or the same operator applied "
+                   help="the assembled operator (the reference's MatMult, default) or the same operator applied "
                         "matrix-free (bitwise the same products, no matrix traffic; gmres, and A_ii for smsm)")
     p.add_argument("--storage", default="dv", choices=["dv", "csr"],
                    help="entry storage of the assembled operator in HBM: dv (one byte per entry, the library's "
                         "choice for any matrix that fits; default) or csr (rowptr/col/val); bitwise the same products")
     p.add_argument("--no-csr-compare", action="store_true",
-                   help="skip the untimed-in-value CSR-storage rerun that N=1 GMRES reports beside the DV figure")
+                   help="skip the CSR-storage rerun that N=1 GMRES reports beside the DV figure")
+    p.add_argument("--no-smsm-n1", action="store_true", help="N=1: skip the smsm_per_gpu measurement")
+    p.add_argument("--smsm-n1-steps", type=int, default=2)
+    p.add_argument("--no-spmv512", action="store_true", help="N=1: skip the 512^3 CSR MatMult measurement")
+    p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--peclet", default=None,
                    help="Px,Py,Pz: the upwind convection-diffusion operator (configs[4]) instead of Poisson")
     a = p.parse_args()
@@ -81,22 +107,64 @@ def parse():
     a.peclet = tuple(float(v) for v in a.peclet.split(",")) if a.peclet else None
     if a.peclet is not None and len(a.peclet) != 3:
         raise SystemExit("--peclet takes three cell Peclet numbers Px,Py,Pz")
+    if a.amam_mesh is None:
+        a.amam_mesh = 512 if a.peclet else 1024
+    if a.amam_planes is None:
+        a.amam_planes = 64 if a.peclet else 128
     return a
+
+
+# ------------------------------------------------------------------ CPU baseline
+def host_topology():
+    """What the host offers: nproc, lscpu sockets/cores, this job's CPU set and cgroup quota."""
+    out = {"nproc": os.cpu_count()}
+    try:
+        out["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        import subprocess
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {k.strip(): v.strip() for k, v in (ln.split(":", 1) for ln in txt.splitlines() if ":" in ln)}
+        sockets = int(kv.get("Socket(s)", "0") or 0)
+        cps = int(kv.get("Core(s) per socket", "0") or 0)
+        out.update({"model": kv.get("Model name"), "sockets": sockets, "cores_per_socket": cps,
+                    "physical_cores": sockets * cps, "threads_per_core": int(kv.get("Thread(s) per core", "1") or 1)})
+    except Exception:
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        out["cgroup_cpu_quota"] = None if q == "max" else float(q) / float(per)
+    except Exception:
+        pass
+    return out
+
+
+def cpu_threads(topo):
+    """This job's CPU share: the cgroup quota (the box grants each GPU job a share of the
+    node), else the CPU set, else OMP_NUM_THREADS -- MSPLIT_CPU_THREADS overrides."""
+    if os.environ.get("MSPLIT_CPU_THREADS"):
+        return max(1, int(os.environ["MSPLIT_CPU_THREADS"]))
+    share = topo.get("cgroup_cpu_quota") or topo.get("affinity_cpus") or topo.get("nproc") or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        share = min(share, omp)
+    return max(1, int(share))
 
 
 def cpu_baseline(n: int, restart: int, its: int, rtol: float):
     """The CPU restatement (oracle/) on a bounded sample of the same workload:
-    the same 256^3 operator, GMRES(restart), pc none, `its` iterations.  Run on
-    the host cores the box gives this job (OMP_NUM_THREADS, at most 16) with
-    PETSc's MPI dot order, one rank per thread (element-wise loops in parallel,
-    each dot as per-thread pieces added in thread order); also, for reference,
-    one core in PETSc's Seq order."""
+    the same 256^3 operator, GMRES(restart), pc none, from x0 = 0.  It runs with
+    one thread per CPU of this job's share of the host (PETSc's MPI order with
+    one rank per thread: element-wise loops split, each dot as per-thread pieces
+    added in thread order), plus, for reference, one core in PETSc's Seq order."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import pyoracle as po
+    topo = host_topology()
+    threads = cpu_threads(topo)
     A = po.poisson3d_rows(n, n, n, 0, n)
     b = A.mult(np.ones(A.shape[0]))
-    threads = max(1, min(16, int(os.environ.get("MSPLIT_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", "1")))))
     out = {}
     for t in ([threads, 1] if threads > 1 else [1]):
         po.set_threads(t)
@@ -109,9 +177,15 @@ def cpu_baseline(n: int, restart: int, its: int, rtol: float):
     po.set_threads(1)
     v, k, dt = out[threads]
     res = {"value": v, "unit": "DOF-updates/s", "cores": threads, "kind": "port",
+           "mode": ("OpenMP, one thread per CPU of the job's share, PETSc MPI dot order (one rank per thread)"
+                    if threads > 1 else "one core, PETSc Seq order"),
            "sample": f"3D 7-pt Poisson {n}^3, GMRES({restart}) pc none, {k} iterations from x0=0, oracle/oracle.c "
-                     f"(no FMA), {threads} thread(s)" + (" in PETSc MPI dot order (one rank per thread)"
-                                                         if threads > 1 else " in PETSc Seq order") + f", {dt:.1f} s"}
+                     f"(no FMA), {threads} thread(s), {dt:.1f} s",
+           "host": topo}
+    pc = topo.get("physical_cores")
+    if pc and pc > threads:
+        res["node_note"] = (f"the node has {pc} physical cores; this job's share is {threads} CPUs (the GPU box "
+                            f"grants each single-GPU job a share of the host), so the baseline uses those")
     if threads > 1:
         v1, k1, dt1 = out[1]
         res["single_core"] = {"value": v1, "iterations": k1, "seconds": dt1, "order": "PETSc Seq"}
@@ -119,9 +193,10 @@ def cpu_baseline(n: int, restart: int, its: int, rtol: float):
 
 
 def load_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-    passes of this benchmark), or None."""
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+    (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    benchmark), or None.  Read from profiles/, not counted in this run: rocprofv3's
+    counter passes cannot run inside the timed process."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None
@@ -129,6 +204,104 @@ def load_traffic():
         return json.load(open(p))
     except Exception:
         return None
+
+
+# ------------------------------------------------------------------ workloads
+def smsm_options(args):
+    return (f"-inner1_ksp_type gmres -inner1_ksp_gmres_restart {args.restart} -inner1_ksp_atol 1e-100 "
+            f"-inner1_ksp_max_it {args.inner_max_it} -inner1_ksp_rtol 1e-20 -inner1_pc_type none "
+            f"-inner1_ksp_norm_type UNPRECONDITIONED "
+            f"-outer1_ksp_type lsqr -outer1_ksp_convergence_test default -outer1_ksp_lsqr_exact_mat_norm "
+            f"-outer1_ksp_atol 1e-100 -outer1_ksp_max_it {args.outer_max_it} -outer1_ksp_rtol 1e-15 "
+            f"-outer1_pc_type none -outer1_ksp_norm_type UNPRECONDITIONED -s {args.s}"
+            + (" -msplit_operator matfree" if args.operator == "matfree" else ""))
+
+
+def build_smsm(ctx, args, comm, world, rank):
+    """configs[2]: SMSM-global (SMSM-global.c:288-363), options of running_bulk_test_g5k:230-248."""
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import GpuBlock, GpuMinimizer
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Options
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
+    n = args.smsm_mesh
+    nz = args.smsm_planes * world
+    kspopts = smsm_options(args)
+    o = Options(kspopts)
+    L = block_layout(3, n, n, nz, world, rank, args.peclet)
+    blk = GpuBlock(ctx, L, o, comm, prefix="inner1_")
+    blk.setup_minimization(args.s)
+    mini = GpuMinimizer(ctx, [blk], comm, o, prefix="outer1_")
+    blk.reset_halo()
+    lsqr_its = []
+
+    def step():
+        its = 0
+        for k in range(args.s):
+            blk.update_rhs()                # updateLocalRHS
+            its += blk.solve()              # inner_solver
+            comm.exchange([blk])            # comm_sync_send_and_receive
+            blk.store_column(k)             # S(:, k) = x
+        blk.form_R()                        # R = A S
+        _, lits, _ = mini.solve([blk])      # LSQR, x = S alpha
+        lsqr_its.append(lits)
+        return its
+    transport = {"local": "single block", "nccl": "one library RCCL communicator",
+                 "gloo": "gloo (rehearsal: the library's host transport)"}[getattr(comm, "backend", "local")]
+    workload = (f"3D 7-pt Poisson {n}x{n}x{nz} SMSM-global, {world} z-slab block(s) of {n}x{n}x{args.smsm_planes} "
+                f"(one per MI355X), s = {args.s} inner GMRES({args.restart}) solves of max_it {args.inner_max_it} "
+                f"per outer iteration, LSQR max_it {args.outer_max_it}; {transport} for the exchange, residual sums "
+                f"and LSQR partials (configs[2] at N = 2)")
+    return step, workload, kspopts, n * n * args.smsm_planes, (blk, mini, lsqr_its)
+
+
+def smsm_n1(ctx, args):
+    """The N > 1 per-GPU workload on this one GPU (LocalComm, one block): the base the
+    driver's N = 2..8 SMSM lines scale from."""
+    import torch
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm
+    step, workload, _, rows, (blk, mini, lsqr_its) = build_smsm(ctx, args, LocalComm(), 1, 0)
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    its = sum(step() for _ in range(args.smsm_n1_steps))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    mini.close()
+    return {"workload": workload, "value": rows * its / dt, "unit": "DOF-updates/s", "steps": args.smsm_n1_steps,
+            "warmup": 1, "ms_per_step": 1e3 * dt / args.smsm_n1_steps,
+            "gmres_iterations_per_step": its / args.smsm_n1_steps, "lsqr_iterations_per_step": lsqr_its[1:],
+            "note": "same per-GPU block and step as the N > 1 lines: N-GPU scaling of SMSM = "
+                    "value(N) / (N x this value)"}
+
+
+def spmv512(ctx, args):
+    """The north star's SpMV target: MatMult y = A x on the 512^3 7-point matrix in CSR
+    storage (rowptr/col/val; 12 B per entry), HIP events on the library's stream."""
+    import numpy as np
+    import torch
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Mat, Vec
+    n = 512
+    A = Mat.box_stencil(ctx, 3, n, n, n)
+    A.set_storage("csr")
+    N = A.shape[0]
+    x = Vec.from_array(ctx, np.random.default_rng(20251121).uniform(-1, 1, N))
+    y = Vec(ctx, N)
+    for _ in range(3):
+        A.mult(x, y)
+    ctx.set_timing(True, 1)
+    ctx.reset_kernel_stats()
+    for _ in range(args.spmv_reps):
+        A.mult(x, y)
+    st = ctx.kernel_stats()["spmv"]
+    ctx.set_timing(False)
+    torch.cuda.synchronize()
+    alg = 12.0 * A.nnz + 20.0 * N + 4.0
+    avg_ms = st["ms"] / st["launches"]
+    gbs = alg / (avg_ms * 1e-3) / 1e9
+    A.destroy()
+    return {"kernel": SPMV_NAMES["csr"], "rows": N, "nnz": A.nnz, "alg_bytes_per_launch": alg,
+            "bytes_formula": "12 nnz + 20 N + 4 (val 8 + col 4 per entry, rowptr, x read once, y written)",
+            "launches": st["launches"], "avg_launch_ms": avg_ms, "achieved_GBps": gbs,
+            "peak_GBps": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS, "target_frac": 0.70}
 
 
 def main():
@@ -149,8 +322,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
-    from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm, TorchComm
-    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import GpuBlock, GpuMinimizer
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import LibComm, LocalComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import GpuBlock
     from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Context, Mat, Options, Vec
     from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
 
@@ -163,6 +336,9 @@ def main():
     variant = args.variant or ("gmres" if world == 1 else "smsm")
     if variant == "gmres" and world > 1:
         raise SystemExit("--variant gmres is the single-GPU workload")
+    comm = LibComm(ctx) if world > 1 else LocalComm()
+    keep = None
+    spmv_storage = "matfree" if args.operator == "matfree" else args.storage
 
     if variant == "gmres":
         # configs[1]: single-block GMRES(30) on 256^3 (gmres_solution.c:50-70 in 3D)
@@ -188,7 +364,6 @@ def main():
         if args.operator == "matfree":
             workload += ", operator applied matrix-free (same arithmetic as the CSR; not the reference's MatMult)"
     elif variant == "sm":
-        comm = TorchComm(device=torch.device("cuda", dev) if args.backend == "nccl" else torch.device("cpu"))
         L = block_layout(3, n, n, n * world, world, rank, args.peclet)
         o = Options(kspopts)
         blk = GpuBlock(ctx, L, None, comm, prefix="")
@@ -205,47 +380,34 @@ def main():
             return its
         workload = (f"3D 7-pt Poisson {n}x{n}x{n * world} synchronous multisplitting, {world} z-slab blocks of "
                     f"{n}^3 (one per MI355X), inner GMRES({args.restart}) max_it {args.max_it}, "
-                    f"{'RCCL' if args.backend == 'nccl' else 'gloo (rehearsal)'} halo exchange")
-    else:
-        # configs[2]: SMSM-global (SMSM-global.c:288-363), options of running_bulk_test_g5k:230-248
-        if world > 1:
-            comm = TorchComm(device=torch.device("cuda", dev) if args.backend == "nccl" else torch.device("cpu"))
-        else:
-            comm = LocalComm()
-        n = args.smsm_mesh
-        nz = args.smsm_planes * world
-        rows = n * n * args.smsm_planes
-        kspopts = (f"-inner1_ksp_type gmres -inner1_ksp_gmres_restart {args.restart} -inner1_ksp_atol 1e-100 "
-                   f"-inner1_ksp_max_it {args.inner_max_it} -inner1_ksp_rtol 1e-20 -inner1_pc_type none "
-                   f"-inner1_ksp_norm_type UNPRECONDITIONED "
-                   f"-outer1_ksp_type lsqr -outer1_ksp_convergence_test default -outer1_ksp_lsqr_exact_mat_norm "
-                   f"-outer1_ksp_atol 1e-100 -outer1_ksp_max_it {args.outer_max_it} -outer1_ksp_rtol 1e-15 "
-                   f"-outer1_pc_type none -outer1_ksp_norm_type UNPRECONDITIONED -s {args.s}"
-                   + (" -msplit_operator matfree" if args.operator == "matfree" else ""))
+                    f"{'library RCCL communicator' if world > 1 else 'single block'}")
+    elif variant == "amam":
+        # configs[3] / configs[4]: AMAM-global, one block per GPU (AMAM-global_prime.c:371-481)
+        from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
+        n = args.amam_mesh
+        nz = args.amam_planes * world
+        kspopts = smsm_options(args)
         o = Options(kspopts)
         L = block_layout(3, n, n, nz, world, rank, args.peclet)
         blk = GpuBlock(ctx, L, o, comm, prefix="inner1_")
-        blk.setup_minimization(args.s)
-        mini = GpuMinimizer(ctx, [blk], comm, o, prefix="outer1_")
-        blk.reset_halo()
-        lsqr_its = []
+        blk.setup_global_async_minimization(args.s, o, prefix="outer1_")
+        rows = L.nrows
+        amres = []
 
         def step():
-            its = 0
-            for k in range(args.s):
-                blk.update_rhs()                # updateLocalRHS
-                its += blk.solve()              # inner_solver
-                comm.exchange([blk])            # comm_sync_send_and_receive
-                blk.store_column(k)             # S(:, k) = x
-            blk.form_R()                        # R = A S
-            _, lits, _ = mini.solve([blk])      # LSQR, x = S alpha
-            lsqr_its.append(lits)
-            return its
-        workload = (f"3D 7-pt Poisson {n}x{n}x{nz} SMSM-global, {world} z-slab block(s) of {n}x{n}x{args.smsm_planes} "
-                    f"(one per MI355X), s = {args.s} inner GMRES({args.restart}) solves of max_it {args.inner_max_it} "
-                    f"per outer iteration, LSQR max_it {args.outer_max_it}; "
-                    f"{'RCCL' if world > 1 and args.backend == 'nccl' else ('gloo (rehearsal)' if world > 1 else 'single block')} "
-                    f"exchange and all-gathers (configs[2] at N = 2)")
+            r = am_solve([blk], comm, rtol=1e-30, max_iterations=args.amam_its, variant="amam_global", s=args.s,
+                         stop_at_limit=True)
+            amres.append(r)
+            return sum(r.inner_its)
+        workload = (f"3D 7-pt {'upwind convection-diffusion' if args.peclet else 'Poisson'} {n}x{n}x{nz} AMAM-global, "
+                    f"{world} z-slab block(s) of {n}x{n}x{args.amam_planes} (one per MI355X; "
+                    f"{'configs[4]' if args.peclet else 'configs[3]'} per-GPU block), s = {args.s} inner GMRES("
+                    f"{args.restart}) steps of max_it {args.inner_max_it}, {args.amam_its} outer iterations per block "
+                    f"per step, LSQR max_it {args.outer_max_it} over the replicated R, HBM mailboxes (xGMI)")
+        keep = amres
+    else:
+        step, workload, kspopts, rows, (blk, mini, lsqr_its) = build_smsm(ctx, args, comm, world, rank)
+        n = args.smsm_mesh
 
     if args.peclet is not None:
         workload = workload.replace("7-pt Poisson", "7-pt upwind convection-diffusion (cell Peclet "
@@ -269,13 +431,12 @@ def main():
         its_total += step()
     barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
     stats = ctx.kernel_stats() if timing else {}
 
     csr_same_run = None
     if (variant == "gmres" and world == 1 and args.operator == "csr" and args.storage == "dv"
             and not args.no_csr_compare):
-        # the same workload with the matrix in CSR storage, same process, after the timed region
+        # the same workload with the matrix in CSR storage, same process, same timing setting
         A.set_storage("csr")
         step()
         torch.cuda.synchronize()
@@ -285,7 +446,9 @@ def main():
         el_c = time.perf_counter() - t1
         A.set_storage("dv")
         csr_same_run = {"matrix_storage": "csr", "value": float(rows) * its_c / el_c,
-                        "ms_per_step": 1e3 * el_c / args.steps}
+                        "ms_per_step": 1e3 * el_c / args.steps,
+                        "timing": f"HIP events 1 in {args.timing_every}" if timing else "off"}
+    ctx.set_timing(False)
 
     my_updates = float(rows) * its_total
     if world > 1:
@@ -298,19 +461,34 @@ def main():
     else:
         elapsed_max, updates = elapsed, my_updates
 
+    extras = {}
+    if world == 1 and variant == "gmres" and rank == 0:
+        # release the headline's objects, then the two side measurements
+        del ksp, A, b, x, ones
+        if not args.no_smsm_n1:
+            extras["smsm_per_gpu"] = smsm_n1(ctx, args)
+        if not args.no_spmv512:
+            extras["spmv_512_csr"] = spmv512(ctx, args)
+
     if rank == 0:
         value = updates / elapsed_max
+        mesh = {"gmres": [n, n, n], "sm": [n, n, n], "smsm": [n, n, args.smsm_planes],
+                "amam": [args.amam_mesh, args.amam_mesh, args.amam_planes]}[variant]
         out = {"metric": METRIC, "value": value, "unit": "DOF-updates/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": 1e3 * elapsed_max / args.steps, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic: b = A*1 (exact solution u = 1), x0 = 0; device-assembled operator",
-               "config": {"workload": workload, "variant": variant,
-                          "mesh_per_gpu": [n, n, rows // (n * n)], "blocks": world,
-                          "ksp": kspopts, "gmres_iterations_per_step_per_block": its_total / args.steps,
+               "config": {"workload": workload, "variant": variant, "mesh_per_gpu": mesh, "blocks": world,
+                          "ksp": kspopts, "gmres_iterations_per_step_per_block": its_total / args.steps / world,
                           "matrix_storage": "none (matrix-free)" if args.operator == "matfree" else args.storage,
                           "parallelism": f"{world} z-slab block(s), one per GPU"}}
         if variant == "smsm":
             out["config"]["lsqr_iterations_per_step"] = lsqr_its[-args.steps:]
+        if variant == "amam":
+            out["config"]["amam"] = [{"iterations": r.iterations, "inner_its": r.inner_its, "converged": r.converged,
+                                      "transport": r.transport,
+                                      "phase_share": {k: v / max(sum(r.timers.values()), 1e-30)
+                                                      for k, v in r.timers.items()}} for r in keep[-args.steps:]]
         if csr_same_run:
             out["same_run_csr_storage"] = csr_same_run
         if stats:
@@ -320,27 +498,35 @@ def main():
             achieved = (s["bytes"] / s["launches"]) / (s["ms"] / s["launches"] * 1e-3) / 1e9 if s["launches"] else 0
             tr = load_traffic()
             traffic = None
-            if tr and tr.get("kernel_class") == dom and tr.get("n") == n:
+            if tr and tr.get("kernel_class") == dom and tr.get("n") == n and variant == "gmres":
                 traffic = tr.get("hbm_bytes_per_launch")
-            out["roofline"] = {"bound": "hbm", "kernel": KERNEL_NAMES[dom], "achieved": achieved,
+            names = dict(KERNEL_NAMES, spmv=SPMV_NAMES[spmv_storage])
+            out["roofline"] = {"bound": "hbm", "kernel": names[dom], "achieved": achieved,
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                               "traffic": traffic, "timed_launches": f"1 in {args.timing_every} per class",
+                               "traffic": traffic,
+                               "traffic_source": ("profiles/traffic.json: rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE "
+                                                  "passes of this benchmark (tools/pmc_traffic.py, gfx950 "
+                                                  "correction), read from profiles/, not counted in this run"
+                                                  if traffic is not None else None),
+                               "timed_launches": f"1 in {args.timing_every} per class",
                                "bytes_per_launch": s["bytes"] / max(s["launches"], 1),
                                "avg_launch_ms": s["ms"] / max(s["launches"], 1)}
-            out["kernels"] = {k: {"launches": v["launches"], "ms_total": v["ms"],
+            out["kernels"] = {k: {"kernel": names.get(k, k), "launches": v["launches"], "ms_total": v["ms"],
                                   "GBps": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] else None,
                                   "share": v["ms"] / total_ms if total_ms else None} for k, v in stats.items()}
             alg_bytes = sum(v["bytes"] for v in stats.values())
             # sampled launches stand for timing_every launches each
             out["hbm_alg_GBps_whole_step"] = alg_bytes * max(1, args.timing_every) / elapsed / 1e9
+        out.update(extras)
         if world == 1 and variant == "gmres" and not args.no_cpu_baseline and args.peclet is None:
             out["cpu_baseline"] = cpu_baseline(n, args.restart, args.cpu_sample_its, args.rtol)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     if variant == "smsm":
-        mini.close()                            # the LSQR communicator before the process group
+        mini.close()
     if world > 1:
+        comm.close()                            # the library communicator before the process group
         dist.barrier()
         dist.destroy_process_group()
 

@@ -18,7 +18,11 @@ with the plane(s) for neighbour nbr, recv_buffer(nbr) -> tensor to receive
 into, unpack_recv(), and, for LocalComm, copy_halo_from(block).
 
   LocalComm  -- every block in this process (one GPU or tests): direct copies;
-  TorchComm  -- one block per rank (one rank per GPU), torch.distributed.
+  LibComm    -- one block per rank (one rank per GPU) over the library's own
+                communicator (msp_comm): halo planes, residual sums and LSQR
+                partials on ONE RCCL communicator, on the context's stream;
+  TorchComm  -- one block per rank over torch.distributed collectives (CPU
+                tests with test-double blocks, gloo).
 """
 from __future__ import annotations
 
@@ -179,3 +183,87 @@ class TorchComm:
             dist.all_gather_into_tensor(out, t, group=group)
             return out.cpu().numpy()
         return Comm.host(ctx, self.world, self.rank, allgather)
+
+
+class LibComm:
+    """One block per rank (block id = rank) over the library's msp_comm, the
+    product's N > 1 path.  The boundary exchange is msp_comm_exchange_neighbors
+    (comm.c:126-141 for chain neighbours: the planes to rank-1 / rank+1 and back,
+    RCCL send/recv in one group enqueued on the context's stream -- no host
+    synchronisation), the outer-residual sum is msp_comm_sum_ordered (rank order,
+    synchronous-multisplitting.c:192) and the LSQR block partials go over the
+    same communicator, so each rank holds one RCCL communicator.
+    torch.distributed only broadcasts its id (and runs barriers).
+
+    transport "rccl" (default with the nccl process group) or "host" (the
+    library's host-callback transport over the process group's all_gather: gloo
+    rehearsals, e.g. two ranks sharing one GPU, which RCCL refuses)."""
+
+    device_buffers = True
+    lsqr_comm_owned = False     # GpuMinimizer must not destroy it: the exchange uses it too
+
+    def __init__(self, ctx, group=None, transport: str | None = None):
+        import torch
+        import torch.distributed as dist
+        from .petsc import Comm
+        self.torch, self.dist, self.group = torch, dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.backend = dist.get_backend(group)
+        self.transport = transport or ("rccl" if self.backend == "nccl" else "host")
+        self.ctx = ctx
+        if self.transport == "rccl":
+            obj = [Comm.unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            self.comm = Comm.rccl(ctx, self.world, self.rank, obj[0])
+        else:
+            dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+            world = self.world
+
+            def allgather(a):
+                t = torch.from_numpy(a).to(dev)
+                out = torch.empty(world * t.numel(), dtype=t.dtype, device=dev)
+                dist.all_gather_into_tensor(out, t, group=group)
+                return out.cpu().numpy()
+            self.comm = Comm.host(ctx, self.world, self.rank, allgather)
+
+    def alloc(self, ctx, n):
+        from .petsc import Vec
+        return Vec(ctx, n), None
+
+    def exchange(self, blocks):
+        (blk,) = blocks
+        L = blk.layout
+        lo_src = hi_src = lo_dst = hi_dst = 0
+        count = 0
+        for nbr, off, cnt in L.send:
+            count = cnt
+            if nbr == self.rank - 1:
+                lo_src = off
+            else:
+                hi_src = off
+        for nbr, hoff, cnt, _ in L.recv:
+            if cnt != count:
+                raise ValueError("msp_comm_exchange_neighbors moves equal planes both ways")
+            if nbr == self.rank - 1:
+                lo_dst = hoff
+            else:
+                hi_dst = hoff
+        if count:
+            self.comm.exchange_neighbors(blk.x, lo_src, hi_src, blk.halo, lo_dst, hi_dst, count)
+
+    def ordered_sum(self, blocks, values):
+        (v,) = values
+        return float(self.comm.sum_ordered([v])[0])
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+    def lsqr_comm(self, ctx):
+        return self.comm
+
+    def close(self):
+        if getattr(self, "comm", None) is not None:
+            self.ctx.synchronize()
+            self.comm.destroy()
+            self.comm = None

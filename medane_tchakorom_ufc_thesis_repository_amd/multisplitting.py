@@ -367,6 +367,7 @@ class GpuMinimizer:
         self.lsqr = initializeOuterKSP(ctx, prefix if prefix is not None else f"outer{b0 + 1}_", opts)
         self.lsqr.set_operators([blk.R for blk in blocks])
         self.comm = comm.lsqr_comm(ctx) if hasattr(comm, "lsqr_comm") else None
+        self._own_comm = getattr(comm, "lsqr_comm_owned", True)   # LibComm shares its communicator
         self.lsqr.set_comm(self.comm)
         self.alpha = Vec(ctx, blocks[0].s)
 
@@ -376,7 +377,8 @@ class GpuMinimizer:
         self.ctx.synchronize()
         if self.comm is not None:
             self.lsqr.set_comm(None)
-            self.comm.destroy()
+            if self._own_comm:
+                self.comm.destroy()
             self.comm = None
 
     def solve(self, blocks):

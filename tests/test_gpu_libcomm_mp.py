@@ -1,0 +1,109 @@
+"""The N > 1 product path with real HIP blocks, rehearsed on the one-GPU box.
+
+comm.LibComm puts the boundary exchange (msp_comm_exchange_neighbors), the
+outer-residual sum and the LSQR partials on one library communicator.  RCCL
+refuses two ranks on one GPU, so the rehearsal runs the same driver code over
+the library's host transport (gloo all_gather callback); the RCCL transport
+differs only inside msplit_comm.hip (ncclSend/ncclRecv/ncclAllGather instead of
+the callback) and runs on the driver's 8-GPU node.  One process per block,
+spawned fresh; each rank's result must equal the single-process DBR oracle bit
+for bit (histories, counts, iterate)."""
+import multiprocessing as mp
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from test_distributed_gloo import _free_port
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _opts(nb, s):
+    inner = " ".join(f"-inner{b + 1}_ksp_max_it 20 -inner{b + 1}_ksp_rtol 1e-20 -inner{b + 1}_pc_type none "
+                     f"-inner{b + 1}_ksp_gmres_restart 30 -inner{b + 1}_ksp_atol 1e-100" for b in range(nb))
+    outer = " ".join(f"-outer{b + 1}_ksp_type lsqr -outer{b + 1}_ksp_convergence_test default "
+                     f"-outer{b + 1}_ksp_lsqr_exact_mat_norm -outer{b + 1}_ksp_atol 1e-100 "
+                     f"-outer{b + 1}_ksp_max_it 70 -outer{b + 1}_ksp_rtol 1e-15 -outer{b + 1}_pc_type none"
+                     for b in range(nb))
+    return f"{inner} {outer} -s {s}"
+
+
+def _worker(rank, world, port, problem, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        import torch  # noqa: F401
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from medane_tchakorom_ufc_thesis_repository_amd.comm import LibComm
+        from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import (make_blocks, make_smsm, sm_solve,
+                                                                              smsm_solve)
+        from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Options
+        ctx = Context(0)
+        comm = LibComm(ctx, transport="host")
+        kind, dim, nx, ny, nz, s, rtol = problem
+        o = Options(_opts(world, s))
+        if kind == "smsm":
+            blocks, mini = make_smsm(ctx, dim, nx, ny, nz, world, [rank], s, o, comm)
+            res = smsm_solve(blocks, comm, s, mini, rtol=rtol, max_outer=60)
+            out = {"outer_its": res.outer_its, "norm0": res.norm0, "hist": list(res.hist),
+                   "lsqr_its": list(res.lsqr_its), "inner_its": np.array(res.inner_its).tolist(),
+                   "final_norm": res.final_norm}
+            mini.close()
+        else:
+            blocks = make_blocks(ctx, dim, nx, ny, nz, world, [rank], o, comm)
+            res = sm_solve(blocks, comm, rtol=rtol, max_outer=200)
+            out = {"outer_its": res.outer_its, "norm0": res.norm0, "hist": list(res.hist),
+                   "inner_its": np.array(res.inner_its).tolist(), "final_norm": res.final_norm}
+        out["x"] = blocks[0].x.get_array()
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out, None))
+    except Exception as e:  # report, do not hang the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc() + str(e)))
+
+
+def _run(world, problem):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, problem, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for _, _, err in out:
+        assert err is None, err
+    return [o for _, o, _ in out]
+
+
+@pytest.mark.parametrize("problem,world", [(("smsm", 3, 12, 10, 8, 4, 1e-6), 2), (("smsm", 2, 32, 32, 1, 4, 1e-6), 2),
+                                           (("sm", 3, 12, 10, 8, 0, 1e-6), 2), (("smsm", 3, 8, 8, 12, 3, 1e-6), 3)])
+def test_libcomm_ranks_bitwise_vs_oracle(oracle, problem, world):
+    kind, dim, nx, ny, nz, s, rtol = problem
+    outs = _run(world, problem)
+    inner = dict(restart=30, max_it=20, rtol=1e-20, abstol=1e-100, reduce_mode=oracle.REDUCE_DBR)
+    if kind == "smsm":
+        ro = oracle.smsm_solve(dim, nx, ny, nz, world, s, rtol, inner,
+                               dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0,
+                                    reduce_mode=oracle.REDUCE_DBR), max_outer=60)
+    else:
+        ro = oracle.sm_solve(dim, nx, ny, nz, world, rtol, inner, max_outer=200)
+    x = np.concatenate([o["x"] for o in outs])
+    assert np.array_equal(x, ro["x"])
+    for r, o in enumerate(outs):
+        assert o["outer_its"] == ro["outer_its"] and o["norm0"] == ro["norm0"]
+        assert np.array_equal(np.array(o["hist"]), ro["hist"])
+        assert o["final_norm"] == ro["final_norm"]
+        if kind == "smsm":
+            assert np.array_equal(np.array(o["lsqr_its"]), ro["lsqr_its"])
+            assert np.array_equal(np.array(o["inner_its"])[:, :, 0], ro["inner_its"][:, :, r])
+        else:
+            assert np.array_equal(np.array(o["inner_its"])[:, 0], ro["inner_its"][:, r])
