@@ -44,7 +44,7 @@ enum { MSK_SPMV_MULT = 0, MSK_SPMV_RESID = 1, MSK_SPMV_SCALED = 2 };
 // tuning flags
 enum {
   MSK_TUNE_MDOT_REV = 1,
-  MSK_TUNE_SPMV_NT = 2,
+  MSK_TUNE_SPMV_NT = 2,             // CSR SpMV: non-temporal col/val loads and y stores (every mode)
   MSK_TUNE_SPMV_XCD = 4,
   MSK_TUNE_SPMV_STAGE1 = 8,
   MSK_TUNE_VEC_TEMPORAL = 16,       // default-policy (not non-temporal) basis loads in MDot / MAXPY / dense
@@ -60,7 +60,8 @@ enum {
   MSK_TUNE_DV_NOELL = 32768,        // DV storage: CSR-order codes even where the ELL layout fits (at assembly)
   MSK_TUNE_GM_OPFUSE = 65536,       // GMRES: W = A (sc x) computed inside MDot and MAXPY instead of a MatMult kernel
   MSK_TUNE_MAXPY_UNROLL1 = 131072,  // MAXPY: one group of four per loop iteration (default: two, unrolled)
-  MSK_TUNE_MDOT_UNROLL2 = 262144    // MDot: two groups of four per loop iteration
+  MSK_TUNE_MDOT_UNROLL2 = 262144,   // MDot: two groups of four per loop iteration
+  MSK_TUNE_ELL_NTY = 1048576        // DV SpMV: non-temporal y stores (every mode)
 };
 
 extern "C" {

@@ -591,7 +591,19 @@ __device__ __forceinline__ void stage_csr_block(int t, int32_t n2, int32_t n4, c
   }
 }
 
-template <int MODE, bool NT, int SU>
+// POL bit 0: non-temporal col/val loads; bit 1: non-temporal y (and vout)
+// stores.  Default policy (POL 0) in every mode; MSK_TUNE_SPMV_NT selects POL 3.
+// In a standalone harness (tools/spmv_lab.hip, same instructions) POL 3 runs
+// the 512^3 MatMult at 0.72-0.76 of peak against 0.69-0.72 for POL 0, but
+// inside the library the same kernel measures 0.66-0.70 against 0.69-0.71
+// (tools/spmv_policy_ab.py, with and without torch in the process;
+// profiles/r02/spmv_nt/): the product keeps POL 0.
+__device__ __forceinline__ void st_pol(double* p, double v, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <int MODE, int POL, int SU>
 __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ col, const double* __restrict__ val,
                                                   const double* __restrict__ x, const double* __restrict__ b,
@@ -618,9 +630,9 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
     k0 = rowptr[r];
     k1 = rowptr[r + 1];
     if (MODE == MSK_SPMV_RESID) bb = b[r];
-    if (MODE == MSK_SPMV_SCALED && vout) vout[r] = x[r] * sc;
+    if (MODE == MSK_SPMV_SCALED && vout) st_pol(vout + r, x[r] * sc, POL & 2);
   }
-  stage_csr_block<NT, SU>(t, n2, n4, v2, c4, sval, scol);
+  stage_csr_block<(POL & 1) != 0, SU>(t, n2, n4, v2, c4, sval, scol);
   __syncthreads();
   if (r < r1) {
     double s = 0.0;
@@ -638,7 +650,7 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
         if (kb + q < k1) s = s + av[q] * xv[q];
       }
     }
-    y[r] = MODE == MSK_SPMV_RESID ? bb - s : s;
+    st_pol(y + r, MODE == MSK_SPMV_RESID ? bb - s : s, POL & 2);
   }
 }
 
@@ -1226,7 +1238,7 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
                                                  int ndict, const double* __restrict__ x,
                                                  const double* __restrict__ b, double* __restrict__ y,
                                                  const double* __restrict__ sdev, double* __restrict__ vout,
-                                                 const int* __restrict__ stop) {
+                                                 const int* __restrict__ stop, bool nty) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   typedef EllWord<W> EW;
   typedef typename EW::T CT;
@@ -1269,8 +1281,8 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
       }
     }
     if (r < nrows) {
-      if (MODE == MSK_SPMV_SCALED && vout) vout[r] = x[r] * sc;
-      y[r] = MODE == MSK_SPMV_RESID ? b[r] - s : s;
+      if (MODE == MSK_SPMV_SCALED && vout) st_pol(vout + r, x[r] * sc, nty);
+      st_pol(y + r, MODE == MSK_SPMV_RESID ? b[r] - s : s, nty);
     }
   }
 }
@@ -1457,6 +1469,7 @@ static void dot1_dispatch(int nv, const double* w, const Vecs& V, int64_t n, dou
 extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
                               int self, const int* stop, hipStream_t s) {
   if (nchunks <= 0) return 0;
+  if (!self && (nv < 1 || nv > MSK_MAX_GROUP)) return (int)hipErrorInvalidValue;
   const int var = vec_var() | ((g_tuning & MSK_TUNE_MDOT_SINGLE) ? 16 : 0) |
                   ((g_tuning & MSK_TUNE_MDOT_UNROLL2) ? 32 : 0);
   if (self)
@@ -1465,7 +1478,9 @@ extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n,
   else if (var == 33) dot1_dispatch<1, 33>(nv, w, *V, n, partial, nchunks, stop, s);
   else if (var == 17) dot1_dispatch<1, 17>(nv, w, *V, n, partial, nchunks, stop, s);
   else if (var == 16) dot1_dispatch<1, 16>(nv, w, *V, n, partial, nchunks, stop, s);
-  else dot1_dispatch<1, 0>(nv, w, *V, n, partial, nchunks, stop, s);
+  else if (var == 0) dot1_dispatch<1, 0>(nv, w, *V, n, partial, nchunks, stop, s);
+  else if (var == 32) dot1_dispatch<1, 32>(nv, w, *V, n, partial, nchunks, stop, s);
+  else return (int)hipErrorInvalidValue;  // a tuning combination with no kernel: fail, never run another one
   return (int)hipGetLastError();
 }
 
@@ -1537,7 +1552,7 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
     case 36: MSK_MAXPY_LAUNCH(36) break;
     case 37: MSK_MAXPY_LAUNCH(37) break;
     case 45: MSK_MAXPY_LAUNCH(45) break;
-    default: MSK_MAXPY_LAUNCH(37) break;
+    default: return (int)hipErrorInvalidValue;  // a tuning combination with no kernel: fail, never run another one
   }
 #undef MSK_MAXPY_LAUNCH
   return (int)hipGetLastError();
@@ -1552,18 +1567,18 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
   const XcdMap xm = xcd_map(nrows, plane);
   if (lds_cap > 0) {
     const bool nt = (g_tuning & MSK_TUNE_SPMV_NT) != 0;
-#define LAUNCH_LDS8(M, NTF)                                                                                   \
+#define LAUNCH_LDS8(M, POL_)                                                                                  \
   do {                                                                                                         \
     if (g_tuning & MSK_TUNE_SPMV_STAGE1)                                                                       \
-      k_spmv_lds8<M, NTF, 1><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,   \
-                                                             vout, stop, xm);                                  \
+      k_spmv_lds8<M, POL_, 1><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,  \
+                                                              vout, stop, xm);                                 \
     else                                                                                                       \
-      k_spmv_lds8<M, NTF, 4><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,   \
-                                                             vout, stop, xm);                                  \
+      k_spmv_lds8<M, POL_, 4><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,  \
+                                                              vout, stop, xm);                                 \
   } while (0)
-    if (mode == MSK_SPMV_RESID) { if (nt) LAUNCH_LDS8(MSK_SPMV_RESID, true); else LAUNCH_LDS8(MSK_SPMV_RESID, false); }
-    else if (mode == MSK_SPMV_SCALED) { if (nt) LAUNCH_LDS8(MSK_SPMV_SCALED, true); else LAUNCH_LDS8(MSK_SPMV_SCALED, false); }
-    else { if (nt) LAUNCH_LDS8(MSK_SPMV_MULT, true); else LAUNCH_LDS8(MSK_SPMV_MULT, false); }
+    if (mode == MSK_SPMV_RESID) { if (nt) LAUNCH_LDS8(MSK_SPMV_RESID, 3); else LAUNCH_LDS8(MSK_SPMV_RESID, 0); }
+    else if (mode == MSK_SPMV_SCALED) { if (nt) LAUNCH_LDS8(MSK_SPMV_SCALED, 3); else LAUNCH_LDS8(MSK_SPMV_SCALED, 0); }
+    else { if (nt) LAUNCH_LDS8(MSK_SPMV_MULT, 3); else LAUNCH_LDS8(MSK_SPMV_MULT, 0); }
 #undef LAUNCH_LDS8
   } else {
     if (mode == MSK_SPMV_RESID)
@@ -1581,12 +1596,16 @@ static void launch_ell(int mode, int32_t nrows, const uint8_t* code8, const int3
                        int ndict, const double* x, const double* b, double* y, const double* sdev, double* vout,
                        const int* stop, hipStream_t s) {
   const unsigned g = (unsigned)((nrows + kT * RPL - 1) / (kT * RPL));
+  const bool nty = (g_tuning & MSK_TUNE_ELL_NTY) != 0;
   if (mode == MSK_SPMV_RESID)
-    k_spmv_ell<MSK_SPMV_RESID, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop);
+    k_spmv_ell<MSK_SPMV_RESID, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop,
+                                                        nty);
   else if (mode == MSK_SPMV_SCALED)
-    k_spmv_ell<MSK_SPMV_SCALED, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop);
+    k_spmv_ell<MSK_SPMV_SCALED, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop,
+                                                         nty);
   else
-    k_spmv_ell<MSK_SPMV_MULT, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop);
+    k_spmv_ell<MSK_SPMV_MULT, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop,
+                                                       nty);
 }
 
 extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const uint8_t* code8,

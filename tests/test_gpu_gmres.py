@@ -158,3 +158,46 @@ def test_gmres_random_operators_bitwise(ctx, oracle, seed):
     xo, ro = oracle.gmres(O, b, x0=x0, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=1 if nonzero else 0, **o)
     assert (rg["its"], rg["reason"]) == (ro["its"], ro["reason"])
     assert np.array_equal(rg["hist"], ro["hist"]) and np.array_equal(xg, xo)
+
+
+@pytest.mark.parametrize("name", ["dtol", "nan_b", "inf_x0", "restart_breakdown", "null", "happy"])
+def test_gmres_termination_branches_vs_oracle(ctx, oracle, name):
+    """DIVERGED_DTOL, DIVERGED_NANORINF (b and x0), the restart breakdown test, the zero-column
+    NULL -> BREAKDOWN path and a mid-cycle happy breakdown (msplit_gmres.hip) against the oracle:
+    iterations, reason, residual history (NaN where the oracle has NaN) and x."""
+    import _gmres_divergence_cases as dc
+    (rp, col, val), b, x0, optstr, kw, want = dc.cases(oracle)[name]
+    n = len(rp) - 1
+    O = oracle.Mat.from_arrays(n, n, rp, col, val)
+    A = Mat.from_csr(ctx, n, n, rp, col, val)
+    xg, rg = _gpu_gmres(ctx, A, b, x0, optstr)
+    xo, ro = oracle.gmres(O, b, x0=x0, reduce_mode=oracle.REDUCE_DBR, **kw)
+    assert ro["reason"] == want
+    assert (rg["its"], rg["reason"]) == (ro["its"], ro["reason"])
+    assert np.array_equal(rg["hist"], ro["hist"], equal_nan=True)
+    assert np.array_equal(xg, xo, equal_nan=True)
+
+
+@pytest.mark.parametrize("flags", [0, 2, 1048576])   # default, MSK_TUNE_SPMV_NT, MSK_TUNE_ELL_NTY
+@pytest.mark.parametrize("storage", ["dv", "csr"])
+@pytest.mark.parametrize("case", [0, 2, 5])
+def test_gmres_storage_and_store_policy_bitwise(ctx, oracle, case, storage, flags):
+    """The GMRES step's SpMV in either storage and either load/store cache policy: same bits as the oracle."""
+    from test_gpu_kernels import tuning
+    dim, (nx, ny, nz), o, nonzero = CASES[case]
+    if dim == 3:
+        O = oracle.poisson3d_rows(nx, ny, nz, 0, nz)
+        A = Mat.box_stencil(ctx, 3, nx, ny, nz)
+    else:
+        O = oracle.poisson2d_rows(nx, ny, 0, nx * ny)
+        A = Mat.box_stencil(ctx, 2, ny, nx)
+    A.set_storage(storage)
+    n = O.shape[0]
+    b = O.mult(np.ones(n))
+    x0 = np.random.default_rng(7).uniform(-1, 1, n) if nonzero else None
+    with tuning(flags):
+        xg, rg = _gpu_gmres(ctx, A, b, x0, _opts_str(o, nonzero))
+    xo, ro = oracle.gmres(O, b, x0=x0, reduce_mode=oracle.REDUCE_DBR, **dict(o, guess_nonzero=1 if nonzero else 0))
+    assert (rg["its"], rg["reason"]) == (ro["its"], ro["reason"])
+    assert np.array_equal(rg["hist"], ro["hist"])
+    assert np.array_equal(xg, xo)

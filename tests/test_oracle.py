@@ -195,3 +195,21 @@ def test_oracle_sm_two_blocks_converges(oracle):
     assert r["hist"][-1] <= 1e-6 * r["norm0"]
     assert np.all(np.diff(r["hist"]) < 0)
     assert np.allclose(r["x"], 1.0, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["dtol", "nan_b", "inf_x0", "restart_breakdown", "null", "happy"])
+def test_oracle_gmres_termination_branches(oracle, name):
+    """Each non-rtol KSPGMRES exit is reached by the oracle on its constructed input (the GPU parity of
+    the same cases is test_gpu_gmres.py::test_gmres_termination_branches_vs_oracle)."""
+    import _gmres_divergence_cases as dc
+    (rp, col, val), b, x0, _, kw, want = dc.cases(oracle)[name]
+    n = len(rp) - 1
+    O = oracle.Mat.from_arrays(n, n, rp, col, val)
+    _, r = oracle.gmres(O, b, x0=x0, reduce_mode=oracle.REDUCE_DBR, **kw)
+    assert r["reason"] == want, (name, r["reason"], r["its"])
+    if name == "happy":
+        assert r["its"] == 2 and r["rnorm"] == 0.0
+    if name == "restart_breakdown":
+        assert r["its"] >= 3
+    if name == "null":
+        assert r["its"] == 1

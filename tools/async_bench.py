@@ -26,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def transport(ctx, n_plane: int, rows: int, s: int, reps: int):
+def transport(ctx, n_plane: int, rows: int, s: int, reps: int, modes=("host", "device")):
     """Payload GB/s of one send + receive, host-staged and through HBM slots."""
     from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncBroadcast, AsyncMessages, DenseMat, Vec
     import numpy as np
@@ -37,7 +37,7 @@ def transport(ctx, n_plane: int, rows: int, s: int, reps: int):
     for j in range(s):
         R.set_column(j, 0, Vec.from_array(ctx, np.full(rows, float(j))))
     R2 = DenseMat(ctx, rows, s)
-    for mode in ("host", "device"):
+    for mode in modes:
         name = f"/msplit_tb_{os.getpid()}_{uuid.uuid4().hex[:8]}"
         a = AsyncMessages(name, 2, 0, n_plane, owner=True)
         b = AsyncMessages(name, 2, 1, n_plane, owner=False)
@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rtol", type=float, default=1e-6)
     ap.add_argument("--transport", default="device", choices=["device", "host"])
+    ap.add_argument("--transport-modes", default="host,device", help="modes of the transport measurement")
+    ap.add_argument("--transport-only", action="store_true", help="measure the transport, skip the solve")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime)
     from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
@@ -103,7 +105,10 @@ def main():
     ctx = Context(0)
     n, nb = args.n, args.nb
     rows = n * n * args.planes
-    out = {"transport": transport(ctx, n * n, rows, args.s, args.reps)}
+    out = {"transport": transport(ctx, n * n, rows, args.s, args.reps, tuple(args.transport_modes.split(",")))}
+    if args.transport_only:
+        print(json.dumps(out, indent=1))
+        return
     inner = " ".join(f"-inner{b + 1}_ksp_max_it {args.inner_max_it} -inner{b + 1}_ksp_rtol 1e-20 "
                      f"-inner{b + 1}_pc_type none" for b in range(nb))
     outer = " ".join(f"-outer{b + 1}_ksp_type lsqr -outer{b + 1}_ksp_convergence_test default "

@@ -74,6 +74,7 @@ def main():
         return s["bytes"] / (s["ms"] * 1e-3) / 1e9, s["ms"] / max(s["launches"], 1) * 1e3
 
     res = {}
+    y_ref, mismatch = None, []
     for _ in range(args.rounds):
         for t in tunings:
             L.msk_set_tuning(t)
@@ -82,6 +83,11 @@ def main():
                 if "spmv" in kernels:
                     gb, us = timed(lambda: A.mult(w, y), "spmv")
                     res.setdefault(f"spmv/t{t}/g{g}", []).append((gb, us))
+                    ya = y.get_array()
+                    if y_ref is None:
+                        y_ref = ya
+                    elif not np.array_equal(ya, y_ref):
+                        mismatch.append(f"spmv/t{t}/g{g}")
             L.msk_set_spmv_group(0)
             if "mdot" in kernels:
                 for k in (1, 8, 16, 30):
@@ -99,6 +105,8 @@ def main():
     L.msk_set_tuning(0)
     out = {k: {"GBps_median": float(np.median([g for g, _ in v])), "GBps_max": float(max(g for g, _ in v)),
                "us_median": float(np.median([u for _, u in v]))} for k, v in res.items()}
+    out["spmv_bitwise_equal_across_tunings"] = not mismatch
+    out["spmv_mismatch"] = sorted(set(mismatch))
     print(json.dumps(out, indent=1))
 
 
