@@ -19,9 +19,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("run")
     ap.add_argument("--tag", default="r01")
+    ap.add_argument("--sub", default="final", help="directory under profiles/<tag>/ (its README.md is written there "
+                                                   "unless --sub is final, which writes profiles/<tag>/README.md)")
     a = ap.parse_args()
     run = a.run
-    D = os.path.join(ROOT, "profiles", a.tag, "final")
+    D = os.path.join(ROOT, "profiles", a.tag, a.sub)
     os.makedirs(D, exist_ok=True)
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), os.path.join(run, "pmc_fetch"),
                     os.path.join(run, "pmc_write"), "--n", "256", "--out", os.path.join(D, "traffic.json")],
@@ -37,7 +39,7 @@ def main():
     mx = [r for r in rows if r["Name"] == "k_maxpy_chunk"][0]
     rf = b["roofline"]
     L = [f"# Round {a.tag[1:]} profiles (MI355X, gfx950, ROCm 7.2)", "",
-         f"Command: `bash tools/gpu_round.sh {os.path.basename(run)}` = pytest -m gpu; `python bench.py`; "
+         f"Command: `bash tools/gpu_round.sh {os.path.basename(run)}` (or tools/gpu_r02.sh, which adds smoke) = pytest -m gpu; `python bench.py`; "
          "`rocprofv3 --kernel-trace --stats -T -- python3 bench.py --steps 3 --no-cpu-baseline`;",
          "two PMC passes (`--pmc FETCH_SIZE`, `--pmc WRITE_SIZE`) of `bench.py --steps 1 --warmup 0 --no-timing`, "
          "reduced by `tools/pmc_traffic.py` (read = 2 x FETCH_SIZE on gfx950, write = WRITE_SIZE). "
@@ -86,7 +88,8 @@ def main():
     if mb:
         L += ["", "## MatMult on the 512^3 7-point matrix (tools/microbench.py, y = A x, median of 3 x 10)", "",
               "| storage | us | algorithmic GB/s | of 8 TB/s |", "|---|---|---|---|"] + mb
-    open(os.path.join(ROOT, "profiles", a.tag, "README.md"), "w").write("\n".join(L) + "\n")
+    readme = os.path.join(ROOT, "profiles", a.tag, "README.md") if a.sub == "final" else os.path.join(D, "README.md")
+    open(readme, "w").write("\n".join(L) + "\n")
 
 
 if __name__ == "__main__":
