@@ -44,7 +44,7 @@ enum { MSK_SPMV_MULT = 0, MSK_SPMV_RESID = 1, MSK_SPMV_SCALED = 2 };
 // tuning flags
 enum {
   MSK_TUNE_MDOT_REV = 1,
-  MSK_TUNE_SPMV_NT = 2,             // CSR SpMV: non-temporal col/val loads and y stores (every mode)
+  MSK_TUNE_SPMV_TEMPORAL = 2,       // CSR SpMV: default-policy col/val loads and y stores (default: non-temporal)
   MSK_TUNE_SPMV_XCD = 4,
   MSK_TUNE_SPMV_STAGE1 = 8,
   MSK_TUNE_VEC_TEMPORAL = 16,       // default-policy (not non-temporal) basis loads in MDot / MAXPY / dense
@@ -61,7 +61,9 @@ enum {
   MSK_TUNE_GM_OPFUSE = 65536,       // GMRES: W = A (sc x) computed inside MDot and MAXPY instead of a MatMult kernel
   MSK_TUNE_MAXPY_UNROLL1 = 131072,  // MAXPY: one group of four per loop iteration (default: two, unrolled)
   MSK_TUNE_MDOT_UNROLL2 = 262144,   // MDot: two groups of four per loop iteration
-  MSK_TUNE_ELL_NTY = 1048576        // DV SpMV: non-temporal y stores (every mode)
+  MSK_TUNE_ELL_TEMPORAL_Y = 1048576, // DV SpMV: default-policy y stores (default: non-temporal)
+  MSK_TUNE_SPMV_NTY = 2097152,      // CSR SpMV: default-policy col/val loads, non-temporal y stores
+  MSK_TUNE_SPMV_GLDS = 4194304      // CSR SpMV: col/val staged by LDS-DMA (global_load_lds_dwordx4), non-temporal y
 };
 
 extern "C" {

@@ -553,10 +553,25 @@ __device__ __forceinline__ int32_t row_block(XcdMap m) {
 // Stage a row block's val/col slice (16-byte aligned-down views v2/c4 with n2/n4
 // slices) into LDS.  SU > 1: issue SU val and SU/2 col loads per lane before the
 // first LDS write, so staging costs one memory latency instead of one per slice.
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// SU == 0: LDS-DMA staging.  Each wave-instruction writes 64 consecutive 16-byte
+// slices (LDS destination wave-uniform, source per lane); the tail lanes of the
+// last instruction re-read the last slice into slack LDS, so the LDS capacity is
+// rounded up to 256 entries (msk_spmv).  The barrier after it waits for vmcnt(0).
 template <bool NT, int SU>
 __device__ __forceinline__ void stage_csr_block(int t, int32_t n2, int32_t n4, const double2* __restrict__ v2,
                                                 const int4* __restrict__ c4, double* sval, int32_t* scol) {
-  if constexpr (SU == 1) {
+  if constexpr (SU == 0) {
+    static_assert(!NT, "LDS-DMA staging runs with the default load policy");
+    const int lane = t & 63, w = t >> 6;
+    for (int32_t ib = w * 64; ib < n2; ib += kT)
+      glds16(v2 + min(ib + lane, n2 - 1), reinterpret_cast<char*>(sval) + (size_t)ib * 16);
+    for (int32_t ib = w * 64; ib < n4; ib += kT)
+      glds16(c4 + min(ib + lane, n4 - 1), reinterpret_cast<char*>(scol) + (size_t)ib * 16);
+  } else if constexpr (SU == 1) {
     for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = NT ? ld_nt(v2 + i) : v2[i];
     for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = NT ? ld_nt(c4 + i) : c4[i];
   } else {
@@ -592,14 +607,19 @@ __device__ __forceinline__ void stage_csr_block(int t, int32_t n2, int32_t n4, c
 }
 
 // POL bit 0: non-temporal col/val loads; bit 1: non-temporal y (and vout)
-// stores.  Default policy (POL 0) in every mode; MSK_TUNE_SPMV_NT selects POL 3.
-// In a standalone harness (tools/spmv_lab.hip, same instructions) POL 3 runs
-// the 512^3 MatMult at 0.72-0.76 of peak against 0.69-0.72 for POL 0, but
-// inside the library the same kernel measures 0.66-0.70 against 0.69-0.71
-// (tools/spmv_policy_ab.py, with and without torch in the process;
-// profiles/r02/spmv_nt/): the product keeps POL 0.
-__device__ __forceinline__ void st_pol(double* p, double v, bool nt) {
-  if (nt) __builtin_nontemporal_store(v, p);
+// stores.  Default POL 3 in every mode: col/val stream through once and y is
+// not re-read by this kernel, so neither should displace x (re-read across the
+// +-plane gathers) from L2/MALL.  Same box, same allocation, interleaved
+// (tools/spmv_policy_ab.py, profiles/r02/nt_ab/): 512^3 MatMult 0.689 (POL 0)
+// -> 0.711 (POL 2) -> 0.723 (POL 3) of 8 TB/s; 256^3 0.696 -> 0.771.
+// MSK_TUNE_SPMV_TEMPORAL selects POL 0, MSK_TUNE_SPMV_NTY POL 2.
+// A template, not a run-time bool: with "if (nt) nontemporal_store(p) else
+// store(p)" the optimizer merges the two stores to the same address into one
+// plain store (the non-temporal hint is dropped), which it did here until
+// round 2 -- the disassembly of every policy now shows the intended store.
+template <bool NT>
+__device__ __forceinline__ void st_pol(double* p, double v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 
@@ -630,7 +650,7 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
     k0 = rowptr[r];
     k1 = rowptr[r + 1];
     if (MODE == MSK_SPMV_RESID) bb = b[r];
-    if (MODE == MSK_SPMV_SCALED && vout) st_pol(vout + r, x[r] * sc, POL & 2);
+    if (MODE == MSK_SPMV_SCALED && vout) st_pol<(POL & 2) != 0>(vout + r, x[r] * sc);
   }
   stage_csr_block<(POL & 1) != 0, SU>(t, n2, n4, v2, c4, sval, scol);
   __syncthreads();
@@ -650,7 +670,7 @@ __global__ __launch_bounds__(kT) void k_spmv_lds8(int32_t nrows, const int32_t* 
         if (kb + q < k1) s = s + av[q] * xv[q];
       }
     }
-    st_pol(y + r, MODE == MSK_SPMV_RESID ? bb - s : s, POL & 2);
+    st_pol<(POL & 2) != 0>(y + r, MODE == MSK_SPMV_RESID ? bb - s : s);
   }
 }
 
@@ -1232,13 +1252,13 @@ struct EllWord<16> {
   static __device__ __forceinline__ T empty() { return T{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}; }
 };
 
-template <int MODE, int W, int RPL>
+template <int MODE, int W, int RPL, bool NTY>
 __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* __restrict__ code8,
                                                  const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
                                                  int ndict, const double* __restrict__ x,
                                                  const double* __restrict__ b, double* __restrict__ y,
                                                  const double* __restrict__ sdev, double* __restrict__ vout,
-                                                 const int* __restrict__ stop, bool nty) {
+                                                 const int* __restrict__ stop) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   typedef EllWord<W> EW;
   typedef typename EW::T CT;
@@ -1281,8 +1301,8 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
       }
     }
     if (r < nrows) {
-      if (MODE == MSK_SPMV_SCALED && vout) st_pol(vout + r, x[r] * sc, nty);
-      st_pol(y + r, MODE == MSK_SPMV_RESID ? b[r] - s : s, nty);
+      if (MODE == MSK_SPMV_SCALED && vout) st_pol<NTY>(vout + r, x[r] * sc);
+      st_pol<NTY>(y + r, MODE == MSK_SPMV_RESID ? b[r] - s : s);
     }
   }
 }
@@ -1566,19 +1586,38 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
   const size_t lds = (size_t)lds_cap * 12;
   const XcdMap xm = xcd_map(nrows, plane);
   if (lds_cap > 0) {
-    const bool nt = (g_tuning & MSK_TUNE_SPMV_NT) != 0;
+    const bool tmp = (g_tuning & MSK_TUNE_SPMV_TEMPORAL) != 0, nty = (g_tuning & MSK_TUNE_SPMV_NTY) != 0;
+    const bool glds = (g_tuning & MSK_TUNE_SPMV_GLDS) != 0, stage1 = (g_tuning & MSK_TUNE_SPMV_STAGE1) != 0;
+    // a combination with no kernel fails instead of running another variant
+    if ((tmp && nty) || (glds && (nty || stage1))) return (int)hipErrorInvalidValue;
+    // LDS-DMA staging has no non-temporal load form here: POL 2 (or 0 with TEMPORAL)
+    const bool nt = !tmp && !nty && !glds;
+    const bool ntst = !tmp;
+    const int32_t cap = glds ? ((lds_cap + 255) & ~255) : lds_cap;
+    const size_t ldsb = (size_t)cap * 12;
+    (void)lds;
 #define LAUNCH_LDS8(M, POL_)                                                                                  \
   do {                                                                                                         \
-    if (g_tuning & MSK_TUNE_SPMV_STAGE1)                                                                       \
-      k_spmv_lds8<M, POL_, 1><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,  \
-                                                              vout, stop, xm);                                 \
+    if (glds)                                                                                                  \
+      k_spmv_lds8<M, (POL_) & 2, 0><<<dim3(g), dim3(kT), ldsb, s>>>(nrows, rowptr, col, val, x, b, y, cap, sdev,     \
+                                                               vout, stop, xm);                                \
+    else if (stage1)                                                                                           \
+      k_spmv_lds8<M, POL_, 1><<<dim3(g), dim3(kT), ldsb, s>>>(nrows, rowptr, col, val, x, b, y, cap, sdev,     \
+                                                               vout, stop, xm);                                \
     else                                                                                                       \
-      k_spmv_lds8<M, POL_, 4><<<dim3(g), dim3(kT), lds, s>>>(nrows, rowptr, col, val, x, b, y, lds_cap, sdev,  \
-                                                              vout, stop, xm);                                 \
+      k_spmv_lds8<M, POL_, 4><<<dim3(g), dim3(kT), ldsb, s>>>(nrows, rowptr, col, val, x, b, y, cap, sdev,     \
+                                                               vout, stop, xm);                                \
   } while (0)
-    if (mode == MSK_SPMV_RESID) { if (nt) LAUNCH_LDS8(MSK_SPMV_RESID, 3); else LAUNCH_LDS8(MSK_SPMV_RESID, 0); }
-    else if (mode == MSK_SPMV_SCALED) { if (nt) LAUNCH_LDS8(MSK_SPMV_SCALED, 3); else LAUNCH_LDS8(MSK_SPMV_SCALED, 0); }
-    else { if (nt) LAUNCH_LDS8(MSK_SPMV_MULT, 3); else LAUNCH_LDS8(MSK_SPMV_MULT, 0); }
+#define LAUNCH_POL(M)                            \
+  do {                                           \
+    if (nt) LAUNCH_LDS8(M, 3);                   \
+    else if (ntst) LAUNCH_LDS8(M, 2);            \
+    else LAUNCH_LDS8(M, 0);                      \
+  } while (0)
+    if (mode == MSK_SPMV_RESID) LAUNCH_POL(MSK_SPMV_RESID);
+    else if (mode == MSK_SPMV_SCALED) LAUNCH_POL(MSK_SPMV_SCALED);
+    else LAUNCH_POL(MSK_SPMV_MULT);
+#undef LAUNCH_POL
 #undef LAUNCH_LDS8
   } else {
     if (mode == MSK_SPMV_RESID)
@@ -1591,21 +1630,30 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
   return (int)hipGetLastError();
 }
 
+template <int W, int RPL, bool NTY>
+static void launch_ell_pol(int mode, unsigned g, int32_t nrows, const uint8_t* code8, const int32_t* ddelta,
+                           const double* dval, int ndict, const double* x, const double* b, double* y,
+                           const double* sdev, double* vout, const int* stop, hipStream_t s) {
+  if (mode == MSK_SPMV_RESID)
+    k_spmv_ell<MSK_SPMV_RESID, W, RPL, NTY><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout,
+                                                             stop);
+  else if (mode == MSK_SPMV_SCALED)
+    k_spmv_ell<MSK_SPMV_SCALED, W, RPL, NTY><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout,
+                                                              stop);
+  else
+    k_spmv_ell<MSK_SPMV_MULT, W, RPL, NTY><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout,
+                                                            stop);
+}
+
 template <int W, int RPL>
 static void launch_ell(int mode, int32_t nrows, const uint8_t* code8, const int32_t* ddelta, const double* dval,
                        int ndict, const double* x, const double* b, double* y, const double* sdev, double* vout,
                        const int* stop, hipStream_t s) {
   const unsigned g = (unsigned)((nrows + kT * RPL - 1) / (kT * RPL));
-  const bool nty = (g_tuning & MSK_TUNE_ELL_NTY) != 0;
-  if (mode == MSK_SPMV_RESID)
-    k_spmv_ell<MSK_SPMV_RESID, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop,
-                                                        nty);
-  else if (mode == MSK_SPMV_SCALED)
-    k_spmv_ell<MSK_SPMV_SCALED, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop,
-                                                         nty);
+  if (!(g_tuning & MSK_TUNE_ELL_TEMPORAL_Y))  // default: non-temporal y (GMRES step +1.1 %, profiles/r02/nt_ab/)
+    launch_ell_pol<W, RPL, true>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, s);
   else
-    k_spmv_ell<MSK_SPMV_MULT, W, RPL><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop,
-                                                       nty);
+    launch_ell_pol<W, RPL, false>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, s);
 }
 
 extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const uint8_t* code8,

@@ -14,3 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run -f cs
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -f csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-csr-compare --no-timing --no-smsm-n1 --no-spmv512 > $OUT/pmc_fetch.out 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run -f csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-csr-compare --no-timing --no-smsm-n1 --no-spmv512 > $OUT/pmc_write.out 2>&1
 echo "exit $?" > $OUT/status
+[ "${POLICY_AB:-0}" = 1 ] && timeout -k 10 300 python tools/spmv_policy_ab.py --n 512 --reps 10 --rounds 5 --flags 0,2,2097152,4194304 > $OUT/spmv_policy_512.json 2> $OUT/policy.err
+exit 0

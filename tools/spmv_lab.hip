@@ -235,10 +235,191 @@ __global__ __launch_bounds__(kT) void k_stream(int32_t nrows, int64_t nnz, const
   }
 }
 
+
+// --- variant: wave-granular staging.  Each wave owns 64 consecutive rows and
+// stages their col/val slice into its own LDS region; no workgroup barrier
+// (LDS ops of one wave complete in order), so waves never wait on each other.
+// VAR bit 0: non-temporal y store.
+template <int VAR>
+__global__ __launch_bounds__(kT) void k_wave(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                             const int32_t* __restrict__ col, const double* __restrict__ val,
+                                             const double* __restrict__ x, double* __restrict__ y, int32_t wcap) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  char* base = smem + (size_t)w * wcap * 12;
+  double* sval = reinterpret_cast<double*>(base);
+  int32_t* scol = reinterpret_cast<int32_t*>(base + (size_t)wcap * 8);
+  const int32_t r0 = ((int32_t)blockIdx.x * 4 + w) * 64;
+  if (r0 >= nrows) return;
+  const int32_t r1 = min(r0 + 64, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s2 = start & ~1, s4 = start & ~3;
+  const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
+  const double2* v2 = reinterpret_cast<const double2*>(val + s2);
+  const int4* c4 = reinterpret_cast<const int4*>(col + s4);
+  const int32_t r = r0 + lane;
+  int32_t k0 = 0, k1 = 0;
+  if (r < r1) {
+    k0 = rowptr[r];
+    k1 = rowptr[r + 1];
+  }
+  for (int32_t i0 = lane; i0 < n2 || i0 < n4; i0 += 4 * 64) {
+    double2 vt[4];
+    int4 ct[2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int32_t i = i0 + u * 64;
+      if (i < n2) vt[u] = v2[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int32_t i = i0 + u * 64;
+      if (i < n4) ct[u] = c4[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int32_t i = i0 + u * 64;
+      if (i < n2) reinterpret_cast<double2*>(sval)[i] = vt[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int32_t i = i0 + u * 64;
+      if (i < n4) reinterpret_cast<int4*>(scol)[i] = ct[u];
+    }
+    for (int32_t i = i0 + 2 * 64; i < n4 && i < i0 + 4 * 64; i += 64) reinterpret_cast<int4*>(scol)[i] = c4[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (r < r1) {
+    double s = 0.0;
+    for (int32_t kb = k0; kb < k1; kb += 8) {
+      double av[8], xv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int32_t k = min(kb + q, k1 - 1);
+        av[q] = sval[k - s2];
+        xv[q] = x[scol[k - s4]];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (kb + q < k1) s = s + av[q] * xv[q];
+    }
+    if (VAR & 1) st_nt(y + r, s); else y[r] = s;
+  }
+}
+
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// --- variant: workgroup staging with LDS-DMA (global_load_lds_dwordx4): the
+// col/val slice goes to LDS with no VGPR round trip.  Each wave-instruction
+// writes 64 consecutive 16-byte slices; tail lanes re-read the last slice into
+// slack LDS (cap rounded up to 256 entries).  VAR bit 0: non-temporal y store.
+template <int VAR>
+__global__ __launch_bounds__(kT) void k_glds(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                             const int32_t* __restrict__ col, const double* __restrict__ val,
+                                             const double* __restrict__ x, double* __restrict__ y, int32_t cap) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sv = smem;
+  char* sc = smem + (size_t)cap * 8;
+  const double* sval = reinterpret_cast<const double*>(sv);
+  const int32_t* scol = reinterpret_cast<const int32_t*>(sc);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int32_t r0 = (int32_t)blockIdx.x * kT;
+  const int32_t r1 = min(r0 + kT, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s2 = start & ~1, s4 = start & ~3;
+  const int32_t n2 = (end - s2 + 1) >> 1, n4 = (end - s4 + 3) >> 2;
+  const double2* v2 = reinterpret_cast<const double2*>(val + s2);
+  const int4* c4 = reinterpret_cast<const int4*>(col + s4);
+  for (int32_t ib = w * 64; ib < n2; ib += kT) glds16(v2 + min(ib + lane, n2 - 1), sv + (size_t)ib * 16);
+  for (int32_t ib = w * 64; ib < n4; ib += kT) glds16(c4 + min(ib + lane, n4 - 1), sc + (size_t)ib * 16);
+  const int32_t r = r0 + t;
+  int32_t k0 = 0, k1 = 0;
+  if (r < r1) {
+    k0 = rowptr[r];
+    k1 = rowptr[r + 1];
+  }
+  __syncthreads();
+  if (r < r1) {
+    double s = 0.0;
+    for (int32_t kb = k0; kb < k1; kb += 8) {
+      double av[8], xv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int32_t k = min(kb + q, k1 - 1);
+        av[q] = sval[k - s2];
+        xv[q] = x[scol[k - s4]];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (kb + q < k1) s = s + av[q] * xv[q];
+    }
+    if (VAR & 1) st_nt(y + r, s); else y[r] = s;
+  }
+}
+
+// --- variant: product staging.  Entry-major (coalesced) pass: lane i loads
+// val pair i and col pair i, gathers the two x values and writes the two
+// products val*x to LDS (8 B per entry instead of 12); then lane r adds its
+// row's products left to right.  Same products, same order: bitwise.
+template <int VAR>
+__global__ __launch_bounds__(kT) void k_prod(int32_t nrows, const int32_t* __restrict__ rowptr,
+                                             const int32_t* __restrict__ col, const double* __restrict__ val,
+                                             const double* __restrict__ x, double* __restrict__ y, int32_t cap) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sp = reinterpret_cast<double*>(smem);
+  const int t = threadIdx.x;
+  const int32_t r0 = (int32_t)blockIdx.x * kT;
+  const int32_t r1 = min(r0 + kT, nrows);
+  const int32_t start = rowptr[r0], end = rowptr[r1];
+  const int32_t s2 = start & ~1;
+  const int32_t n2 = (end - s2 + 1) >> 1;
+  const double2* v2 = reinterpret_cast<const double2*>(val + s2);
+  const int2* c2 = reinterpret_cast<const int2*>(col + s2);
+  for (int32_t i0 = t; i0 < n2; i0 += 4 * kT) {
+    double2 vt[4];
+    int2 ct[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int32_t i = min(i0 + u * kT, n2 - 1);
+      vt[u] = v2[i];
+      ct[u] = c2[i];
+    }
+    double xa[4], xb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int32_t e = s2 + 2 * (i0 + u * kT);
+      xa[u] = (e >= start && e < end) ? x[ct[u].x] : 0.0;
+      xb[u] = (e + 1 >= start && e + 1 < end) ? x[ct[u].y] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int32_t i = i0 + u * kT;
+      if (i < n2) reinterpret_cast<double2*>(sp)[i] = make_double2(vt[u].x * xa[u], vt[u].y * xb[u]);
+    }
+  }
+  const int32_t r = r0 + t;
+  int32_t k0 = 0, k1 = 0;
+  if (r < r1) {
+    k0 = rowptr[r];
+    k1 = rowptr[r + 1];
+  }
+  __syncthreads();
+  if (r < r1) {
+    double s = 0.0;
+    for (int32_t k = k0; k < k1; ++k) s = s + sp[k - s2];
+    if (VAR & 1) st_nt(y + r, s); else y[r] = s;
+  }
+}
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 512;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
   const bool per_launch_events = argc > 3 && atoi(argv[3]) != 0;
+  const int group = argc > 4 ? atoi(argv[4]) : 0;  // 0: the original set; 1: staging variants
   const int64_t N = (int64_t)n * n * n;
   const int nblk = (int)((N + kT - 1) / kT);
   int32_t *rowptr, *col;
@@ -275,6 +456,14 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   const int32_t cap = (int32_t)((maxblk + 8 + 3) & ~3LL);
   const int32_t cap2 = (int32_t)((maxblk2 + 8 + 3) & ~3LL);
+  int64_t maxw = 0;
+  for (int64_t b = 0; b < (N + 63) / 64; ++b) {
+    const int64_t e = std::min<int64_t>((b + 1) * 64, N);
+    maxw = std::max<int64_t>(maxw, hp[e] - hp[b * 64]);
+  }
+  const int32_t wcap = (int32_t)((maxw + 8 + 3) & ~3LL);
+  const int32_t gcap = (int32_t)((maxblk + 8 + 255) & ~255LL);
+  const int nblk_w = (int)((N + 255) / 256);
   const double bytes = 12.0 * nnz + 4.0 * (N + 1) + 16.0 * N;
   printf("{\"n\": %d, \"nnz\": %lld, \"alg_bytes\": %.0f, \"lds_cap\": %d, \"results\": {", n, (long long)nnz, bytes, cap);
   hipEvent_t e0, e1;
@@ -283,6 +472,7 @@ int main(int argc, char** argv) {
   std::vector<double> hy(N), hy0(N);
   bool first = true;
   int round_ = 0;
+  double* ycheck = nullptr;
   auto run = [&](const char* name, auto launch, bool check) {
     launch();
     CK(hipDeviceSynchronize());
@@ -313,7 +503,7 @@ int main(int argc, char** argv) {
     const double gbs = bytes / (us * 1e-6) / 1e9;
     const char* eq = "null";
     if (check) {
-      CK(hipMemcpy(hy.data(), y, N * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hy.data(), ycheck ? ycheck : y, N * 8, hipMemcpyDeviceToHost));
       eq = memcmp(hy.data(), hy0.data(), N * 8) == 0 ? "true" : "false";
     }
     printf("%s\"%s/%d\": {\"us\": %.1f, \"GBps\": %.1f, \"frac\": %.4f, \"bitwise\": %s}", first ? "" : ", ", name, round_, us, gbs,
@@ -325,7 +515,44 @@ int main(int argc, char** argv) {
   k_lds8<0, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y0, cap);
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(hy0.data(), y0, N * 8, hipMemcpyDeviceToHost));
-  for (round_ = 0; round_ < 3; ++round_) {
+  if (group == 2) {  // the same arrays allocated physically contiguous (hipDeviceMallocContiguous)
+    int32_t *colC, *rpC;
+    double *valC, *xC, *yC;
+    CK(hipExtMallocWithFlags((void**)&rpC, (N + 1) * 4, hipDeviceMallocContiguous));
+    CK(hipExtMallocWithFlags((void**)&colC, (nnz + 4) * 4, hipDeviceMallocContiguous));
+    CK(hipExtMallocWithFlags((void**)&valC, (nnz + 2) * 8, hipDeviceMallocContiguous));
+    CK(hipExtMallocWithFlags((void**)&xC, N * 8, hipDeviceMallocContiguous));
+    CK(hipExtMallocWithFlags((void**)&yC, N * 8, hipDeviceMallocContiguous));
+    CK(hipMemcpy(rpC, rowptr, (N + 1) * 4, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(colC, col, (nnz + 4) * 4, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(valC, val, (nnz + 2) * 8, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(xC, x, N * 8, hipMemcpyDeviceToDevice));
+    CK(hipDeviceSynchronize());
+    for (round_ = 0; round_ < 3; ++round_) {
+      ycheck = nullptr;
+      run("lib_t", [&] { k_lds8<16, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
+      run("glds_nty", [&] { k_glds<1><<<nblk, kT, gcap * 12>>>((int32_t)N, rowptr, col, val, x, y, gcap); }, true);
+      run("lib_ntvcy", [&] { k_lds8<29, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
+      ycheck = yC;
+      run("lib_t_contig", [&] { k_lds8<16, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rpC, colC, valC, xC, yC, cap); }, true);
+      run("glds_nty_contig", [&] { k_glds<1><<<nblk, kT, gcap * 12>>>((int32_t)N, rpC, colC, valC, xC, yC, gcap); }, true);
+      run("lib_ntvcy_contig", [&] { k_lds8<29, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rpC, colC, valC, xC, yC, cap); }, true);
+    }
+    ycheck = nullptr;
+  }
+  for (round_ = 0; round_ < 3 && group == 1; ++round_) {
+    run("lib_t", [&] { k_lds8<16, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
+    run("lib_nty", [&] { k_lds8<17, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
+    run("lib_ntvcy", [&] { k_lds8<29, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
+    run("wave", [&] { k_wave<0><<<nblk_w, kT, wcap * 12 * 4>>>((int32_t)N, rowptr, col, val, x, y, wcap); }, true);
+    run("wave_nty", [&] { k_wave<1><<<nblk_w, kT, wcap * 12 * 4>>>((int32_t)N, rowptr, col, val, x, y, wcap); }, true);
+    run("glds", [&] { k_glds<0><<<nblk, kT, gcap * 12>>>((int32_t)N, rowptr, col, val, x, y, gcap); }, true);
+    run("glds_nty", [&] { k_glds<1><<<nblk, kT, gcap * 12>>>((int32_t)N, rowptr, col, val, x, y, gcap); }, true);
+    run("prod", [&] { k_prod<0><<<nblk, kT, cap * 8>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
+    run("prod_nty", [&] { k_prod<1><<<nblk, kT, cap * 8>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
+    run("stream", [&] { k_stream<1><<<nblk, kT>>>((int32_t)N, nnz, rowptr, col, val, x, y); }, false);
+  }
+  for (round_ = 0; round_ < 3 && group == 0; ++round_) {
     run("lds8", [&] { k_lds8<0, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
     run("lds8_nty", [&] { k_lds8<1, 1><<<nblk, kT, cap * 12>>>((int32_t)N, rowptr, col, val, x, y, cap); }, true);
     run("lds8_rpl2", [&] { k_lds8<0, 2><<<(nblk + 1) / 2, kT, cap2 * 12>>>((int32_t)N, rowptr, col, val, x, y, cap2); }, true);
