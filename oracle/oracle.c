@@ -786,10 +786,11 @@ static void ls_mult_transpose(const ls_layout *L, const double *const *R, const 
 }
 
 /* MatNorm(R, NORM_FROBENIUS).  SEQ: one sum of squares over the columns in
- * order (each over all N rows), then sqrt -- PETSc calls BLAS dnrm2 here,
- * whose scaled evaluation can differ in the last bits; the value only enters
- * the KSPLSQRConvergedDefault threshold rtol*anorm*rnorm.  DBR: per block the
- * column sums of squares (DBR) added in column order, then blocks in order. */
+ * order (each over all N rows), then sqrt -- PETSc 3.22.1's MatNorm_SeqDense in
+ * a double build (R is MATMPIDENSE on a one-process block communicator,
+ * SMSM-global.c:136): a plain running sum over the column-major array; BLASnrm2
+ * only under PETSC_USE_REAL___FP16.  DBR: per block the column sums of squares
+ * (DBR) added in column order, then blocks in order. */
 static double ls_frobenius(const ls_layout *L, const double *const *R, const int64_t *lda) {
   double t = 0.0;
   if (L->mode == ORC_REDUCE_SEQ) {
