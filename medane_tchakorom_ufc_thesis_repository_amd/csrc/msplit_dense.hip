@@ -41,6 +41,22 @@ __device__ __forceinline__ double2 ld_col(const double* p) {
   }
 }
 
+// y/wout stores: NT (template, never a run-time bool: the optimizer merges the two
+// stores of "if (nt) nontemporal_store else store" into one plain store) -- the
+// vectors u and u/beta of an LSQR step stream through once per launch and exceed
+// the MALL from ~32 M rows on (msplit_kernels.hip, st_pol).
+template <bool NT>
+__device__ __forceinline__ void st2(double* p, double a, double b) {
+  if constexpr (NT) {
+    dx2 o;
+    o.x = a;
+    o.y = b;
+    __builtin_nontemporal_store(o, reinterpret_cast<dx2*>(p));
+  } else {
+    *reinterpret_cast<double2*>(p) = make_double2(a, b);
+  }
+}
+
 __device__ __forceinline__ double wave_butterfly(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
@@ -50,15 +66,42 @@ __device__ __forceinline__ double wave_butterfly(double v) {
 // ------------------------------------------------------------------ gemv
 // y = A[:, 0:nc] coef (+ nal * U, VecAXPY skipped when nal == 0), per row
 // ((0 + c0 a0) + c1 a1) + ...; NORM: the DBR partial of ||y||^2 of this chunk.
-template <bool AXPY, bool NORM, bool FULL, int VEC>
+// G columns per load group (FULL chunks): G x kIters 16-byte loads per lane issued
+// together before their products are added; every u[j] still takes the columns in
+// order q = 0, 1, ... (the dgemv order), so the result does not depend on G.
+template <bool AXPY, bool NORM, bool FULL, int VEC, int G, bool NTS>
 __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t lda, int nc,
                                           const double* __restrict__ coef, double nal, const double* __restrict__ U,
                                           double* __restrict__ y, int64_t base, int64_t n, double& sq) {
   double u[2 * kIters];
 #pragma unroll
   for (int j = 0; j < 2 * kIters; ++j) u[j] = 0.0;
+  int q0 = 0;
+  if constexpr (FULL && G > 1) {
 #pragma unroll 1
-  for (int q = 0; q < nc; ++q) {
+    for (; q0 + G <= nc; q0 += G) {
+      double a[G];
+      double2 p[G][kIters];
+#pragma unroll
+      for (int g = 0; g < G; ++g) a[g] = coef[q0 + g];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const double* __restrict__ col = A + (int64_t)(q0 + g) * lda;
+#pragma unroll
+        for (int j = 0; j < kIters; ++j) p[g][j] = ld_col<VEC>(col + base + j * (2 * kT));
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int j = 0; j < kIters; ++j) {
+          u[2 * j] = u[2 * j] + a[g] * p[g][j].x;
+          u[2 * j + 1] = u[2 * j + 1] + a[g] * p[g][j].y;
+        }
+      }
+    }
+  }
+#pragma unroll 1
+  for (int q = q0; q < nc; ++q) {
     const double a = coef[q];  // wave-uniform scalar load
     const double* __restrict__ col = A + (int64_t)q * lda;
     double p[2 * kIters];
@@ -88,7 +131,7 @@ __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t 
         r0 = r0 + nal * q.x;
         r1 = r1 + nal * q.y;
       }
-      *reinterpret_cast<double2*>(y + e) = make_double2(r0, r1);
+      st2<NTS>(y + e, r0, r1);
       if (NORM) {
         acc = acc + r0 * r0;
         acc = acc + r1 * r1;
@@ -109,7 +152,7 @@ __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t 
   sq = acc;
 }
 
-template <bool AXPY, bool NORM, int VEC>
+template <bool AXPY, bool NORM, int VEC, int G, bool NTS>
 __global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A, int64_t lda, int nc,
                                                    const double* __restrict__ coef, const double* __restrict__ naldev,
                                                    const double* __restrict__ U, double* __restrict__ y, int64_t n,
@@ -120,8 +163,8 @@ __global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A,
   const int64_t base = c * kChunk + 2 * t;
   const double nal = AXPY ? *naldev : 0.0;
   double sq = 0.0;
-  if (VEC && (c + 1) * kChunk <= n) gemv_body<AXPY, NORM, true, VEC>(A, lda, nc, coef, nal, U, y, base, n, sq);
-  else gemv_body<AXPY, NORM, false, VEC>(A, lda, nc, coef, nal, U, y, base, n, sq);
+  if (VEC && (c + 1) * kChunk <= n) gemv_body<AXPY, NORM, true, VEC, G, NTS>(A, lda, nc, coef, nal, U, y, base, n, sq);
+  else gemv_body<AXPY, NORM, false, VEC, 1, NTS>(A, lda, nc, coef, nal, U, y, base, n, sq);
   if (NORM) {
     __shared__ double red[4];
     sq = wave_butterfly(sq);
@@ -134,7 +177,7 @@ __global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A,
 // ------------------------------------------------------- scaled column dots
 // w' = w * (*sc) (VecScale, written back to wout) when SCALE, then the DBR
 // stage-1 partials of column_v . w' for v < nc: partial[v*nchunks + c].
-template <bool SCALE, int VEC>
+template <bool SCALE, int VEC, int G, bool NTS>
 __global__ __launch_bounds__(kT) void k_scaled_dot(const double* win, double* wout, const double* __restrict__ scdev,
                                                    const double* __restrict__ A, int64_t lda, int nc, int64_t n,
                                                    double* __restrict__ partial, int64_t nchunks,
@@ -162,15 +205,45 @@ __global__ __launch_bounds__(kT) void k_scaled_dot(const double* win, double* wo
       wr[2 * j] = wr[2 * j] * sc;
       wr[2 * j + 1] = wr[2 * j + 1] * sc;
       if (full) {
-        *reinterpret_cast<double2*>(wout + e) = make_double2(wr[2 * j], wr[2 * j + 1]);
+        st2<NTS>(wout + e, wr[2 * j], wr[2 * j + 1]);
       } else {
         if (e < n) wout[e] = wr[2 * j];
         if (e + 1 < n) wout[e + 1] = wr[2 * j + 1];
       }
     }
   }
+  int v0 = 0;
+  if constexpr (G > 1) {
+    if (full) {  // G columns' loads together, then G independent sums and butterflies
 #pragma unroll 1
-  for (int v = 0; v < nc; ++v) {
+      for (; v0 + G <= nc; v0 += G) {
+        double2 q[G][kIters];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const double* __restrict__ col = A + (int64_t)(v0 + g) * lda;
+#pragma unroll
+          for (int j = 0; j < kIters; ++j) q[g][j] = ld_col<VEC>(col + base + j * (2 * kT));
+        }
+        double acc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          acc[g] = 0.0;
+#pragma unroll
+          for (int j = 0; j < kIters; ++j) {
+            acc[g] = acc[g] + wr[2 * j] * q[g][j].x;
+            acc[g] = acc[g] + wr[2 * j + 1] * q[g][j].y;
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const double r = wave_butterfly(acc[g]);
+          if (lane == 0) red[v0 + g][wv] = r;
+        }
+      }
+    }
+  }
+#pragma unroll 1
+  for (int v = v0; v < nc; ++v) {
     const double* __restrict__ col = A + (int64_t)v * lda;
     double acc = 0.0;
     if (full) {
@@ -244,8 +317,27 @@ extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc,
   const bool axpy = U != nullptr, norm = sumsq_dev != nullptr;
   KTimer kt(c, MSP_KERNEL_DGEMV, 8.0 * (double)n * (nc + 1 + (axpy ? 1 : 0)));
   const dim3 g((unsigned)nch), b(kT);
-#define GEMV(AX, NO, VE) \
-  k_dense_gemv<AX, NO, VE><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, y, n, partial, stop)
+  const int tu = msk_get_tuning();
+  const int grp = (tu & MSK_TUNE_DENSE_G1) ? 1 : (tu & MSK_TUNE_DENSE_G2) ? 2 : 4;
+  const bool nts = !(tu & MSK_TUNE_DENSE_TEMPORAL_ST);
+  if ((tu & MSK_TUNE_DENSE_G1) && (tu & MSK_TUNE_DENSE_G2)) {
+    mspi_set_error(MSP_ERR_ARG_OUTOFRANGE, "tuning: DENSE_G1 and DENSE_G2 together select no kernel");
+    return MSP_ERR_ARG_OUTOFRANGE;
+  }
+#define GEMVK(AX, NO, VE, G_, NT_) \
+  k_dense_gemv<AX, NO, VE, G_, NT_><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, y, n, partial, stop)
+#define GEMV(AX, NO, VE)                                         \
+  do {                                                           \
+    if (nts) {                                                   \
+      if (grp == 4) GEMVK(AX, NO, VE, 4, true);                  \
+      else if (grp == 2) GEMVK(AX, NO, VE, 2, true);             \
+      else GEMVK(AX, NO, VE, 1, true);                           \
+    } else {                                                     \
+      if (grp == 4) GEMVK(AX, NO, VE, 4, false);                 \
+      else if (grp == 2) GEMVK(AX, NO, VE, 2, false);            \
+      else GEMVK(AX, NO, VE, 1, false);                          \
+    }                                                            \
+  } while (0)
 #define GEMV3(AX, NO) \
   if (vec == 2) GEMV(AX, NO, 2); else if (vec == 1) GEMV(AX, NO, 1); else GEMV(AX, NO, 0);
   if (axpy && norm) { GEMV3(true, true) }
@@ -254,6 +346,7 @@ extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc,
   else { GEMV3(false, false) }
 #undef GEMV3
 #undef GEMV
+#undef GEMVK
   KCHK((int)hipGetLastError());
   if (norm && mspi_reduce_seq(c)) {  // ||y||^2 in PETSc's order (msplit_seq.hip)
     Vecs v = {};
@@ -273,6 +366,13 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
     return MSP_SUCCESS;
   }
   KTimer kt(c, MSP_KERNEL_DGEMVT, 8.0 * (double)n * (nc + 1 + (sc_dev ? 1 : 0)));
+  const int tu = msk_get_tuning();
+  const int grp = (tu & MSK_TUNE_DENSE_G1) ? 1 : (tu & MSK_TUNE_DENSE_G2) ? 2 : 4;
+  const bool nts = !(tu & MSK_TUNE_DENSE_TEMPORAL_ST);
+  if ((tu & MSK_TUNE_DENSE_G1) && (tu & MSK_TUNE_DENSE_G2)) {
+    mspi_set_error(MSP_ERR_ARG_OUTOFRANGE, "tuning: DENSE_G1 and DENSE_G2 together select no kernel");
+    return MSP_ERR_ARG_OUTOFRANGE;
+  }
   const int vec = !(aligned16(A) && (lda % 2 == 0) && aligned16(win) && (!sc_dev || aligned16(wout))) ? 0
                   : (msk_get_tuning() & MSK_TUNE_VEC_TEMPORAL) ? 1 : 2;
   for (int g0 = 0; g0 < nc; g0 += kMaxCols) {
@@ -281,7 +381,20 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
     const bool scale = sc_dev && g0 == 0;          // scale once, later groups read the scaled vector
     const double* src = (sc_dev && g0 > 0) ? wout : win;
     const dim3 gr((unsigned)nch), b(kT);
-#define SDOT(SC, VE, WO, SD) k_scaled_dot<SC, VE><<<gr, b, 0, c->stream>>>(src, WO, SD, Ag, lda, g, n, partial, nch, stop)
+#define SDOTK(SC, VE, WO, SD, G_, NT_) \
+  k_scaled_dot<SC, VE, G_, NT_><<<gr, b, 0, c->stream>>>(src, WO, SD, Ag, lda, g, n, partial, nch, stop)
+#define SDOT(SC, VE, WO, SD)                                        \
+  do {                                                              \
+    if (nts) {                                                      \
+      if (grp == 4) SDOTK(SC, VE, WO, SD, 4, true);                 \
+      else if (grp == 2) SDOTK(SC, VE, WO, SD, 2, true);            \
+      else SDOTK(SC, VE, WO, SD, 1, true);                          \
+    } else {                                                        \
+      if (grp == 4) SDOTK(SC, VE, WO, SD, 4, false);                \
+      else if (grp == 2) SDOTK(SC, VE, WO, SD, 2, false);           \
+      else SDOTK(SC, VE, WO, SD, 1, false);                         \
+    }                                                               \
+  } while (0)
     if (scale) {
       if (vec == 2) SDOT(true, 2, wout, sc_dev);
       else if (vec == 1) SDOT(true, 1, wout, sc_dev);
@@ -292,6 +405,7 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
       else SDOT(false, 0, nullptr, nullptr);
     }
 #undef SDOT
+#undef SDOTK
     KCHK((int)hipGetLastError());
     if (mspi_reduce_seq(c)) {  // dgemv 'T' order: each column . w in sequence (msplit_seq.hip)
       Vecs v = {};

@@ -63,7 +63,10 @@ enum {
   MSK_TUNE_MDOT_UNROLL2 = 262144,   // MDot: two groups of four per loop iteration
   MSK_TUNE_ELL_TEMPORAL_Y = 1048576, // DV SpMV: default-policy y stores (default: non-temporal)
   MSK_TUNE_SPMV_NTY = 2097152,      // CSR SpMV: default-policy col/val loads, non-temporal y stores
-  MSK_TUNE_SPMV_GLDS = 4194304      // CSR SpMV: col/val staged by LDS-DMA (global_load_lds_dwordx4), non-temporal y
+  MSK_TUNE_SPMV_GLDS = 4194304,     // CSR SpMV: col/val staged by LDS-DMA (global_load_lds_dwordx4), non-temporal y
+  MSK_TUNE_DENSE_G1 = 8388608,      // LSQR dense kernels: one column per load group (round-1 kernels; default four)
+  MSK_TUNE_DENSE_G2 = 16777216,     // LSQR dense kernels: two columns per load group
+  MSK_TUNE_DENSE_TEMPORAL_ST = 33554432  // LSQR dense kernels: default-policy u / u/beta stores (default: non-temporal)
 };
 
 extern "C" {

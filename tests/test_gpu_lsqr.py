@@ -91,8 +91,15 @@ CASES = [
 ]
 
 
+# msplit_kernels.h: the LSQR dense kernels' load grouping and store policy (default: four columns, non-temporal)
+DENSE_G1, DENSE_G2, DENSE_TEMPORAL_ST = 8388608, 16777216, 33554432
+
+
+@pytest.mark.parametrize("flags", [0, DENSE_G1, DENSE_G2, DENSE_TEMPORAL_ST, DENSE_G1 | DENSE_TEMPORAL_ST])
 @pytest.mark.parametrize("case", CASES)
-def test_lsqr_bitwise_vs_oracle(ctx, oracle, case):
+def test_lsqr_bitwise_vs_oracle(ctx, oracle, case, flags):
+    """Every load grouping / store policy of k_dense_gemv and k_scaled_dot gives the oracle's bits."""
+    from test_gpu_kernels import tuning
     case = dict(case)
     cuts, s = case.pop("cuts"), case.pop("s")
     n = sum(cuts)
@@ -101,13 +108,22 @@ def test_lsqr_bitwise_vs_oracle(ctx, oracle, case):
     edges = np.cumsum([0] + cuts)
     Rs = [R[a:c] for a, c in zip(edges[:-1], edges[1:])]
     bs = [b[a:c] for a, c in zip(edges[:-1], edges[1:])]
-    x, l = _lsqr_gpu(ctx, Rs, bs, **case)
+    with tuning(flags):
+        x, l = _lsqr_gpu(ctx, Rs, bs, **case)
     xo, ro = oracle.lsqr(Rs, bs, reduce_mode=oracle.REDUCE_DBR, **case)
     assert (l.get_iteration_number(), l.get_converged_reason()) == (ro["its"], ro["reason"])
     assert l.get_residual_norm() == ro["rnorm"]
     assert l.get_norms() == (ro["arnorm"], ro["anorm"])
     assert np.array_equal(l.get_residual_history(), ro["hist"])
     assert np.array_equal(x, xo)
+
+
+def test_dense_tuning_without_kernel_fails_loudly(ctx):
+    from test_gpu_kernels import tuning
+    R = RNG.standard_normal((5000, 3))
+    with tuning(DENSE_G1 | DENSE_G2), pytest.raises(Exception):
+        _lsqr_gpu(ctx, [R], [RNG.standard_normal(5000)], max_it=5, rtol=1e-15, abstol=1e-100, exact_norm=1,
+                  conv_test=0)
 
 
 def test_lsqr_edge_cases(ctx, oracle):

@@ -56,8 +56,8 @@ def main():
     if "lsqr" in kernels:
         s = 20
         R = DenseMat(ctx, N, s)
-        for j in range(s):
-            R.set_column(j, 0, w)
+        for j in range(s):    # independent columns, so the LSQR runs its max_it steps
+            R.set_column(j, 0, Vec.from_array(ctx, rng.uniform(-1, 1, N)))
         l = LSQR(ctx)
         l._set(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
         l.set_operators([R])
