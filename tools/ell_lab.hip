@@ -452,6 +452,87 @@ __global__ __launch_bounds__(kT) void k_pair(int32_t nrows, const uint8_t* __res
   }
 }
 
+
+// --- dord: loop over the DICTIONARY (sorted by delta, then value) instead of over a
+// row's code positions.  A row holds at most one entry per column, so visiting the
+// dictionary in ascending delta visits each row's entries in CSR order: the same
+// sum.  The delta of entry e is wave-uniform (scalar load), so x[r] serves d = 0, its
+// lane neighbours (shuffles) d = -1 / +1, and only the other deltas gather; a row
+// without entry e masks its lane off (presence bitmask from its 8 codes).
+// ND: dictionary size bound (<= 32), all entries' loads in flight together.
+template <int RPL, int ND>
+__global__ __launch_bounds__(kT) void k_dord(int32_t nrows, const uint8_t* __restrict__ code8,
+                                             const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
+                                             int ndict, const double* __restrict__ x, double* __restrict__ y) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int32_t r0 = (int32_t)blockIdx.x * (kT * RPL);
+  uint32_t pm[RPL];
+  double xr[RPL], xm[RPL], xp[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    const u32x2 cw = r < nrows ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r)
+                               : u32x2{0xFFFFFFFFu, 0xFFFFFFFFu};
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = cbyte(cw, q);
+      if (c != 255) m |= 1u << c;
+    }
+    pm[j] = m;
+    xr[j] = r < nrows ? x[r] : 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    xm[j] = __shfl_up(xr[j], 1, 64);
+    xp[j] = __shfl_down(xr[j], 1, 64);
+    if (lane == 0) xm[j] = (r >= 1 && r - 1 < nrows) ? x[r - 1] : 0.0;
+    if (lane == 63) xp[j] = (r + 1 < nrows) ? x[r + 1] : 0.0;
+  }
+  int32_t dd[ND];
+  double dv[ND];
+#pragma unroll
+  for (int e = 0; e < ND; ++e) {
+    dd[e] = e < ndict ? ddelta[e] : 0x40000000;   // beyond ndict: no row is marked present
+    dv[e] = e < ndict ? dval[e] : 0.0;
+  }
+  double xv[RPL][ND];
+#pragma unroll
+  for (int e = 0; e < ND; ++e) {
+    const int32_t d = dd[e];  // wave-uniform: these are scalar branches
+    if (d == 0) {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) xv[j][e] = xr[j];
+    } else if (d == -1) {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) xv[j][e] = xm[j];
+    } else if (d == 1) {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) xv[j][e] = xp[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) {
+        const int32_t r = r0 + t + kT * j;
+        xv[j][e] = ((pm[j] >> e) & 1) ? x[r + d] : 0.0;
+      }
+    }
+  }
+  double s[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    s[j] = 0.0;
+#pragma unroll
+    for (int e = 0; e < ND; ++e)
+      if ((pm[j] >> e) & 1) s[j] = s[j] + dv[e] * xv[j][e];
+  }
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    if (r < nrows) st_nt(y + r, s[j]);
+  }
+}
+
 // block order remap: XCD x (blockIdx % 8) takes the blocks of its eighth of a z-window
 template <int RPL>
 __global__ __launch_bounds__(kT) void k_basex(int32_t nrows, const uint8_t* __restrict__ code8,
@@ -558,6 +639,9 @@ int main(int argc, char** argv) {
     run("base2", [&] { k_base<2><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("uni4", [&] { k_uni<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
 
+    run("dord4", [&] { k_dord<4, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
+    run("dord2", [&] { k_dord<2, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
+    run("dord1", [&] { k_dord<1, 8><<<g1, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("pair2", [&] { k_pair<2, false><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("pair2s", [&] { k_pair<2, true><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("pair1s", [&] { k_pair<1, true><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
