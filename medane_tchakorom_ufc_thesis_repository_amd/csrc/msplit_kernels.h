@@ -46,7 +46,7 @@ enum {
   MSK_TUNE_MDOT_REV = 1,
   MSK_TUNE_SPMV_TEMPORAL = 2,       // CSR SpMV: default-policy col/val loads and y stores (default: non-temporal)
   MSK_TUNE_SPMV_XCD = 4,
-  MSK_TUNE_SPMV_STAGE1 = 8,
+  MSK_TUNE_SPMV_STAGE1 = 8,         // CSR SpMV: register staging, one slice per lane at a time
   MSK_TUNE_VEC_TEMPORAL = 16,       // default-policy (not non-temporal) basis loads in MDot / MAXPY / dense
   MSK_TUNE_MAXPY_TEMPORAL_ST = 64,  // default-policy store of w in MAXPY
   MSK_TUNE_GM_UNFUSED = 128,        // separate ||w||^2 stage-2 and one-lane Hessenberg update launches
@@ -63,7 +63,8 @@ enum {
   MSK_TUNE_MDOT_UNROLL2 = 262144,   // MDot: two groups of four per loop iteration
   MSK_TUNE_ELL_TEMPORAL_Y = 1048576, // DV SpMV: default-policy y stores (default: non-temporal)
   MSK_TUNE_SPMV_NTY = 2097152,      // CSR SpMV: default-policy col/val loads, non-temporal y stores
-  MSK_TUNE_SPMV_GLDS = 4194304,     // CSR SpMV: col/val staged by LDS-DMA (global_load_lds_dwordx4), non-temporal y
+  MSK_TUNE_SPMV_REG_STAGE = 4194304, // CSR SpMV: col/val staged through registers, 4 val + 2 col slices per lane
+                                     // (round-1 form; default: LDS-DMA, global_load_lds_dwordx4)
   MSK_TUNE_DENSE_G1 = 8388608,      // LSQR dense kernels: one column per load group (round-1 kernels; default four)
   MSK_TUNE_DENSE_G2 = 16777216,     // LSQR dense kernels: two columns per load group
   MSK_TUNE_DENSE_TEMPORAL_ST = 33554432  // LSQR dense kernels: default-policy u / u/beta stores (default: non-temporal)

@@ -553,8 +553,10 @@ __device__ __forceinline__ int32_t row_block(XcdMap m) {
 // Stage a row block's val/col slice (16-byte aligned-down views v2/c4 with n2/n4
 // slices) into LDS.  SU > 1: issue SU val and SU/2 col loads per lane before the
 // first LDS write, so staging costs one memory latency instead of one per slice.
+// aux (cache policy) 2 = nt on gfx950 (global_load_lds_dwordx4 ... nt)
+template <bool NT>
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, NT ? 2 : 0);
 }
 
 // SU == 0: LDS-DMA staging.  Each wave-instruction writes 64 consecutive 16-byte
@@ -565,12 +567,11 @@ template <bool NT, int SU>
 __device__ __forceinline__ void stage_csr_block(int t, int32_t n2, int32_t n4, const double2* __restrict__ v2,
                                                 const int4* __restrict__ c4, double* sval, int32_t* scol) {
   if constexpr (SU == 0) {
-    static_assert(!NT, "LDS-DMA staging runs with the default load policy");
     const int lane = t & 63, w = t >> 6;
     for (int32_t ib = w * 64; ib < n2; ib += kT)
-      glds16(v2 + min(ib + lane, n2 - 1), reinterpret_cast<char*>(sval) + (size_t)ib * 16);
+      glds16<NT>(v2 + min(ib + lane, n2 - 1), reinterpret_cast<char*>(sval) + (size_t)ib * 16);
     for (int32_t ib = w * 64; ib < n4; ib += kT)
-      glds16(c4 + min(ib + lane, n4 - 1), reinterpret_cast<char*>(scol) + (size_t)ib * 16);
+      glds16<NT>(c4 + min(ib + lane, n4 - 1), reinterpret_cast<char*>(scol) + (size_t)ib * 16);
   } else if constexpr (SU == 1) {
     for (int32_t i = t; i < n2; i += kT) reinterpret_cast<double2*>(sval)[i] = NT ? ld_nt(v2 + i) : v2[i];
     for (int32_t i = t; i < n4; i += kT) reinterpret_cast<int4*>(scol)[i] = NT ? ld_nt(c4 + i) : c4[i];
@@ -1587,11 +1588,13 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
   const XcdMap xm = xcd_map(nrows, plane);
   if (lds_cap > 0) {
     const bool tmp = (g_tuning & MSK_TUNE_SPMV_TEMPORAL) != 0, nty = (g_tuning & MSK_TUNE_SPMV_NTY) != 0;
-    const bool glds = (g_tuning & MSK_TUNE_SPMV_GLDS) != 0, stage1 = (g_tuning & MSK_TUNE_SPMV_STAGE1) != 0;
+    // staging: LDS-DMA by default (512^3 MatMult +1.4 %, CSR GMRES step +0.3 % same box, profiles/r02/glds/);
+    // MSK_TUNE_SPMV_REG_STAGE / _STAGE1: through registers (round-1 forms)
+    const bool reg = (g_tuning & MSK_TUNE_SPMV_REG_STAGE) != 0, stage1 = (g_tuning & MSK_TUNE_SPMV_STAGE1) != 0;
+    const bool glds = !reg && !stage1;
     // a combination with no kernel fails instead of running another variant
-    if ((tmp && nty) || (glds && (nty || stage1))) return (int)hipErrorInvalidValue;
-    // LDS-DMA staging has no non-temporal load form here: POL 2 (or 0 with TEMPORAL)
-    const bool nt = !tmp && !nty && !glds;
+    if ((tmp && nty) || (reg && stage1)) return (int)hipErrorInvalidValue;
+    const bool nt = !tmp && !nty;
     const bool ntst = !tmp;
     const int32_t cap = glds ? ((lds_cap + 255) & ~255) : lds_cap;
     const size_t ldsb = (size_t)cap * 12;
@@ -1599,7 +1602,7 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
 #define LAUNCH_LDS8(M, POL_)                                                                                  \
   do {                                                                                                         \
     if (glds)                                                                                                  \
-      k_spmv_lds8<M, (POL_) & 2, 0><<<dim3(g), dim3(kT), ldsb, s>>>(nrows, rowptr, col, val, x, b, y, cap, sdev,     \
+      k_spmv_lds8<M, POL_, 0><<<dim3(g), dim3(kT), ldsb, s>>>(nrows, rowptr, col, val, x, b, y, cap, sdev,     \
                                                                vout, stop, xm);                                \
     else if (stage1)                                                                                           \
       k_spmv_lds8<M, POL_, 1><<<dim3(g), dim3(kT), ldsb, s>>>(nrows, rowptr, col, val, x, b, y, cap, sdev,     \

@@ -178,7 +178,7 @@ def test_gmres_termination_branches_vs_oracle(ctx, oracle, name):
     assert np.array_equal(xg, xo, equal_nan=True)
 
 
-@pytest.mark.parametrize("flags", [0, 2, 1048576, 2097152, 4194304])   # default, MSK_TUNE_SPMV_TEMPORAL, _ELL_TEMPORAL_Y, _SPMV_NTY, _SPMV_GLDS
+@pytest.mark.parametrize("flags", [0, 2, 1048576, 2097152, 4194304])   # default, MSK_TUNE_SPMV_TEMPORAL, _ELL_TEMPORAL_Y, _SPMV_NTY, _SPMV_REG_STAGE
 @pytest.mark.parametrize("storage", ["dv", "csr"])
 @pytest.mark.parametrize("case", [0, 2, 5])
 def test_gmres_storage_and_store_policy_bitwise(ctx, oracle, case, storage, flags):

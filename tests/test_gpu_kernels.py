@@ -22,7 +22,7 @@ SEED = 20251121
 SPMV_TEMPORAL, SPMV_STAGE1, VEC_TEMPORAL, MAXPY_TEMPORAL_ST = 2, 8, 16, 64
 MAXPY_HALVES, MDOT_SINGLE, MAXPY_UNROLL1, MDOT_UNROLL2 = 256, 1024, 131072, 262144
 ELL_TEMPORAL_Y = 1048576
-SPMV_NTY, SPMV_GLDS = 2097152, 4194304
+SPMV_NTY, SPMV_REG_STAGE = 2097152, 4194304
 
 
 @contextlib.contextmanager
@@ -74,7 +74,7 @@ def _random_csr(n, ncols, maxlen, r):
 
 
 @pytest.mark.parametrize("flags", [0, SPMV_TEMPORAL, SPMV_STAGE1, SPMV_STAGE1 | SPMV_TEMPORAL, ELL_TEMPORAL_Y,
-                                   SPMV_NTY, SPMV_GLDS, SPMV_GLDS | SPMV_TEMPORAL])
+                                   SPMV_NTY, SPMV_REG_STAGE, SPMV_REG_STAGE | SPMV_TEMPORAL, SPMV_REG_STAGE | SPMV_NTY])
 @pytest.mark.parametrize("storage", ["default", "csr"])
 @pytest.mark.parametrize("case", ["box3d", "slab-coupled", "2d", "random", "random-short", "one-row", "empty"])
 def test_spmv_and_residual_bitwise(ctx, oracle, case, storage, flags):
@@ -153,14 +153,14 @@ def test_maxpy_bitwise(ctx, oracle, nv, n, flags):
     assert np.array_equal(wv.get_array(), oracle.maxpy(w, a, V))
 
 
-@pytest.mark.parametrize("flags", [MAXPY_HALVES | VEC_TEMPORAL, MDOT_SINGLE | MDOT_UNROLL2, SPMV_GLDS | SPMV_NTY,
-                                   SPMV_TEMPORAL | SPMV_NTY, SPMV_GLDS | SPMV_STAGE1])
+@pytest.mark.parametrize("flags", [MAXPY_HALVES | VEC_TEMPORAL, MDOT_SINGLE | MDOT_UNROLL2,
+                                   SPMV_TEMPORAL | SPMV_NTY, SPMV_REG_STAGE | SPMV_STAGE1])
 def test_tuning_combination_without_kernel_fails_loudly(ctx, flags):
     """A tuning combination no kernel is instantiated for returns an error; it never runs another variant."""
     n, nv = 5000, 3
     wv = Vec.from_array(ctx, np.ones(n))
     V = [Vec.from_array(ctx, np.ones(n)) for _ in range(nv)]
-    if flags & (SPMV_GLDS | SPMV_NTY | SPMV_TEMPORAL):
+    if flags & (SPMV_REG_STAGE | SPMV_NTY | SPMV_TEMPORAL):
         A = Mat.box_stencil(ctx, 3, 8, 8, 8)
         A.set_storage("csr")
         x, y = Vec.from_array(ctx, np.ones(512)), Vec(ctx, 512)
