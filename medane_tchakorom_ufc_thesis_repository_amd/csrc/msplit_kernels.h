@@ -67,7 +67,10 @@ enum {
                                      // (round-1 form; default: LDS-DMA, global_load_lds_dwordx4)
   MSK_TUNE_DENSE_G1 = 8388608,      // LSQR dense kernels: one column per load group (round-1 kernels; default four)
   MSK_TUNE_DENSE_G2 = 16777216,     // LSQR dense kernels: two columns per load group
-  MSK_TUNE_DENSE_TEMPORAL_ST = 33554432  // LSQR dense kernels: default-policy u / u/beta stores (default: non-temporal)
+  MSK_TUNE_DENSE_TEMPORAL_ST = 33554432, // LSQR dense kernels: default-policy u / u/beta stores (default: non-temporal)
+  MSK_TUNE_ELL_XCD_ON = 67108864,   // DV (ELL) SpMV: XCD-contiguous block order at any plane size
+  MSK_TUNE_ELL_XCD_OFF = 134217728  // DV (ELL) SpMV: identity block order at any plane size (default: XCD order
+                                    // from 2^18 rows per plane)
 };
 
 extern "C" {

@@ -1253,20 +1253,36 @@ struct EllWord<16> {
   static __device__ __forceinline__ T empty() { return T{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}; }
 };
 
+// Block order of the ELL SpMV.  xwin > 0: in each window of 8*xwin blocks, XCD x
+// (blockIdx % 8) takes the x-th contiguous run of xwin blocks, so neighbouring row
+// blocks -- which share the +-1 / +-line x gathers across their edges -- run on one
+// XCD and meet in its L2.  Pays for long lines (512^3: 833 -> 772 us, 1024-wide:
+// see DESIGN), costs 2-4 % at 256^3 (tools/ell_lab.hip, profiles/r02/ell_lab/), so
+// msk_spmv_dv turns it on from 2^18 rows per plane.  Tail blocks keep their order.
+__device__ __forceinline__ int32_t ell_block(int32_t xwin) {
+  const int32_t i = (int32_t)blockIdx.x;
+  if (xwin <= 0) return i;
+  const int32_t span = 8 * xwin;
+  const int32_t full = (int32_t)(gridDim.x / (unsigned)span) * span;
+  if (i >= full) return i;
+  const int32_t w = i / span, rem = i - w * span;
+  return w * span + (rem & 7) * xwin + (rem >> 3);
+}
+
 template <int MODE, int W, int RPL, bool NTY>
 __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* __restrict__ code8,
                                                  const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
                                                  int ndict, const double* __restrict__ x,
                                                  const double* __restrict__ b, double* __restrict__ y,
                                                  const double* __restrict__ sdev, double* __restrict__ vout,
-                                                 const int* __restrict__ stop) {
+                                                 const int* __restrict__ stop, int32_t xwin) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   typedef EllWord<W> EW;
   typedef typename EW::T CT;
   __shared__ int32_t sdel[256];
   __shared__ double sval[256];
   const int t = threadIdx.x;
-  const int32_t r0 = (int32_t)blockIdx.x * (kT * RPL);
+  const int32_t r0 = ell_block(xwin) * (kT * RPL);
   CT cw[RPL];
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
@@ -1636,27 +1652,29 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
 template <int W, int RPL, bool NTY>
 static void launch_ell_pol(int mode, unsigned g, int32_t nrows, const uint8_t* code8, const int32_t* ddelta,
                            const double* dval, int ndict, const double* x, const double* b, double* y,
-                           const double* sdev, double* vout, const int* stop, hipStream_t s) {
+                           const double* sdev, double* vout, const int* stop, int32_t xwin, hipStream_t s) {
   if (mode == MSK_SPMV_RESID)
     k_spmv_ell<MSK_SPMV_RESID, W, RPL, NTY><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout,
-                                                             stop);
+                                                             stop, xwin);
   else if (mode == MSK_SPMV_SCALED)
     k_spmv_ell<MSK_SPMV_SCALED, W, RPL, NTY><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout,
-                                                              stop);
+                                                              stop, xwin);
   else
     k_spmv_ell<MSK_SPMV_MULT, W, RPL, NTY><<<g, kT, 0, s>>>(nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout,
-                                                            stop);
+                                                            stop, xwin);
 }
 
 template <int W, int RPL>
 static void launch_ell(int mode, int32_t nrows, const uint8_t* code8, const int32_t* ddelta, const double* dval,
                        int ndict, const double* x, const double* b, double* y, const double* sdev, double* vout,
-                       const int* stop, hipStream_t s) {
+                       const int* stop, int64_t plane, hipStream_t s) {
   const unsigned g = (unsigned)((nrows + kT * RPL - 1) / (kT * RPL));
+  const bool xon = (g_tuning & MSK_TUNE_ELL_XCD_ON) || (plane >= (1 << 18) && !(g_tuning & MSK_TUNE_ELL_XCD_OFF));
+  const int32_t xwin = xon ? 8 : 0;
   if (!(g_tuning & MSK_TUNE_ELL_TEMPORAL_Y))  // default: non-temporal y (GMRES step +1.1 %, profiles/r02/nt_ab/)
-    launch_ell_pol<W, RPL, true>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, s);
+    launch_ell_pol<W, RPL, true>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, xwin, s);
   else
-    launch_ell_pol<W, RPL, false>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, s);
+    launch_ell_pol<W, RPL, false>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, xwin, s);
 }
 
 extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const uint8_t* code8,
@@ -1665,10 +1683,11 @@ extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* 
                            const int* stop, int64_t plane, hipStream_t s) {
   if (nrows <= 0) return 0;
   if (max_block < 0 || ndict < 0 || ndict > 256) return (int)hipErrorInvalidValue;
+  if ((g_tuning & MSK_TUNE_ELL_XCD_ON) && (g_tuning & MSK_TUNE_ELL_XCD_OFF)) return (int)hipErrorInvalidValue;
   if (ell_w) {
     if (ndict > 255) return (int)hipErrorInvalidValue;
     const int rpl = (g_tuning & MSK_TUNE_DV_RPL1) ? 1 : (g_tuning & MSK_TUNE_DV_RPL2) ? 2 : (ell_w == 16 ? 2 : 4);
-#define MSK_ELL(W_, R_) launch_ell<W_, R_>(mode, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, s)
+#define MSK_ELL(W_, R_) launch_ell<W_, R_>(mode, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, plane, s)
     if (ell_w == 4) { if (rpl == 1) MSK_ELL(4, 1); else if (rpl == 2) MSK_ELL(4, 2); else MSK_ELL(4, 4); }
     else if (ell_w == 8) { if (rpl == 1) MSK_ELL(8, 1); else if (rpl == 2) MSK_ELL(8, 2); else MSK_ELL(8, 4); }
     else if (ell_w == 16) { if (rpl == 1) MSK_ELL(16, 1); else MSK_ELL(16, 2); }

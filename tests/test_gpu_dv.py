@@ -281,3 +281,18 @@ def test_tall_matrix_dv(ctx, oracle):
     A = Mat.from_csr(ctx, nr, nc, rp, col, val)
     O = oracle.Mat.from_arrays(nr, nc, rp, col, val)
     _both_storages(ctx, A, O)
+
+
+@pytest.mark.parametrize("flags", [67108864, 67108864 | 8192, 67108864 | 16384, 134217728])
+@pytest.mark.parametrize("nz", [40, 64, 1])
+def test_ell_xcd_block_order_bitwise(ctx, oracle, flags, nz):
+    """The XCD-contiguous block order of the ELL SpMV (MSK_TUNE_ELL_XCD_ON, forced here on a small plane; the
+    default turns it on from 2^18 rows per plane) over full windows of 64 blocks and a ragged tail, and the
+    identity order forced off: MatMult, MatResidual and the scaled GMRES form equal the oracle."""
+    from test_gpu_kernels import tuning
+    A = Mat.box_stencil_ext(ctx, 3, 64, 64, nz, nz > 1, False)
+    rp, col, val = A.get_csr()
+    O = oracle.Mat.from_arrays(A.shape[0], A.shape[1], rp, col, val)
+    assert A.get_storage() == "dv"
+    with tuning(flags):
+        _products(ctx, A, O, np.random.default_rng(SEED))

@@ -23,6 +23,7 @@ SPMV_TEMPORAL, SPMV_STAGE1, VEC_TEMPORAL, MAXPY_TEMPORAL_ST = 2, 8, 16, 64
 MAXPY_HALVES, MDOT_SINGLE, MAXPY_UNROLL1, MDOT_UNROLL2 = 256, 1024, 131072, 262144
 ELL_TEMPORAL_Y = 1048576
 SPMV_NTY, SPMV_REG_STAGE = 2097152, 4194304
+ELL_XCD_ON, ELL_XCD_OFF = 67108864, 134217728
 
 
 @contextlib.contextmanager
@@ -74,7 +75,8 @@ def _random_csr(n, ncols, maxlen, r):
 
 
 @pytest.mark.parametrize("flags", [0, SPMV_TEMPORAL, SPMV_STAGE1, SPMV_STAGE1 | SPMV_TEMPORAL, ELL_TEMPORAL_Y,
-                                   SPMV_NTY, SPMV_REG_STAGE, SPMV_REG_STAGE | SPMV_TEMPORAL, SPMV_REG_STAGE | SPMV_NTY])
+                                   SPMV_NTY, SPMV_REG_STAGE, SPMV_REG_STAGE | SPMV_TEMPORAL, SPMV_REG_STAGE | SPMV_NTY,
+                                   ELL_XCD_ON, ELL_XCD_ON | ELL_TEMPORAL_Y])
 @pytest.mark.parametrize("storage", ["default", "csr"])
 @pytest.mark.parametrize("case", ["box3d", "slab-coupled", "2d", "random", "random-short", "one-row", "empty"])
 def test_spmv_and_residual_bitwise(ctx, oracle, case, storage, flags):
@@ -154,15 +156,15 @@ def test_maxpy_bitwise(ctx, oracle, nv, n, flags):
 
 
 @pytest.mark.parametrize("flags", [MAXPY_HALVES | VEC_TEMPORAL, MDOT_SINGLE | MDOT_UNROLL2,
-                                   SPMV_TEMPORAL | SPMV_NTY, SPMV_REG_STAGE | SPMV_STAGE1])
+                                   SPMV_TEMPORAL | SPMV_NTY, SPMV_REG_STAGE | SPMV_STAGE1, ELL_XCD_ON | ELL_XCD_OFF])
 def test_tuning_combination_without_kernel_fails_loudly(ctx, flags):
     """A tuning combination no kernel is instantiated for returns an error; it never runs another variant."""
     n, nv = 5000, 3
     wv = Vec.from_array(ctx, np.ones(n))
     V = [Vec.from_array(ctx, np.ones(n)) for _ in range(nv)]
-    if flags & (SPMV_REG_STAGE | SPMV_NTY | SPMV_TEMPORAL):
+    if flags & (SPMV_REG_STAGE | SPMV_NTY | SPMV_TEMPORAL | ELL_XCD_ON):
         A = Mat.box_stencil(ctx, 3, 8, 8, 8)
-        A.set_storage("csr")
+        A.set_storage("dv" if flags & ELL_XCD_ON else "csr")
         x, y = Vec.from_array(ctx, np.ones(512)), Vec(ctx, 512)
         with tuning(flags), pytest.raises(Exception):
             A.mult(x, y)

@@ -533,6 +533,71 @@ __global__ __launch_bounds__(kT) void k_dord(int32_t nrows, const uint8_t* __res
   }
 }
 
+
+// --- dspec: dord with the gathers issued for every lane, independent of the codes
+// (addresses clamped into [0, nrows)); presence only gates the sum.  All loads of a
+// row (codes, x[r], the far deltas) leave together; d = -1/+1 from lane shuffles.
+template <int RPL, int ND>
+__global__ __launch_bounds__(kT) void k_dspec(int32_t nrows, const uint8_t* __restrict__ code8,
+                                              const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
+                                              int ndict, const double* __restrict__ x, double* __restrict__ y) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int32_t r0 = (int32_t)blockIdx.x * (kT * RPL);
+  int32_t dd[ND];
+  double dv[ND];
+#pragma unroll
+  for (int e = 0; e < ND; ++e) {
+    dd[e] = e < ndict ? ddelta[e] : 0;
+    dv[e] = e < ndict ? dval[e] : 0.0;
+  }
+  u32x2 cw[RPL];
+  double xr[RPL];
+  double xv[RPL][ND];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    const int32_t rc = min(r, nrows - 1);
+    cw[j] = r < nrows ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r)
+                      : u32x2{0xFFFFFFFFu, 0xFFFFFFFFu};
+    xr[j] = x[rc];
+#pragma unroll
+    for (int e = 0; e < ND; ++e) {
+      const int32_t d = dd[e];
+      if (d != 0 && d != -1 && d != 1) xv[j][e] = x[min(max(rc + d, 0), nrows - 1)];
+    }
+  }
+  double s[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    double xm = __shfl_up(xr[j], 1, 64), xp = __shfl_down(xr[j], 1, 64);
+    if (lane == 0) xm = (r >= 1 && r - 1 < nrows) ? x[r - 1] : 0.0;
+    if (lane == 63) xp = (r + 1 < nrows) ? x[r + 1] : 0.0;
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = cbyte(cw[j], q);
+      if (c != 255) m |= 1u << c;
+    }
+    s[j] = 0.0;
+#pragma unroll
+    for (int e = 0; e < ND; ++e) {
+      const int32_t d = dd[e];
+      double v;
+      if (d == 0) v = xr[j];
+      else if (d == -1) v = xm;
+      else if (d == 1) v = xp;
+      else v = xv[j][e];
+      if ((m >> e) & 1) s[j] = s[j] + dv[e] * v;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int32_t r = r0 + t + kT * j;
+    if (r < nrows) st_nt(y + r, s[j]);
+  }
+}
+
 // block order remap: XCD x (blockIdx % 8) takes the blocks of its eighth of a z-window
 template <int RPL>
 __global__ __launch_bounds__(kT) void k_basex(int32_t nrows, const uint8_t* __restrict__ code8,
@@ -639,13 +704,12 @@ int main(int argc, char** argv) {
     run("base2", [&] { k_base<2><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("uni4", [&] { k_uni<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
 
+    run("dspec4", [&] { k_dspec<4, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
+    run("dspec2", [&] { k_dspec<2, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
+    run("dspec1", [&] { k_dspec<1, 8><<<g1, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("dord4", [&] { k_dord<4, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("dord2", [&] { k_dord<2, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("dord1", [&] { k_dord<1, 8><<<g1, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("pair2", [&] { k_pair<2, false><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("pair2s", [&] { k_pair<2, true><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("pair1s", [&] { k_pair<1, true><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("pair1", [&] { k_pair<1, false><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("near4", [&] { k_part<4, 0x36><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, false);
     run("far4", [&] { k_part<4, 0x41><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, false);
 
