@@ -1600,7 +1600,6 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
                         const int* stop, int64_t plane, hipStream_t s) {
   if (nrows <= 0) return 0;
   const unsigned g = (unsigned)((nrows + kT - 1) / kT);
-  const size_t lds = (size_t)lds_cap * 12;
   const XcdMap xm = xcd_map(nrows, plane);
   if (lds_cap > 0) {
     const bool tmp = (g_tuning & MSK_TUNE_SPMV_TEMPORAL) != 0, nty = (g_tuning & MSK_TUNE_SPMV_NTY) != 0;
@@ -1613,8 +1612,7 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
     const bool nt = !tmp && !nty;
     const bool ntst = !tmp;
     const int32_t cap = glds ? ((lds_cap + 255) & ~255) : lds_cap;
-    const size_t ldsb = (size_t)cap * 12;
-    (void)lds;
+    const size_t ldsb = (size_t)cap * 12;  // LDS-DMA: slack for the last instruction's tail lanes
 #define LAUNCH_LDS8(M, POL_)                                                                                  \
   do {                                                                                                         \
     if (glds)                                                                                                  \
