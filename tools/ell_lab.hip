@@ -598,6 +598,73 @@ __global__ __launch_bounds__(kT) void k_dspec(int32_t nrows, const uint8_t* __re
   }
 }
 
+
+// --- dpair: dictionary-ordered (deltas wave-uniform, ascending = CSR order) over
+// PAIRS of consecutive rows per lane: one 16-byte load at x + r + d (8-byte aligned;
+// clamped into [0, nrows-2], the element picked by select) serves both rows' entry d,
+// and one 16-byte code load both rows' codes.  VMEM per row pair: 1 + ndict (base: 2 + 2W).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int P, int ND>
+__global__ __launch_bounds__(kT) void k_dpair(int32_t nrows, const uint8_t* __restrict__ code8,
+                                              const int32_t* __restrict__ ddelta, const double* __restrict__ dval,
+                                              int ndict, const double* __restrict__ x, double* __restrict__ y) {
+  const int t = threadIdx.x;
+  const int32_t r0 = (int32_t)blockIdx.x * (2 * kT * P);
+  int32_t dd[ND];
+  double dv[ND];
+#pragma unroll
+  for (int e = 0; e < ND; ++e) {
+    dd[e] = e < ndict ? ddelta[e] : 0;
+    dv[e] = e < ndict ? dval[e] : 0.0;
+  }
+  uint32_t ma[P], mb[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int32_t r = r0 + 2 * (t + kT * k);
+    u32x4 cw = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (r < nrows) cw = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(code8 + (size_t)r * 8));
+    if (r + 1 >= nrows) cw.z = cw.w = 0xFFFFFFFFu;
+    uint32_t a = 0, b = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int ca = ((q < 4 ? cw.x : cw.y) >> (8 * (q & 3))) & 255;
+      const int cb = ((q < 4 ? cw.z : cw.w) >> (8 * (q & 3))) & 255;
+      if (ca != 255) a |= 1u << ca;
+      if (cb != 255) b |= 1u << cb;
+    }
+    ma[k] = a;
+    mb[k] = b;
+  }
+  double xa[P][ND], xb[P][ND];
+#pragma unroll
+  for (int e = 0; e < ND; ++e) {
+    if (e < ndict) {
+      const int32_t d = dd[e];
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const int32_t r = r0 + 2 * (t + kT * k);
+        const int32_t a = r + d, ac = min(max(a, 0), nrows - 2);
+        double2 q = make_double2(0.0, 0.0);
+        if (((ma[k] | mb[k]) >> e) & 1) q = *reinterpret_cast<const double2*>(x + ac);
+        xa[k][e] = ac == a ? q.x : q.y;
+        xb[k][e] = ac == a ? q.y : q.x;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int32_t r = r0 + 2 * (t + kT * k);
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int e = 0; e < ND; ++e) {
+      if ((ma[k] >> e) & 1) sa = sa + dv[e] * xa[k][e];
+      if ((mb[k] >> e) & 1) sb = sb + dv[e] * xb[k][e];
+    }
+    if (r + 1 < nrows) __builtin_nontemporal_store(dx2{sa, sb}, reinterpret_cast<dx2*>(y + r));
+    else if (r < nrows) st_nt(y + r, sa);
+  }
+}
+
 // block order remap: XCD x (blockIdx % 8) takes the blocks of its eighth of a z-window
 template <int RPL>
 __global__ __launch_bounds__(kT) void k_basex(int32_t nrows, const uint8_t* __restrict__ code8,
@@ -704,6 +771,8 @@ int main(int argc, char** argv) {
     run("base2", [&] { k_base<2><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("uni4", [&] { k_uni<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
 
+    run("dpair2", [&] { k_dpair<2, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
+    run("dpair1", [&] { k_dpair<1, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("dspec4", [&] { k_dspec<4, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("dspec2", [&] { k_dspec<2, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("dspec1", [&] { k_dspec<1, 8><<<g1, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
