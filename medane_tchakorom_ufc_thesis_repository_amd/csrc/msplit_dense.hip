@@ -303,6 +303,19 @@ using namespace msd;
 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// The dense kernels' tuning (msplit_kernels.h): columns per load group (4; DENSE_G1 / DENSE_G2) and the
+// u, u/beta store policy (non-temporal; DENSE_TEMPORAL_ST).  false (error set) for a combination with no kernel.
+static bool dense_tuning(int* grp, bool* nts) {
+  const int tu = msk_get_tuning();
+  if ((tu & MSK_TUNE_DENSE_G1) && (tu & MSK_TUNE_DENSE_G2)) {
+    mspi_set_error(MSP_ERR_ARG_OUTOFRANGE, "tuning: DENSE_G1 and DENSE_G2 together select no kernel");
+    return false;
+  }
+  *grp = (tu & MSK_TUNE_DENSE_G1) ? 1 : (tu & MSK_TUNE_DENSE_G2) ? 2 : 4;
+  *nts = !(tu & MSK_TUNE_DENSE_TEMPORAL_ST);
+  return true;
+}
+
 // ===================================================================== internal
 extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc, int64_t n, const double* coef_dev,
                                const double* nal_dev, const double* U, double* y, double* partial, double* sumsq_dev,
@@ -317,13 +330,9 @@ extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc,
   const bool axpy = U != nullptr, norm = sumsq_dev != nullptr;
   KTimer kt(c, MSP_KERNEL_DGEMV, 8.0 * (double)n * (nc + 1 + (axpy ? 1 : 0)));
   const dim3 g((unsigned)nch), b(kT);
-  const int tu = msk_get_tuning();
-  const int grp = (tu & MSK_TUNE_DENSE_G1) ? 1 : (tu & MSK_TUNE_DENSE_G2) ? 2 : 4;
-  const bool nts = !(tu & MSK_TUNE_DENSE_TEMPORAL_ST);
-  if ((tu & MSK_TUNE_DENSE_G1) && (tu & MSK_TUNE_DENSE_G2)) {
-    mspi_set_error(MSP_ERR_ARG_OUTOFRANGE, "tuning: DENSE_G1 and DENSE_G2 together select no kernel");
-    return MSP_ERR_ARG_OUTOFRANGE;
-  }
+  int grp = 4;
+  bool nts = true;
+  if (!dense_tuning(&grp, &nts)) return MSP_ERR_ARG_OUTOFRANGE;
 #define GEMVK(AX, NO, VE, G_, NT_) \
   k_dense_gemv<AX, NO, VE, G_, NT_><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, y, n, partial, stop)
 #define GEMV(AX, NO, VE)                                         \
@@ -366,13 +375,9 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
     return MSP_SUCCESS;
   }
   KTimer kt(c, MSP_KERNEL_DGEMVT, 8.0 * (double)n * (nc + 1 + (sc_dev ? 1 : 0)));
-  const int tu = msk_get_tuning();
-  const int grp = (tu & MSK_TUNE_DENSE_G1) ? 1 : (tu & MSK_TUNE_DENSE_G2) ? 2 : 4;
-  const bool nts = !(tu & MSK_TUNE_DENSE_TEMPORAL_ST);
-  if ((tu & MSK_TUNE_DENSE_G1) && (tu & MSK_TUNE_DENSE_G2)) {
-    mspi_set_error(MSP_ERR_ARG_OUTOFRANGE, "tuning: DENSE_G1 and DENSE_G2 together select no kernel");
-    return MSP_ERR_ARG_OUTOFRANGE;
-  }
+  int grp = 4;
+  bool nts = true;
+  if (!dense_tuning(&grp, &nts)) return MSP_ERR_ARG_OUTOFRANGE;
   const int vec = !(aligned16(A) && (lda % 2 == 0) && aligned16(win) && (!sc_dev || aligned16(wout))) ? 0
                   : (msk_get_tuning() & MSK_TUNE_VEC_TEMPORAL) ? 1 : 2;
   for (int g0 = 0; g0 < nc; g0 += kMaxCols) {
