@@ -207,3 +207,32 @@ def test_configs0_full_size_petsc_order_bitwise(sctx, oracle):
                            dict(C1_INNER, reduce_mode=oracle.REDUCE_SEQ),
                            dict(C1_OUTER, reduce_mode=oracle.REDUCE_SEQ), max_outer=C1_SEQ_CAP)
     _check_smsm(res, ro, blocks)
+
+
+# ---------------------------------------------------------------- configs[1]
+def test_configs1_full_size_petsc_order_bitwise(sctx):
+    """BASELINE configs[1] at full size (3D 256^3, GMRES(30), 300 iterations) in PETSc's reduction order: the
+    device equals the PETSc-order oracle bit for bit -- every history entry and the iterate.  The oracle's
+    single-threaded run takes minutes, so its result is the committed fixture tests/golden/configs1_seq.json
+    (tests/golden/make_configs1_seq.py), which also records the DBR-vs-SEQ deviation the default mode carries."""
+    import hashlib
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "configs1_seq.json")))["seq"]
+    n = 256
+    A = Mat.box_stencil(sctx, 3, n, n, n)
+    N = A.shape[0]
+    ones = Vec(sctx, N)
+    ones.set(1.0)
+    b = Vec(sctx, N)
+    A.mult(ones, b)
+    x = Vec(sctx, N)
+    ksp = KSP(sctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options("-ksp_gmres_restart 30 -ksp_max_it 300 -ksp_rtol 1e-30 -pc_type none "
+                                 "-ksp_norm_type unpreconditioned"))
+    ksp.solve(b, x)
+    hist = ksp.get_residual_history()
+    assert (ksp.get_iteration_number(), ksp.get_converged_reason()) == (g["its"], g["reason"])
+    assert [float(h).hex() for h in hist] == g["hist_hex"]
+    assert hashlib.sha256(np.ascontiguousarray(x.get_array(), np.float64).tobytes()).hexdigest() == g["x_sha256"]
