@@ -213,3 +213,16 @@ def test_oracle_gmres_termination_branches(oracle, name):
         assert r["its"] >= 3
     if name == "null":
         assert r["its"] == 1
+
+
+def test_configs1_seq_fixture_is_consistent():
+    """tests/golden/configs1_seq.json (the PETSc-order oracle on configs[1], for the GPU SEQ-mode test): 300
+    iterations in both orders, monotone histories, and the recorded DBR-vs-SEQ deviation is what the two stored
+    histories give."""
+    g = json.load(open(os.path.join(GOLDEN, "configs1_seq.json")))
+    hs = np.array([float.fromhex(h) for h in g["seq"]["hist_hex"]])
+    hd = np.array([float.fromhex(h) for h in g["dbr"]["hist_hex"]])
+    assert g["seq"]["its"] == g["dbr"]["its"] == 300 and len(hs) == len(hd) == 301
+    assert np.all(np.diff(hs) <= 0) and np.all(np.diff(hd) <= 0)
+    assert not np.array_equal(hs, hd)                      # the two orders really differ
+    assert float(np.max(np.abs(hd - hs) / np.abs(hs))) == g["dbr_vs_seq"]["max_rel_dev_hist"]
