@@ -18,7 +18,22 @@
 
 #include "msplit_kernels.h"
 
+// The launchers are split into parts that the Makefile compiles as separate objects (-DMSK_PART=1..6), so the
+// large template sets (MDot and MAXPY over 1..32 vectors and their variants) build in parallel.  Without
+// MSK_PART the file compiles every part into one object.
+#ifndef MSK_PART
+#define MSK_PART 0
+#endif
+#define MSK_IN(p) (MSK_PART == 0 || MSK_PART == (p))
+#define MSK_PART_DOT 1
+#define MSK_PART_MAXPY 2
+#define MSK_PART_SPMV 3
+#define MSK_PART_MISC 4
+#define MSK_PART_DOT_A 5
+#define MSK_PART_DOT_B 6
+
 namespace msk {
+namespace {  // internal linkage: this file is compiled once per part (see MSK_PART below)
 
 constexpr int kT = 256;                  // threads per workgroup (4 wave64)
 constexpr int kIters = 8;                // double2 slices per thread per DBR chunk
@@ -1450,21 +1465,27 @@ __global__ __launch_bounds__(kT) void k_blas1(double* __restrict__ y, const doub
   }
 }
 
+}  // namespace
 }  // namespace msk
 
 // ===================================================================== launchers
 using namespace msk;
 
-// Tuning flags (A/B experiments; MSPLIT_TUNING at context creation).
-static int g_tuning = 0;
-static int g_spmv_gb = 0;  // XCD group size override (0: auto)
-extern "C" void msk_set_tuning(int flags) { g_tuning = flags; }
-extern "C" int msk_get_tuning(void) { return g_tuning; }
-extern "C" void msk_set_spmv_group(int gb) { g_spmv_gb = gb; }
+// Tuning flags (A/B experiments; MSPLIT_TUNING at context creation), defined once (the MISC part).
+#if MSK_IN(MSK_PART_MISC)
+__attribute__((visibility("hidden"))) int msk_tuning_flags = 0;
+__attribute__((visibility("hidden"))) int msk_spmv_gb_override = 0;  // XCD group size override (0: auto)
+extern "C" void msk_set_tuning(int flags) { msk_tuning_flags = flags; }
+extern "C" int msk_get_tuning(void) { return msk_tuning_flags; }
+extern "C" void msk_set_spmv_group(int gb) { msk_spmv_gb_override = gb; }
+#else
+extern __attribute__((visibility("hidden"))) int msk_tuning_flags;
+extern __attribute__((visibility("hidden"))) int msk_spmv_gb_override;
+#endif
 
-static XcdMap xcd_map(int32_t nrows, int64_t plane) {
+[[maybe_unused]] static inline XcdMap xcd_map(int32_t nrows, int64_t plane) {
   XcdMap m = {0, 0, 0};
-  if (g_tuning & MSK_TUNE_SPMV_ZCHUNK) {  // A/B: each XCD a contiguous eighth of the rows
+  if (msk_tuning_flags & MSK_TUNE_SPMV_ZCHUNK) {  // A/B: each XCD a contiguous eighth of the rows
     const int32_t nblk = (nrows + kT - 1) / kT;
     if (nblk % 8 == 0) {
       m.bp = -1;
@@ -1472,9 +1493,9 @@ static XcdMap xcd_map(int32_t nrows, int64_t plane) {
     }
     return m;
   }
-  if (!(g_tuning & MSK_TUNE_SPMV_XCD) || plane <= 0 || plane % kT || nrows % plane) return m;
+  if (!(msk_tuning_flags & MSK_TUNE_SPMV_XCD) || plane <= 0 || plane % kT || nrows % plane) return m;
   const int32_t bp = (int32_t)(plane / kT);
-  int32_t gb = g_spmv_gb > 0 ? g_spmv_gb : std::min(bp / 8, 64);
+  int32_t gb = msk_spmv_gb_override > 0 ? msk_spmv_gb_override : std::min(bp / 8, 64);
   if (gb <= 0 || bp % gb || (bp / gb) % 8) return m;
   m.bp = bp;
   m.gb = gb;
@@ -1482,7 +1503,7 @@ static XcdMap xcd_map(int32_t nrows, int64_t plane) {
   return m;
 }
 
-static inline int grid_for(int64_t work, int cap) {
+[[maybe_unused]] static inline int grid_for(int64_t work, int cap) {
   int64_t g = (work + kT - 1) / kT;
   if (g < 1) g = 1;
   if (g > cap) g = cap;
@@ -1490,36 +1511,65 @@ static inline int grid_for(int64_t work, int cap) {
 }
 
 // basis-vector load policy: non-temporal unless MSK_TUNE_VEC_TEMPORAL (A/B)
-static inline int vec_var() { return (g_tuning & MSK_TUNE_VEC_TEMPORAL) ? 0 : 1; }
+[[maybe_unused]] static inline int vec_var() { return (msk_tuning_flags & MSK_TUNE_VEC_TEMPORAL) ? 0 : 1; }
+
+__attribute__((visibility("hidden"))) int msk_dot1_variants_a(int var, int nv, const double* w, const Vecs& V,
+                                                               int64_t n, double* partial, int64_t nchunks,
+                                                               const int* stop, hipStream_t s);
+__attribute__((visibility("hidden"))) int msk_dot1_variants_b(int var, int nv, const double* w, const Vecs& V,
+                                                               int64_t n, double* partial, int64_t nchunks,
+                                                               const int* stop, hipStream_t s);
 
 template <int NV, int VAR>
 static void dot1_dispatch(int nv, const double* w, const Vecs& V, int64_t n, double* partial, int64_t nchunks,
                           const int* stop, hipStream_t s) {
   if (nv == NV) {
     k_dot_stage1<NV, false, VAR><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(
-        w, V, n, partial, nchunks, stop, (g_tuning & MSK_TUNE_MDOT_REV) ? 1 : 0);
+        w, V, n, partial, nchunks, stop, (msk_tuning_flags & MSK_TUNE_MDOT_REV) ? 1 : 0);
   } else if constexpr (NV < MSK_MAX_GROUP) {
     dot1_dispatch<NV + 1, VAR>(nv, w, V, n, partial, nchunks, stop, s);
   }
 }
 
+#if MSK_IN(MSK_PART_DOT)
 extern "C" int msk_dot_stage1(const double* w, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
                               int self, const int* stop, hipStream_t s) {
   if (nchunks <= 0) return 0;
   if (!self && (nv < 1 || nv > MSK_MAX_GROUP)) return (int)hipErrorInvalidValue;
-  const int var = vec_var() | ((g_tuning & MSK_TUNE_MDOT_SINGLE) ? 16 : 0) |
-                  ((g_tuning & MSK_TUNE_MDOT_UNROLL2) ? 32 : 0);
+  const int var = vec_var() | ((msk_tuning_flags & MSK_TUNE_MDOT_SINGLE) ? 16 : 0) |
+                  ((msk_tuning_flags & MSK_TUNE_MDOT_UNROLL2) ? 32 : 0);
   if (self)
     k_dot_stage1<1, true, 0><<<dim3((unsigned)nchunks), dim3(kT), 0, s>>>(w, *V, n, partial, nchunks, stop, 0);
   else if (var == 1) dot1_dispatch<1, 1>(nv, w, *V, n, partial, nchunks, stop, s);
-  else if (var == 33) dot1_dispatch<1, 33>(nv, w, *V, n, partial, nchunks, stop, s);
-  else if (var == 17) dot1_dispatch<1, 17>(nv, w, *V, n, partial, nchunks, stop, s);
-  else if (var == 16) dot1_dispatch<1, 16>(nv, w, *V, n, partial, nchunks, stop, s);
-  else if (var == 0) dot1_dispatch<1, 0>(nv, w, *V, n, partial, nchunks, stop, s);
-  else if (var == 32) dot1_dispatch<1, 32>(nv, w, *V, n, partial, nchunks, stop, s);
-  else return (int)hipErrorInvalidValue;  // a tuning combination with no kernel: fail, never run another one
+  else if (msk_dot1_variants_a(var, nv, w, *V, n, partial, nchunks, stop, s) &&
+           msk_dot1_variants_b(var, nv, w, *V, n, partial, nchunks, stop, s))
+    return (int)hipErrorInvalidValue;  // a tuning combination with no kernel: fail, never run another one
   return (int)hipGetLastError();
 }
+#endif  // part
+
+// The A/B variants of the MDot kernel, in parts of their own (each variant is 32 instantiations).
+// Return 0 when they launched the variant, 1 when it is not theirs.
+#if MSK_IN(MSK_PART_DOT_A)
+int msk_dot1_variants_a(int var, int nv, const double* w, const Vecs& V, int64_t n, double* partial,
+                        int64_t nchunks, const int* stop, hipStream_t s) {
+  if (var == 0) dot1_dispatch<1, 0>(nv, w, V, n, partial, nchunks, stop, s);
+  else if (var == 16) dot1_dispatch<1, 16>(nv, w, V, n, partial, nchunks, stop, s);
+  else return 1;
+  return 0;
+}
+#endif  // part
+#if MSK_IN(MSK_PART_DOT_B)
+int msk_dot1_variants_b(int var, int nv, const double* w, const Vecs& V, int64_t n, double* partial,
+                        int64_t nchunks, const int* stop, hipStream_t s) {
+  if (var == 17) dot1_dispatch<1, 17>(nv, w, V, n, partial, nchunks, stop, s);
+  else if (var == 32) dot1_dispatch<1, 32>(nv, w, V, n, partial, nchunks, stop, s);
+  else if (var == 33) dot1_dispatch<1, 33>(nv, w, V, n, partial, nchunks, stop, s);
+  else return 1;
+  return 0;
+}
+#endif  // part
+#if MSK_IN(MSK_PART_DOT)
 
 template <int NV, int VAR>
 static void dot1_op_dispatch(int nv, const EllOp& op, const Vecs& V, int64_t n, double* partial, int64_t nchunks,
@@ -1539,34 +1589,40 @@ extern "C" int msk_dot_stage1_op(const EllOp* op, const Vecs* V, int nv, int64_t
   else dot1_op_dispatch<1, 0>(nv, *op, *V, n, partial, nchunks, stop, s);
   return (int)hipGetLastError();
 }
+#endif  // part
 
+#if MSK_IN(MSK_PART_MAXPY)
 extern "C" int msk_maxpy_op(const EllOp* op, double* wout, const Vecs* V, int nv, const double* adev, int64_t n,
                             double* partial, const int* stop, hipStream_t s) {
   if (n <= 0 || nv <= 0) return 0;
   if (op->ndict > 255) return (int)hipErrorInvalidValue;
   const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
-  const int var = vec_var() | ((g_tuning & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4);
+  const int var = vec_var() | ((msk_tuning_flags & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4);
   if (var == 5) k_maxpy_op<5><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
   else if (var == 4) k_maxpy_op<4><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
   else if (var == 1) k_maxpy_op<1><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
   else k_maxpy_op<0><<<g, kT, 0, s>>>(*op, wout, *V, adev, nv, n, partial, stop);
   return (int)hipGetLastError();
 }
+#endif  // part
 
+#if MSK_IN(MSK_PART_DOT)
 extern "C" int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, const int* stop,
                               hipStream_t s) {
   k_dot_stage2<<<dim3(nv), dim3(kT), 0, s>>>(partial, nchunks, out, stop);
   return (int)hipGetLastError();
 }
+#endif  // part
 
+#if MSK_IN(MSK_PART_MAXPY)
 extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, int nv, const int* nvdev,
                                const Coefs* A, const double* adev, int negate, int64_t n, int accum, double* partial,
                                const int* stop, hipStream_t s) {
   if (n <= 0 || (nv <= 0 && !nvdev)) return 0;
   // non-temporal store of w too unless MSK_TUNE_MAXPY_TEMPORAL_ST (+0.4 % per step); the group loop
   // unrolled by two unless MSK_TUNE_MAXPY_UNROLL1 (+1.7 % per step: 64-load bursts at one wave per SIMD)
-  const int var = vec_var() | ((g_tuning & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4) |
-                  ((g_tuning & MSK_TUNE_MAXPY_HALVES) ? 8 : 0) | ((g_tuning & MSK_TUNE_MAXPY_UNROLL1) ? 0 : 32);
+  const int var = vec_var() | ((msk_tuning_flags & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4) |
+                  ((msk_tuning_flags & MSK_TUNE_MAXPY_HALVES) ? 8 : 0) | ((msk_tuning_flags & MSK_TUNE_MAXPY_UNROLL1) ? 0 : 32);
   const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
 #define MSK_MAXPY_LAUNCH(V_)                                                                                     \
   if (partial)                                                                                                  \
@@ -1594,7 +1650,9 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
 #undef MSK_MAXPY_LAUNCH
   return (int)hipGetLastError();
 }
+#endif  // part
 
+#if MSK_IN(MSK_PART_SPMV)
 extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col, const double* val, const double* x,
                         const double* b, double* y, int32_t lds_cap, int mode, const double* sdev, double* vout,
                         const int* stop, int64_t plane, hipStream_t s) {
@@ -1602,10 +1660,10 @@ extern "C" int msk_spmv(int32_t nrows, const int32_t* rowptr, const int32_t* col
   const unsigned g = (unsigned)((nrows + kT - 1) / kT);
   const XcdMap xm = xcd_map(nrows, plane);
   if (lds_cap > 0) {
-    const bool tmp = (g_tuning & MSK_TUNE_SPMV_TEMPORAL) != 0, nty = (g_tuning & MSK_TUNE_SPMV_NTY) != 0;
+    const bool tmp = (msk_tuning_flags & MSK_TUNE_SPMV_TEMPORAL) != 0, nty = (msk_tuning_flags & MSK_TUNE_SPMV_NTY) != 0;
     // staging: LDS-DMA by default (512^3 MatMult +1.4 %, CSR GMRES step +0.3 % same box, profiles/r02/glds/);
     // MSK_TUNE_SPMV_REG_STAGE / _STAGE1: through registers (round-1 forms)
-    const bool reg = (g_tuning & MSK_TUNE_SPMV_REG_STAGE) != 0, stage1 = (g_tuning & MSK_TUNE_SPMV_STAGE1) != 0;
+    const bool reg = (msk_tuning_flags & MSK_TUNE_SPMV_REG_STAGE) != 0, stage1 = (msk_tuning_flags & MSK_TUNE_SPMV_STAGE1) != 0;
     const bool glds = !reg && !stage1;
     // a combination with no kernel fails instead of running another variant
     if ((tmp && nty) || (reg && stage1)) return (int)hipErrorInvalidValue;
@@ -1667,9 +1725,9 @@ static void launch_ell(int mode, int32_t nrows, const uint8_t* code8, const int3
                        int ndict, const double* x, const double* b, double* y, const double* sdev, double* vout,
                        const int* stop, int64_t plane, hipStream_t s) {
   const unsigned g = (unsigned)((nrows + kT * RPL - 1) / (kT * RPL));
-  const bool xon = (g_tuning & MSK_TUNE_ELL_XCD_ON) || (plane >= (1 << 18) && !(g_tuning & MSK_TUNE_ELL_XCD_OFF));
+  const bool xon = (msk_tuning_flags & MSK_TUNE_ELL_XCD_ON) || (plane >= (1 << 18) && !(msk_tuning_flags & MSK_TUNE_ELL_XCD_OFF));
   const int32_t xwin = xon ? 8 : 0;
-  if (!(g_tuning & MSK_TUNE_ELL_TEMPORAL_Y))  // default: non-temporal y (GMRES step +1.1 %, profiles/r02/nt_ab/)
+  if (!(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y))  // default: non-temporal y (GMRES step +1.1 %, profiles/r02/nt_ab/)
     launch_ell_pol<W, RPL, true>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, xwin, s);
   else
     launch_ell_pol<W, RPL, false>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, xwin, s);
@@ -1681,10 +1739,10 @@ extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* 
                            const int* stop, int64_t plane, hipStream_t s) {
   if (nrows <= 0) return 0;
   if (max_block < 0 || ndict < 0 || ndict > 256) return (int)hipErrorInvalidValue;
-  if ((g_tuning & MSK_TUNE_ELL_XCD_ON) && (g_tuning & MSK_TUNE_ELL_XCD_OFF)) return (int)hipErrorInvalidValue;
+  if ((msk_tuning_flags & MSK_TUNE_ELL_XCD_ON) && (msk_tuning_flags & MSK_TUNE_ELL_XCD_OFF)) return (int)hipErrorInvalidValue;
   if (ell_w) {
     if (ndict > 255) return (int)hipErrorInvalidValue;
-    const int rpl = (g_tuning & MSK_TUNE_DV_RPL1) ? 1 : (g_tuning & MSK_TUNE_DV_RPL2) ? 2 : (ell_w == 16 ? 2 : 4);
+    const int rpl = (msk_tuning_flags & MSK_TUNE_DV_RPL1) ? 1 : (msk_tuning_flags & MSK_TUNE_DV_RPL2) ? 2 : (ell_w == 16 ? 2 : 4);
 #define MSK_ELL(W_, R_) launch_ell<W_, R_>(mode, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, plane, s)
     if (ell_w == 4) { if (rpl == 1) MSK_ELL(4, 1); else if (rpl == 2) MSK_ELL(4, 2); else MSK_ELL(4, 4); }
     else if (ell_w == 8) { if (rpl == 1) MSK_ELL(8, 1); else if (rpl == 2) MSK_ELL(8, 2); else MSK_ELL(8, 4); }
@@ -1693,7 +1751,7 @@ extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* 
 #undef MSK_ELL
     return (int)hipGetLastError();
   }
-  const int rpl = (g_tuning & MSK_TUNE_DV_RPL1) ? 1 : (g_tuning & MSK_TUNE_DV_RPL2) ? 2 : 4;
+  const int rpl = (msk_tuning_flags & MSK_TUNE_DV_RPL1) ? 1 : (msk_tuning_flags & MSK_TUNE_DV_RPL2) ? 2 : 4;
   // LDS for the codes of one block: its entries plus both 16-byte roundings
   const size_t cap = ((size_t)rpl * max_block + 30 + 15) & ~(size_t)15;
   if (rpl == 1) {
@@ -1763,7 +1821,7 @@ extern "C" int msk_spmv_mdot(int32_t nrows, const int32_t* rowptr, const int32_t
   const dim3 g((unsigned)nchunks), b(kT);
 #define MSK_SMD(VAR_, GF_) \
   k_spmv_mdot<VAR_, GF_><<<g, b, lds, s>>>(nrows, rowptr, col, val, x, sdev, y, lds_cap, *V, nv, partial, nchunks, stop)
-  const bool g2 = (g_tuning & MSK_TUNE_SPMV_MDOT_G2) != 0;
+  const bool g2 = (msk_tuning_flags & MSK_TUNE_SPMV_MDOT_G2) != 0;
   if (vec_var()) { if (g2) MSK_SMD(1, 2); else MSK_SMD(1, 4); }
   else { if (g2) MSK_SMD(0, 2); else MSK_SMD(0, 4); }
 #undef MSK_SMD
@@ -1788,7 +1846,9 @@ extern "C" int msk_spmv_rows(int32_t nlisted, const int32_t* row_ids, const int3
   else k_spmv_rows<false><<<dim3(g), dim3(kT), 0, s>>>(nlisted, row_ids, rowptr, col, val, x, b, y);
   return (int)hipGetLastError();
 }
+#endif  // part
 
+#if MSK_IN(MSK_PART_MISC)
 extern "C" int msk_box_stencil(int dim, int32_t nx, int32_t ny, int32_t nz, int64_t nrows, int lo, int hi,
                                const BoxCoef* cf, int32_t* rowptr, int32_t* col, double* val, hipStream_t s) {
   const int g = grid_for(nrows + 1, 8192);
@@ -1830,3 +1890,4 @@ extern "C" int msk_blas1(int op, double* y, const double* x, const double* z, do
   }
   return (int)hipGetLastError();
 }
+#endif  // part
