@@ -167,8 +167,14 @@ typedef struct {
   /* asynchronous state */
   msp_amsg *am;
   msp_cvd *cvd;
-  int it, inner, tag, state;
+  int it, inner, tag, state, steps;
   double local_norm;
+  /* AMAM-global: the replicated R (own rows = R), the global b, the block's own LSQR */
+  msp_abcast *bc;
+  msp_dense *Rrep[64];
+  msp_vec *ball[64];
+  msp_lsqr *lsqr;
+  msp_vec *alpha;
 } msd_block;
 
 static int ksp_from_options(msp_ksp *k, const msd_options *o, const char *p, msp_ksp_opts *ko) {
@@ -633,6 +639,182 @@ int msd_am_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const
     }
     barrier(&R);
   }
+  free_run(&R);
+  return limited ? MSP_ERR_ARG_OUTOFRANGE : MSP_SUCCESS;
+}
+
+/* ---------------------------------------------------------- AMAM-global */
+/* asynchronous-multisplitting-asynchronous-minimization-global_prime.c:238-481; asynchronous.py am_solve
+ * (variant "amam_global") over multisplitting.py setup_global_async_minimization / global_async_minimize.
+ * Every block holds the whole R (each block's rows as last received, zero before the first message, the
+ * reference's MatZeroEntries(R)) and the global b, and solves its own LSQR over the nb row blocks in block
+ * order; R rows travel newest-value through msp_abcast. */
+static int amam_setup_block(msp_ctx *ctx, const msd_problem *p, const msd_options *o, msd_block *B) {
+  const msd_layout *L = &B->L;
+  CK(msp_dense_create(ctx, B->lo + B->n + B->hi, p->s, &B->S));
+  CK(msp_dense_create(ctx, B->n, p->s, &B->R));
+  for (int j = 0; j < p->nb; ++j) {
+    if (j == L->b) {
+      B->Rrep[j] = B->R;
+      B->ball[j] = B->b;
+      continue;
+    }
+    msd_layout Lj;
+    CK(msd_layout_make(p->dim, p->nx, p->ny, p->nz, p->nb, j, p->peclet, &Lj));
+    const int64_t nj = Lj.r1 - Lj.r0, loj = Lj.has_lo ? Lj.plane : 0, hij = Lj.has_hi ? Lj.plane : 0;
+    CK(msp_dense_create(ctx, nj, p->s, &B->Rrep[j]));
+    CK(msp_dense_zero_entries(B->Rrep[j]));
+    /* b_j = A_block_j 1 (utils.c:623-650) */
+    msp_mat *Aj;
+    msp_vec *ones, *bj;
+    CK(msp_mat_create_box_convdiff(ctx, Lj.box[0], Lj.box[1], Lj.box[2], Lj.box[3], loj > 0, hij > 0, Lj.peclet,
+                                   &Aj));
+    CK(msp_vec_create(ctx, loj + nj + hij, &ones));
+    CK(msp_vec_set(ones, 1.0));
+    CK(msp_vec_create(ctx, nj, &bj));
+    CK(msp_mat_mult(Aj, ones, bj));
+    msp_vec_destroy(&ones);
+    msp_mat_destroy(&Aj);
+    B->ball[j] = bj;
+  }
+  char prefix[32];
+  snprintf(prefix, sizeof(prefix), "outer%d_", L->b + 1);
+  CK(msp_lsqr_create(ctx, &B->lsqr));
+  CK(lsqr_from_options(B->lsqr, o, prefix));
+  CK(msp_lsqr_set_operators(B->lsqr, p->nb, B->Rrep));
+  CK(msp_lsqr_set_comm(B->lsqr, NULL));
+  CK(msp_vec_create(ctx, p->s, &B->alpha));
+  return MSP_SUCCESS;
+}
+
+static void amam_free_block(msd_block *B, int nb) {
+  for (int j = 0; j < nb; ++j) {
+    if (j == B->L.b) continue;
+    msp_dense_destroy(&B->Rrep[j]);
+    msp_vec_destroy(&B->ball[j]);
+  }
+  msp_lsqr_destroy(&B->lsqr);
+  msp_vec_destroy(&B->alpha);
+}
+
+static int amam_minimize(msd_block *B, int nb) { /* global_async_minimize, AMAM-global_prime.c:415-440 */
+  int32_t done;
+  CK(msp_mat_matmult_dense(B->A_ext, B->S, B->R)); /* R_i = A_block S */
+  CK(msp_abcast_publish_dense(B->bc, B->R, &done)); /* comm_async_test_and_send_min */
+  for (int j = 0; j < nb; ++j)                      /* comm_async_probe_and_receive_min */
+    if (j != B->L.b) CK(msp_abcast_fetch_dense(B->bc, j, B->Rrep[j], &done));
+  CK(msp_lsqr_solve(B->lsqr, B->ball, B->alpha)); /* outer_solver_norm_equation, utils.c:1061-1078 */
+  return apply_alpha(B, B->alpha);
+}
+
+static int amam_iterate(msd_block *B, const msd_problem *p, double thr) { /* AMAM-global_prime.c:378-447 */
+  for (int k = 0; k < p->s; ++k) {
+    int its;
+    CK(am_receive(B));
+    CK(update_rhs(B));
+    CK(inner_solve(B, &its));
+    B->inner += its;
+    CK(am_publish(B, B->steps));
+    CK(am_receive(B));
+    CK(store_column(B, k));
+    B->steps++;
+  }
+  CK(amam_minimize(B, p->nb));
+  double sq;
+  CK(block_residual_sq(B, &sq)); /* MatResidual(A_block, b_i, x_minimized) + VecNorm */
+  B->local_norm = sqrt(sq);
+  CK(msp_cvd_step(B->cvd, B->local_norm <= thr));
+  B->it++;
+  return msp_cvd_get_state(B->cvd, &B->state, &B->tag);
+}
+
+int msd_amam_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const msd_transport *t,
+                          msd_result *res) {
+  static msd_block store[MSD_MAX_BLOCKS];
+  msd_run R;
+  memset(res, 0, sizeof(*res));
+  CK(setup_run(ctx, p, o, t, &R, store));
+  for (int i = 0; i < R.nlocal; ++i) CK(amam_setup_block(ctx, p, o, R.blk[i]));
+  CK(sum_over_blocks(&R, norm0_sq, &res->norm0));
+  /* the largest block of R any block broadcasts: block 0's replicated R (asynchronous.py) */
+  int64_t cap = 0;
+  for (int j = 0; j < p->nb; ++j) {
+    msd_layout Lj;
+    CK(msd_layout_make(p->dim, p->nx, p->ny, p->nz, p->nb, j, p->peclet, &Lj));
+    const int64_t c = (Lj.r1 - Lj.r0) * (int64_t)p->s;
+    if (c > cap) cap = c;
+  }
+  char name[128], rname[136];
+  snprintf(name, sizeof(name), "/msplit_camam_%d_%ld", (int)getpid(), (long)(now_s() * 1e6) % 1000000000L);
+  if (t->world > 1 && t->bcast) t->bcast(t->user, name, (int)sizeof(name), 0);
+  snprintf(rname, sizeof(rname), "%s_R", name);
+  for (int pass = 0; pass < 2; ++pass) { /* the owner, then everyone else */
+    for (int i = 0; i < R.nlocal; ++i) {
+      msd_block *B = R.blk[i];
+      const int owner = B->L.b == 0;
+      if (owner != (pass == 0)) continue;
+      CK(msp_amsg_create(name, p->nb, B->L.b, B->L.plane > 0 ? B->L.plane : 1, owner, &B->am));
+      CK(msp_abcast_create(rname, p->nb, B->L.b, cap, owner, &B->bc));
+      int32_t nbrs[2], nn = 0;
+      if (B->L.has_lo) nbrs[nn++] = B->L.b - 1;
+      if (B->L.has_hi) nbrs[nn++] = B->L.b + 1;
+      CK(msp_cvd_create(B->am, B->L.b, nn, nbrs, nn, nbrs, 0, &B->cvd));
+    }
+    barrier(&R);
+  }
+  if (!p->async_host) { /* HBM slots and R buffers, peer copies over xGMI */
+    const char *e = getenv("MSPLIT_ABCAST_NBUF");
+    const int nbuf = e && atoi(e) == 1 ? 1 : 2;
+    for (int i = 0; i < R.nlocal; ++i) {
+      CK(msp_amsg_enable_device(R.blk[i]->am, ctx));
+      CK(msp_abcast_enable_device(R.blk[i]->bc, ctx, nbuf));
+    }
+    barrier(&R);
+  }
+  for (int i = 0; i < R.nlocal; ++i) {
+    CK(msp_vec_set(R.blk[i]->halo, 0.0));
+    CK(update_rhs(R.blk[i]));
+  }
+  barrier(&R);
+  const double thr = fmax(p->atol, p->rtol / sqrt((double)p->nb) * res->norm0);
+  const double t0 = now_s();
+  int active[MSD_MAX_BLOCKS], na = R.nlocal, limited = 0;
+  for (int i = 0; i < na; ++i) active[i] = i;
+  while (na > 0) {
+    for (int a = 0; a < na; ++a) CK(amam_iterate(R.blk[active[a]], p, thr)); /* round-robin */
+    int keep = 0;
+    for (int a = 0; a < na; ++a)
+      if (R.blk[active[a]]->state != MSP_CVD_FINISHED) active[keep++] = active[a];
+    na = keep;
+    for (int a = 0; a < na; ++a)
+      if (R.blk[active[a]]->it >= p->max_outer) limited = 1;
+    if (limited) break;
+  }
+  barrier(&R);
+  res->elapsed = now_s() - t0;
+  CK(exchange(&R)); /* comm_sync_send_and_receive_final */
+  CK(sum_over_blocks(&R, block_residual_sq, &res->final_norm));
+  CK(sum_over_blocks(&R, error_sq, &res->error));
+  res->nlocal = R.nlocal;
+  for (int i = 0; i < R.nlocal; ++i) res->iterations[i] = R.blk[i]->it;
+  res->last_norm = limited ? -1.0 : 0.0;
+  barrier(&R);
+  for (int i = 0; i < R.nlocal; ++i) {
+    msp_amsg_close_peers(R.blk[i]->am);
+    msp_abcast_close_peers(R.blk[i]->bc);
+  }
+  barrier(&R);
+  for (int pass = 0; pass < 2; ++pass) { /* the owner unlinks the regions last */
+    for (int i = 0; i < R.nlocal; ++i) {
+      msd_block *B = R.blk[i];
+      if ((B->L.b == 0) != (pass == 1)) continue;
+      msp_cvd_destroy(&B->cvd);
+      msp_amsg_destroy(&B->am);
+      msp_abcast_destroy(&B->bc);
+    }
+    barrier(&R);
+  }
+  for (int i = 0; i < R.nlocal; ++i) amam_free_block(R.blk[i], p->nb);
   free_run(&R);
   return limited ? MSP_ERR_ARG_OUTOFRANGE : MSP_SUCCESS;
 }

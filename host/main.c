@@ -6,7 +6,8 @@
  *
  * <program>: synchronous-multisplitting,
  *            synchronous-multisplitting-synchronous-minimization-global,
- *            asynchronous-multisplitting.
+ *            asynchronous-multisplitting,
+ *            asynchronous-multisplitting-asynchronous-minimization-global.
  * Built with MPI (msplit_driver_mpi, MPICH): one block per rank, each rank on
  * GPU (rank mod devices); the neighbour exchange, ordered sums and LSQR
  * partials go through msp_comm -- RCCL (-msplit_transport rccl, the default)
@@ -42,7 +43,8 @@ static int mpi_allgather(void *u, const double *send, double *recv, int64_t coun
 
 static int usage(void) {
   fprintf(stderr, "usage: msplit_driver <synchronous-multisplitting | "
-                  "synchronous-multisplitting-synchronous-minimization-global | asynchronous-multisplitting> "
+                  "synchronous-multisplitting-synchronous-minimization-global | asynchronous-multisplitting | "
+                  "asynchronous-multisplitting-asynchronous-minimization-global> "
                   "-m M -n N [-s S] [-rtol R] [-dim 3 -p P] [-peclet px,py,pz] [-nb B] [-json] ...\n");
   return 2;
 }
@@ -60,6 +62,7 @@ int main(int argc, char **argv) {
   if (!strcmp(prog, "synchronous-multisplitting")) kind = 0;
   else if (!strcmp(prog, "synchronous-multisplitting-synchronous-minimization-global")) kind = 1;
   else if (!strcmp(prog, "asynchronous-multisplitting")) kind = 2;
+  else if (!strcmp(prog, "asynchronous-multisplitting-asynchronous-minimization-global")) kind = 3;
   else return usage();
   msd_options *o = msd_options_parse(argc - 1, argv + 1);
   msd_problem p;
@@ -119,14 +122,16 @@ int main(int argc, char **argv) {
   }
 #endif
   msd_result r;
-  int rc = kind == 0 ? msd_sm_solve(ctx, &p, o, &t, &r)
+  int rc = kind == 0   ? msd_sm_solve(ctx, &p, o, &t, &r)
            : kind == 1 ? msd_smsm_global_solve(ctx, &p, o, &t, &r)
-                       : msd_am_solve(ctx, &p, o, &t, &r);
-  if (rc == MSP_ERR_ARG_OUTOFRANGE && kind == 2) rc = 0; /* stopped at -max_outer: still report */
+           : kind == 2 ? msd_am_solve(ctx, &p, o, &t, &r)
+                       : msd_amam_global_solve(ctx, &p, o, &t, &r);
+  const int async = kind >= 2;
+  if (rc == MSP_ERR_ARG_OUTOFRANGE && async) rc = 0; /* stopped at -max_outer: still report */
   if (!rc && rank == 0) {
     if (msd_opt_has(o, NULL, "json")) {
       printf("{\"program\": \"%s\", \"host\": \"c\", \"ranks\": %d, \"blocks\": %d, ", prog, world, p.nb);
-      if (kind == 2) {
+      if (async) {
         printf("\"iterations\": [");
         for (int i = 0; i < r.nlocal; ++i) printf("%s%d", i ? ", " : "", r.iterations[i]);
         printf("], ");
@@ -137,7 +142,7 @@ int main(int argc, char **argv) {
              r.error, r.elapsed);
     } else {
       printf("Elapsed time (iterations):   %f  seconds \n", r.elapsed);
-      if (kind == 2)
+      if (async)
         for (int i = 0; i < r.nlocal; ++i)
           printf("[ Block rank %d ] Total number of iterations (outer_iterations) = %d \n", i, r.iterations[i]);
       else

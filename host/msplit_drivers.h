@@ -5,6 +5,8 @@
  *   synchronous-multisplitting                       (synchronous-multisplitting.c:155-206)
  *   synchronous-multisplitting-synchronous-minimization-global   (SMSM-global.c:288-363)
  *   asynchronous-multisplitting                      (asynchronous-multisplitting_prime.c:333-427)
+ *   asynchronous-multisplitting-asynchronous-minimization-global  (AMAM-global_prime.c:238-481;
+ *                                                     configs[3] / configs[4]'s algorithm)
  *
  * One block per MPI rank (one GPU each; RCCL or MPI all-gathers through
  * msp_comm), or every block in one process (nb blocks, round-robin on one GPU).
@@ -78,6 +80,8 @@ int msd_sm_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const
 int msd_smsm_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const msd_transport *t,
                           msd_result *r);
 int msd_am_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const msd_transport *t, msd_result *r);
+int msd_amam_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const msd_transport *t,
+                          msd_result *r);
 
 #ifdef __cplusplus
 }

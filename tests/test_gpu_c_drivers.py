@@ -78,3 +78,40 @@ def test_c_host_mpi_am_terminates(ctx, built):
     r = _run(["asynchronous-multisplitting", "-dim", "3", "-m", "8", "-n", "8", "-p", "16", "-rtol", "1e-6"] + inner,
              mpi=2)
     assert len(r["iterations"]) == 1 and r["final_norm"] < 1e-4 * r["norm0"]
+
+
+def _inner(nb, its):
+    return [a for b in range(1, nb + 1) for a in (f"-inner{b}_ksp_max_it", str(its), f"-inner{b}_ksp_rtol", "1e-20")]
+
+
+def _outer(nb):
+    return [a for b in range(1, nb + 1) for a in (f"-outer{b}_ksp_type", "lsqr", f"-outer{b}_ksp_convergence_test",
+                                                  "default", f"-outer{b}_ksp_lsqr_exact_mat_norm",
+                                                  f"-outer{b}_ksp_max_it", "70", f"-outer{b}_ksp_rtol", "1e-15",
+                                                  f"-outer{b}_ksp_atol", "1e-100")]
+
+
+AMAM = "asynchronous-multisplitting-asynchronous-minimization-global"
+
+
+@pytest.mark.parametrize("args", [
+    ["-dim", "3", "-m", "8", "-n", "8", "-p", "8", "-s", "4", "-rtol", "1e-6"] + _inner(2, 5) + _outer(2),
+    ["-m", "32", "-n", "32", "-s", "3", "-rtol", "1e-6"] + _inner(2, 8) + _outer(2),
+    ["-dim", "3", "-m", "8", "-n", "8", "-p", "12", "-nb", "3", "-s", "4", "-rtol", "1e-6",
+     "-peclet", "0.5,0.25,-0.3"] + _inner(3, 5) + _outer(3),
+])
+def test_c_host_amam_global_matches_python_host(ctx, built, args):
+    """AMAM-global (configs[3]/[4]'s algorithm) in the C host, blocks round-robin in one process: the same
+    per-block iteration counts, final residual and error as the Python host, to the last bit."""
+    c = _run([AMAM] + args)
+    py = drivers.run([AMAM] + args + ["-json"])
+    assert c["iterations"] == py["iterations"]
+    assert c["final_norm"] == py["final_norm"] and c["error"] == py["error"]
+
+
+def test_c_host_mpi_amam_global_terminates(ctx, built):
+    """One block per MPI rank (both on the one GPU): the R rows travel between the processes' HBM through the
+    msp_abcast buffers, the detection ends the run, and the residual meets the tolerance."""
+    r = _run([AMAM, "-dim", "3", "-m", "8", "-n", "8", "-p", "16", "-s", "4", "-rtol", "1e-6"] + _inner(2, 5)
+             + _outer(2), mpi=2)
+    assert len(r["iterations"]) == 1 and r["final_norm"] < 1e-4 * r["norm0"]
