@@ -465,10 +465,10 @@ def main():
     if world == 1 and variant == "gmres" and rank == 0:
         # release the headline's objects, then the two side measurements
         del ksp, A, b, x, ones
+        if not args.no_spmv512:      # before the SMSM block's ~30 GB come and go
+            extras["spmv_512_csr"] = spmv512(ctx, args)
         if not args.no_smsm_n1:
             extras["smsm_per_gpu"] = smsm_n1(ctx, args)
-        if not args.no_spmv512:
-            extras["spmv_512_csr"] = spmv512(ctx, args)
 
     if rank == 0:
         value = updates / elapsed_max
