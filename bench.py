@@ -246,6 +246,8 @@ def build_smsm(ctx, args, comm, world, rank):
         return its
     transport = {"local": "single block", "nccl": "one library RCCL communicator",
                  "gloo": "gloo (rehearsal: the library's host transport)"}[getattr(comm, "backend", "local")]
+    if getattr(comm, "backend", None) == "nccl" and getattr(comm, "transport", "rccl") != "rccl":
+        transport = "the library's host transport over the NCCL process group (RCCL communicator unavailable)"
     workload = (f"3D 7-pt Poisson {n}x{n}x{nz} SMSM-global, {world} z-slab block(s) of {n}x{n}x{args.smsm_planes} "
                 f"(one per MI355X), s = {args.s} inner GMRES({args.restart}) solves of max_it {args.inner_max_it} "
                 f"per outer iteration, LSQR max_it {args.outer_max_it}; {transport} for the exchange, residual sums "

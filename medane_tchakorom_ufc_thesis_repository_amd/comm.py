@@ -212,11 +212,30 @@ class LibComm:
         self.backend = dist.get_backend(group)
         self.transport = transport or ("rccl" if self.backend == "nccl" else "host")
         self.ctx = ctx
+        self.comm = None
         if self.transport == "rccl":
             obj = [Comm.unique_id() if self.rank == 0 else None]
             dist.broadcast_object_list(obj, src=0, group=group)
-            self.comm = Comm.rccl(ctx, self.world, self.rank, obj[0])
-        else:
+            err = None
+            try:
+                self.comm = Comm.rccl(ctx, self.world, self.rank, obj[0])
+            except Exception as e:          # e.g. ranks sharing a GPU, which RCCL refuses
+                err = e
+            # every rank takes the same transport (the C host's MPI_Allreduce MIN, host/main.c)
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32,
+                              device=torch.device("cuda", torch.cuda.current_device())
+                              if self.backend == "nccl" else torch.device("cpu"))
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            if int(ok.item()) == 0:
+                if self.comm is not None:
+                    self.comm.destroy()
+                    self.comm = None
+                if self.rank == 0:
+                    import sys
+                    print(f"msplit: RCCL communicator unavailable ({err or 'on another rank'}); "
+                          "using the host transport over the process group", file=sys.stderr)
+                self.transport = "host"
+        if self.transport == "host":
             dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
             world = self.world
 
