@@ -32,7 +32,7 @@ def _opts(nb, s):
     return f"{inner} {outer} -s {s}"
 
 
-def _worker(rank, world, port, problem, q):
+def _worker(rank, world, port, problem, q, transport="host"):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
@@ -44,7 +44,7 @@ def _worker(rank, world, port, problem, q):
                                                                               smsm_solve)
         from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Options
         ctx = Context(0)
-        comm = LibComm(ctx, transport="host")
+        comm = LibComm(ctx, transport=transport)
         kind, dim, nx, ny, nz, s, rtol = problem
         o = Options(_opts(world, s))
         if kind == "smsm":
@@ -60,6 +60,7 @@ def _worker(rank, world, port, problem, q):
             out = {"outer_its": res.outer_its, "norm0": res.norm0, "hist": list(res.hist),
                    "inner_its": np.array(res.inner_its).tolist()}
         out["x"] = blocks[0].x.get_array()
+        out["transport"] = comm.transport
         comm.close()
         dist.barrier()
         dist.destroy_process_group()
@@ -69,11 +70,11 @@ def _worker(rank, world, port, problem, q):
         q.put((rank, None, traceback.format_exc() + str(e)))
 
 
-def _run(world, problem):
+def _run(world, problem, transport="host"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, problem, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, problem, q, transport)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
@@ -107,3 +108,15 @@ def test_libcomm_ranks_bitwise_vs_oracle(oracle, problem, world):
             assert np.array_equal(np.array(o["inner_its"])[:, :, 0], ro["inner_its"][:, :, r])
         else:
             assert np.array_equal(np.array(o["inner_its"])[:, 0], ro["inner_its"][:, r])
+
+
+def test_libcomm_falls_back_when_rccl_is_refused(oracle):
+    """Asked for the RCCL transport with two ranks on one GPU (which RCCL refuses), every rank agrees to take
+    the host transport instead, and the run is still bitwise the oracle."""
+    problem = ("sm", 3, 12, 10, 8, 0, 1e-6)
+    outs = _run(2, problem, transport="rccl")
+    assert all(o["transport"] == "host" for o in outs)
+    ro = oracle.sm_solve(3, 12, 10, 8, 2, 1e-6, dict(restart=30, max_it=20, rtol=1e-20, abstol=1e-100,
+                                                      reduce_mode=oracle.REDUCE_DBR), max_outer=200)
+    assert np.array_equal(np.concatenate([o["x"] for o in outs]), ro["x"])
+    assert all(o["outer_its"] == ro["outer_its"] for o in outs)
