@@ -122,3 +122,22 @@ def test_drivers_command_line():
         with pytest.raises(ValueError):
             drivers.parse(bad)
     assert len(drivers.PROGRAMS) == 9                                 # every driver directory of the reference's src/
+
+
+def test_bench_cpu_share_and_topology(monkeypatch):
+    """bench.py's CPU baseline uses the job's CPU share: MSPLIT_CPU_THREADS, else the cgroup quota / CPU set,
+    capped by OMP_NUM_THREADS; the topology it reports has the fields the JSON promises."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    topo = bench.host_topology()
+    assert topo["nproc"] == os.cpu_count()
+    monkeypatch.delenv("MSPLIT_CPU_THREADS", raising=False)
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.cpu_threads({"cgroup_cpu_quota": 16.0, "nproc": 256}) == 3
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.cpu_threads({"cgroup_cpu_quota": 16.0, "nproc": 256}) == 16
+    assert bench.cpu_threads({"affinity_cpus": 8, "nproc": 256}) == 8
+    monkeypatch.setenv("MSPLIT_CPU_THREADS", "5")
+    assert bench.cpu_threads({"cgroup_cpu_quota": 16.0}) == 5
