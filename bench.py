@@ -57,6 +57,16 @@ KERNEL_NAMES = {"mdot": "k_dot_stage1+2 (VecMDot, DBR)",
 SPMV_NAMES = {"dv": "k_spmv_ell (MatMult/MatResidual, DV storage: one byte per entry)",
               "csr": "k_spmv_lds8 (MatMult/MatResidual, CSR storage)",
               "matfree": "k_stencil_spmv (MatMult/MatResidual, matrix-free)"}
+MARCH_NAME = "k_spmv_box_march (MatMult/MatResidual, DV storage: one byte per entry; box stencil marched in z)"
+TUNE_ELL_MARCH_OFF = 268435456
+
+
+def spmv_name(storage, nx):
+    """The kernel the library picks for a box stencil's products (msk_box_march_pick)."""
+    tune = int(os.environ.get("MSPLIT_TUNING", "0") or 0)
+    if storage == "dv" and nx % 256 == 0 and not tune & TUNE_ELL_MARCH_OFF:
+        return MARCH_NAME
+    return SPMV_NAMES[storage]
 
 
 def parse():
@@ -502,7 +512,7 @@ def main():
             traffic = None
             if tr and tr.get("kernel_class") == dom and tr.get("n") == n and variant == "gmres":
                 traffic = tr.get("hbm_bytes_per_launch")
-            names = dict(KERNEL_NAMES, spmv=SPMV_NAMES[spmv_storage])
+            names = dict(KERNEL_NAMES, spmv=spmv_name(spmv_storage, n))
             out["roofline"] = {"bound": "hbm", "kernel": names[dom], "achieved": achieved,
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                                "traffic": traffic,

@@ -69,8 +69,11 @@ enum {
   MSK_TUNE_DENSE_G2 = 16777216,     // LSQR dense kernels: two columns per load group
   MSK_TUNE_DENSE_TEMPORAL_ST = 33554432, // LSQR dense kernels: default-policy u / u/beta stores (default: non-temporal)
   MSK_TUNE_ELL_XCD_ON = 67108864,   // DV (ELL) SpMV: XCD-contiguous block order at any plane size
-  MSK_TUNE_ELL_XCD_OFF = 134217728  // DV (ELL) SpMV: identity block order at any plane size (default: XCD order
+  MSK_TUNE_ELL_XCD_OFF = 134217728, // DV (ELL) SpMV: identity block order at any plane size (default: XCD order
                                     // from 2^18 rows per plane)
+  MSK_TUNE_ELL_MARCH_OFF = 268435456, // box-stencil DV SpMV: the row-parallel ELL kernel (default: the z-march
+                                      // kernel wherever nx % 256 == 0)
+  MSK_TUNE_ELL_MARCH_NOXCD = 536870912 // z-march kernel: identity block order (default: XCD-contiguous runs)
 };
 
 extern "C" {
@@ -109,6 +112,14 @@ int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const
                 const int32_t* ddelta, const double* dval, int ndict, int32_t max_block, int ell_w,
                 const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
                 const int* stop, int64_t plane, hipStream_t s);
+// The same products for a 3D box stencil in the ELL layout with 8 codes per row whose dictionary is
+// exactly the seven stencil pairs in column order (-nx*ny, -nx, -1, 0, +1, +nx, +nx*ny), lo = hi = 0:
+// a z-marching kernel without gathers (needs nx % 256 == 0).  msk_box_march_pick: 1 when the tuning
+// policy takes it for this box (default: whenever nx % 256 == 0).
+int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz);
+int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8, const double* dval,
+                       const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
+                       const int* stop, hipStream_t s);
 // R[:, 0:nc] = A S[:, 0:nc] over DV storage in the ELL layout (W codes per row)
 int msk_spmm_ell(int32_t nrows, int W, const uint8_t* code8, const int32_t* ddelta, const double* dval, int ndict,
                  const double* S, int64_t lds, int nc, double* R, int64_t ldr, hipStream_t s);

@@ -1339,6 +1339,76 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
   }
 }
 
+// The ELL SpMV of a 3D box stencil, marching in z.  The dictionary is the stencil's
+// seven pairs in column order (-P, -nx, -1, 0, +1, +nx, +P) -- the host guarantees it
+// (msp_mat_create_box_convdiff, lo = hi = 0) -- so code e always names neighbour e
+// and a row's codes only say which neighbours exist.  A workgroup owns a 256-wide x
+// segment of one y line and marches kMarchZ planes: x(z-1), x(z), x(z+1) stay in
+// registers, x(y-+1) are coalesced loads, x(i-+1) come from the segment's row in
+// LDS.  No gathers.  xwin > 0: XCD x takes runs of xwin consecutive workgroups
+// (ell_block), i.e. neighbouring y lines of one z tile, so the x(y-+1) loads of one
+// workgroup are the x(z) rows of its neighbours and meet in that XCD's L2.  With
+// xwin = 32: 256^3 92 -> 74 us, 512^3 821 -> 628 us; in identity order 99 / 697 us
+// (tools/ell_lab.hip, profiles/r02/ell_lab/).  The products are added in CSR order
+// from 0.0, the same terms as k_spmv_ell, so the result is bitwise identical.
+// nx % 256 == 0.
+constexpr int kMarchZ = 16;
+template <int MODE, bool NTY>
+__global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, int32_t nz,
+                                                       const uint8_t* __restrict__ code8,
+                                                       const double* __restrict__ dval, const double* __restrict__ x,
+                                                       const double* __restrict__ b, double* __restrict__ y,
+                                                       const double* __restrict__ sdev, double* __restrict__ vout,
+                                                       const int* __restrict__ stop, int32_t xwin) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
+  __shared__ double sx[kT + 2];
+  const int t = threadIdx.x;
+  const int32_t nseg = nx / kT;
+  const int32_t bid = ell_block(xwin);
+  const int32_t seg = bid % nseg, yl = (bid / nseg) % ny, z0 = (bid / (nseg * ny)) * kMarchZ;
+  const int32_t z1 = min(z0 + kMarchZ, nz);
+  const int32_t i = seg * kT + t;
+  const int64_t P = (int64_t)nx * ny;
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  double v[7];
+#pragma unroll
+  for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  const int64_t rl = i + (int64_t)yl * nx;  // the row's offset within its plane
+  const bool hs = yl > 0, hn = yl < ny - 1, hl = t == 0 && i > 0, hr = t == kT - 1 && i + 1 < nx;
+  double xm = z0 > 0 ? x[rl + (z0 - 1) * P] : 0.0;
+  double xc = x[rl + z0 * P];
+  for (int32_t z = z0; z < z1; ++z) {
+    const int64_t r = rl + z * P;
+    const u32x2 cw = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r);
+    const double xp = z + 1 < nz ? x[r + P] : 0.0;
+    const double xs = hs ? x[r - nx] : 0.0;
+    const double xn = hn ? x[r + nx] : 0.0;
+    const double el = hl ? x[r - 1] : 0.0;
+    const double er = hr ? x[r + 1] : 0.0;
+    __syncthreads();  // the previous plane's reads of sx are done
+    sx[t + 1] = xc;
+    if (t == 0) sx[0] = el;
+    if (t == kT - 1) sx[kT + 1] = er;
+    __syncthreads();
+    const double xl = sx[t], xr = sx[t + 2];
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = EllWord<8>::byte(cw, q);
+      if (c != 255) m |= 1u << c;
+    }
+    const double xq[7] = {xm, xs, xl, xc, xr, xn, xp};
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < 7; ++e)
+      if (m & (1u << e)) s = s + v[e] * (MODE == MSK_SPMV_SCALED ? xq[e] * sc : xq[e]);
+    if (MODE == MSK_SPMV_SCALED && vout) st_pol<NTY>(vout + r, xc * sc);
+    st_pol<NTY>(y + r, MODE == MSK_SPMV_RESID ? b[r] - s : s);
+    xm = xc;
+    xc = xp;
+  }
+}
+
 // MatMatMult R = A S over DV storage (ELL layout): lane per row, its codes
 // decoded once into (delta, value) registers, then every column of S streamed
 // past them; each R(r, q) is the CSR row sum of k_spmm_lds8 term for term.
@@ -1733,6 +1803,37 @@ static void launch_ell(int mode, int32_t nrows, const uint8_t* code8, const int3
     launch_ell_pol<W, RPL, false>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, xwin, s);
 }
 
+template <bool NTY>
+static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8,
+                             const double* dval, const double* x, const double* b, double* y, const double* sdev,
+                             double* vout, const int* stop, int32_t xwin, hipStream_t s) {
+#define MSK_BM(M) k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, xwin)
+  if (mode == MSK_SPMV_RESID) MSK_BM(MSK_SPMV_RESID);
+  else if (mode == MSK_SPMV_SCALED) MSK_BM(MSK_SPMV_SCALED);
+  else MSK_BM(MSK_SPMV_MULT);
+#undef MSK_BM
+}
+
+extern "C" int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz) {
+  const int f = msk_tuning_flags;
+  if (nx <= 0 || ny <= 0 || nz <= 0 || nx % kT) return 0;
+  return !(f & MSK_TUNE_ELL_MARCH_OFF);
+}
+
+extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8, const double* dval,
+                                  const double* x, const double* b, double* y, int mode, const double* sdev,
+                                  double* vout, const int* stop, hipStream_t s) {
+  if (nx <= 0 || ny <= 0 || nz <= 0 || nx % kT) return (int)hipErrorInvalidValue;
+  const int64_t g = (int64_t)(nx / kT) * ny * ((nz + kMarchZ - 1) / kMarchZ);
+  if (g > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
+  const int32_t xwin = (msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) ? 0 : 32;
+  if (!(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y))
+    launch_box_march<true>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, xwin, s);
+  else
+    launch_box_march<false>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, xwin, s);
+  return (int)hipGetLastError();
+}
+
 extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const uint8_t* code8,
                            const int32_t* ddelta, const double* dval, int ndict, int32_t max_block, int ell_w,
                            const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
@@ -1740,6 +1841,8 @@ extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* 
   if (nrows <= 0) return 0;
   if (max_block < 0 || ndict < 0 || ndict > 256) return (int)hipErrorInvalidValue;
   if ((msk_tuning_flags & MSK_TUNE_ELL_XCD_ON) && (msk_tuning_flags & MSK_TUNE_ELL_XCD_OFF)) return (int)hipErrorInvalidValue;
+  if ((msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) && (msk_tuning_flags & MSK_TUNE_ELL_MARCH_OFF))
+    return (int)hipErrorInvalidValue;
   if (ell_w) {
     if (ndict > 255) return (int)hipErrorInvalidValue;
     const int rpl = (msk_tuning_flags & MSK_TUNE_DV_RPL1) ? 1 : (msk_tuning_flags & MSK_TUNE_DV_RPL2) ? 2 : (ell_w == 16 ? 2 : 4);

@@ -422,6 +422,9 @@ struct msp_mat {
   int32_t dv_mb = 0;           // most entries in one 256-row block (sizes the LDS stage)
   int32_t dv_w = 0;            // ELL layout: codes per row (4, 8, 16); 0: CSR-order codes + row lengths
   bool dv_on = false;          // products read the DV storage
+  // 3D box stencil (lo = hi = 0) whose ELL dictionary is the seven stencil pairs in column order:
+  // its extents, for the z-march SpMV (msk_spmv_box_march); 0 otherwise
+  int32_t march_nx = 0, march_ny = 0, march_nz = 0;
   bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
   uint64_t version = next_version();  // unique per object and bumped when its products' kernels change
 };
@@ -464,6 +467,7 @@ static void dv_free(msp_mat* A) {
   A->dv_mb = 0;
   A->dv_w = 0;
   A->dv_on = false;
+  A->march_nx = A->march_ny = A->march_nz = 0;
 }
 
 // Encode the device CSR of A against the dictionary (host arrays, nd <= 256).
@@ -743,6 +747,11 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
       msp_mat_destroy(&A);
       return rc;
     }
+    if (dim == 3 && !lo && !hi && A->ndict == 7 && A->dv_w == 8) {
+      A->march_nx = nx;
+      A->march_ny = ny;
+      A->march_nz = nz;
+    }
   }
   *out = A;
   return MSP_SUCCESS;
@@ -841,6 +850,11 @@ static double dv_bytes(const msp_mat* A, bool resid, bool vout) {
   const double codes = A->dv_w ? (double)A->dv_w * rows : (double)A->nnz + rows + 4.0 * (rows / 256.0 + 1.0);
   return codes + 8.0 * (double)A->ncols + 8.0 * rows +
          (resid ? 8.0 * rows : 0.0) + (vout ? 8.0 * rows : 0.0);
+}
+
+// DV products of a box stencil take the z-march kernel when the tuning policy picks it
+static bool box_march(const msp_mat* A) {
+  return A->march_nx > 0 && msk_box_march_pick(A->march_nx, A->march_ny, A->march_nz);
 }
 
 extern "C" int msp_mat_set_storage(msp_mat* A, int storage) {
@@ -1029,6 +1043,11 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
   }
   if (A->dv_on) {
     KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, resid, false));
+    if (box_march(A)) {
+      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->dv_code, A->dv_val, x, b, y,
+                              resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
+      return MSP_SUCCESS;
+    }
     KCHK(msk_spmv_dv(A->nrows, A->rowptr, A->dv_len, A->dv_code, A->dv_delta, A->dv_val, A->ndict, A->dv_mb, A->dv_w, x, b,
                      y, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, A->plane, c->stream));
     return MSP_SUCCESS;
@@ -1059,6 +1078,11 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
   }
   if (A->dv_on) {
     KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, false, vout != nullptr));
+    if (box_march(A)) {
+      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->dv_code, A->dv_val, x, nullptr, y,
+                              MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
+      return MSP_SUCCESS;
+    }
     KCHK(msk_spmv_dv(A->nrows, A->rowptr, A->dv_len, A->dv_code, A->dv_delta, A->dv_val, A->ndict, A->dv_mb, A->dv_w, x,
                      nullptr, y, MSK_SPMV_SCALED, sdev, vout, stop, A->plane, c->stream));
     return MSP_SUCCESS;

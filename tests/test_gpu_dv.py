@@ -296,3 +296,61 @@ def test_ell_xcd_block_order_bitwise(ctx, oracle, flags, nz):
     assert A.get_storage() == "dv"
     with tuning(flags):
         _products(ctx, A, O, np.random.default_rng(SEED))
+
+
+
+MARCH_OFF, MARCH_NOXCD = 268435456, 536870912
+
+
+@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF])
+@pytest.mark.parametrize("shape", [(256, 16, 40), (512, 3, 17), (256, 1, 1), (256, 5, 16), (768, 2, 33),
+                                   (256, 40, 7), (256, 100, 40)])
+@pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 0.3)])
+def test_box_march_bitwise(ctx, oracle, flags, shape, peclet):
+    """The z-march SpMV of box stencils (the default wherever nx % 256 == 0; MSK_TUNE_ELL_MARCH_NOXCD: identity
+    workgroup order; MSK_TUNE_ELL_MARCH_OFF: the row-parallel ELL kernel): whole and ragged z tiles (16 planes per
+    workgroup), one and several y lines, one and several 256-wide x segments, full XCD runs of 32 workgroups and a
+    ragged tail.  MatMult and MatResidual equal the oracle; GMRES -- the scaled MatMult with its stop flag -- equals
+    the oracle's DBR GMRES bit for bit."""
+    from test_gpu_kernels import tuning
+    nx, ny, nz = shape
+    A = Mat.box_stencil(ctx, 3, nx, ny, nz) if peclet is None else Mat.box_convdiff(ctx, 3, nx, ny, nz, False,
+                                                                                    False, peclet)
+    rp, col, val = A.get_csr()
+    O = oracle.Mat.from_arrays(A.shape[0], A.shape[1], rp, col, val)
+    assert A.get_storage() == "dv"
+    n = A.shape[0]
+    b = O.mult(np.random.default_rng(SEED).uniform(-1, 1, n))
+    o = dict(restart=12, max_it=40, rtol=1e-30)
+    with tuning(flags):
+        _products(ctx, A, O, np.random.default_rng(SEED))
+        ksp = KSP(ctx)
+        ksp.set_operators(A)
+        ksp.set_from_options(Options(f"-ksp_type gmres -pc_type none -ksp_norm_type unpreconditioned "
+                                     f"-ksp_gmres_restart {o['restart']} -ksp_max_it {o['max_it']} "
+                                     f"-ksp_rtol {o['rtol']}"))
+        xv = Vec(ctx, n)
+        ksp.solve(Vec.from_array(ctx, b), xv)
+    xo, ro = oracle.gmres(O, b, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=0, **o)
+    assert ksp.get_iteration_number() == ro["its"]
+    assert np.array_equal(ksp.get_residual_history(), ro["hist"])
+    assert np.array_equal(xv.get_array(), xo)
+
+
+def test_box_march_large_plane(ctx, oracle):
+    """512 x 512 planes: the z-march kernel equals the row-parallel ELL kernel (MSK_TUNE_ELL_MARCH_OFF, XCD order
+    at this plane size) and the oracle bit for bit.  A flag combination with no kernel is an error."""
+    from test_gpu_kernels import tuning
+    from medane_tchakorom_ufc_thesis_repository_amd import MsplitError
+    A = Mat.box_stencil(ctx, 3, 512, 512, 5)
+    rp, col, val = A.get_csr()
+    O = oracle.Mat.from_arrays(A.shape[0], A.shape[1], rp, col, val)
+    y0, r0 = _products(ctx, A, O, np.random.default_rng(SEED))
+    with tuning(MARCH_OFF):
+        y1, r1 = _products(ctx, A, O, np.random.default_rng(SEED))
+    assert np.array_equal(y0, y1) and np.array_equal(r0, r1)
+    x = Vec.from_array(ctx, np.ones(A.shape[0]))
+    y = Vec(ctx, A.shape[0])
+    with tuning(MARCH_OFF | MARCH_NOXCD):
+        with pytest.raises(MsplitError):
+            A.mult(x, y)

@@ -665,6 +665,143 @@ __global__ __launch_bounds__(kT) void k_dpair(int32_t nrows, const uint8_t* __re
   }
 }
 
+
+// --- zm: stencil-aware marching.  The dictionary is the box stencil's seven pairs in the
+// order (-P, -n, -1, 0, +1, +n, +P) (the host checks it), so each code names a fixed neighbour.
+// A workgroup owns a 256-wide x segment of one y line and marches Z planes in z: x(z-1), x(z)
+// and x(z+1) stay in registers, x(y+-1) are two coalesced loads, x(i+-1) come from the
+// segment's values in LDS (edges loaded by the end lanes).  No gathers; per row: codes,
+// 3 coalesced x loads, 1 store.  Same products in CSR order: bitwise.
+template <int Z>
+__global__ __launch_bounds__(kT) void k_zm(int nx, int ny, int nz, const uint8_t* __restrict__ code8,
+                                           const double* __restrict__ dval, const double* __restrict__ x,
+                                           double* __restrict__ y, int xwin = 0) {
+  __shared__ double sx[kT + 2];
+  const int t = threadIdx.x;
+  const int nseg = nx / kT;
+  int bid = (int)blockIdx.x;
+  if (xwin > 0) {  // XCD x (blockIdx % 8) takes a contiguous run of xwin blocks in each window of 8*xwin
+    const int span = 8 * xwin, full = (int)(gridDim.x / (unsigned)span) * span;
+    if (bid < full) {
+      const int w = bid / span, rem = bid - w * span;
+      bid = w * span + (rem & 7) * xwin + (rem >> 3);
+    }
+  }
+  const int seg = bid % nseg, yl = (bid / nseg) % ny, zt = bid / (nseg * ny);
+  const int z0 = zt * Z, z1 = min(z0 + Z, nz);
+  const int i = seg * kT + t;
+  const int64_t P = (int64_t)nx * ny;
+  double v[7];
+#pragma unroll
+  for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  const int64_t rl = i + (int64_t)yl * nx;   // row offset within a plane
+  double xm = z0 > 0 ? x[rl + (z0 - 1) * P] : 0.0;
+  double xc = x[rl + z0 * P];
+  for (int z = z0; z < z1; ++z) {
+    const int64_t r = rl + z * P;
+    const u32x2 cw = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r);
+    const double xp = z + 1 < nz ? x[r + P] : 0.0;
+    const double xs = yl > 0 ? x[r - nx] : 0.0;
+    const double xn = yl < ny - 1 ? x[r + nx] : 0.0;
+    double el = 0.0, er = 0.0;
+    if (t == 0 && i > 0) el = x[r - 1];
+    if (t == kT - 1 && i + 1 < nx) er = x[r + 1];
+    __syncthreads();               // the previous step's reads of sx are done
+    sx[t + 1] = xc;
+    if (t == 0) sx[0] = el;
+    if (t == kT - 1) sx[kT + 1] = er;
+    __syncthreads();
+    const double xl = sx[t], xr = sx[t + 2];
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = cbyte(cw, q);
+      if (c != 255) m |= 1u << c;
+    }
+    double s = 0.0;
+    if (m & 1) s = s + v[0] * xm;
+    if (m & 2) s = s + v[1] * xs;
+    if (m & 4) s = s + v[2] * xl;
+    if (m & 8) s = s + v[3] * xc;
+    if (m & 16) s = s + v[4] * xr;
+    if (m & 32) s = s + v[5] * xn;
+    if (m & 64) s = s + v[6] * xp;
+    st_nt(y + r, s);
+    xm = xc;
+    xc = xp;
+  }
+}
+
+
+// --- zmp: k_zm with the next plane's loads (codes, the y+-1 lines, x(z+2), the segment
+// edges) issued before the current plane is summed, and the LDS row in two buffers (one
+// barrier per plane): the march keeps one plane of loads in flight.
+template <int Z>
+__global__ __launch_bounds__(kT) void k_zmp(int nx, int ny, int nz, const uint8_t* __restrict__ code8,
+                                            const double* __restrict__ dval, const double* __restrict__ x,
+                                            double* __restrict__ y) {
+  __shared__ double sx[2][kT + 2];
+  const int t = threadIdx.x;
+  const int nseg = nx / kT;
+  const int seg = (int)(blockIdx.x % nseg), yl = (int)((blockIdx.x / nseg) % ny), zt = (int)(blockIdx.x / (nseg * ny));
+  const int z0 = zt * Z, z1 = min(z0 + Z, nz);
+  const int i = seg * kT + t;
+  const int64_t P = (int64_t)nx * ny;
+  double v[7];
+#pragma unroll
+  for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  const int64_t rl = i + (int64_t)yl * nx;
+  const bool hs = yl > 0, hn = yl < ny - 1, hl = t == 0 && i > 0, hr = t == kT - 1 && i + 1 < nx;
+  auto load = [&](int z, u32x2& cw, double& xs, double& xn, double& xp, double& el, double& er) {
+    const int64_t r = rl + z * P;
+    cw = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r);
+    xs = hs ? x[r - nx] : 0.0;
+    xn = hn ? x[r + nx] : 0.0;
+    xp = z + 1 < nz ? x[r + P] : 0.0;
+    el = hl ? x[r - 1] : 0.0;
+    er = hr ? x[r + 1] : 0.0;
+  };
+  double xm = z0 > 0 ? x[rl + (z0 - 1) * P] : 0.0;
+  double xc = x[rl + z0 * P];
+  u32x2 cw;
+  double xs, xn, xp, el, er;
+  load(z0, cw, xs, xn, xp, el, er);
+  for (int z = z0; z < z1; ++z) {
+    u32x2 cwN = cw;
+    double xsN = 0.0, xnN = 0.0, xpN = 0.0, elN = 0.0, erN = 0.0;
+    if (z + 1 < z1) load(z + 1, cwN, xsN, xnN, xpN, elN, erN);
+    const int b = z & 1;
+    sx[b][t + 1] = xc;
+    if (t == 0) sx[b][0] = el;
+    if (t == kT - 1) sx[b][kT + 1] = er;
+    __syncthreads();
+    const double xl = sx[b][t], xr = sx[b][t + 2];
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = cbyte(cw, q);
+      if (c != 255) m |= 1u << c;
+    }
+    double s = 0.0;
+    if (m & 1) s = s + v[0] * xm;
+    if (m & 2) s = s + v[1] * xs;
+    if (m & 4) s = s + v[2] * xl;
+    if (m & 8) s = s + v[3] * xc;
+    if (m & 16) s = s + v[4] * xr;
+    if (m & 32) s = s + v[5] * xn;
+    if (m & 64) s = s + v[6] * xp;
+    st_nt(y + rl + z * P, s);
+    xm = xc;
+    xc = xp;
+    cw = cwN;
+    xs = xsN;
+    xn = xnN;
+    xp = xpN;
+    el = elN;
+    er = erN;
+  }
+}
+
 // block order remap: XCD x (blockIdx % 8) takes the blocks of its eighth of a z-window
 template <int RPL>
 __global__ __launch_bounds__(kT) void k_basex(int32_t nrows, const uint8_t* __restrict__ code8,
@@ -769,24 +906,27 @@ int main(int argc, char** argv) {
   for (round_ = 0; round_ < 3; ++round_) {
     run("base4", [&] { k_base<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
     run("base2", [&] { k_base<2><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("uni4", [&] { k_uni<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
 
+    {
+      const int nseg = n / kT;
+      for (int Z : {8, 16}) {
+        const unsigned gz = (unsigned)(nseg * n * ((n + Z - 1) / Z));
+        for (int xw : {0, 8, 32, 128}) {
+          char nm[32];
+          snprintf(nm, sizeof(nm), "zm%d_x%d", Z, xw);
+          if (Z == 8) run(nm, [&] { k_zm<8><<<gz, kT>>>(n, n, n, code8, dval, x, y, xw); }, true);
+          if (Z == 16) run(nm, [&] { k_zm<16><<<gz, kT>>>(n, n, n, code8, dval, x, y, xw); }, true);
+        }
+      }
+      const unsigned gz = (unsigned)(nseg * n * ((n + 31) / 32));
+      run("zmp32", [&] { k_zmp<32><<<gz, kT>>>(n, n, n, code8, dval, x, y); }, true);
+    }
     run("dpair2", [&] { k_dpair<2, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("dpair1", [&] { k_dpair<1, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("dspec4", [&] { k_dspec<4, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("dspec2", [&] { k_dspec<2, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("dspec1", [&] { k_dspec<1, 8><<<g1, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("dord4", [&] { k_dord<4, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("dord2", [&] { k_dord<2, 8><<<g2, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("dord1", [&] { k_dord<1, 8><<<g1, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
-    run("near4", [&] { k_part<4, 0x36><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, false);
-    run("far4", [&] { k_part<4, 0x41><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, false);
 
     run("noxg4", [&] { k_noxg<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, false);
     if (g4 % 64 == 0) {
       run("basex4_w8", [&] { k_basex<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y, 8); }, true);
-      run("basex4_w32", [&] { k_basex<4><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y, 32); }, true);
-    }
+      }
   }
   printf("}}\n");
   return 0;
