@@ -90,11 +90,11 @@ def main():
                         mismatch.append(f"spmv/t{t}/g{g}")
             L.msk_set_spmv_group(0)
             if "mdot" in kernels:
-                for k in (1, 8, 16, 30):
+                for k in (1, 2, 4, 8, 12, 16, 20, 30):
                     gb, us = timed(lambda: w.mdot(V[:k]), "mdot")
                     res.setdefault(f"mdot{k}/t{t}", []).append((gb, us))
             if "maxpy" in kernels:
-                for k in (1, 8, 16, 30):
+                for k in (1, 2, 4, 8, 12, 16, 20, 30):
                     a = np.full(k, 1e-300)
                     gb, us = timed(lambda: w.maxpy(a, V[:k]), "maxpy")
                     res.setdefault(f"maxpy{k}/t{t}", []).append((gb, us))
