@@ -64,7 +64,7 @@ TUNE_ELL_MARCH_OFF = 268435456
 def spmv_name(storage, nx):
     """The kernel the library picks for a box stencil's products (msk_box_march_pick)."""
     tune = int(os.environ.get("MSPLIT_TUNING", "0") or 0)
-    if storage == "dv" and nx % 256 == 0 and not tune & TUNE_ELL_MARCH_OFF:
+    if storage == "dv" and not tune & TUNE_ELL_MARCH_OFF:
         return MARCH_NAME
     return SPMV_NAMES[storage]
 

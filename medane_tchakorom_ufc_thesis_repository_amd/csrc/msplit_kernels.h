@@ -72,7 +72,7 @@ enum {
   MSK_TUNE_ELL_XCD_OFF = 134217728, // DV (ELL) SpMV: identity block order at any plane size (default: XCD order
                                     // from 2^18 rows per plane)
   MSK_TUNE_ELL_MARCH_OFF = 268435456, // box-stencil DV SpMV: the row-parallel ELL kernel (default: the z-march
-                                      // kernel wherever nx % 256 == 0)
+                                      // kernel for every 3D box stencil with lo = hi = 0)
   MSK_TUNE_ELL_MARCH_NOXCD = 536870912 // z-march kernel: identity block order (default: XCD-contiguous runs)
 };
 
@@ -80,6 +80,7 @@ extern "C" {
 void msk_set_tuning(int flags);
 int msk_get_tuning(void);
 void msk_set_spmv_group(int gb);
+void msk_set_march_z(int z);  // z-march planes per workgroup (0: auto; A/B experiments)
 // The CGS block with W = A (sc x) computed in the kernel (op) instead of read from w: stage 1 of
 // W . V_v (v < nv <= 32), and the MAXPY wout = W - sum_j adev_j V_j with the ||wout||^2 partials.
 int msk_dot_stage1_op(const EllOp* op, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,
@@ -114,8 +115,8 @@ int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const
                 const int* stop, int64_t plane, hipStream_t s);
 // The same products for a 3D box stencil in the ELL layout with 8 codes per row whose dictionary is
 // exactly the seven stencil pairs in column order (-nx*ny, -nx, -1, 0, +1, +nx, +nx*ny), lo = hi = 0:
-// a z-marching kernel without gathers (needs nx % 256 == 0).  msk_box_march_pick: 1 when the tuning
-// policy takes it for this box (default: whenever nx % 256 == 0).
+// a z-marching kernel without gathers.  msk_box_march_pick: 1 when the tuning policy takes it for this
+// box (default: always).
 int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz);
 int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8, const double* dval,
                        const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,

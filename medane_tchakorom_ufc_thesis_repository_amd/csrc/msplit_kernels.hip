@@ -1342,45 +1342,45 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
 // The ELL SpMV of a 3D box stencil, marching in z.  The dictionary is the stencil's
 // seven pairs in column order (-P, -nx, -1, 0, +1, +nx, +P) -- the host guarantees it
 // (msp_mat_create_box_convdiff, lo = hi = 0) -- so code e always names neighbour e
-// and a row's codes only say which neighbours exist.  A workgroup owns a 256-wide x
-// segment of one y line and marches kMarchZ planes: x(z-1), x(z), x(z+1) stay in
-// registers, x(y-+1) are coalesced loads, x(i-+1) come from the segment's row in
-// LDS.  No gathers.  xwin > 0: XCD x takes runs of xwin consecutive workgroups
-// (ell_block), i.e. neighbouring y lines of one z tile, so the x(y-+1) loads of one
+// and a row's codes only say which neighbours exist.  A workgroup owns 256
+// consecutive rows of a plane (a 256-wide x segment of one y line when nx % 256 == 0;
+// parts of several lines otherwise, the plane's last segment ragged) and marches
+// zt planes: x(z-1), x(z), x(z+1) stay in registers, x(y-+1) = x[r -+ nx] are
+// coalesced loads, x(i-+1) come from the segment's row in LDS.  No gathers.  A
+// neighbour is read only where it lies inside the plane, and added only where the
+// row's codes name it.  xwin > 0: XCD x takes runs of xwin consecutive workgroups
+// (ell_block), i.e. neighbouring segments of one z tile, so the x(y-+1) loads of one
 // workgroup are the x(z) rows of its neighbours and meet in that XCD's L2.  With
 // xwin = 32: 256^3 92 -> 74 us, 512^3 821 -> 628 us; in identity order 99 / 697 us
 // (tools/ell_lab.hip, profiles/r02/ell_lab/).  The products are added in CSR order
 // from 0.0, the same terms as k_spmv_ell, so the result is bitwise identical.
-// nx % 256 == 0.
-constexpr int kMarchZ = 16;
 template <int MODE, bool NTY>
 __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, int32_t nz,
                                                        const uint8_t* __restrict__ code8,
                                                        const double* __restrict__ dval, const double* __restrict__ x,
                                                        const double* __restrict__ b, double* __restrict__ y,
                                                        const double* __restrict__ sdev, double* __restrict__ vout,
-                                                       const int* __restrict__ stop, int32_t xwin) {
+                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   __shared__ double sx[kT + 2];
   const int t = threadIdx.x;
-  const int32_t nseg = nx / kT;
+  const int32_t P = nx * ny;  // nx * ny * nz <= INT32_MAX (checked by the launcher)
+  const int32_t nps = (P + kT - 1) / kT;
   const int32_t bid = ell_block(xwin);
-  const int32_t seg = bid % nseg, yl = (bid / nseg) % ny, z0 = (bid / (nseg * ny)) * kMarchZ;
-  const int32_t z1 = min(z0 + kMarchZ, nz);
-  const int32_t i = seg * kT + t;
-  const int64_t P = (int64_t)nx * ny;
+  const int32_t z0 = (bid / nps) * zt, z1 = min(z0 + zt, nz);
+  const int32_t rl = (bid % nps) * kT + t;  // the row's offset within its plane
+  const bool in = rl < P;
   const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   double v[7];
 #pragma unroll
   for (int e = 0; e < 7; ++e) v[e] = dval[e];
-  const int64_t rl = i + (int64_t)yl * nx;  // the row's offset within its plane
-  const bool hs = yl > 0, hn = yl < ny - 1, hl = t == 0 && i > 0, hr = t == kT - 1 && i + 1 < nx;
-  double xm = z0 > 0 ? x[rl + (z0 - 1) * P] : 0.0;
-  double xc = x[rl + z0 * P];
+  const bool hs = in && rl >= nx, hn = in && rl + nx < P, hl = t == 0 && rl > 0, hr = t == kT - 1 && rl + 1 < P;
+  double xm = in && z0 > 0 ? x[rl + (int64_t)(z0 - 1) * P] : 0.0;
+  double xc = in ? x[rl + (int64_t)z0 * P] : 0.0;
   for (int32_t z = z0; z < z1; ++z) {
-    const int64_t r = rl + z * P;
-    const u32x2 cw = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r);
-    const double xp = z + 1 < nz ? x[r + P] : 0.0;
+    const int64_t r = rl + (int64_t)z * P;
+    const u32x2 cw = in ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r) : u32x2{~0u, ~0u};
+    const double xp = in && z + 1 < nz ? x[r + P] : 0.0;
     const double xs = hs ? x[r - nx] : 0.0;
     const double xn = hn ? x[r + nx] : 0.0;
     const double el = hl ? x[r - 1] : 0.0;
@@ -1402,8 +1402,10 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
 #pragma unroll
     for (int e = 0; e < 7; ++e)
       if (m & (1u << e)) s = s + v[e] * (MODE == MSK_SPMV_SCALED ? xq[e] * sc : xq[e]);
-    if (MODE == MSK_SPMV_SCALED && vout) st_pol<NTY>(vout + r, xc * sc);
-    st_pol<NTY>(y + r, MODE == MSK_SPMV_RESID ? b[r] - s : s);
+    if (in) {
+      if (MODE == MSK_SPMV_SCALED && vout) st_pol<NTY>(vout + r, xc * sc);
+      st_pol<NTY>(y + r, MODE == MSK_SPMV_RESID ? b[r] - s : s);
+    }
     xm = xc;
     xc = xp;
   }
@@ -1545,12 +1547,15 @@ using namespace msk;
 #if MSK_IN(MSK_PART_MISC)
 __attribute__((visibility("hidden"))) int msk_tuning_flags = 0;
 __attribute__((visibility("hidden"))) int msk_spmv_gb_override = 0;  // XCD group size override (0: auto)
+__attribute__((visibility("hidden"))) int msk_march_z_override = 0;  // z-march planes per workgroup (0: auto)
 extern "C" void msk_set_tuning(int flags) { msk_tuning_flags = flags; }
 extern "C" int msk_get_tuning(void) { return msk_tuning_flags; }
 extern "C" void msk_set_spmv_group(int gb) { msk_spmv_gb_override = gb; }
+extern "C" void msk_set_march_z(int z) { msk_march_z_override = z; }
 #else
 extern __attribute__((visibility("hidden"))) int msk_tuning_flags;
 extern __attribute__((visibility("hidden"))) int msk_spmv_gb_override;
+extern __attribute__((visibility("hidden"))) int msk_march_z_override;
 #endif
 
 [[maybe_unused]] static inline XcdMap xcd_map(int32_t nrows, int64_t plane) {
@@ -1803,34 +1808,52 @@ static void launch_ell(int mode, int32_t nrows, const uint8_t* code8, const int3
     launch_ell_pol<W, RPL, false>(mode, g, nrows, code8, ddelta, dval, ndict, x, b, y, sdev, vout, stop, xwin, s);
 }
 
+// DV SpMV flag pairs that name no kernel: an error on every DV path, whichever kernel the operator takes
+static bool dv_flags_bad() {
+  const int f = msk_tuning_flags;
+  return ((f & MSK_TUNE_ELL_XCD_ON) && (f & MSK_TUNE_ELL_XCD_OFF)) ||
+         ((f & MSK_TUNE_ELL_MARCH_NOXCD) && (f & MSK_TUNE_ELL_MARCH_OFF));
+}
+
 template <bool NTY>
 static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8,
                              const double* dval, const double* x, const double* b, double* y, const double* sdev,
-                             double* vout, const int* stop, int32_t xwin, hipStream_t s) {
-#define MSK_BM(M) k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, xwin)
+                             double* vout, const int* stop, int32_t zt, int32_t xwin, hipStream_t s) {
+#define MSK_BM(M) \
+  k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin)
   if (mode == MSK_SPMV_RESID) MSK_BM(MSK_SPMV_RESID);
   else if (mode == MSK_SPMV_SCALED) MSK_BM(MSK_SPMV_SCALED);
   else MSK_BM(MSK_SPMV_MULT);
 #undef MSK_BM
 }
 
+// Planes per workgroup: 16, halved while the grid would hold fewer than 2048 workgroups
+static int32_t march_z(int32_t nx, int32_t ny, int32_t nz) {
+  if (msk_march_z_override > 0) return msk_march_z_override;
+  const int64_t nps = ((int64_t)nx * ny + kT - 1) / kT;
+  int32_t z = 16;
+  while (z > 1 && nps * ((nz + z - 1) / z) < 2048) z /= 2;
+  return z;
+}
+
 extern "C" int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz) {
   const int f = msk_tuning_flags;
-  if (nx <= 0 || ny <= 0 || nz <= 0 || nx % kT) return 0;
+  if (nx <= 0 || ny <= 0 || nz <= 0) return 0;
   return !(f & MSK_TUNE_ELL_MARCH_OFF);
 }
 
 extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8, const double* dval,
                                   const double* x, const double* b, double* y, int mode, const double* sdev,
                                   double* vout, const int* stop, hipStream_t s) {
-  if (nx <= 0 || ny <= 0 || nz <= 0 || nx % kT) return (int)hipErrorInvalidValue;
-  const int64_t g = (int64_t)(nx / kT) * ny * ((nz + kMarchZ - 1) / kMarchZ);
+  if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad()) return (int)hipErrorInvalidValue;
+  const int32_t zt = march_z(nx, ny, nz);
+  const int64_t g = (((int64_t)nx * ny + kT - 1) / kT) * ((nz + zt - 1) / zt);
   if (g > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
   const int32_t xwin = (msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) ? 0 : 32;
   if (!(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y))
-    launch_box_march<true>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, xwin, s);
+    launch_box_march<true>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s);
   else
-    launch_box_march<false>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, xwin, s);
+    launch_box_march<false>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s);
   return (int)hipGetLastError();
 }
 
@@ -1840,9 +1863,7 @@ extern "C" int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* 
                            const int* stop, int64_t plane, hipStream_t s) {
   if (nrows <= 0) return 0;
   if (max_block < 0 || ndict < 0 || ndict > 256) return (int)hipErrorInvalidValue;
-  if ((msk_tuning_flags & MSK_TUNE_ELL_XCD_ON) && (msk_tuning_flags & MSK_TUNE_ELL_XCD_OFF)) return (int)hipErrorInvalidValue;
-  if ((msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) && (msk_tuning_flags & MSK_TUNE_ELL_MARCH_OFF))
-    return (int)hipErrorInvalidValue;
+  if (dv_flags_bad()) return (int)hipErrorInvalidValue;
   if (ell_w) {
     if (ndict > 255) return (int)hipErrorInvalidValue;
     const int rpl = (msk_tuning_flags & MSK_TUNE_DV_RPL1) ? 1 : (msk_tuning_flags & MSK_TUNE_DV_RPL2) ? 2 : (ell_w == 16 ? 2 : 4);

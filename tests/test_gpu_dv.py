@@ -304,13 +304,14 @@ MARCH_OFF, MARCH_NOXCD = 268435456, 536870912
 
 @pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF])
 @pytest.mark.parametrize("shape", [(256, 16, 40), (512, 3, 17), (256, 1, 1), (256, 5, 16), (768, 2, 33),
-                                   (256, 40, 7), (256, 100, 40)])
+                                   (256, 40, 7), (256, 100, 40), (37, 11, 9), (64, 64, 64), (100, 30, 20),
+                                   (300, 7, 5), (1, 1, 9), (16, 16, 1), (2, 3, 50), (129, 2, 3)])
 @pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 0.3)])
 def test_box_march_bitwise(ctx, oracle, flags, shape, peclet):
-    """The z-march SpMV of box stencils (the default wherever nx % 256 == 0; MSK_TUNE_ELL_MARCH_NOXCD: identity
-    workgroup order; MSK_TUNE_ELL_MARCH_OFF: the row-parallel ELL kernel): whole and ragged z tiles (16 planes per
-    workgroup), one and several y lines, one and several 256-wide x segments, full XCD runs of 32 workgroups and a
-    ragged tail.  MatMult and MatResidual equal the oracle; GMRES -- the scaled MatMult with its stop flag -- equals
+    """The z-march SpMV of box stencils (the default for 3D boxes; MSK_TUNE_ELL_MARCH_NOXCD: identity workgroup
+    order; MSK_TUNE_ELL_MARCH_OFF: the row-parallel ELL kernel): whole and ragged z tiles (16 planes per workgroup),
+    one and several y lines, one and several 256-wide x segments, segments spanning several lines (nx < 256 or not
+    a multiple of 256) and a ragged last segment per plane, full XCD runs of 32 workgroups and a ragged tail.  MatMult and MatResidual equal the oracle; GMRES -- the scaled MatMult with its stop flag -- equals
     the oracle's DBR GMRES bit for bit."""
     from test_gpu_kernels import tuning
     nx, ny, nz = shape

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--tunings", default="0")
     ap.add_argument("--groups", default="0", help="SpMV XCD group sizes to sweep (0 = auto)")
+    ap.add_argument("--march-z", default="0", help="z-march planes per workgroup to sweep (0 = auto)")
     ap.add_argument("--kernels", default="spmv,mdot,maxpy")
     ap.add_argument("--storage", default="csr", choices=["csr", "dv"], help="SpMV entry storage")
     args = ap.parse_args()
@@ -39,6 +40,9 @@ def main():
     L.msk_set_tuning.restype = None
     L.msk_set_spmv_group.argtypes = [ctypes.c_int]
     L.msk_set_spmv_group.restype = None
+    L.msk_set_march_z.argtypes = [ctypes.c_int]
+    L.msk_set_march_z.restype = None
+    zs = [int(z) for z in args.march_z.split(",")]
     kernels = args.kernels.split(",")
     tunings = [int(t) for t in args.tunings.split(",")]
     groups = [int(g) for g in args.groups.split(",")]
@@ -80,14 +84,18 @@ def main():
             L.msk_set_tuning(t)
             for g in (groups if "spmv" in kernels else [0]):
                 L.msk_set_spmv_group(g)
-                if "spmv" in kernels:
-                    gb, us = timed(lambda: A.mult(w, y), "spmv")
-                    res.setdefault(f"spmv/t{t}/g{g}", []).append((gb, us))
-                    ya = y.get_array()
-                    if y_ref is None:
-                        y_ref = ya
-                    elif not np.array_equal(ya, y_ref):
-                        mismatch.append(f"spmv/t{t}/g{g}")
+                for z in (zs if "spmv" in kernels else [0]):
+                    L.msk_set_march_z(z)
+                    if "spmv" in kernels:
+                        key = f"spmv/t{t}/g{g}" + (f"/z{z}" if len(zs) > 1 else "")
+                        gb, us = timed(lambda: A.mult(w, y), "spmv")
+                        res.setdefault(key, []).append((gb, us))
+                        ya = y.get_array()
+                        if y_ref is None:
+                            y_ref = ya
+                        elif not np.array_equal(ya, y_ref):
+                            mismatch.append(key)
+                L.msk_set_march_z(0)
             L.msk_set_spmv_group(0)
             if "mdot" in kernels:
                 for k in (1, 2, 4, 8, 12, 16, 20, 30):
