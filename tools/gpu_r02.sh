@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 GPU session: the whole -m gpu suite, smoke, the default bench, a
+# Round-2 GPU session (reference profiles s3..s8): the whole -m gpu suite, smoke, the default bench, a
 # kernel-trace stats profile of the bench and the two PMC traffic passes.
 # Each GPU step has its own time limit; steps are chained with && so the
 # script stops at the first failure.

@@ -72,7 +72,7 @@ def main():
           f"(bench.py's figure), PMC {tr['hbm_bytes_per_launch'] / 1e9:.4f}.",
           (f"SpMV ({b['config'].get('matrix_storage', 'csr')} storage; GMRES's scaled form reads T once and writes "
            f"VV(it+1)): algorithmic {tr['classes']['spmv']['alg_bytes_per_launch'] / 1e9:.4f} GB/launch, PMC "
-           f"{tr['classes']['spmv']['hbm_over_alg']:.2f}x (x gathers re-read through the MALL)."
+           f"{tr['classes']['spmv']['hbm_over_alg']:.2f}x (x rows read more than once: the z-march reads x(z+1) and the y-+1 lines, which miss L2 at the edges of an XCD run)."
            if tr['classes'].get('spmv', {}).get('alg_bytes_per_launch') else ""), "",
           "Other directories: `smsm/` (SMSM-global), `convdiff/`, `async/` (transports and async drivers), "
           "`configs/` (BASELINE configurations end to end), `spmv_ab/`, `skew_ab/`, `dv/`, `opfuse/`, `graphs/`, "
