@@ -90,6 +90,10 @@ int msp_ctx_destroy(msp_ctx **ctx);
 int msp_ctx_synchronize(msp_ctx *ctx);
 int msp_get_device_count(int *count);
 const char *msp_get_last_error(void);
+/* SHA-256 (hex) of the library sources this build was compiled from (csrc/Makefile
+ * DIGEST_SRCS): lets a host check that the loaded .so matches its source tree.
+ * No reference counterpart (build identity only). */
+const char *msp_build_source_digest(void);
 /* Per-kernel-class HIP-event timing (used by bench.py; off by default).
  * enable = 0: off; 1: every logical kernel; N > 1: one in N of each class
  * (the event records between kernels cost ~2 % of a GMRES step when every

@@ -196,8 +196,30 @@ def load() -> C.CDLL:
         f.restype = C.c_int
     L.msp_get_last_error.argtypes = []
     L.msp_get_last_error.restype = C.c_char_p
+    L.msp_build_source_digest.argtypes = []
+    L.msp_build_source_digest.restype = C.c_char_p
     _lib = L
     return L
+
+
+def source_digest() -> str:
+    """SHA-256 of the library sources in this tree, hashed as csrc/Makefile does (DIGEST_SRCS: *.hip *.c *.h
+    *.hpp, Makefile and include/msplit.h, in sorted path order, concatenated)."""
+    import glob
+    import hashlib
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    names = [os.path.basename(f) for pat in ("*.hip", "*.c", "*.h", "*.hpp") for f in glob.glob(os.path.join(csrc, pat))]
+    names += ["Makefile", "../../include/msplit.h"]
+    h = hashlib.sha256()
+    for n in sorted(set(names)):
+        with open(os.path.join(csrc, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def build_digest() -> str:
+    """The digest libmsplit_hip.so was built with (msp_build_source_digest)."""
+    return load().msp_build_source_digest().decode()
 
 
 def check(rc: int):

@@ -22,7 +22,14 @@ def test_library_loads_and_exports_every_header_symbol():
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert set(syms) <= exported, sorted(set(syms) - exported)
     # every header symbol has a binding signature
-    assert set(syms) == set(_lib._SIGS) | {"msp_get_last_error"}
+    assert set(syms) == set(_lib._SIGS) | {"msp_get_last_error", "msp_build_source_digest"}
+
+
+def test_library_built_from_this_tree():
+    """The .so in the tree was compiled from the sources in the tree (csrc/Makefile's digest of them), so every
+    GPU result is evidence for these sources and not for a stale build."""
+    assert _lib.build_digest() == _lib.source_digest(), \
+        "libmsplit_hip.so is stale: rebuild with `python -c 'import __graft_entry__ as g; g.build()'`"
 
 
 def test_library_is_gfx950_code():
