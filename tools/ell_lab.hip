@@ -739,11 +739,19 @@ __global__ __launch_bounds__(kT) void k_zm(int nx, int ny, int nz, const uint8_t
 template <int Z>
 __global__ __launch_bounds__(kT) void k_zmp(int nx, int ny, int nz, const uint8_t* __restrict__ code8,
                                             const double* __restrict__ dval, const double* __restrict__ x,
-                                            double* __restrict__ y) {
+                                            double* __restrict__ y, int xwin = 0) {
   __shared__ double sx[2][kT + 2];
   const int t = threadIdx.x;
   const int nseg = nx / kT;
-  const int seg = (int)(blockIdx.x % nseg), yl = (int)((blockIdx.x / nseg) % ny), zt = (int)(blockIdx.x / (nseg * ny));
+  int bid = (int)blockIdx.x;
+  if (xwin > 0) {
+    const int span = 8 * xwin, full = (int)(gridDim.x / (unsigned)span) * span;
+    if (bid < full) {
+      const int w = bid / span, rem = bid - w * span;
+      bid = w * span + (rem & 7) * xwin + (rem >> 3);
+    }
+  }
+  const int seg = bid % nseg, yl = (bid / nseg) % ny, zt = bid / (nseg * ny);
   const int z0 = zt * Z, z1 = min(z0 + Z, nz);
   const int i = seg * kT + t;
   const int64_t P = (int64_t)nx * ny;
@@ -799,6 +807,88 @@ __global__ __launch_bounds__(kT) void k_zmp(int nx, int ny, int nz, const uint8_
     xp = xpN;
     el = elN;
     er = erN;
+  }
+}
+
+// --- zt: z-march over a tile of L y lines (256-wide x segment): the tile's lines in LDS,
+// so x(y-+1) of interior lines come from LDS and only the two halo lines are loaded.
+template <int L, int Z>
+__global__ __launch_bounds__(kT) void k_zt(int nx, int ny, int nz, const uint8_t* __restrict__ code8,
+                                           const double* __restrict__ dval, const double* __restrict__ x,
+                                           double* __restrict__ y, int xwin) {
+  __shared__ double sx[L + 2][kT + 2];
+  const int t = threadIdx.x;
+  const int nseg = nx / kT, nyt = (ny + L - 1) / L;
+  int bid = (int)blockIdx.x;
+  if (xwin > 0) {
+    const int span = 8 * xwin, full = (int)(gridDim.x / (unsigned)span) * span;
+    if (bid < full) {
+      const int w = bid / span, rem = bid - w * span;
+      bid = w * span + (rem & 7) * xwin + (rem >> 3);
+    }
+  }
+  const int seg = bid % nseg, yt = (bid / nseg) % nyt, zt = bid / (nseg * nyt);
+  const int y0 = yt * L, z0 = zt * Z, z1 = min(z0 + Z, nz);
+  const int i = seg * kT + t;
+  const int64_t P = (int64_t)nx * ny;
+  double v[7];
+#pragma unroll
+  for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  double xm[L], xc[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const bool ok = y0 + l < ny;
+    const int64_t rl = i + (int64_t)(y0 + l) * nx;
+    xm[l] = ok && z0 > 0 ? x[rl + (z0 - 1) * P] : 0.0;
+    xc[l] = ok ? x[rl + z0 * P] : 0.0;
+  }
+  const bool hs = y0 > 0, hn = y0 + L < ny;
+  for (int z = z0; z < z1; ++z) {
+    u32x2 cw[L];
+    double xp[L], el[L], er[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const bool ok = y0 + l < ny;
+      const int64_t r = i + (int64_t)(y0 + l) * nx + z * P;
+      cw[l] = ok ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r) : u32x2{~0u, ~0u};
+      xp[l] = ok && z + 1 < nz ? x[r + P] : 0.0;
+      el[l] = ok && t == 0 && i > 0 ? x[r - 1] : 0.0;
+      er[l] = ok && t == kT - 1 && i + 1 < nx ? x[r + 1] : 0.0;
+    }
+    const int64_t rb = i + (int64_t)y0 * nx + z * P;
+    const double hsv = hs ? x[rb - nx] : 0.0;
+    const double hnv = hn ? x[rb + (int64_t)L * nx] : 0.0;
+    __syncthreads();
+    sx[0][t + 1] = hsv;
+    sx[L + 1][t + 1] = hnv;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      sx[l + 1][t + 1] = xc[l];
+      if (t == 0) sx[l + 1][0] = el[l];
+      if (t == kT - 1) sx[l + 1][kT + 1] = er[l];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      if (y0 + l >= ny) continue;
+      uint32_t m = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int c = cbyte(cw[l], q);
+        if (c != 255) m |= 1u << c;
+      }
+      const double xq[7] = {xm[l], sx[l][t + 1], sx[l + 1][t], xc[l], sx[l + 1][t + 2], sx[l + 2][t + 1], xp[l]};
+      double s = 0.0;
+#pragma unroll
+      for (int e = 0; e < 7; ++e)
+        if (m & (1u << e)) s = s + v[e] * xq[e];
+      st_nt(y + i + (int64_t)(y0 + l) * nx + z * P, s);
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      xm[l] = xc[l];
+      xc[l] = xp[l];
+    }
   }
 }
 
@@ -909,17 +999,25 @@ int main(int argc, char** argv) {
 
     {
       const int nseg = n / kT;
-      for (int Z : {8, 16}) {
+      for (int Z : {16}) {
         const unsigned gz = (unsigned)(nseg * n * ((n + Z - 1) / Z));
-        for (int xw : {0, 8, 32, 128}) {
+        for (int xw : {32}) {
           char nm[32];
           snprintf(nm, sizeof(nm), "zm%d_x%d", Z, xw);
           if (Z == 8) run(nm, [&] { k_zm<8><<<gz, kT>>>(n, n, n, code8, dval, x, y, xw); }, true);
           if (Z == 16) run(nm, [&] { k_zm<16><<<gz, kT>>>(n, n, n, code8, dval, x, y, xw); }, true);
         }
       }
-      const unsigned gz = (unsigned)(nseg * n * ((n + 31) / 32));
-      run("zmp32", [&] { k_zmp<32><<<gz, kT>>>(n, n, n, code8, dval, x, y); }, true);
+      for (int Lq : {2, 4, 8}) {
+        const unsigned gz = (unsigned)(nseg * ((n + Lq - 1) / Lq) * ((n + 15) / 16));
+        for (int xw : {8, 32}) {
+          char nm[32];
+          snprintf(nm, sizeof(nm), "zt%d_x%d", Lq, xw);
+          if (Lq == 2) run(nm, [&] { k_zt<2, 16><<<gz, kT>>>(n, n, n, code8, dval, x, y, xw); }, true);
+          if (Lq == 4) run(nm, [&] { k_zt<4, 16><<<gz, kT>>>(n, n, n, code8, dval, x, y, xw); }, true);
+          if (Lq == 8) run(nm, [&] { k_zt<8, 16><<<gz, kT>>>(n, n, n, code8, dval, x, y, xw); }, true);
+        }
+      }
     }
     run("dpair2", [&] { k_dpair<2, 8><<<g4, kT>>>((int32_t)N, code8, ddelta, dval, 7, x, y); }, true);
 
