@@ -86,6 +86,9 @@ typedef struct msp_abcast msp_abcast;
  * per-rank PETSc/MPI setup: PetscInitialize + PetscSubcommCreate
  * (synchronous-multisplitting.c:40, :66-73) -- npb = 1, one block per GPU. */
 int msp_ctx_create(int device, void *stream, msp_ctx **ctx);
+/* msp_ctx_destroy drops the caller's reference: every object made on the context (Vec, Mat,
+ * dense block, KSP, LSQR, comm, device slots) holds one of its own, so objects may be destroyed
+ * before or after their context, in any order; the context is freed with the last of them. */
 int msp_ctx_destroy(msp_ctx **ctx);
 int msp_ctx_synchronize(msp_ctx *ctx);
 int msp_get_device_count(int *count);

@@ -179,6 +179,7 @@ int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   }
   b->dbufs = (double *)p;
   b->dctx = ctx;
+  mspi_ctx_retain(ctx);
   e->pid = (int32_t)getpid();
   e->rawptr = (uint64_t)(uintptr_t)p;
   atomic_store_explicit(&e->ready, 1, memory_order_release);
@@ -228,8 +229,10 @@ int msp_abcast_destroy(msp_abcast **pb) {
   munmap(b->base, b->bytes);
   if (b->owner) shm_unlink(b->name);
   free(b->seen);
+  msp_ctx *c = b->dctx;
   free(b);
   *pb = NULL;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 

@@ -202,6 +202,7 @@ int msp_amsg_enable_device(msp_amsg *m, msp_ctx *ctx) {
   }
   m->dslots = (double *)p;
   m->dctx = ctx;
+  mspi_ctx_retain(ctx);
   e->pid = (int32_t)getpid();
   e->rawptr = (uint64_t)(uintptr_t)p;
   atomic_store_explicit(&e->ready, 1, memory_order_release);
@@ -252,8 +253,10 @@ int msp_amsg_destroy(msp_amsg **pm) {
   munmap(m->base, m->bytes);
   if (m->owner) shm_unlink(m->name);
   free(m->seen);
+  msp_ctx *c = m->dctx;
   free(m);
   *pm = NULL;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 

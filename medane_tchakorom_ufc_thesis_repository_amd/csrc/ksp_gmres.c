@@ -99,6 +99,7 @@ int msp_ksp_create(msp_ctx *ctx, msp_ksp **out) {
     return MSP_ERR_MEM;
   }
   k->ctx = ctx;
+  mspi_ctx_retain(ctx);
   msp_ksp_get_default_opts(&k->o);
   *out = k;
   return MSP_SUCCESS;
@@ -130,10 +131,12 @@ static void ksp_free_work(msp_ksp *k) {
 
 int msp_ksp_destroy(msp_ksp **pk) {
   if (!pk || !*pk) return MSP_SUCCESS;
-  msp_ctx_synchronize((*pk)->ctx);
+  msp_ctx *c = (*pk)->ctx;
+  msp_ctx_synchronize(c);
   ksp_free_work(*pk);
   free(*pk);
   *pk = NULL;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 

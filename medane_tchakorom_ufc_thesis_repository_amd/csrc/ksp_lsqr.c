@@ -72,6 +72,7 @@ int msp_lsqr_create(msp_ctx *ctx, msp_lsqr **out) {
   msp_lsqr *l = (msp_lsqr *)calloc(1, sizeof(msp_lsqr));
   if (!l) return err(MSP_ERR_MEM, "LSQR allocation failed");
   l->ctx = ctx;
+  mspi_ctx_retain(ctx);
   msp_lsqr_get_default_opts(&l->o);
   *out = l;
   return MSP_SUCCESS;
@@ -101,11 +102,13 @@ static void lsqr_free_work(msp_lsqr *l) {
 
 int msp_lsqr_destroy(msp_lsqr **pl) {
   if (!pl || !*pl) return MSP_SUCCESS;
-  msp_ctx_synchronize((*pl)->ctx);
+  msp_ctx *c = (*pl)->ctx;
+  msp_ctx_synchronize(c);
   lsqr_free_work(*pl);
   free((*pl)->R);
   free(*pl);
   *pl = NULL;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 

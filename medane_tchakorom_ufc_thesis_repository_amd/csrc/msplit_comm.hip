@@ -102,6 +102,7 @@ extern "C" int msp_comm_create_rccl(msp_ctx* c, int32_t nranks, int32_t rank, co
   NCCLCHK(rccl().comm_init_rank(&nc, nranks, u, rank));
   msp_comm* m = new msp_comm();
   m->ctx = c;
+  mspi_ctx_retain(c);
   m->kind = COMM_RCCL;
   m->nranks = nranks;
   m->rank = rank;
@@ -116,6 +117,7 @@ extern "C" int msp_comm_create_host(msp_ctx* c, int32_t nranks, int32_t rank, ms
   ARGCHK(nranks >= 1 && rank >= 0 && rank < nranks, MSP_ERR_ARG_OUTOFRANGE, "rank %d of %d", rank, nranks);
   msp_comm* m = new msp_comm();
   m->ctx = c;
+  mspi_ctx_retain(c);
   m->kind = COMM_HOST;
   m->nranks = nranks;
   m->rank = rank;
@@ -132,8 +134,10 @@ extern "C" int msp_comm_destroy(msp_comm** pm) {
   if (m->nccl) (void)rccl().comm_destroy(m->nccl);
   if (m->hsend) (void)hipHostFree(m->hsend);
   if (m->hrecv) (void)hipHostFree(m->hrecv);
+  msp_ctx* c = m->ctx;
   delete m;
   *pm = nullptr;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 

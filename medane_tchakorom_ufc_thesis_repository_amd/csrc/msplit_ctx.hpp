@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <atomic>
 #include <vector>
 
 #include "msplit.h"
@@ -47,6 +48,9 @@ struct TimedRec {
 };
 
 struct msp_ctx {
+  // msp_ctx_destroy drops the caller's reference; every object made on the context holds one more
+  // (mspi_ctx_retain / mspi_ctx_release), so objects may be destroyed after their context in any order
+  std::atomic<int> refs{1};
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;

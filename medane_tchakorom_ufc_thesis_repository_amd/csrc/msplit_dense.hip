@@ -451,12 +451,14 @@ extern "C" int msp_dense_create(msp_ctx* c, int64_t nrows, int32_t ncols, msp_de
   ARGCHK(nrows >= 0 && ncols >= 1, MSP_ERR_ARG_SIZ, "dense block %lld x %d", (long long)nrows, ncols);
   msp_dense* A = new msp_dense();
   A->ctx = c;
+  mspi_ctx_retain(c);
   A->nrows = nrows;
   A->ncols = ncols;
   A->lda = lda_for(nrows);
   const size_t bytes = (size_t)(A->lda * ncols + 512) * sizeof(double);
   if (hipMalloc((void**)&A->d, bytes) != hipSuccess) {
     delete A;
+    mspi_ctx_release(c);
     mspi_set_error(MSP_ERR_MEM, "hipMalloc of a %lld x %d dense block failed", (long long)nrows, ncols);
     return MSP_ERR_MEM;
   }
@@ -470,8 +472,10 @@ extern "C" int msp_dense_destroy(msp_dense** pA) {
   msp_dense* A = *pA;
   if (A->ctx && A->ctx->stream) (void)hipStreamSynchronize(A->ctx->stream);
   if (A->d) (void)hipFree(A->d);
+  msp_ctx* c = A->ctx;
   delete A;
   *pA = nullptr;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 

@@ -37,6 +37,9 @@ int mspi_free(msp_ctx *ctx, void *p);
 int mspi_host_malloc(void **p, size_t bytes);
 int mspi_host_free(void *p);
 int mspi_set_device(msp_ctx *ctx);
+/* reference counting of the context by the objects made on it (msp_ctx_destroy releases the caller's) */
+void mspi_ctx_retain(msp_ctx *ctx);
+void mspi_ctx_release(msp_ctx *ctx);
 /* async device->host copy followed by a stream synchronise */
 int mspi_d2h_sync(msp_ctx *ctx, void *host, const void *dev, size_t bytes);
 

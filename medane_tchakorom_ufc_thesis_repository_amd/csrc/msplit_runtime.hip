@@ -77,9 +77,7 @@ extern "C" int msp_ctx_create(int device, void* stream, msp_ctx** out) {
   return MSP_SUCCESS;
 }
 
-extern "C" int msp_ctx_destroy(msp_ctx** pc) {
-  if (!pc || !*pc) return MSP_SUCCESS;
-  msp_ctx* c = *pc;
+static void ctx_free(msp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->partial) (void)hipFree(c->partial);
@@ -87,7 +85,21 @@ extern "C" int msp_ctx_destroy(msp_ctx** pc) {
   if (c->hscratch) (void)hipHostFree(c->hscratch);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+extern "C" void mspi_ctx_retain(msp_ctx* c) {
+  if (c) c->refs.fetch_add(1);
+}
+extern "C" void mspi_ctx_release(msp_ctx* c) {
+  if (c && c->refs.fetch_sub(1) == 1) ctx_free(c);
+}
+
+// The context is freed when the caller's reference and those of every object made on it are gone.
+extern "C" int msp_ctx_destroy(msp_ctx** pc) {
+  if (!pc || !*pc) return MSP_SUCCESS;
+  msp_ctx* c = *pc;
   *pc = nullptr;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 
@@ -604,6 +616,7 @@ extern "C" int msp_mat_create_csr(msp_ctx* c, int32_t nrows, int32_t ncols, cons
   ARGCHK(nnz == 0 || (col && val), MSP_ERR_ARG_NULL, "col/val NULL with nnz=%lld", (long long)nnz);
   msp_mat* A = new msp_mat();
   A->ctx = c;
+  mspi_ctx_retain(c);
   A->nrows = nrows;
   A->ncols = ncols;
   A->nnz = nnz;
@@ -650,6 +663,7 @@ extern "C" int msp_mat_create_csr_rows(msp_ctx* c, int32_t nrows, int32_t ncols,
   if (rc) return rc;
   msp_mat* A = new msp_mat();
   A->ctx = c;
+  mspi_ctx_retain(c);
   A->nrows = nrows;
   A->ncols = ncols;
   A->nnz = nnz;
@@ -713,6 +727,7 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
          "box of %lld rows exceeds 32-bit PetscInt indexing", (long long)nrows);
   msp_mat* A = new msp_mat();
   A->ctx = c;
+  mspi_ctx_retain(c);
   A->nrows = (int32_t)nrows;
   A->ncols = (int32_t)ncols;
   // exact nnz: deg*N minus missing neighbours on each face, plus the halo couplings
@@ -771,6 +786,7 @@ extern "C" int msp_mat_create_box_matfree(msp_ctx* c, int dim, int32_t nx, int32
   ARGCHK(ny <= 65535 && nz <= 65535, MSP_ERR_ARG_SIZ, "matrix-free box: at most 65535 lines / planes (grid y, z)");
   msp_mat* A = new msp_mat();
   A->ctx = c;
+  mspi_ctx_retain(c);
   A->matfree = true;
   A->dim = dim;
   A->bx = nx;
@@ -809,8 +825,10 @@ extern "C" int msp_mat_destroy(msp_mat** pA) {
   if (A->val) (void)hipFree(A->val);
   if (A->row_ids) (void)hipFree(A->row_ids);
   dv_free(A);
+  msp_ctx* c = A->ctx;
   delete A;
   *pA = nullptr;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 
@@ -1157,12 +1175,14 @@ extern "C" int msp_vec_create(msp_ctx* c, int64_t n, msp_vec** out) {
   ARGCHK(n >= 0, MSP_ERR_ARG_SIZ, "negative vector size %lld", (long long)n);
   msp_vec* v = new msp_vec();
   v->ctx = c;
+  mspi_ctx_retain(c);
   v->n = n;
   v->owned = 1;
   // pad to 512 doubles so every vector is 4 KiB aligned and double2 loads stay in bounds
   const size_t bytes = (size_t)((n + 511) / 512 * 512 + 512) * sizeof(double);
   if (hipMalloc((void**)&v->d, bytes) != hipSuccess) {
     delete v;
+    mspi_ctx_release(c);
     mspi_set_error(MSP_ERR_MEM, "hipMalloc of a %lld-entry vector failed", (long long)n);
     return MSP_ERR_MEM;
   }
@@ -1177,6 +1197,7 @@ extern "C" int msp_vec_create_with_array(msp_ctx* c, int64_t n, double* dptr, ms
   ARGCHK(((uintptr_t)dptr & 15) == 0, MSP_ERR_ARG_WRONG, "device array must be 16-byte aligned");
   msp_vec* v = new msp_vec();
   v->ctx = c;
+  mspi_ctx_retain(c);
   v->n = n;
   v->d = dptr;
   v->owned = 0;
@@ -1191,8 +1212,10 @@ extern "C" int msp_vec_destroy(msp_vec** pv) {
     (void)hipStreamSynchronize(v->ctx->stream);
     (void)hipFree(v->d);
   }
+  msp_ctx* c = v->ctx;
   delete v;
   *pv = nullptr;
+  mspi_ctx_release(c);
   return MSP_SUCCESS;
 }
 
