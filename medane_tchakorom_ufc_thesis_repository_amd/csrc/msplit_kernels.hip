@@ -1351,8 +1351,8 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
 // row's codes name it.  xwin > 0: XCD x takes runs of xwin consecutive workgroups
 // (ell_block), i.e. neighbouring segments of one z tile, so the x(y-+1) loads of one
 // workgroup are the x(z) rows of its neighbours and meet in that XCD's L2.  With
-// xwin = 32: 256^3 92 -> 74 us, 512^3 821 -> 628 us; in identity order 99 / 697 us
-// (tools/ell_lab.hip, profiles/r02/ell_lab/).  The products are added in CSR order
+// xwin = 32 (tools/ell_lab.hip, back to back): 256^3 92 -> 74 us, 512^3 821 -> 628 us; in identity
+// order 99 / 697 us (profiles/r02/ell_lab/).  Inside the GMRES step: 103 -> 82 us (rocprof).  The products are added in CSR order
 // from 0.0, the same terms as k_spmv_ell, so the result is bitwise identical.
 template <int MODE, bool NTY>
 __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, int32_t nz,
@@ -1408,6 +1408,93 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
     }
     xm = xc;
     xc = xp;
+  }
+}
+
+// The same march over tiles of L whole y lines (nx % 256 == 0): a workgroup owns a
+// 256-wide x segment of L consecutive lines; the tile's x(z) rows and the two halo line
+// segments (y0 - 1 and y0 + L) go to LDS each plane, so x(y-+1) of interior lines is
+// read from LDS and only 2 / L halo loads per row remain (against 2 for one line).
+// Lines past ny are idle (a ragged last tile).  Back to back: 256^3 74 us against 82 for one
+// line, 512^3 590 against 679 (profiles/r02/march/sizes4/); inside the GMRES step 82 against 85 us,
+// SMSM block 283 against 301 (march/lines_ab/).
+// Bitwise k_spmv_box_march (same terms, same order).
+template <int MODE, bool NTY, int L>
+__global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, int32_t nz,
+                                                       const uint8_t* __restrict__ code8,
+                                                       const double* __restrict__ dval, const double* __restrict__ x,
+                                                       const double* __restrict__ b, double* __restrict__ y,
+                                                       const double* __restrict__ sdev, double* __restrict__ vout,
+                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
+  __shared__ double sx[L + 2][kT + 2];
+  const int t = threadIdx.x;
+  const int32_t nseg = nx / kT, nyt = (ny + L - 1) / L;
+  const int32_t bid = ell_block(xwin);
+  const int32_t seg = bid % nseg, yt = (bid / nseg) % nyt, z0 = (bid / (nseg * nyt)) * zt;
+  const int32_t z1 = min(z0 + zt, nz), y0 = yt * L;
+  const int32_t i = seg * kT + t;
+  const int32_t P = nx * ny;  // nx * ny * nz <= INT32_MAX (checked by the launcher)
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  double v[7];
+#pragma unroll
+  for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  double xm[L], xc[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const bool ok = y0 + l < ny;
+    const int32_t rl = i + (y0 + l) * nx;
+    xm[l] = ok && z0 > 0 ? x[rl + (int64_t)(z0 - 1) * P] : 0.0;
+    xc[l] = ok ? x[rl + (int64_t)z0 * P] : 0.0;
+  }
+  const bool hs = y0 > 0, hn = y0 + L < ny, hl = t == 0 && i > 0, hr = t == kT - 1 && i + 1 < nx;
+  for (int32_t z = z0; z < z1; ++z) {
+    const int64_t zP = (int64_t)z * P;
+    u32x2 cw[L];
+    double xp[L], el[L], er[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const bool ok = y0 + l < ny;
+      const int64_t r = i + (int64_t)(y0 + l) * nx + zP;
+      cw[l] = ok ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r) : u32x2{~0u, ~0u};
+      xp[l] = ok && z + 1 < nz ? x[r + P] : 0.0;
+      el[l] = ok && hl ? x[r - 1] : 0.0;
+      er[l] = ok && hr ? x[r + 1] : 0.0;
+    }
+    const int64_t rb = i + (int64_t)y0 * nx + zP;
+    const double hsv = hs ? x[rb - nx] : 0.0;
+    const double hnv = hn ? x[rb + (int64_t)L * nx] : 0.0;
+    __syncthreads();  // the previous plane's reads of sx are done
+    sx[0][t + 1] = hsv;
+    sx[L + 1][t + 1] = hnv;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      sx[l + 1][t + 1] = xc[l];
+      if (t == 0) sx[l + 1][0] = el[l];
+      if (t == kT - 1) sx[l + 1][kT + 1] = er[l];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int c = EllWord<8>::byte(cw[l], q);
+        if (c != 255) m |= 1u << c;
+      }
+      const double xq[7] = {xm[l], sx[l][t + 1], sx[l + 1][t], xc[l], sx[l + 1][t + 2], sx[l + 2][t + 1], xp[l]};
+      double s = 0.0;
+#pragma unroll
+      for (int e = 0; e < 7; ++e)
+        if (m & (1u << e)) s = s + v[e] * (MODE == MSK_SPMV_SCALED ? xq[e] * sc : xq[e]);
+      if (y0 + l < ny) {
+        const int64_t r = i + (int64_t)(y0 + l) * nx + zP;
+        if (MODE == MSK_SPMV_SCALED && vout) st_pol<NTY>(vout + r, xc[l] * sc);
+        st_pol<NTY>(y + r, MODE == MSK_SPMV_RESID ? b[r] - s : s);
+      }
+      xm[l] = xc[l];
+      xc[l] = xp[l];
+    }
   }
 }
 
@@ -1548,14 +1635,17 @@ using namespace msk;
 __attribute__((visibility("hidden"))) int msk_tuning_flags = 0;
 __attribute__((visibility("hidden"))) int msk_spmv_gb_override = 0;  // XCD group size override (0: auto)
 __attribute__((visibility("hidden"))) int msk_march_z_override = 0;  // z-march planes per workgroup (0: auto)
+__attribute__((visibility("hidden"))) int msk_march_lines_override = 0;  // z-march tile: 1 row block, 4 lines (0: auto)
 extern "C" void msk_set_tuning(int flags) { msk_tuning_flags = flags; }
 extern "C" int msk_get_tuning(void) { return msk_tuning_flags; }
 extern "C" void msk_set_spmv_group(int gb) { msk_spmv_gb_override = gb; }
 extern "C" void msk_set_march_z(int z) { msk_march_z_override = z; }
+extern "C" void msk_set_march_lines(int l) { msk_march_lines_override = l; }
 #else
 extern __attribute__((visibility("hidden"))) int msk_tuning_flags;
 extern __attribute__((visibility("hidden"))) int msk_spmv_gb_override;
 extern __attribute__((visibility("hidden"))) int msk_march_z_override;
+extern __attribute__((visibility("hidden"))) int msk_march_lines_override;
 #endif
 
 [[maybe_unused]] static inline XcdMap xcd_map(int32_t nrows, int64_t plane) {
@@ -1815,25 +1905,44 @@ static bool dv_flags_bad() {
          ((f & MSK_TUNE_ELL_MARCH_NOXCD) && (f & MSK_TUNE_ELL_MARCH_OFF));
 }
 
-template <bool NTY>
+// L = 0: k_spmv_box_march (256 plane rows per workgroup); L = 4: k_spmv_box_lines
+template <bool NTY, int L>
 static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8,
                              const double* dval, const double* x, const double* b, double* y, const double* sdev,
                              double* vout, const int* stop, int32_t zt, int32_t xwin, hipStream_t s) {
-#define MSK_BM(M) \
-  k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin)
+#define MSK_BM(M)                                                                                                 \
+  do {                                                                                                            \
+    if constexpr (L == 0)                                                                                         \
+      k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin);    \
+    else                                                                                                          \
+      k_spmv_box_lines<M, NTY, L><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin); \
+  } while (0)
   if (mode == MSK_SPMV_RESID) MSK_BM(MSK_SPMV_RESID);
   else if (mode == MSK_SPMV_SCALED) MSK_BM(MSK_SPMV_SCALED);
   else MSK_BM(MSK_SPMV_MULT);
 #undef MSK_BM
 }
 
-// Planes per workgroup: 16, halved while the grid would hold fewer than 2048 workgroups
-static int32_t march_z(int32_t nx, int32_t ny, int32_t nz) {
-  if (msk_march_z_override > 0) return msk_march_z_override;
-  const int64_t nps = ((int64_t)nx * ny + kT - 1) / kT;
-  int32_t z = 16;
-  while (z > 1 && nps * ((nz + z - 1) / z) < 2048) z /= 2;
-  return z;
+// Kernel and shape: nx % 256 == 0 takes tiles of 4 lines (k_spmv_box_lines) when 16 planes per workgroup,
+// halved down to 1, give at least 1024 workgroups; otherwise k_spmv_box_march with 16 planes per workgroup,
+// halved while the grid would hold fewer than 2048.  msk_set_march_lines (1: the 256-row kernel; 4: lines)
+// and msk_set_march_z override the choice (A/B experiments, tests).
+static void march_shape(int32_t nx, int32_t ny, int32_t nz, int32_t* lines, int32_t* zt, int64_t* grid) {
+  const int32_t Lq = 4;
+  int32_t L = 1, z = 16;
+  if (nx % kT == 0 && msk_march_lines_override != 1) {
+    const int64_t tiles = (int64_t)(nx / kT) * ((ny + Lq - 1) / Lq);
+    while (z > 1 && tiles * ((nz + z - 1) / z) < 1024) z /= 2;
+    if (tiles * ((nz + z - 1) / z) >= 1024 || msk_march_lines_override == Lq) L = Lq;
+    else z = 16;
+  }
+  const int64_t tiles = L > 1 ? (int64_t)(nx / kT) * ((ny + L - 1) / L) : ((int64_t)nx * ny + kT - 1) / kT;
+  if (L == 1)
+    while (z > 1 && tiles * ((nz + z - 1) / z) < 2048) z /= 2;
+  if (msk_march_z_override > 0) z = msk_march_z_override;
+  *lines = L;
+  *zt = z;
+  *grid = tiles * ((nz + z - 1) / z);
 }
 
 extern "C" int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz) {
@@ -1846,14 +1955,25 @@ extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, const uint
                                   const double* x, const double* b, double* y, int mode, const double* sdev,
                                   double* vout, const int* stop, hipStream_t s) {
   if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad()) return (int)hipErrorInvalidValue;
-  const int32_t zt = march_z(nx, ny, nz);
-  const int64_t g = (((int64_t)nx * ny + kT - 1) / kT) * ((nz + zt - 1) / zt);
+  if (msk_march_lines_override != 0 && msk_march_lines_override != 1 && msk_march_lines_override != 4)
+    return (int)hipErrorInvalidValue;
+  if (msk_march_lines_override == 4 && nx % kT) return (int)hipErrorInvalidValue;
+  int32_t L, zt;
+  int64_t g;
+  march_shape(nx, ny, nz, &L, &zt, &g);
   if (g > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
   const int32_t xwin = (msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) ? 0 : 32;
-  if (!(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y))
-    launch_box_march<true>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s);
-  else
-    launch_box_march<false>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s);
+  const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
+#define MSK_BML(NT, LL) \
+  launch_box_march<NT, LL>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s)
+  if (L == 4) {
+    if (nty) MSK_BML(true, 4);
+    else MSK_BML(false, 4);
+  } else {
+    if (nty) MSK_BML(true, 0);
+    else MSK_BML(false, 0);
+  }
+#undef MSK_BML
   return (int)hipGetLastError();
 }
 

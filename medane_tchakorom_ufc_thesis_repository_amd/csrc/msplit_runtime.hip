@@ -54,6 +54,7 @@ extern "C" int msp_ctx_create(int device, void* stream, msp_ctx** out) {
   ARGCHK(device >= 0 && device < ndev, MSP_ERR_ARG_OUTOFRANGE, "device %d out of range [0,%d)", device, ndev);
   HIPCHK(hipSetDevice(device));
   if (const char* e = getenv("MSPLIT_TUNING")) msk_set_tuning(atoi(e));
+  if (const char* e = getenv("MSPLIT_MARCH_LINES")) msk_set_march_lines(atoi(e));  // A/B: 1 or 4 (0: auto)
   msp_ctx* c = new msp_ctx();
   c->device = device;
   if (const char* e = getenv("MSPLIT_REDUCTION")) c->reduce = (e[0] == 's' || e[0] == 'S') ? MSP_REDUCE_SEQ : MSP_REDUCE_DBR;

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--tunings", default="0")
     ap.add_argument("--groups", default="0", help="SpMV XCD group sizes to sweep (0 = auto)")
     ap.add_argument("--march-z", default="0", help="z-march planes per workgroup to sweep (0 = auto)")
+    ap.add_argument("--march-lines", default="0", help="z-march tiles to sweep (1 = 256 plane rows, 4 = 4 lines)")
     ap.add_argument("--kernels", default="spmv,mdot,maxpy")
     ap.add_argument("--storage", default="csr", choices=["csr", "dv"], help="SpMV entry storage")
     args = ap.parse_args()
@@ -42,7 +43,9 @@ def main():
     L.msk_set_spmv_group.restype = None
     L.msk_set_march_z.argtypes = [ctypes.c_int]
     L.msk_set_march_z.restype = None
-    zs = [int(z) for z in args.march_z.split(",")]
+    L.msk_set_march_lines.argtypes = [ctypes.c_int]
+    L.msk_set_march_lines.restype = None
+    zs = [(int(z), int(m)) for z in args.march_z.split(",") for m in args.march_lines.split(",")]
     kernels = args.kernels.split(",")
     tunings = [int(t) for t in args.tunings.split(",")]
     groups = [int(g) for g in args.groups.split(",")]
@@ -84,10 +87,11 @@ def main():
             L.msk_set_tuning(t)
             for g in (groups if "spmv" in kernels else [0]):
                 L.msk_set_spmv_group(g)
-                for z in (zs if "spmv" in kernels else [0]):
+                for z, ml in (zs if "spmv" in kernels else [(0, 0)]):
                     L.msk_set_march_z(z)
+                    L.msk_set_march_lines(ml)
                     if "spmv" in kernels:
-                        key = f"spmv/t{t}/g{g}" + (f"/z{z}" if len(zs) > 1 else "")
+                        key = f"spmv/t{t}/g{g}" + (f"/z{z}/l{ml}" if len(zs) > 1 else "")
                         gb, us = timed(lambda: A.mult(w, y), "spmv")
                         res.setdefault(key, []).append((gb, us))
                         ya = y.get_array()
@@ -96,6 +100,7 @@ def main():
                         elif not np.array_equal(ya, y_ref):
                             mismatch.append(key)
                 L.msk_set_march_z(0)
+                L.msk_set_march_lines(0)
             L.msk_set_spmv_group(0)
             if "mdot" in kernels:
                 for k in (1, 2, 4, 8, 12, 16, 20, 30):
