@@ -58,6 +58,8 @@ SPMV_NAMES = {"dv": "k_spmv_ell (MatMult/MatResidual, DV storage: one byte per e
               "csr": "k_spmv_lds8 (MatMult/MatResidual, CSR storage)",
               "matfree": "k_stencil_spmv (MatMult/MatResidual, matrix-free)"}
 MARCH_NAME = "k_spmv_box_march (MatMult/MatResidual, DV storage: one byte per entry; box stencil marched in z)"
+LINES_NAME = ("k_spmv_box_lines (MatMult/MatResidual, DV storage: one byte per entry; box stencil marched in z "
+              "over tiles of four y lines)")
 TUNE_ELL_MARCH_OFF = 268435456
 
 
@@ -65,7 +67,8 @@ def spmv_name(storage, nx):
     """The kernel the library picks for a box stencil's products (msk_box_march_pick)."""
     tune = int(os.environ.get("MSPLIT_TUNING", "0") or 0)
     if storage == "dv" and not tune & TUNE_ELL_MARCH_OFF:
-        return MARCH_NAME
+        lines = os.environ.get("MSPLIT_MARCH_LINES", "0")
+        return LINES_NAME if nx % 256 == 0 and lines != "1" else MARCH_NAME
     return SPMV_NAMES[storage]
 
 
