@@ -1339,6 +1339,25 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
   }
 }
 
+// The march kernels name neighbours e = 0..6 as (-P, -nx, -1, 0, +1, +nx, +P).  A 2D box
+// stencil (d2 = 1) is marched as a 3D box of nx x 1 x ny: its five codes (-nx, -1, 0, +1,
+// +nx) are neighbours 0, 2, 3, 4, 6 with P = nx.
+__device__ __forceinline__ int march_code(int c, int32_t d2) { return d2 ? c + (c >= 1) + (c >= 4) : c; }
+__device__ __forceinline__ void march_values(const double* __restrict__ dval, int32_t d2, double* v) {
+  if (d2) {
+    v[0] = dval[0];
+    v[1] = 0.0;
+    v[2] = dval[1];
+    v[3] = dval[2];
+    v[4] = dval[3];
+    v[5] = 0.0;
+    v[6] = dval[4];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  }
+}
+
 // The ELL SpMV of a 3D box stencil, marching in z.  The dictionary is the stencil's
 // seven pairs in column order (-P, -nx, -1, 0, +1, +nx, +P) -- the host guarantees it
 // (msp_mat_create_box_convdiff, lo = hi = 0) -- so code e always names neighbour e
@@ -1360,7 +1379,8 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
                                                        const double* __restrict__ dval, const double* __restrict__ x,
                                                        const double* __restrict__ b, double* __restrict__ y,
                                                        const double* __restrict__ sdev, double* __restrict__ vout,
-                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin) {
+                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin,
+                                                       int32_t d2) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   __shared__ double sx[kT + 2];
   const int t = threadIdx.x;
@@ -1372,8 +1392,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
   const bool in = rl < P;
   const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   double v[7];
-#pragma unroll
-  for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  march_values(dval, d2, v);
   const bool hs = in && rl >= nx, hn = in && rl + nx < P, hl = t == 0 && rl > 0, hr = t == kT - 1 && rl + 1 < P;
   double xm = in && z0 > 0 ? x[rl + (int64_t)(z0 - 1) * P] : 0.0;
   double xc = in ? x[rl + (int64_t)z0 * P] : 0.0;
@@ -1395,7 +1414,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int c = EllWord<8>::byte(cw, q);
-      if (c != 255) m |= 1u << c;
+      if (c != 255) m |= 1u << march_code(c, d2);
     }
     const double xq[7] = {xm, xs, xl, xc, xr, xn, xp};
     double s = 0.0;
@@ -1425,7 +1444,8 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
                                                        const double* __restrict__ dval, const double* __restrict__ x,
                                                        const double* __restrict__ b, double* __restrict__ y,
                                                        const double* __restrict__ sdev, double* __restrict__ vout,
-                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin) {
+                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin,
+                                                       int32_t d2) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   __shared__ double sx[L + 2][kT + 2];
   const int t = threadIdx.x;
@@ -1437,8 +1457,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
   const int32_t P = nx * ny;  // nx * ny * nz <= INT32_MAX (checked by the launcher)
   const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   double v[7];
-#pragma unroll
-  for (int e = 0; e < 7; ++e) v[e] = dval[e];
+  march_values(dval, d2, v);
   double xm[L], xc[L];
 #pragma unroll
   for (int l = 0; l < L; ++l) {
@@ -1480,7 +1499,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int c = EllWord<8>::byte(cw[l], q);
-        if (c != 255) m |= 1u << c;
+        if (c != 255) m |= 1u << march_code(c, d2);
       }
       const double xq[7] = {xm[l], sx[l][t + 1], sx[l + 1][t], xc[l], sx[l + 1][t + 2], sx[l + 2][t + 1], xp[l]};
       double s = 0.0;
@@ -1909,13 +1928,13 @@ static bool dv_flags_bad() {
 template <bool NTY, int L>
 static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8,
                              const double* dval, const double* x, const double* b, double* y, const double* sdev,
-                             double* vout, const int* stop, int32_t zt, int32_t xwin, hipStream_t s) {
+                             double* vout, const int* stop, int32_t zt, int32_t xwin, int32_t d2, hipStream_t s) {
 #define MSK_BM(M)                                                                                                 \
   do {                                                                                                            \
     if constexpr (L == 0)                                                                                         \
-      k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin);    \
+      k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, d2);    \
     else                                                                                                          \
-      k_spmv_box_lines<M, NTY, L><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin); \
+      k_spmv_box_lines<M, NTY, L><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, d2); \
   } while (0)
   if (mode == MSK_SPMV_RESID) MSK_BM(MSK_SPMV_RESID);
   else if (mode == MSK_SPMV_SCALED) MSK_BM(MSK_SPMV_SCALED);
@@ -1930,7 +1949,7 @@ static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32
 static void march_shape(int32_t nx, int32_t ny, int32_t nz, int32_t* lines, int32_t* zt, int64_t* grid) {
   const int32_t Lq = 4;
   int32_t L = 1, z = 16;
-  if (nx % kT == 0 && msk_march_lines_override != 1) {
+  if (nx % kT == 0 && ny >= Lq && msk_march_lines_override != 1) {
     const int64_t tiles = (int64_t)(nx / kT) * ((ny + Lq - 1) / Lq);
     while (z > 1 && tiles * ((nz + z - 1) / z) < 1024) z /= 2;
     if (tiles * ((nz + z - 1) / z) >= 1024 || msk_march_lines_override == Lq) L = Lq;
@@ -1951,9 +1970,9 @@ extern "C" int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz) {
   return !(f & MSK_TUNE_ELL_MARCH_OFF);
 }
 
-extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8, const double* dval,
-                                  const double* x, const double* b, double* y, int mode, const double* sdev,
-                                  double* vout, const int* stop, hipStream_t s) {
+extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* code8,
+                                  const double* dval, const double* x, const double* b, double* y, int mode,
+                                  const double* sdev, double* vout, const int* stop, hipStream_t s) {
   if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad()) return (int)hipErrorInvalidValue;
   if (msk_march_lines_override != 0 && msk_march_lines_override != 1 && msk_march_lines_override != 4)
     return (int)hipErrorInvalidValue;
@@ -1965,7 +1984,7 @@ extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, const uint
   const int32_t xwin = (msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) ? 0 : 32;
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
 #define MSK_BML(NT, LL) \
-  launch_box_march<NT, LL>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s)
+  launch_box_march<NT, LL>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, d2, s)
   if (L == 4) {
     if (nty) MSK_BML(true, 4);
     else MSK_BML(false, 4);

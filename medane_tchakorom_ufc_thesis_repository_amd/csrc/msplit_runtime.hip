@@ -435,9 +435,10 @@ struct msp_mat {
   int32_t dv_mb = 0;           // most entries in one 256-row block (sizes the LDS stage)
   int32_t dv_w = 0;            // ELL layout: codes per row (4, 8, 16); 0: CSR-order codes + row lengths
   bool dv_on = false;          // products read the DV storage
-  // 3D box stencil (lo = hi = 0) whose ELL dictionary is the seven stencil pairs in column order:
+  // box stencil (lo = hi = 0) whose ELL dictionary is the seven (3D) or five (2D) stencil pairs in column order:
   // its extents, for the z-march SpMV (msk_spmv_box_march); 0 otherwise
   int32_t march_nx = 0, march_ny = 0, march_nz = 0;
+  int32_t march_d2 = 0;        // 2D box stencil (five pairs), marched as nx x 1 x ny
   bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
   uint64_t version = next_version();  // unique per object and bumped when its products' kernels change
 };
@@ -481,6 +482,7 @@ static void dv_free(msp_mat* A) {
   A->dv_w = 0;
   A->dv_on = false;
   A->march_nx = A->march_ny = A->march_nz = 0;
+  A->march_d2 = 0;
 }
 
 // Encode the device CSR of A against the dictionary (host arrays, nd <= 256).
@@ -767,6 +769,11 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
       A->march_nx = nx;
       A->march_ny = ny;
       A->march_nz = nz;
+    } else if (dim == 2 && !lo && !hi && A->ndict == 5 && A->dv_w == 8) {  // marched as nx x 1 x ny
+      A->march_nx = nx;
+      A->march_ny = 1;
+      A->march_nz = ny;
+      A->march_d2 = 1;
     }
   }
   *out = A;
@@ -1063,7 +1070,7 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
   if (A->dv_on) {
     KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, resid, false));
     if (box_march(A)) {
-      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->dv_code, A->dv_val, x, b, y,
+      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->dv_code, A->dv_val, x, b, y,
                               resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
       return MSP_SUCCESS;
     }
@@ -1098,7 +1105,7 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
   if (A->dv_on) {
     KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, false, vout != nullptr));
     if (box_march(A)) {
-      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->dv_code, A->dv_val, x, nullptr, y,
+      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->dv_code, A->dv_val, x, nullptr, y,
                               MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
       return MSP_SUCCESS;
     }

@@ -398,3 +398,34 @@ def test_box_march_lines_bitwise(ctx, oracle, lines, zt, shape, mode):
     xo, ro = oracle.gmres(O, b, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=0, **o)
     assert np.array_equal(ksp.get_residual_history(), ro["hist"])
     assert np.array_equal(xv.get_array(), xo)
+
+
+@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF])
+@pytest.mark.parametrize("shape", [(256, 64), (100, 37), (1024, 9), (33, 7), (1, 50), (300, 1), (512, 40)])
+@pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 0.0)])
+def test_box_march_2d_bitwise(ctx, oracle, flags, shape, peclet):
+    """2D box stencils take the march too, as an nx x 1 x ny box (five codes -nx, -1, 0, +1, +nx mapped onto the
+    3D neighbours): MatMult, MatResidual and GMRES equal the oracle bit for bit, as do the identity order and the
+    row-parallel kernel."""
+    from test_gpu_kernels import tuning
+    nx, ny = shape
+    A = Mat.box_stencil(ctx, 2, nx, ny) if peclet is None else Mat.box_convdiff(ctx, 2, nx, ny, 1, False, False,
+                                                                                peclet)
+    rp, col, val = A.get_csr()
+    O = oracle.Mat.from_arrays(A.shape[0], A.shape[1], rp, col, val)
+    assert A.get_storage() == "dv"
+    n = A.shape[0]
+    b = O.mult(np.random.default_rng(SEED).uniform(-1, 1, n))
+    o = dict(restart=10, max_it=30, rtol=1e-30)
+    with tuning(flags):
+        _products(ctx, A, O, np.random.default_rng(SEED))
+        ksp = KSP(ctx)
+        ksp.set_operators(A)
+        ksp.set_from_options(Options(f"-ksp_type gmres -pc_type none -ksp_norm_type unpreconditioned "
+                                     f"-ksp_gmres_restart {o['restart']} -ksp_max_it {o['max_it']} "
+                                     f"-ksp_rtol {o['rtol']}"))
+        xv = Vec(ctx, n)
+        ksp.solve(Vec.from_array(ctx, b), xv)
+    xo, ro = oracle.gmres(O, b, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=0, **o)
+    assert np.array_equal(ksp.get_residual_history(), ro["hist"])
+    assert np.array_equal(xv.get_array(), xo)
