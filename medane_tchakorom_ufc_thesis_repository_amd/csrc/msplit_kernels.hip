@@ -1342,9 +1342,11 @@ __global__ __launch_bounds__(kT) void k_spmv_ell(int32_t nrows, const uint8_t* _
 // The march kernels name neighbours e = 0..6 as (-P, -nx, -1, 0, +1, +nx, +P).  A 2D box
 // stencil (d2 = 1) is marched as a 3D box of nx x 1 x ny: its five codes (-nx, -1, 0, +1,
 // +nx) are neighbours 0, 2, 3, 4, 6 with P = nx.
-__device__ __forceinline__ int march_code(int c, int32_t d2) { return d2 ? c + (c >= 1) + (c >= 4) : c; }
-__device__ __forceinline__ void march_values(const double* __restrict__ dval, int32_t d2, double* v) {
-  if (d2) {
+template <bool D2>
+__device__ __forceinline__ int march_code(int c) { return D2 ? c + (c >= 1) + (c >= 4) : c; }
+template <bool D2>
+__device__ __forceinline__ void march_values(const double* __restrict__ dval, double* v) {
+  if constexpr (D2) {
     v[0] = dval[0];
     v[1] = 0.0;
     v[2] = dval[1];
@@ -1373,14 +1375,13 @@ __device__ __forceinline__ void march_values(const double* __restrict__ dval, in
 // xwin = 32 (tools/ell_lab.hip, back to back): 256^3 92 -> 74 us, 512^3 821 -> 628 us; in identity
 // order 99 / 697 us (profiles/r02/ell_lab/).  Inside the GMRES step: 103 -> 82 us (rocprof).  The products are added in CSR order
 // from 0.0, the same terms as k_spmv_ell, so the result is bitwise identical.
-template <int MODE, bool NTY>
+template <int MODE, bool NTY, bool D2>
 __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, int32_t nz,
                                                        const uint8_t* __restrict__ code8,
                                                        const double* __restrict__ dval, const double* __restrict__ x,
                                                        const double* __restrict__ b, double* __restrict__ y,
                                                        const double* __restrict__ sdev, double* __restrict__ vout,
-                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin,
-                                                       int32_t d2) {
+                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   __shared__ double sx[kT + 2];
   const int t = threadIdx.x;
@@ -1392,7 +1393,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
   const bool in = rl < P;
   const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   double v[7];
-  march_values(dval, d2, v);
+  march_values<D2>(dval, v);
   const bool hs = in && rl >= nx, hn = in && rl + nx < P, hl = t == 0 && rl > 0, hr = t == kT - 1 && rl + 1 < P;
   double xm = in && z0 > 0 ? x[rl + (int64_t)(z0 - 1) * P] : 0.0;
   double xc = in ? x[rl + (int64_t)z0 * P] : 0.0;
@@ -1414,7 +1415,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int c = EllWord<8>::byte(cw, q);
-      if (c != 255) m |= 1u << march_code(c, d2);
+      if (c != 255) m |= 1u << march_code<D2>(c);
     }
     const double xq[7] = {xm, xs, xl, xc, xr, xn, xp};
     double s = 0.0;
@@ -1438,14 +1439,13 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
 // line, 512^3 590 against 679 (profiles/r02/march/sizes4/); inside the GMRES step 82 against 85 us,
 // SMSM block 283 against 301 (march/lines_ab/).
 // Bitwise k_spmv_box_march (same terms, same order).
-template <int MODE, bool NTY, int L>
+template <int MODE, bool NTY, int L, bool D2 = false>
 __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, int32_t nz,
                                                        const uint8_t* __restrict__ code8,
                                                        const double* __restrict__ dval, const double* __restrict__ x,
                                                        const double* __restrict__ b, double* __restrict__ y,
                                                        const double* __restrict__ sdev, double* __restrict__ vout,
-                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin,
-                                                       int32_t d2) {
+                                                       const int* __restrict__ stop, int32_t zt, int32_t xwin) {
   if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
   __shared__ double sx[L + 2][kT + 2];
   const int t = threadIdx.x;
@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
   const int32_t P = nx * ny;  // nx * ny * nz <= INT32_MAX (checked by the launcher)
   const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   double v[7];
-  march_values(dval, d2, v);
+  march_values<D2>(dval, v);
   double xm[L], xc[L];
 #pragma unroll
   for (int l = 0; l < L; ++l) {
@@ -1499,7 +1499,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int c = EllWord<8>::byte(cw[l], q);
-        if (c != 255) m |= 1u << march_code(c, d2);
+        if (c != 255) m |= 1u << march_code<D2>(c);
       }
       const double xq[7] = {xm[l], sx[l][t + 1], sx[l + 1][t], xc[l], sx[l + 1][t + 2], sx[l + 2][t + 1], xp[l]};
       double s = 0.0;
@@ -1924,17 +1924,17 @@ static bool dv_flags_bad() {
          ((f & MSK_TUNE_ELL_MARCH_NOXCD) && (f & MSK_TUNE_ELL_MARCH_OFF));
 }
 
-// L = 0: k_spmv_box_march (256 plane rows per workgroup); L = 4: k_spmv_box_lines
-template <bool NTY, int L>
+// L = 0: k_spmv_box_march (256 plane rows per workgroup); L = 4: k_spmv_box_lines (3D only)
+template <bool NTY, int L, bool D2>
 static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8,
                              const double* dval, const double* x, const double* b, double* y, const double* sdev,
-                             double* vout, const int* stop, int32_t zt, int32_t xwin, int32_t d2, hipStream_t s) {
+                             double* vout, const int* stop, int32_t zt, int32_t xwin, hipStream_t s) {
 #define MSK_BM(M)                                                                                                 \
   do {                                                                                                            \
     if constexpr (L == 0)                                                                                         \
-      k_spmv_box_march<M, NTY><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, d2);    \
+      k_spmv_box_march<M, NTY, D2><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin);    \
     else                                                                                                          \
-      k_spmv_box_lines<M, NTY, L><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, d2); \
+      k_spmv_box_lines<M, NTY, L><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin); \
   } while (0)
   if (mode == MSK_SPMV_RESID) MSK_BM(MSK_SPMV_RESID);
   else if (mode == MSK_SPMV_SCALED) MSK_BM(MSK_SPMV_SCALED);
@@ -1977,20 +1977,24 @@ extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, co
   if (msk_march_lines_override != 0 && msk_march_lines_override != 1 && msk_march_lines_override != 4)
     return (int)hipErrorInvalidValue;
   if (msk_march_lines_override == 4 && nx % kT) return (int)hipErrorInvalidValue;
+  if (d2 && msk_march_lines_override == 4) return (int)hipErrorInvalidValue;
   int32_t L, zt;
   int64_t g;
   march_shape(nx, ny, nz, &L, &zt, &g);
   if (g > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
   const int32_t xwin = (msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) ? 0 : 32;
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
-#define MSK_BML(NT, LL) \
-  launch_box_march<NT, LL>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, d2, s)
-  if (L == 4) {
-    if (nty) MSK_BML(true, 4);
-    else MSK_BML(false, 4);
+#define MSK_BML(NT, LL, D) \
+  launch_box_march<NT, LL, D>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s)
+  if (d2) {
+    if (nty) MSK_BML(true, 0, true);
+    else MSK_BML(false, 0, true);
+  } else if (L == 4) {
+    if (nty) MSK_BML(true, 4, false);
+    else MSK_BML(false, 4, false);
   } else {
-    if (nty) MSK_BML(true, 0);
-    else MSK_BML(false, 0);
+    if (nty) MSK_BML(true, 0, false);
+    else MSK_BML(false, 0, false);
   }
 #undef MSK_BML
   return (int)hipGetLastError();
