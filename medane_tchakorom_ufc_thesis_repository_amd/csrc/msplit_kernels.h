@@ -119,8 +119,10 @@ int msk_spmv_dv(int32_t nrows, const int32_t* rowptr, const uint8_t* len8, const
 // a z-marching kernel without gathers.  msk_box_march_pick: 1 when the tuning policy takes it for this
 // box (default: always).
 int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz);
-// d2 = 1: a 2D box stencil (five pairs -nx, -1, 0, +1, +nx) passed as nx x 1 x ny.
-int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* code8, const double* dval,
+// d2 = 1: a 2D box stencil (five pairs -nx, -1, 0, +1, +nx) passed as nx x 1 x ny.  mask: one presence
+// byte per row (msk_march_mask: bit e = neighbour e of (-P, -nx, -1, 0, +1, +nx, +P)), read instead of the codes.
+int msk_march_mask(int32_t nrows, int d2, const uint8_t* code8, uint8_t* mask, hipStream_t s);
+int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* mask, const double* dval,
                        const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
                        const int* stop, hipStream_t s);
 // R[:, 0:nc] = A S[:, 0:nc] over DV storage in the ELL layout (W codes per row)

@@ -1363,7 +1363,9 @@ __device__ __forceinline__ void march_values(const double* __restrict__ dval, do
 // The ELL SpMV of a 3D box stencil, marching in z.  The dictionary is the stencil's
 // seven pairs in column order (-P, -nx, -1, 0, +1, +nx, +P) -- the host guarantees it
 // (msp_mat_create_box_convdiff, lo = hi = 0) -- so code e always names neighbour e
-// and a row's codes only say which neighbours exist.  A workgroup owns 256
+// and a row's codes only say which neighbours exist: the kernels read them as one
+// presence byte per row (bit e: neighbour e; k_march_mask builds it from the ELL codes
+// at assembly), 1 B/row instead of the 8 code bytes.  A workgroup owns 256
 // consecutive rows of a plane (a 256-wide x segment of one y line when nx % 256 == 0;
 // parts of several lines otherwise, the plane's last segment ragged) and marches
 // zt planes: x(z-1), x(z), x(z+1) stay in registers, x(y-+1) = x[r -+ nx] are
@@ -1377,7 +1379,7 @@ __device__ __forceinline__ void march_values(const double* __restrict__ dval, do
 // from 0.0, the same terms as k_spmv_ell, so the result is bitwise identical.
 template <int MODE, bool NTY, bool D2>
 __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, int32_t nz,
-                                                       const uint8_t* __restrict__ code8,
+                                                       const uint8_t* __restrict__ mask,
                                                        const double* __restrict__ dval, const double* __restrict__ x,
                                                        const double* __restrict__ b, double* __restrict__ y,
                                                        const double* __restrict__ sdev, double* __restrict__ vout,
@@ -1399,7 +1401,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
   double xc = in ? x[rl + (int64_t)z0 * P] : 0.0;
   for (int32_t z = z0; z < z1; ++z) {
     const int64_t r = rl + (int64_t)z * P;
-    const u32x2 cw = in ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r) : u32x2{~0u, ~0u};
+    const uint32_t m = in ? __builtin_nontemporal_load(mask + r) : 0u;
     const double xp = in && z + 1 < nz ? x[r + P] : 0.0;
     const double xs = hs ? x[r - nx] : 0.0;
     const double xn = hn ? x[r + nx] : 0.0;
@@ -1411,12 +1413,6 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
     if (t == kT - 1) sx[kT + 1] = er;
     __syncthreads();
     const double xl = sx[t], xr = sx[t + 2];
-    uint32_t m = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = EllWord<8>::byte(cw, q);
-      if (c != 255) m |= 1u << march_code<D2>(c);
-    }
     const double xq[7] = {xm, xs, xl, xc, xr, xn, xp};
     double s = 0.0;
 #pragma unroll
@@ -1441,7 +1437,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_march(int32_t nx, int32_t ny, i
 // Bitwise k_spmv_box_march (same terms, same order).
 template <int MODE, bool NTY, int L, bool D2 = false>
 __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, int32_t nz,
-                                                       const uint8_t* __restrict__ code8,
+                                                       const uint8_t* __restrict__ mask,
                                                        const double* __restrict__ dval, const double* __restrict__ x,
                                                        const double* __restrict__ b, double* __restrict__ y,
                                                        const double* __restrict__ sdev, double* __restrict__ vout,
@@ -1469,13 +1465,13 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
   const bool hs = y0 > 0, hn = y0 + L < ny, hl = t == 0 && i > 0, hr = t == kT - 1 && i + 1 < nx;
   for (int32_t z = z0; z < z1; ++z) {
     const int64_t zP = (int64_t)z * P;
-    u32x2 cw[L];
+    uint32_t mk[L];
     double xp[L], el[L], er[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       const bool ok = y0 + l < ny;
       const int64_t r = i + (int64_t)(y0 + l) * nx + zP;
-      cw[l] = ok ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(code8) + r) : u32x2{~0u, ~0u};
+      mk[l] = ok ? __builtin_nontemporal_load(mask + r) : 0u;
       xp[l] = ok && z + 1 < nz ? x[r + P] : 0.0;
       el[l] = ok && hl ? x[r - 1] : 0.0;
       er[l] = ok && hr ? x[r + 1] : 0.0;
@@ -1495,12 +1491,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
     __syncthreads();
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int c = EllWord<8>::byte(cw[l], q);
-        if (c != 255) m |= 1u << march_code<D2>(c);
-      }
+      const uint32_t m = mk[l];
       const double xq[7] = {xm[l], sx[l][t + 1], sx[l + 1][t], xc[l], sx[l + 1][t + 2], sx[l + 2][t + 1], xp[l]};
       double s = 0.0;
 #pragma unroll
@@ -1515,6 +1506,23 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
       xc[l] = xp[l];
     }
   }
+}
+
+// The presence byte of each row of a box stencil in the ELL layout (8 codes per row):
+// bit e set when the row holds neighbour e (march_code).  Built once at assembly.
+template <bool D2>
+__global__ __launch_bounds__(kT) void k_march_mask(int32_t nrows, const uint8_t* __restrict__ code8,
+                                                   uint8_t* __restrict__ mask) {
+  const int32_t r = (int32_t)blockIdx.x * kT + (int32_t)threadIdx.x;
+  if (r >= nrows) return;
+  const u32x2 cw = reinterpret_cast<const u32x2*>(code8)[r];
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = EllWord<8>::byte(cw, q);
+    if (c != 255) m |= 1u << march_code<D2>(c);
+  }
+  mask[r] = (uint8_t)m;
 }
 
 // MatMatMult R = A S over DV storage (ELL layout): lane per row, its codes
@@ -1926,15 +1934,15 @@ static bool dv_flags_bad() {
 
 // L = 0: k_spmv_box_march (256 plane rows per workgroup); L = 4: k_spmv_box_lines (3D only)
 template <bool NTY, int L, bool D2>
-static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32_t nz, const uint8_t* code8,
+static void launch_box_march(int mode, unsigned g, int32_t nx, int32_t ny, int32_t nz, const uint8_t* mask,
                              const double* dval, const double* x, const double* b, double* y, const double* sdev,
                              double* vout, const int* stop, int32_t zt, int32_t xwin, hipStream_t s) {
 #define MSK_BM(M)                                                                                                 \
   do {                                                                                                            \
     if constexpr (L == 0)                                                                                         \
-      k_spmv_box_march<M, NTY, D2><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin);    \
+      k_spmv_box_march<M, NTY, D2><<<g, kT, 0, s>>>(nx, ny, nz, mask, dval, x, b, y, sdev, vout, stop, zt, xwin);    \
     else                                                                                                          \
-      k_spmv_box_lines<M, NTY, L><<<g, kT, 0, s>>>(nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin); \
+      k_spmv_box_lines<M, NTY, L><<<g, kT, 0, s>>>(nx, ny, nz, mask, dval, x, b, y, sdev, vout, stop, zt, xwin); \
   } while (0)
   if (mode == MSK_SPMV_RESID) MSK_BM(MSK_SPMV_RESID);
   else if (mode == MSK_SPMV_SCALED) MSK_BM(MSK_SPMV_SCALED);
@@ -1970,7 +1978,7 @@ extern "C" int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz) {
   return !(f & MSK_TUNE_ELL_MARCH_OFF);
 }
 
-extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* code8,
+extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* mask,
                                   const double* dval, const double* x, const double* b, double* y, int mode,
                                   const double* sdev, double* vout, const int* stop, hipStream_t s) {
   if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad()) return (int)hipErrorInvalidValue;
@@ -1985,7 +1993,7 @@ extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, co
   const int32_t xwin = (msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD) ? 0 : 32;
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
 #define MSK_BML(NT, LL, D) \
-  launch_box_march<NT, LL, D>(mode, (unsigned)g, nx, ny, nz, code8, dval, x, b, y, sdev, vout, stop, zt, xwin, s)
+  launch_box_march<NT, LL, D>(mode, (unsigned)g, nx, ny, nz, mask, dval, x, b, y, sdev, vout, stop, zt, xwin, s)
   if (d2) {
     if (nty) MSK_BML(true, 0, true);
     else MSK_BML(false, 0, true);
@@ -1997,6 +2005,14 @@ extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, co
     else MSK_BML(false, 0, false);
   }
 #undef MSK_BML
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_march_mask(int32_t nrows, int d2, const uint8_t* code8, uint8_t* mask, hipStream_t s) {
+  if (nrows <= 0) return 0;
+  const unsigned g = (unsigned)((nrows + kT - 1) / kT);
+  if (d2) k_march_mask<true><<<g, kT, 0, s>>>(nrows, code8, mask);
+  else k_march_mask<false><<<g, kT, 0, s>>>(nrows, code8, mask);
   return (int)hipGetLastError();
 }
 

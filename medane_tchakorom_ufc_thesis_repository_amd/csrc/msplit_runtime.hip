@@ -439,6 +439,7 @@ struct msp_mat {
   // its extents, for the z-march SpMV (msk_spmv_box_march); 0 otherwise
   int32_t march_nx = 0, march_ny = 0, march_nz = 0;
   int32_t march_d2 = 0;        // 2D box stencil (five pairs), marched as nx x 1 x ny
+  uint8_t* march_mask = nullptr;  // nrows (+16 pad): the rows' presence bytes (msk_march_mask)
   bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
   uint64_t version = next_version();  // unique per object and bumped when its products' kernels change
 };
@@ -481,6 +482,8 @@ static void dv_free(msp_mat* A) {
   A->dv_mb = 0;
   A->dv_w = 0;
   A->dv_on = false;
+  if (A->march_mask) (void)hipFree(A->march_mask);
+  A->march_mask = nullptr;
   A->march_nx = A->march_ny = A->march_nz = 0;
   A->march_d2 = 0;
 }
@@ -775,6 +778,16 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
       A->march_nz = ny;
       A->march_d2 = 1;
     }
+    if (A->march_nx) {  // the presence bytes the march kernels read instead of the codes
+      if (hipMalloc((void**)&A->march_mask, (size_t)A->nrows + 16) != hipSuccess) {
+        msp_mat_destroy(&A);
+        mspi_set_error(MSP_ERR_MEM, "hipMalloc of the march presence bytes failed");
+        return MSP_ERR_MEM;
+      }
+      HIPCHK(hipMemsetAsync(A->march_mask + A->nrows, 0, 16, c->stream));
+      KCHK(msk_march_mask(A->nrows, A->march_d2, A->dv_code, A->march_mask, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
   }
   *out = A;
   return MSP_SUCCESS;
@@ -881,6 +894,12 @@ static double dv_bytes(const msp_mat* A, bool resid, bool vout) {
 // DV products of a box stencil take the z-march kernel when the tuning policy picks it
 static bool box_march(const msp_mat* A) {
   return A->march_nx > 0 && msk_box_march_pick(A->march_nx, A->march_ny, A->march_nz);
+}
+
+// the march reads one presence byte per row instead of the codes
+static double march_bytes(const msp_mat* A, bool resid, bool vout) {
+  const double rows = (double)A->nrows;
+  return rows + 8.0 * (double)A->ncols + 8.0 * rows + (resid ? 8.0 * rows : 0.0) + (vout ? 8.0 * rows : 0.0);
 }
 
 extern "C" int msp_mat_set_storage(msp_mat* A, int storage) {
@@ -1068,9 +1087,10 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
     return MSP_SUCCESS;
   }
   if (A->dv_on) {
-    KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, resid, false));
-    if (box_march(A)) {
-      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->dv_code, A->dv_val, x, b, y,
+    const bool bm = box_march(A);
+    KTimer kt(c, MSP_KERNEL_SPMV, bm ? march_bytes(A, resid, false) : dv_bytes(A, resid, false));
+    if (bm) {
+      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->march_mask, A->dv_val, x, b, y,
                               resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
       return MSP_SUCCESS;
     }
@@ -1103,9 +1123,10 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
     return MSP_SUCCESS;
   }
   if (A->dv_on) {
-    KTimer kt(c, MSP_KERNEL_SPMV, dv_bytes(A, false, vout != nullptr));
-    if (box_march(A)) {
-      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->dv_code, A->dv_val, x, nullptr, y,
+    const bool bm = box_march(A);
+    KTimer kt(c, MSP_KERNEL_SPMV, bm ? march_bytes(A, false, vout != nullptr) : dv_bytes(A, false, vout != nullptr));
+    if (bm) {
+      KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->march_mask, A->dv_val, x, nullptr, y,
                               MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
       return MSP_SUCCESS;
     }

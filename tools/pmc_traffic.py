@@ -50,9 +50,9 @@ def spmv_alg(name: str, n: int):
         mode, w = int(m.group(1)), int(m.group(2))
         return w * N + 16.0 * N + (8.0 * N if mode == 1 else 0.0)
     m = re.search(r"k_spmv_box_(?:march|lines)<(\d+),", nm)
-    if m:  # DV-ELL with 8 codes per row (the 7-point box stencil)
+    if m:  # the box-stencil march: one presence byte per row
         mode = int(m.group(1))
-        return 8.0 * N + 16.0 * N + (8.0 * N if mode == 1 else 0.0)
+        return 1.0 * N + 16.0 * N + (8.0 * N if mode == 1 else 0.0)
     m = re.search(r"k_spmv_lds8<(\d+),", nm)
     if m:
         mode = int(m.group(1))
