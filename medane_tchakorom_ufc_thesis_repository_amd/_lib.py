@@ -114,6 +114,7 @@ _SIGS = {
     "msp_mat_set_storage": [_vp, C.c_int],
     "msp_mat_get_storage": [_vp, _i32p, _i32p],
     "msp_mat_release_csr": [_vp],
+    "msp_mat_get_spmv_kernel": [_vp, _P(C.c_char_p)],
     "msp_dense_create": [_vp, C.c_int64, C.c_int32, _P(_vp)],
     "msp_dense_destroy": [_P(_vp)],
     "msp_dense_get_info": [_vp, _P(C.c_int64), _i32p, _P(C.c_int64)],

@@ -40,7 +40,7 @@
 
 /* Captured restart cycles (HIP graphs), keyed by everything the capture baked
  * in: the operator and the kernels its products launch, the context's DBR
- * partial buffer (its epoch), x, the cycle length K and the tuning flags.  The basis, W and the device state are fixed
+ * partial buffer (its epoch), x, the cycle length K, the tuning flags and the launch-shape overrides.  The basis, W and the device state are fixed
  * between ksp_free_work calls, which drop the cache. */
 #define KSP_NGRAPH 4
 typedef struct {
@@ -48,7 +48,7 @@ typedef struct {
   const msp_mat *A;
   uint64_t aver, epoch;
   const double *x;
-  int K, tuning;
+  int K, tuning, shape;
 } ksp_graph;
 
 struct msp_ksp {
@@ -282,11 +282,11 @@ static int run_cycle(msp_ksp *k, double *x, int K) {
   int rc = mspi_reserve_partial(c, k->n); /* before the lookup: it may reallocate (a new epoch) */
   if (rc) return rc;
   const uint64_t aver = mspi_mat_version(k->A), epoch = mspi_ctx_epoch(c);
-  const int tuning = msk_get_tuning();
+  const int tuning = msk_get_tuning(), shape = msk_get_shape_epoch();
   for (int i = 0; i < KSP_NGRAPH; ++i) {
     const ksp_graph *g = &k->graphs[i];
     if (g->exec && g->A == k->A && g->aver == aver && g->epoch == epoch && g->x == x && g->K == K &&
-        g->tuning == tuning)
+        g->tuning == tuning && g->shape == shape)
       return mspi_graph_launch(c, g->exec);
   }
   if (mspi_capture_begin(c)) { /* stream cannot be captured: run it eagerly */
@@ -311,6 +311,7 @@ static int run_cycle(msp_ksp *k, double *x, int K) {
   g->x = x;
   g->K = K;
   g->tuning = tuning;
+  g->shape = shape;
   return mspi_graph_launch(c, exec);
 }
 

@@ -166,6 +166,8 @@ uint64_t mspi_mat_version(const msp_mat *A);
 /* changes whenever a context buffer that enqueued work points at (the DBR partials) is reallocated */
 uint64_t mspi_ctx_epoch(const msp_ctx *ctx);
 int msk_get_tuning(void);
+/* bumped by every launch-shape override (msk_set_march_z / _lines / msk_set_spmv_group) */
+int msk_get_shape_epoch(void);
 int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 /* ---- HBM mailboxes shared between processes (msplit_ipc.hip) ---- */
 #define MSPI_IPC_HANDLE_BYTES 64

@@ -122,6 +122,9 @@ int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz);
 // d2 = 1: a 2D box stencil (five pairs -nx, -1, 0, +1, +nx) passed as nx x 1 x ny.  mask: one presence
 // byte per row (msk_march_mask: bit e = neighbour e of (-P, -nx, -1, 0, +1, +nx, +P)), read instead of the codes.
 int msk_march_mask(int32_t nrows, int d2, const uint8_t* code8, uint8_t* mask, hipStream_t s);
+// *fail (device) set when a row's presence byte names a neighbour across a line or plane edge of the
+// nx x ny (x nz) box (the march kernels would read it as 0.0): such a matrix must keep the ELL kernel.
+int msk_march_check(int32_t nrows, int32_t nx, int32_t ny, int d2, const uint8_t* mask, int* fail, hipStream_t s);
 int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* mask, const double* dval,
                        const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
                        const int* stop, hipStream_t s);

@@ -1525,6 +1525,25 @@ __global__ __launch_bounds__(kT) void k_march_mask(int32_t nrows, const uint8_t*
   mask[r] = (uint8_t)m;
 }
 
+// Whether the march kernels compute every row of an assembled matrix exactly: they read
+// neighbour e at its place in the box, and x(i-+1) / x(y-+1) as 0.0 across a line / plane
+// edge, so a row whose entry wraps across one (a -1 entry at i = 0, +1 at i = nx - 1, -nx at
+// y = 0, +nx at y = ny - 1; in 3D) would be summed wrong.  *fail is set for any such row
+// (msp_mat_create_csr's box detection; a generated box stencil never has one).
+__global__ __launch_bounds__(kT) void k_march_check(int32_t nrows, int32_t nx, int32_t ny, int d2,
+                                                    const uint8_t* __restrict__ mask, int* __restrict__ fail) {
+  const int32_t r = (int32_t)blockIdx.x * kT + (int32_t)threadIdx.x;
+  if (r >= nrows) return;
+  const uint32_t m = mask[r];
+  const int32_t i = r % nx;
+  bool bad = ((m & 4u) && i == 0) || ((m & 16u) && i == nx - 1);
+  if (!d2) {
+    const int32_t yy = (r / nx) % ny;
+    bad = bad || ((m & 2u) && yy == 0) || ((m & 32u) && yy == ny - 1);
+  }
+  if (bad) atomicOr(fail, 1);
+}
+
 // MatMatMult R = A S over DV storage (ELL layout): lane per row, its codes
 // decoded once into (delta, value) registers, then every column of S streamed
 // past them; each R(r, q) is the CSR row sum of k_spmm_lds8 term for term.
@@ -1665,9 +1684,22 @@ __attribute__((visibility("hidden"))) int msk_march_z_override = 0;  // z-march 
 __attribute__((visibility("hidden"))) int msk_march_lines_override = 0;  // z-march tile: 1 row block, 4 lines (0: auto)
 extern "C" void msk_set_tuning(int flags) { msk_tuning_flags = flags; }
 extern "C" int msk_get_tuning(void) { return msk_tuning_flags; }
-extern "C" void msk_set_spmv_group(int gb) { msk_spmv_gb_override = gb; }
-extern "C" void msk_set_march_z(int z) { msk_march_z_override = z; }
-extern "C" void msk_set_march_lines(int l) { msk_march_lines_override = l; }
+// Launch-shape overrides change what a captured GMRES cycle (ksp_gmres.c run_cycle) would replay:
+// every change bumps msk_shape_epoch, which is part of the graph key.
+__attribute__((visibility("hidden"))) int msk_shape_epoch = 0;
+extern "C" void msk_set_spmv_group(int gb) {
+  msk_spmv_gb_override = gb;
+  ++msk_shape_epoch;
+}
+extern "C" void msk_set_march_z(int z) {
+  msk_march_z_override = z;
+  ++msk_shape_epoch;
+}
+extern "C" void msk_set_march_lines(int l) {
+  msk_march_lines_override = l;
+  ++msk_shape_epoch;
+}
+extern "C" int msk_get_shape_epoch(void) { return msk_shape_epoch; }
 #else
 extern __attribute__((visibility("hidden"))) int msk_tuning_flags;
 extern __attribute__((visibility("hidden"))) int msk_spmv_gb_override;
@@ -2013,6 +2045,14 @@ extern "C" int msk_march_mask(int32_t nrows, int d2, const uint8_t* code8, uint8
   const unsigned g = (unsigned)((nrows + kT - 1) / kT);
   if (d2) k_march_mask<true><<<g, kT, 0, s>>>(nrows, code8, mask);
   else k_march_mask<false><<<g, kT, 0, s>>>(nrows, code8, mask);
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_march_check(int32_t nrows, int32_t nx, int32_t ny, int d2, const uint8_t* mask, int* fail,
+                               hipStream_t s) {
+  if (nrows <= 0) return 0;
+  if (nx <= 0 || ny <= 0) return (int)hipErrorInvalidValue;
+  k_march_check<<<(unsigned)((nrows + kT - 1) / kT), kT, 0, s>>>(nrows, nx, ny, d2, mask, fail);
   return (int)hipGetLastError();
 }
 

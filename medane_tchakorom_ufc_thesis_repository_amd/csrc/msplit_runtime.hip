@@ -576,6 +576,87 @@ static int dv_dictionary(int32_t nrows, const int32_t* rowptr, const int32_t* co
   return (int)delta.size();
 }
 
+// Attach the z-march SpMV (msk_spmv_box_march) to a matrix in DV storage whose ELL dictionary
+// (8 codes per row) is the box stencil's pairs in column order: (-P, -nx, -1, 0, +1, +nx, +P) in 3D
+// (nx x ny x nz, P = nx ny), or (-nx, -1, 0, +1, +nx) for a 2D box marched as nx x 1 x nz.  The
+// deltas must be distinct (nx > 1, and ny > 1 in 3D): with ny == 1, +nx and +P are one column
+// offset, the encoder names the +P coupling +nx and the march would drop it.  check: verify on the
+// device that no row holds a neighbour across a line or plane edge (k_march_check), for matrices
+// the caller assembled; a failed check leaves the matrix on the row-parallel ELL kernel.
+static int march_attach(msp_mat* A, int32_t nx, int32_t ny, int32_t nz, int d2, bool check) {
+  msp_ctx* c = A->ctx;
+  const int nd = d2 ? 5 : 7;
+  if (A->ndict != nd || A->dv_w != 8 || nx <= 1 || (!d2 && ny <= 1) || nz < 1 ||
+      (int64_t)nx * ny * nz != (int64_t)A->nrows || A->ncols != A->nrows)
+    return MSP_SUCCESS;
+  if (hipMalloc((void**)&A->march_mask, (size_t)A->nrows + 16) != hipSuccess) {
+    A->march_mask = nullptr;
+    mspi_set_error(MSP_ERR_MEM, "hipMalloc of the march presence bytes failed");
+    return MSP_ERR_MEM;
+  }
+  HIPCHK(hipMemsetAsync(A->march_mask + A->nrows, 0, 16, c->stream));
+  KCHK(msk_march_mask(A->nrows, d2, A->dv_code, A->march_mask, c->stream));
+  if (check) {
+    int* fail = reinterpret_cast<int*>(mspi_dev_scratch(c));
+    HIPCHK(hipMemsetAsync(fail, 0, sizeof(int), c->stream));
+    KCHK(msk_march_check(A->nrows, nx, d2 ? 1 : ny, d2, A->march_mask, fail, c->stream));
+    int hfail = 0;
+    HIPCHK(hipMemcpyAsync(&hfail, fail, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (hfail) {
+      (void)hipFree(A->march_mask);
+      A->march_mask = nullptr;
+      return MSP_SUCCESS;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  A->march_nx = nx;
+  A->march_ny = d2 ? 1 : ny;
+  A->march_nz = nz;
+  A->march_d2 = d2;
+  return MSP_SUCCESS;
+}
+
+// A host dictionary that is a box stencil's, up to order: 7 pairs with distinct deltas
+// {-a b, -a, -1, 0, 1, a, a b} (a > 1, b > 1, nrows % (a b) == 0) or 5 with {-a, -1, 0, 1, a}
+// (a > 1, nrows % a == 0).  On success the pairs are sorted into column order and the box
+// extents returned (2D: nx = a, nz = nrows / a, d2 = 1).
+static bool box_dictionary(int32_t nrows, std::vector<int32_t>& dd, std::vector<double>& dv, int32_t* nx,
+                           int32_t* ny, int32_t* nz, int* d2) {
+  const size_t nd = dd.size();
+  if (nd != 5 && nd != 7) return false;
+  std::vector<size_t> ord(nd);
+  for (size_t q = 0; q < nd; ++q) ord[q] = q;
+  std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return dd[a] < dd[b]; });
+  std::vector<int32_t> sd(nd);
+  std::vector<double> sv(nd);
+  for (size_t q = 0; q < nd; ++q) {
+    sd[q] = dd[ord[q]];
+    sv[q] = dv[ord[q]];
+    if (q && sd[q] == sd[q - 1]) return false;  // two values on one diagonal: not a constant stencil
+  }
+  const size_t m = nd / 2;  // the diagonal
+  if (sd[m] != 0 || sd[m - 1] != -1 || sd[m + 1] != 1 || sd[m - 2] != -sd[m + 2]) return false;
+  const int32_t a = sd[m + 2];
+  if (a <= 1 || nrows % a) return false;
+  if (nd == 7) {
+    const int32_t P = sd[6];
+    if (sd[0] != -P || P <= a || P % a || nrows % P) return false;
+    *nx = a;
+    *ny = P / a;
+    *nz = nrows / P;
+    *d2 = 0;
+  } else {
+    *nx = a;
+    *ny = 1;
+    *nz = nrows / a;
+    *d2 = 1;
+  }
+  dd = sd;
+  dv = sv;
+  return true;
+}
+
 static int mat_alloc(msp_ctx* c, msp_mat* A, int64_t nptr, int64_t nnz) {
   HIPCHK(hipMalloc((void**)&A->rowptr, (size_t)nptr * sizeof(int32_t)));
   HIPCHK(hipMalloc((void**)&A->col, (size_t)(nnz + 4) * sizeof(int32_t)));
@@ -644,7 +725,17 @@ extern "C" int msp_mat_create_csr(msp_ctx* c, int32_t nrows, int32_t ncols, cons
     const int nd = dv_dictionary(nrows, rowptr, col, val, dd, dvv);
     int32_t ml = 0;
     for (int32_t r = 0; r < nrows; ++r) ml = std::max(ml, rowptr[r + 1] - rowptr[r]);
+    // an assembled box stencil (the reference's poisson3DMatrix / poisson2DMatrix rows cut to a
+    // block, utils.c:30-121, :247-293, :450-478): its dictionary in column order, so the z-march
+    // SpMV can take it once the device has checked that no entry wraps across an edge
+    int32_t bx = 0, by = 0, bz = 0;
+    int d2 = 0;
+    const bool box = nd && ncols == nrows && box_dictionary(nrows, dd, dvv, &bx, &by, &bz, &d2);
     if (nd && (rc = dv_build(A, nd, dd.data(), dvv.data(), mb, ml))) {
+      msp_mat_destroy(&A);
+      return rc;
+    }
+    if (box && (rc = march_attach(A, bx, by, bz, d2, true))) {
       msp_mat_destroy(&A);
       return rc;
     }
@@ -731,6 +822,8 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
   const int64_t deg = dim == 3 ? 7 : 5;
   ARGCHK(ncols <= INT32_MAX && deg * nrows <= INT32_MAX, MSP_ERR_ARG_OUTOFRANGE,
          "box of %lld rows exceeds 32-bit PetscInt indexing", (long long)nrows);
+  ARGCHK(!peclet || (std::isfinite(peclet[0]) && std::isfinite(peclet[1]) && std::isfinite(peclet[2])),
+         MSP_ERR_ARG_WRONG, "Peclet numbers must be finite");
   msp_mat* A = new msp_mat();
   A->ctx = c;
   mspi_ctx_retain(c);
@@ -749,11 +842,16 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
     msp_mat_destroy(&A);
     return rc;
   }
-  ARGCHK(!peclet || (std::isfinite(peclet[0]) && std::isfinite(peclet[1]) && std::isfinite(peclet[2])),
-         MSP_ERR_ARG_WRONG, "Peclet numbers must be finite");
   const BoxCoef cf = box_coefs(dim, peclet);
-  KCHK(msk_box_stencil(dim, nx, ny, nz, nrows, lo, hi, &cf, A->rowptr, A->col, A->val, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  {  // on a HIP failure A is destroyed, which also drops its reference on the context
+    const int e1 = msk_box_stencil(dim, nx, ny, nz, nrows, lo, hi, &cf, A->rowptr, A->col, A->val, c->stream);
+    const int e2 = e1 ? 0 : (int)hipStreamSynchronize(c->stream);
+    if (e1 || e2) {
+      msp_mat_destroy(&A);
+      mspi_set_error(MSP_ERR_LIB, "box stencil assembly failed: %s", hipGetErrorString((hipError_t)(e1 ? e1 : e2)));
+      return MSP_ERR_LIB;
+    }
+  }
   {  // the stencil's pairs: (slow-, y-, x-, diagonal, x+, y+, slow+) with the column shift of a lo plane
     const int32_t off = lo ? (int32_t)plane : 0, P = (int32_t)plane;
     std::vector<int32_t> dd;
@@ -768,25 +866,10 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
       msp_mat_destroy(&A);
       return rc;
     }
-    if (dim == 3 && !lo && !hi && A->ndict == 7 && A->dv_w == 8) {
-      A->march_nx = nx;
-      A->march_ny = ny;
-      A->march_nz = nz;
-    } else if (dim == 2 && !lo && !hi && A->ndict == 5 && A->dv_w == 8) {  // marched as nx x 1 x ny
-      A->march_nx = nx;
-      A->march_ny = 1;
-      A->march_nz = ny;
-      A->march_d2 = 1;
-    }
-    if (A->march_nx) {  // the presence bytes the march kernels read instead of the codes
-      if (hipMalloc((void**)&A->march_mask, (size_t)A->nrows + 16) != hipSuccess) {
-        msp_mat_destroy(&A);
-        mspi_set_error(MSP_ERR_MEM, "hipMalloc of the march presence bytes failed");
-        return MSP_ERR_MEM;
-      }
-      HIPCHK(hipMemsetAsync(A->march_mask + A->nrows, 0, 16, c->stream));
-      KCHK(msk_march_mask(A->nrows, A->march_d2, A->dv_code, A->march_mask, c->stream));
-      HIPCHK(hipStreamSynchronize(c->stream));
+    // the presence bytes the march kernels read instead of the codes (2D: marched as nx x 1 x ny)
+    if (!lo && !hi && (rc = march_attach(A, nx, dim == 3 ? ny : 1, dim == 3 ? nz : ny, dim == 2, false))) {
+      msp_mat_destroy(&A);
+      return rc;
     }
   }
   *out = A;
@@ -1064,6 +1147,16 @@ extern "C" int msp_mat_get_storage(const msp_mat* A, int* storage, int* ndict) {
   ARGCHK(A && storage, MSP_ERR_ARG_NULL, "NULL argument");
   *storage = A->matfree ? MSP_STORAGE_NONE : (A->dv_on ? MSP_STORAGE_DV : MSP_STORAGE_CSR);
   if (ndict) *ndict = A->ndict;
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_mat_get_spmv_kernel(const msp_mat* A, const char** name) {
+  ARGCHK(A && name, MSP_ERR_ARG_NULL, "NULL argument");
+  if (A->matfree) *name = "k_stencil_spmv";
+  else if (A->compressed) *name = "k_spmv_rows";
+  else if (A->dv_on && box_march(A)) *name = "k_spmv_box_march";
+  else if (A->dv_on) *name = A->dv_w ? "k_spmv_ell" : "k_spmv_dv";
+  else *name = A->lds_cap > 0 ? "k_spmv_lds8" : "k_spmv_csr";
   return MSP_SUCCESS;
 }
 

@@ -351,6 +351,12 @@ class Mat:
         call("msp_mat_get_storage", self.h, C.byref(st), C.byref(nd))
         return {v: k for k, v in self.STORAGE.items()}[st.value]
 
+    def spmv_kernel(self) -> str:
+        """The kernel family MatMult / MatResidual / the GMRES products launch (msp_mat_get_spmv_kernel)."""
+        name = C.c_char_p()
+        call("msp_mat_get_spmv_kernel", self.h, C.byref(name))
+        return name.value.decode()
+
     def release_csr(self):
         """Free the CSR arrays of a matrix in DV storage (msp_mat_release_csr); products keep working."""
         call("msp_mat_release_csr", self.h)

@@ -429,3 +429,107 @@ def test_box_march_2d_bitwise(ctx, oracle, flags, shape, peclet):
     xo, ro = oracle.gmres(O, b, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=0, **o)
     assert np.array_equal(ksp.get_residual_history(), ro["hist"])
     assert np.array_equal(xv.get_array(), xo)
+
+
+@pytest.mark.parametrize("shape", [(64, 1, 64), (1, 30, 20), (2, 1, 40), (1, 1, 33), (300, 1, 17)])
+@pytest.mark.parametrize("peclet", [None, (0.5, 0.25, 0.25), (0.0, 0.7, 0.7)])
+def test_box_march_degenerate_lines(ctx, oracle, shape, peclet):
+    """3D boxes with one y line (ny == 1) or one x column (nx == 1): two stencil deltas coincide (+nx = +P, or
+    -1 = -nx), so the encoder would name the +z coupling +nx when the two values are equal (py = pz >= 0, and the
+    Poisson operator) and the march would drop it.  Such boxes keep the row-parallel ELL kernel; products and
+    GMRES equal the oracle bit for bit."""
+    nx, ny, nz = shape
+    A = Mat.box_stencil(ctx, 3, nx, ny, nz) if peclet is None else Mat.box_convdiff(ctx, 3, nx, ny, nz, False,
+                                                                                    False, peclet)
+    assert A.spmv_kernel() != "k_spmv_box_march"
+    rp, col, val = A.get_csr()
+    O = oracle.Mat.from_arrays(A.shape[0], A.shape[1], rp, col, val)
+    n = A.shape[0]
+    _products(ctx, A, O, np.random.default_rng(SEED))
+    b = O.mult(np.random.default_rng(SEED).uniform(-1, 1, n))
+    o = dict(restart=8, max_it=24, rtol=1e-30)
+    ksp = KSP(ctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options(f"-ksp_type gmres -pc_type none -ksp_norm_type unpreconditioned "
+                                 f"-ksp_gmres_restart {o['restart']} -ksp_max_it {o['max_it']} -ksp_rtol {o['rtol']}"))
+    xv = Vec(ctx, n)
+    ksp.solve(Vec.from_array(ctx, b), xv)
+    xo, ro = oracle.gmres(O, b, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=0, **o)
+    assert np.array_equal(ksp.get_residual_history(), ro["hist"])
+    assert np.array_equal(xv.get_array(), xo)
+
+
+def _gmres_vs_oracle(ctx, oracle, A, O, b, restart=30, max_it=30):
+    ksp = KSP(ctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options(f"-ksp_type gmres -pc_type none -ksp_norm_type unpreconditioned "
+                                 f"-ksp_gmres_restart {restart} -ksp_max_it {max_it} -ksp_rtol 1e-30"))
+    xv = Vec(ctx, A.shape[0])
+    ksp.solve(Vec.from_array(ctx, b), xv)
+    xo, ro = oracle.gmres(O, b, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=0, restart=restart, max_it=max_it,
+                          rtol=1e-30)
+    assert ksp.get_iteration_number() == ro["its"]
+    assert np.array_equal(ksp.get_residual_history(), ro["hist"])
+    assert np.array_equal(xv.get_array(), xo)
+
+
+@pytest.mark.parametrize("case", ["3d_256", "3d_ragged", "2d_configs0_block", "3d_convdiff", "3d_dropped"])
+def test_assembled_box_takes_the_march(ctx, oracle, case):
+    """An operator the caller assembles (the reference's poisson3DMatrix / poisson2DMatrix rows cut to a block by
+    MatCreateSubMatrix, utils.c:30-121, :247-293, :450-478) handed to msp_mat_create_csr -- the path the PETSc
+    plugin's MatAssemblyEnd takes -- is recognised as a box stencil and runs the z-march SpMV: MatMult, MatResidual
+    and GMRES(30) equal the oracle bit for bit.  3d_256 is configs[1]'s operator; 2d_configs0_block one of
+    configs[0]'s two diagonal blocks; 3d_dropped a box with random entries left out (the presence bytes, not the
+    geometry, say which neighbours a row holds)."""
+    r = np.random.default_rng(SEED)
+    if case == "3d_256":
+        O = oracle.poisson3d_rows(256, 256, 256, 0, 256)
+    elif case == "3d_ragged":
+        O = oracle.poisson3d_rows(37, 11, 9, 0, 9)
+    elif case == "2d_configs0_block":
+        Ab = oracle.poisson2d_rows(256, 256, 256 * 128, 256 * 256)     # block 1 of configs[0]
+        O, _ = oracle.split(Ab, 256 * 128, 256 * 256)
+    elif case == "3d_convdiff":
+        O = oracle.convdiff_rows(3, 64, 48, 40, 0, 64 * 48 * 40, (0.5, -0.25, 0.3))
+    else:
+        B = oracle.poisson3d_rows(48, 40, 24, 0, 24)
+        rp0, c0, v0 = B.arrays()
+        keep = (r.random(len(c0)) > 0.15) | (np.repeat(np.arange(B.shape[0]), np.diff(rp0)) == c0)
+        rows = np.repeat(np.arange(B.shape[0]), np.diff(rp0))[keep]
+        rp = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=B.shape[0]))]).astype(np.int32)
+        O = oracle.Mat.from_arrays(B.shape[0], B.shape[1], rp, c0[keep], v0[keep])
+    rp, col, val = O.arrays()
+    n = O.shape[0]
+    A = Mat.from_csr(ctx, n, n, rp, col, val)
+    assert A.get_storage() == "dv"
+    assert A.spmv_kernel() == "k_spmv_box_march"
+    _products(ctx, A, O, np.random.default_rng(SEED))
+    b = O.mult(np.ones(n)) if case == "3d_256" else O.mult(r.uniform(-1, 1, n))
+    _gmres_vs_oracle(ctx, oracle, A, O, b, max_it=30 if case == "3d_256" else 45)
+
+
+@pytest.mark.parametrize("wrap", ["x_minus", "x_plus", "y_minus", "y_plus", "x_minus_2d"])
+def test_assembled_box_with_wrapped_entry_keeps_ell(ctx, oracle, wrap):
+    """The same dictionary, but one row holds a neighbour across a line or plane edge (a -1 entry at i = 0, ...):
+    the march would read it as 0.0, so the device check keeps the row-parallel ELL kernel, whose products and GMRES
+    still equal the oracle bit for bit."""
+    nx, ny, nz = (20, 12, 10) if wrap != "x_minus_2d" else (30, 16, 1)
+    O0 = oracle.poisson3d_rows(nx, ny, nz, 0, nz) if nz > 1 else oracle.poisson2d_rows(ny, nx, 0, nx * ny)
+    rp, col, val = (a.copy() for a in O0.arrays())
+    n = O0.shape[0]
+    P = nx * ny
+    row, delta = {"x_minus": (5 * P + 3 * nx, -1), "x_plus": (5 * P + 3 * nx + nx - 1, 1),
+                  "y_minus": (4 * P + 7, -nx), "y_plus": (4 * P + (ny - 1) * nx + 7, nx),
+                  "x_minus_2d": (3 * nx, -1)}[wrap]
+    rows = [list(zip(col[rp[i]:rp[i + 1]], val[rp[i]:rp[i + 1]])) for i in range(n)]
+    assert all(c != row + delta for c, _ in rows[row])
+    rows[row] = sorted(rows[row] + [(row + delta, -1.0)])
+    rp = np.concatenate([[0], np.cumsum([len(x) for x in rows])]).astype(np.int32)
+    col = np.array([c for x in rows for c, _ in x], np.int32)
+    val = np.array([v for x in rows for _, v in x])
+    O = oracle.Mat.from_arrays(n, n, rp, col, val)
+    A = Mat.from_csr(ctx, n, n, rp, col, val)
+    assert A.get_storage() == "dv"
+    assert A.spmv_kernel() == "k_spmv_ell"
+    _products(ctx, A, O, np.random.default_rng(SEED))
+    _gmres_vs_oracle(ctx, oracle, A, O, O.mult(np.random.default_rng(SEED).uniform(-1, 1, n)), max_it=40)
