@@ -113,6 +113,11 @@ def parse():
     p.add_argument("--smsm-n1-steps", type=int, default=2)
     p.add_argument("--no-spmv512", action="store_true", help="N=1: skip the 512^3 CSR MatMult measurement")
     p.add_argument("--spmv-reps", type=int, default=20)
+    p.add_argument("--no-seq-mode", action="store_true",
+                   help="N=1: skip the seq_mode measurement (one configs[1] step in PETSc's reduction order)")
+    p.add_argument("--require-rccl", action="store_true",
+                   help="N>1: exit non-zero when the library communicator could not be created over RCCL and the "
+                        "run would fall back to the host transport (for the driver's scaling runs)")
     p.add_argument("--peclet", default=None,
                    help="Px,Py,Pz: the upwind convection-diffusion operator (configs[4]) instead of Poisson")
     a = p.parse_args()
@@ -319,6 +324,54 @@ def spmv512(ctx, args):
             "peak_GBps": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS, "target_frac": 0.70}
 
 
+GOLDEN = os.path.join(ROOT, "tests", "golden", "configs1_seq.json")
+
+
+def golden_configs1(args, n):
+    """The committed oracle result of exactly this GMRES step (tests/golden/configs1_seq.json:
+    configs[1], b = A*1, x0 = 0, GMRES(30), 300 iterations; "dbr" = the default reduction
+    order, "seq" = PETSc's), or None when the bench runs another workload."""
+    if not (n == 256 and args.max_it == 300 and args.restart == 30 and args.peclet is None
+            and args.rtol <= 1e-4 and os.path.exists(GOLDEN)):
+        return None
+    return json.load(open(GOLDEN))
+
+
+def check_step(ksp, x, ref):
+    """Compare one GMRES step's result (iteration count, reason, every history entry as hex,
+    SHA-256 of x) with a committed oracle record; outside any timed region."""
+    import hashlib
+    import numpy as np
+    hist = [float(h).hex() for h in ksp.get_residual_history()]
+    xs = hashlib.sha256(np.ascontiguousarray(x.get_array(), np.float64).tobytes()).hexdigest()
+    got = {"its": ksp.get_iteration_number(), "reason": ksp.get_converged_reason(), "hist_hex": hist,
+           "x_sha256": xs}
+    bad = [k for k in ("its", "reason", "hist_hex", "x_sha256") if got[k] != ref[k]]
+    return not bad, bad
+
+
+def seq_mode_step(ctx, ksp, b, x, ref):
+    """One configs[1] step with every reduction in PETSc's sequential order (MSP_REDUCE_SEQ, the parity
+    mode -msplit_reduction seq selects), timed and checked against the PETSc-order oracle record."""
+    import torch
+    ctx.set_reduction("seq")
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ksp.solve(b, x)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        its = ksp.get_iteration_number()
+        ok, bad = check_step(ksp, x, ref["seq"]) if ref else (None, [])
+    finally:
+        ctx.set_reduction("dbr")
+    return {"reduction": "seq (PETSc's order: one running sum per dot/norm/MDot entry)",
+            "value": float(x.n) * its / dt, "unit": "DOF-updates/s", "seconds_per_step": dt,
+            "gmres_iterations": its, "verified": ok, "mismatch": bad,
+            "reference": "tests/golden/configs1_seq.json['seq'] (oracle/oracle.c ORC_REDUCE_SEQ)",
+            "note": "the parity mode: identical iteration counts and bitwise PETSc-order histories, at this cost"}
+
+
 def main():
     args = parse()
     import torch
@@ -352,6 +405,14 @@ def main():
     if variant == "gmres" and world > 1:
         raise SystemExit("--variant gmres is the single-GPU workload")
     comm = LibComm(ctx) if world > 1 else LocalComm()
+    transport = getattr(comm, "transport", "none") if world > 1 else "none"
+    if args.require_rccl and world > 1 and transport != "rccl":
+        # every rank agreed on the same transport (LibComm), so every rank exits here
+        print(f"bench.py: --require-rccl, but the library communicator runs over the {transport} transport",
+              file=sys.stderr, flush=True)
+        comm.close()
+        dist.destroy_process_group()
+        sys.exit(3)
     keep = None
     spmv_storage = "matfree" if args.operator == "matfree" else args.storage
 
@@ -448,6 +509,12 @@ def main():
     elapsed = time.perf_counter() - t0
     stats = ctx.kernel_stats() if timing else {}
 
+    # the result of the last timed step against the committed oracle record (outside the timed region)
+    verified, mismatch = None, []
+    ref = golden_configs1(args, n) if variant == "gmres" and world == 1 else None
+    if ref is not None:
+        verified, mismatch = check_step(ksp, x, ref["dbr"])
+
     csr_same_run = None
     if (variant == "gmres" and world == 1 and args.operator == "csr" and args.storage == "dv"
             and not args.no_csr_compare):
@@ -460,8 +527,9 @@ def main():
         torch.cuda.synchronize()
         el_c = time.perf_counter() - t1
         A.set_storage("dv")
+        ok_c = check_step(ksp, x, ref["dbr"])[0] if ref is not None else None
         csr_same_run = {"matrix_storage": "csr", "value": float(rows) * its_c / el_c,
-                        "ms_per_step": 1e3 * el_c / args.steps,
+                        "ms_per_step": 1e3 * el_c / args.steps, "verified": ok_c,
                         "timing": f"HIP events 1 in {args.timing_every}" if timing else "off"}
     ctx.set_timing(False)
 
@@ -478,6 +546,8 @@ def main():
 
     extras = {}
     if world == 1 and variant == "gmres" and rank == 0:
+        if not args.no_seq_mode and ref is not None:
+            extras["seq_mode"] = seq_mode_step(ctx, ksp, b, x, ref)
         # release the headline's objects, then the two side measurements
         del ksp, A, b, x, ones
         if not args.no_spmv512:      # before the SMSM block's ~30 GB come and go
@@ -496,7 +566,13 @@ def main():
                "config": {"workload": workload, "variant": variant, "mesh_per_gpu": mesh, "blocks": world,
                           "ksp": kspopts, "gmres_iterations_per_step_per_block": its_total / args.steps / world,
                           "matrix_storage": "none (matrix-free)" if args.operator == "matfree" else args.storage,
-                          "parallelism": f"{world} z-slab block(s), one per GPU"}}
+                          "parallelism": f"{world} z-slab block(s), one per GPU",
+                          "transport": transport},
+               "verified": verified}
+        if ref is not None:
+            out["verification"] = {"reference": "tests/golden/configs1_seq.json['dbr'] (oracle/oracle.c, DBR order)",
+                                   "checked": "iterations, reason, every residual-history entry (hex), SHA-256 of x",
+                                   "mismatch": mismatch}
         if variant == "smsm":
             out["config"]["lsqr_iterations_per_step"] = lsqr_its[-args.steps:]
         if variant == "amam":
@@ -538,12 +614,16 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    failed = verified is False or (extras.get("seq_mode") or {}).get("verified") is False
     if variant == "smsm":
         mini.close()
     if world > 1:
         comm.close()                            # the library communicator before the process group
         dist.barrier()
         dist.destroy_process_group()
+    if failed:
+        print("bench.py: the timed step's result differs from the committed oracle record", file=sys.stderr)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

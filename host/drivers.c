@@ -416,6 +416,7 @@ int msd_sm_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const
     }
     CK(ordered_sum(&R, sq, &norm));
     norm = sqrt(norm);
+    if (res->outer_its < MSD_HIST_CAP) res->hist[res->outer_its] = norm;
     res->outer_its++;
     res->last_norm = norm;
     if (norm <= fmax(p->atol, p->rtol * res->norm0)) break;
@@ -514,6 +515,12 @@ int msd_smsm_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options 
     for (int i = 0; i < R.nlocal; ++i) CK(apply_alpha(R.blk[i], alpha));
     double norm;
     CK(msp_lsqr_get_residual_norm(lsqr, &norm)); /* KSPGetResidualNorm, SMSM-global.c:341 */
+    if (res->outer_its < MSD_HIST_CAP) {
+      int32_t lits = 0;
+      CK(msp_lsqr_get_iteration_number(lsqr, &lits));
+      res->hist[res->outer_its] = norm;
+      res->lsqr_its[res->outer_its] = lits;
+    }
     res->outer_its++;
     res->last_norm = norm;
     if (norm <= fmax(p->atol, p->rtol * res->norm0)) break;

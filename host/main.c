@@ -45,7 +45,7 @@ static int usage(void) {
   fprintf(stderr, "usage: msplit_driver <synchronous-multisplitting | "
                   "synchronous-multisplitting-synchronous-minimization-global | asynchronous-multisplitting | "
                   "asynchronous-multisplitting-asynchronous-minimization-global> "
-                  "-m M -n N [-s S] [-rtol R] [-dim 3 -p P] [-peclet px,py,pz] [-nb B] [-json] ...\n");
+                  "-m M -n N [-s S] [-rtol R] [-dim 3 -p P] [-peclet px,py,pz] [-nb B] [-msplit_reduction dbr|seq] [-json] ...\n");
   return 2;
 }
 
@@ -89,6 +89,14 @@ int main(int argc, char **argv) {
   msp_ctx *ctx;
   if (msp_ctx_create(ndev > 0 ? rank % ndev : 0, NULL, &ctx)) {
     fprintf(stderr, "msp_ctx_create: %s\n", msp_get_last_error());
+    return 1;
+  }
+  /* -msplit_reduction seq: every dot, norm and MDot in PETSc's Seq order (the parity mode,
+   * msp_ctx_set_reduction): iteration counts and histories are the reference's bit for bit */
+  const char *red = msd_opt_str(o, NULL, "msplit_reduction", "dbr");
+  if (strcmp(red, "dbr") && strcmp(red, "seq")) return usage();
+  if (!strcmp(red, "seq") && msp_ctx_set_reduction(ctx, MSP_REDUCE_SEQ)) {
+    fprintf(stderr, "msp_ctx_set_reduction: %s\n", msp_get_last_error());
     return 1;
   }
   msd_transport t;
@@ -136,7 +144,15 @@ int main(int argc, char **argv) {
         for (int i = 0; i < r.nlocal; ++i) printf("%s%d", i ? ", " : "", r.iterations[i]);
         printf("], ");
       } else {
-        printf("\"outer_its\": %d, ", r.outer_its);
+        printf("\"outer_its\": %d, \"hist_hex\": [", r.outer_its);
+        const int nh = r.outer_its < MSD_HIST_CAP ? r.outer_its : MSD_HIST_CAP;
+        for (int i = 0; i < nh; ++i) printf("%s\"%a\"", i ? ", " : "", r.hist[i]);
+        printf("], ");
+        if (kind == 1) {
+          printf("\"lsqr_its\": [");
+          for (int i = 0; i < nh; ++i) printf("%s%d", i ? ", " : "", r.lsqr_its[i]);
+          printf("], ");
+        }
       }
       printf("\"norm0\": %.17g, \"final_norm\": %.17g, \"error\": %.17g, \"elapsed\": %.6f}\n", r.norm0, r.final_norm,
              r.error, r.elapsed);

@@ -58,8 +58,11 @@ typedef struct {
 } msd_transport;
 
 /* ---- results ---- */
+#define MSD_HIST_CAP 4096
 typedef struct {
   int outer_its;           /* SM / SMSM */
+  double hist[MSD_HIST_CAP]; /* SM / SMSM: the stop test's norm of each outer iteration (first MSD_HIST_CAP) */
+  int lsqr_its[MSD_HIST_CAP]; /* SMSM: the outer LSQR's iteration count of each outer iteration */
   int iterations[64];      /* AM: per local block */
   int nlocal;
   double norm0, final_norm, error, elapsed;

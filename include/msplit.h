@@ -295,6 +295,22 @@ int msp_dense_mult(msp_dense *A, const msp_vec *alpha, int64_t row0, int64_t n, 
 /* out[j] = column_j . u over this block's rows (DBR order) -- the local part of
  * MatMultTranspose (KSPSolve_LSQR); out has ncols entries. */
 int msp_dense_mult_transpose(msp_dense *A, const msp_vec *u, msp_vec *out);
+/* The normal-equations minimization of outer_solver (src/utils/utils.c:972-996: MatTransposeMatMult(R, R,
+ * R_transpose_R), MatMultTranspose(R, b), then the outer KSP on R^T R; the step the reference's profiled
+ * run took, tmp/function-calling-stack:32-41).  Gc = [R^T R | R^T b] over this block's rows, an
+ * s x (s+1) dense block (column s = R^T b): one HBM pass over R and b.  Each entry is a sum over the
+ * rows in the context's reduction order -- DBR: entry (i, j) = VecDot(R_i, R_j) bit for bit (the DBR
+ * order of msp_vec_dot), G symmetric bit for bit; SEQ: the reference BLAS dgemm 'T','N' / dgemv 'T'
+ * order, one running sum per entry (at most 31 columns).  A block publishes Gc (s(s+1) doubles)
+ * instead of its rows of R. */
+int msp_dense_gram(const msp_dense *R, const msp_vec *b, msp_dense *Gc);
+/* out = ((0 + parts[0]) + parts[1]) + ... elementwise, parts in block order (all of out's shape):
+ * the block-ordered sum of the Gram parts, bitwise the same on every rank that sums the same parts. */
+int msp_dense_sum(int32_t nparts, const msp_dense *const *parts, msp_dense *out);
+/* A dense block over columns [col0, col0+ncols) of A, sharing its storage (MatDenseGetSubMatrix,
+ * as the reference's getHalfSubMatrixFromR, utils.c:926-931, takes column ranges); destroying the
+ * view frees nothing of A.  The view must not outlive A's storage. */
+int msp_dense_create_view(msp_dense *A, int32_t col0, int32_t ncols, msp_dense **view);
 /* R = A S -- MatMatMult(A_block_jacobi_resdistributed, S, MAT_REUSE_MATRIX, R)
  * (SMSM-global.c:325-327): A is nrows(R) x nrows(S), R and S have the same
  * column count.  Per row of A and column of S: ascending columns, from 0. */

@@ -125,6 +125,9 @@ _SIGS = {
     "msp_dense_set_column": [_vp, C.c_int32, C.c_int64, _vp, C.c_int64, C.c_int64],
     "msp_dense_mult": [_vp, _vp, C.c_int64, C.c_int64, _vp, C.c_int64],
     "msp_dense_mult_transpose": [_vp, _vp, _vp],
+    "msp_dense_gram": [_vp, _vp, _vp],
+    "msp_dense_sum": [C.c_int32, _P(_vp), _vp],
+    "msp_dense_create_view": [_vp, C.c_int32, C.c_int32, _P(_vp)],
     "msp_mat_matmult_dense": [_vp, _vp, _vp],
     "msp_comm_get_unique_id": [_P(C.c_uint8)],
     "msp_comm_create_rccl": [_vp, C.c_int32, C.c_int32, _P(C.c_uint8), _P(_vp)],

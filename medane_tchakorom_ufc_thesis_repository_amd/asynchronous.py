@@ -195,8 +195,10 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
     name = _channel_name(comm)
     ordered = sorted(blocks, key=lambda b: b.layout.b)
     cap = 0
-    if variant == "amam_global":                     # the largest block of R any block broadcasts
-        cap = max(R.shape[0] * R.shape[1] for R in ordered[0].R_rep)
+    if variant == "amam_global":                     # the largest block (of R, or Gram part) any block broadcasts
+        cap = ordered[0].bcast_cap()
+        if getattr(ordered[0], "minimization", "lsqr") == "lsqr":
+            cap = max(R.shape[0] * R.shape[1] for R in ordered[0].R_rep)
     asyncs = {}
     owner_here = ordered[0].layout.b == 0
     if owner_here:                                   # block 0 creates the regions, the others open them

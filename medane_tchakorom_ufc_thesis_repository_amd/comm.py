@@ -214,19 +214,33 @@ class LibComm:
         self.ctx = ctx
         self.comm = None
         if self.transport == "rccl":
-            obj = [Comm.unique_id() if self.rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0, group=group)
+            dev = (torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl"
+                   else torch.device("cpu"))
+
+            def agree(flag: bool) -> bool:  # every rank takes the same path (MPI_Allreduce MIN, host/main.c)
+                t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+                return bool(int(t.item()))
+
+            # readiness before the collective ncclCommInitRank: a rank that cannot load RCCL (or get an id)
+            # must not leave the others blocked inside init, so all ranks agree first
             err = None
             try:
-                self.comm = Comm.rccl(ctx, self.world, self.rank, obj[0])
-            except Exception as e:          # e.g. ranks sharing a GPU, which RCCL refuses
-                err = e
-            # every rank takes the same transport (the C host's MPI_Allreduce MIN, host/main.c)
-            ok = torch.tensor([0 if err else 1], dtype=torch.int32,
-                              device=torch.device("cuda", torch.cuda.current_device())
-                              if self.backend == "nccl" else torch.device("cpu"))
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-            if int(ok.item()) == 0:
+                uid = Comm.unique_id()
+            except Exception as e:
+                err, uid = e, None
+            ready = agree(err is None)
+            if ready:
+                obj = [uid if self.rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0, group=group)
+                try:
+                    self.comm = Comm.rccl(ctx, self.world, self.rank, obj[0])
+                except Exception as e:          # e.g. ranks sharing a GPU, which RCCL refuses on every rank
+                    err = e
+            # a failure inside init itself is assumed symmetric (RCCL fails on every rank, as for ranks
+            # sharing a GPU); the agreement below then moves every rank to the host transport
+            ok = ready and agree(err is None)
+            if not ok:
                 if self.comm is not None:
                     self.comm.destroy()
                     self.comm = None

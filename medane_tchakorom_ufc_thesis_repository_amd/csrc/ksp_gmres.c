@@ -27,7 +27,7 @@
  * vector makes the MAXPY write a different vector than it reads (an in-place
  * MAXPY measured 5 % slower, same box).
  *
- * Data layout: VV(0..m) are one allocation, (m+1) x stride doubles, stride =
+ * Data layout: VV(0..min(m, max_it)) are one allocation, (min(m, max_it)+1) x stride doubles, stride =
  * n rounded up to 512 (4 KiB aligned); W is separate.  KSPInitialResidual
  * writes VV(0).
  */
@@ -192,6 +192,10 @@ int msp_ksp_set_up(msp_ksp *k) {
   }
   if (k->setup) return MSP_SUCCESS;
   const int64_t m = k->o.restart;
+  /* a cycle runs K <= min(restart, max_it) steps and touches VV(0..K): with max_it < restart (the campaign's
+   * inner solves, max_it 20 under GMRES(30)) only max_it + 1 basis vectors are ever used -- 11 of 32 GB less
+   * per configs[3] block.  A larger max_it frees the work (hist_cap, msp_ksp_set_opts). */
+  const int64_t mv = (k->o.max_it < m ? k->o.max_it : m) + 1;
   int64_t skew = 0; /* an extra skew between basis vectors measured no gain (profiles/r01/skew_ab) */
   const char *env = getenv("MSPLIT_BASIS_SKEW");
   if (env) skew = (atoll(env) + 511) / 512 * 512;
@@ -200,7 +204,7 @@ int msp_ksp_set_up(msp_ksp *k) {
   /* one device block for the recurrence: state, then hh, cc, ss, grs, h, sc, hist */
   const size_t nd = (size_t)((m + 2) * (m + 1) + 5 * (m + 2) + k->hist_cap);
   const size_t st_bytes = (sizeof(mspi_gmres_state) + 63) / 64 * 64;
-  int rc = mspi_malloc(k->ctx, (void **)&k->basis, (size_t)(m + 1) * (size_t)k->stride * sizeof(double) + 4096);
+  int rc = mspi_malloc(k->ctx, (void **)&k->basis, (size_t)mv * (size_t)k->stride * sizeof(double) + 4096);
   if (!rc) rc = mspi_malloc(k->ctx, (void **)&k->tmp, (size_t)k->stride * sizeof(double) + 4096);
   if (!rc) rc = mspi_malloc(k->ctx, &k->gblock, st_bytes + nd * sizeof(double));
   if (!rc) rc = mspi_host_malloc((void **)&k->hst, sizeof(mspi_gmres_state));

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "msplit_ctx.hpp"
 
@@ -297,6 +298,107 @@ __global__ __launch_bounds__(kT) void k_spmm(int32_t nrows, const int32_t* __res
     if (q < nc) R[r + (int64_t)q * ldr] = acc[q];
 }
 
+// ------------------------------------------------------------------ Gram
+// Gc = [R b]^T [R b] partials over one DBR chunk: the columns of R and b (column s) in tiles
+// of kTB; workgroup (chunk c, tile pair p <= q) forms the kTB x kTB dots of tile p's columns with
+// tile q's, each in the DBR lane order of k_scaled_dot (lane t: its 16 elements in order, then the
+// wave butterfly and the fixed wave combine), so entry (i, j) is VecDot(col_i, col_j) bit for bit,
+// and (i, j), (j, i) are the same sum (IEEE products commute).  Upper-triangle entries only:
+// partial[tri(i, j) * nchunks + c].  Workgroups run XCD-major: XCD x takes the chunks c = x mod 8,
+// each chunk's tile pairs back to back, so a chunk's columns (<= 8 x 32 KiB per workgroup) are
+// read from HBM once and the other pairs find them in that XCD's L2.
+constexpr int kTB = 4;
+// packed upper triangle, column by column: entries (0..j, j) are contiguous
+__device__ __forceinline__ int gram_tri(int i, int j) { return j * (j + 1) / 2 + i; }
+
+__global__ __launch_bounds__(kT) void k_gram(const double* __restrict__ R, int64_t lda, int s,
+                                             const double* __restrict__ b, int64_t n, int nbt, int npairs,
+                                             int64_t nch, double* __restrict__ partial) {
+  __shared__ double red[kTB * kTB][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t bid = blockIdx.x;
+  const int64_t slot = bid / 8;
+  const int64_t c = (slot / npairs) * 8 + (bid % 8);
+  int pr = (int)(slot % npairs), p = 0;  // pair index -> (p, q), p <= q
+  while (pr >= nbt - p) {
+    pr -= nbt - p;
+    ++p;
+  }
+  const int q = p + pr;
+  if (c >= nch) return;  // uniform per workgroup
+  const int m = s + 1;
+  const int64_t base = c * kChunk + 2 * t;
+  const bool full = (c + 1) * kChunk <= n;
+  const double* colp[2 * kTB];
+#pragma unroll
+  for (int a = 0; a < 2 * kTB; ++a) {
+    const int k = (a < kTB ? p : q) * kTB + (a % kTB);
+    colp[a] = k < s ? R + (int64_t)k * lda : (k == s ? b : nullptr);
+  }
+  double acc[kTB][kTB];
+#pragma unroll
+  for (int a = 0; a < kTB; ++a)
+#pragma unroll
+    for (int e = 0; e < kTB; ++e) acc[a][e] = 0.0;
+#pragma unroll 2
+  for (int j = 0; j < kIters; ++j) {
+    const int64_t e0 = base + j * (2 * kT);
+    double2 v[2 * kTB];
+#pragma unroll
+    for (int a = 0; a < 2 * kTB; ++a) {
+      if (!colp[a]) {
+        v[a] = make_double2(0.0, 0.0);
+      } else if (full) {
+        v[a] = ld_col<2>(colp[a] + e0);
+      } else {
+        v[a].x = e0 < n ? colp[a][e0] : 0.0;
+        v[a].y = e0 + 1 < n ? colp[a][e0 + 1] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < kTB; ++a)
+#pragma unroll
+      for (int e = 0; e < kTB; ++e) {
+        acc[a][e] = acc[a][e] + v[a].x * v[kTB + e].x;
+        acc[a][e] = acc[a][e] + v[a].y * v[kTB + e].y;
+      }
+  }
+#pragma unroll
+  for (int a = 0; a < kTB; ++a)
+#pragma unroll
+    for (int e = 0; e < kTB; ++e) {
+      const double r = wave_butterfly(acc[a][e]);
+      if (lane == 0) red[a * kTB + e][wv] = r;
+    }
+  __syncthreads();
+  if (t < kTB * kTB) {
+    const int i = p * kTB + t / kTB, jj = q * kTB + t % kTB;
+    if (i < m && jj < m && i <= jj)
+      partial[(int64_t)gram_tri(i, jj) * nch + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+  }
+}
+
+// Gc(i, j) = Gc(j, i) = out[tri(i, j)] for i, j < s, Gc(i, s) = out[tri(i, s)] (R^T b)
+__global__ void k_gram_scatter(const double* __restrict__ out, int s, double* __restrict__ Gc, int64_t ldg) {
+  for (int e = threadIdx.x; e < s * (s + 1); e += blockDim.x) {
+    const int i = e % s, j = e / s;
+    Gc[i + (int64_t)j * ldg] = out[i <= j ? gram_tri(i, j) : gram_tri(j, i)];
+  }
+}
+
+// out = ((0 + parts[0]) + parts[1]) + ... elementwise (block order)
+__global__ __launch_bounds__(kT) void k_dense_sum(const double* const* __restrict__ parts, const int64_t* __restrict__ ldp,
+                                                  int np, int64_t nrows, int ncols, double* __restrict__ out,
+                                                  int64_t ldo) {
+  const int64_t total = nrows * ncols;
+  for (int64_t e = (int64_t)blockIdx.x * kT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kT) {
+    const int64_t i = e % nrows, j = e / nrows;
+    double acc = 0.0;
+    for (int k = 0; k < np; ++k) acc = acc + parts[k][i + j * ldp[k]];
+    out[i + j * ldo] = acc;
+  }
+}
+
 }  // namespace msd
 
 using namespace msd;
@@ -443,6 +545,134 @@ extern "C" int mspi_dense_colsumsq(msp_ctx* c, const double* A, int64_t lda, int
   return MSP_SUCCESS;
 }
 
+// ======================================================================= Gram
+extern "C" int msp_dense_gram(const msp_dense* R, const msp_vec* b, msp_dense* Gc) {
+  ARGCHK(R && b && Gc, MSP_ERR_ARG_NULL, "NULL argument");
+  const int s = R->ncols;
+  ARGCHK(b->n == R->nrows, MSP_ERR_ARG_SIZ, "b has %lld entries, R %lld rows", (long long)b->n, (long long)R->nrows);
+  ARGCHK(Gc->nrows == s && Gc->ncols == s + 1, MSP_ERR_ARG_SIZ, "Gc must be %d x %d, got %lld x %d", s, s + 1,
+         (long long)Gc->nrows, Gc->ncols);
+  ARGCHK(R->ctx == Gc->ctx && b->ctx == R->ctx, MSP_ERR_ARG_WRONG, "R, b and Gc must share one context");
+  msp_ctx* c = R->ctx;
+  const int64_t n = R->nrows;
+  const int m = s + 1, ntri = m * (m + 1) / 2;
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0) {  // no rows: every sum is the empty sum 0
+    HIPCHK(hipMemsetAsync(Gc->d, 0, (size_t)Gc->lda * Gc->ncols * sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  const bool seq = mspi_reduce_seq(c);
+  ARGCHK(!seq || m <= MSK_MAX_GROUP, MSP_ERR_SUP, "MSP_REDUCE_SEQ Gram of more than %d columns",
+         MSK_MAX_GROUP - 1);
+  ARGCHK(seq || (aligned16(R->d) && aligned16(b->d)), MSP_ERR_ARG_WRONG, "Gram operands must be 16-byte aligned");
+  const int64_t pch = seq ? 1 : nch;  // SEQ: one running sum per entry (chunk 0)
+  double* partial = nullptr;
+  double* out = nullptr;
+  int rc = mspi_malloc(c, (void**)&partial, (size_t)ntri * pch * sizeof(double));
+  if (rc) return rc;
+  if ((rc = mspi_malloc(c, (void**)&out, (size_t)ntri * sizeof(double)))) {
+    mspi_free(c, partial);
+    return rc;
+  }
+  {
+    // each column of R and b read once (the tile pairs of a chunk meet in L2), Gc written
+    KTimer kt(c, MSP_KERNEL_DGEMVT, 8.0 * (double)n * m + 8.0 * (double)s * m);
+    if (seq) {  // reference dgemm 'T','N' / dgemv 'T': per entry one running sum over the rows in order
+      // column j against columns 0..j (b = column s against R's columns, then b . b): entries (0..j, j),
+      // contiguous in the packed triangle, each written as its own one-chunk sum (msk_seq_stage1)
+      for (int j = 0; j < m && !rc; ++j) {
+        Vecs v = {};
+        v.base = R->d;
+        v.stride = R->lda;
+        const double* w = j < s ? R->d + (int64_t)j * R->lda : b->d;
+        double* dst = out + j * (j + 1) / 2;
+        rc = msk_seq_stage1(w, &v, std::min(j + 1, s), n, 0, dst, 1, nullptr, c->stream);
+        if (!rc && j == s) {
+          Vecs vb = {};
+          rc = msk_seq_stage1(b->d, &vb, 1, n, 1, dst + s, 1, nullptr, c->stream);
+        }
+      }
+    } else {
+      const int nbt = (m + kTB - 1) / kTB, npairs = nbt * (nbt + 1) / 2;
+      const int64_t grid = (nch + 7) / 8 * 8 * npairs;
+      if (grid > INT32_MAX) rc = MSP_ERR_ARG_OUTOFRANGE;
+      else {
+        k_gram<<<dim3((unsigned)grid), dim3(kT), 0, c->stream>>>(R->d, R->lda, s, b->d, n, nbt, npairs, nch, partial);
+        rc = (int)hipGetLastError();
+        if (!rc) rc = msk_dot_stage2(partial, nch, ntri, out, nullptr, c->stream);
+      }
+    }
+    if (!rc) {
+      k_gram_scatter<<<1, 256, 0, c->stream>>>(out, s, Gc->d, Gc->lda);
+      rc = (int)hipGetLastError();
+    }
+  }
+  (void)hipStreamSynchronize(c->stream);
+  mspi_free(c, partial);
+  mspi_free(c, out);
+  if (rc) {
+    mspi_set_error(MSP_ERR_LIB, "Gram kernels failed: %s", hipGetErrorString((hipError_t)rc));
+    return MSP_ERR_LIB;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_sum(int32_t nparts, const msp_dense* const* parts, msp_dense* out) {
+  ARGCHK(parts && out && nparts >= 1, MSP_ERR_ARG_NULL, "NULL argument or no parts");
+  ARGCHK(nparts <= 4096, MSP_ERR_ARG_OUTOFRANGE, "at most 4096 parts");
+  msp_ctx* c = out->ctx;
+  std::vector<const double*> hp((size_t)nparts);
+  std::vector<int64_t> hl((size_t)nparts);
+  for (int k = 0; k < nparts; ++k) {
+    ARGCHK(parts[k], MSP_ERR_ARG_NULL, "part %d is NULL", k);
+    ARGCHK(parts[k]->nrows == out->nrows && parts[k]->ncols == out->ncols, MSP_ERR_ARG_SIZ,
+           "part %d is %lld x %d, out %lld x %d", k, (long long)parts[k]->nrows, parts[k]->ncols,
+           (long long)out->nrows, out->ncols);
+    ARGCHK(parts[k]->ctx == c, MSP_ERR_ARG_WRONG, "parts and out must share one context");
+    hp[k] = parts[k]->d;
+    hl[k] = parts[k]->lda;
+  }
+  if (out->nrows == 0) return MSP_SUCCESS;
+  void* tab = nullptr;
+  const size_t bytes = (size_t)nparts * (sizeof(double*) + sizeof(int64_t));
+  int rc = mspi_malloc(c, &tab, bytes);
+  if (rc) return rc;
+  const double** dp = (const double**)tab;
+  int64_t* dl = (int64_t*)((char*)tab + (size_t)nparts * sizeof(double*));
+  rc = (int)hipMemcpyAsync(dp, hp.data(), (size_t)nparts * sizeof(double*), hipMemcpyHostToDevice, c->stream);
+  if (!rc) rc = (int)hipMemcpyAsync(dl, hl.data(), (size_t)nparts * sizeof(int64_t), hipMemcpyHostToDevice, c->stream);
+  if (!rc) {
+    KTimer kt(c, MSP_KERNEL_OTHER, 8.0 * (double)out->nrows * out->ncols * (nparts + 1));
+    const int64_t total = out->nrows * out->ncols;
+    const unsigned g = (unsigned)std::min<int64_t>((total + kT - 1) / kT, 4096);
+    k_dense_sum<<<g, kT, 0, c->stream>>>(dp, dl, nparts, out->nrows, out->ncols, out->d, out->lda);
+    rc = (int)hipGetLastError();
+  }
+  (void)hipStreamSynchronize(c->stream);
+  mspi_free(c, tab);
+  if (rc) {
+    mspi_set_error(MSP_ERR_LIB, "dense sum failed: %s", hipGetErrorString((hipError_t)rc));
+    return MSP_ERR_LIB;
+  }
+  return MSP_SUCCESS;
+}
+
+extern "C" int msp_dense_create_view(msp_dense* A, int32_t col0, int32_t ncols, msp_dense** out) {
+  ARGCHK(A && out, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(col0 >= 0 && ncols >= 1 && col0 + ncols <= A->ncols, MSP_ERR_ARG_OUTOFRANGE,
+         "columns [%d, %d) outside the block's %d", col0, col0 + ncols, A->ncols);
+  msp_dense* V = new msp_dense();
+  V->ctx = A->ctx;
+  mspi_ctx_retain(A->ctx);
+  V->nrows = A->nrows;
+  V->ncols = ncols;
+  V->lda = A->lda;
+  V->d = A->d + (int64_t)col0 * A->lda;
+  V->view = 1;
+  *out = V;
+  return MSP_SUCCESS;
+}
+
 // ======================================================================= dense
 static int64_t lda_for(int64_t nrows) { return std::max<int64_t>(512, (nrows + 511) / 512 * 512); }
 
@@ -471,7 +701,7 @@ extern "C" int msp_dense_destroy(msp_dense** pA) {
   if (!pA || !*pA) return MSP_SUCCESS;
   msp_dense* A = *pA;
   if (A->ctx && A->ctx->stream) (void)hipStreamSynchronize(A->ctx->stream);
-  if (A->d) (void)hipFree(A->d);
+  if (A->d && !A->view) (void)hipFree(A->d);
   msp_ctx* c = A->ctx;
   delete A;
   *pA = nullptr;

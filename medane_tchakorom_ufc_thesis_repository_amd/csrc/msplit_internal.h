@@ -63,6 +63,7 @@ struct msp_dense {
   int32_t ncols;
   int64_t lda;
   double *d;
+  int view; /* msp_dense_create_view: columns of another block, storage not freed */
 };
 
 /* y = A[:, 0:nc] coef (+ (*nal_dev) U when U != NULL, skipped when *nal_dev == 0);

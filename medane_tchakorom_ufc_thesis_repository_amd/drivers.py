@@ -114,6 +114,11 @@ def run(argv) -> dict:
                 dist.init_process_group("gloo")
     dev = torch.cuda.current_device() if torch.cuda.device_count() > 0 else 0
     ctx = Context(dev)
+    # -msplit_reduction seq: PETSc's reduction order on the device (the parity mode, msp_ctx_set_reduction)
+    red = opts.get_string("msplit_reduction", "dbr").lower()
+    if red not in Context.REDUCTIONS:
+        raise ValueError(f"-msplit_reduction {red}: expected one of {sorted(Context.REDUCTIONS)}")
+    ctx.set_reduction(red)
     dim, nx, ny, nz = p["dim"], p["m"], p["n"], p["p"] or 1
     if kind == "gmres":
         out = _gmres(ctx, opts, p)
@@ -133,7 +138,8 @@ def run(argv) -> dict:
     if kind == "sm":
         r = sm_solve(blocks, comm, rtol, atol, p["max_outer"])
         fin = r.hist[-1] if r.hist else float("nan")
-        out = {"outer_its": r.outer_its, "final_norm": fin, "error": r.error, "elapsed": r.elapsed}
+        out = {"outer_its": r.outer_its, "final_norm": fin, "error": r.error, "elapsed": r.elapsed,
+               "hist": list(r.hist)}
     elif kind == "smsm":
         if variant == "global":
             for blk in blocks:
@@ -149,7 +155,8 @@ def run(argv) -> dict:
             for blk in blocks:
                 blk.setup_minimization(s)
             r = smsm_semi_local_solve(blocks, comm, s, rtol, atol, p["max_outer"])
-        out = {"outer_its": r.outer_its, "final_norm": r.final_norm, "error": r.error, "elapsed": r.elapsed}
+        out = {"outer_its": r.outer_its, "final_norm": r.final_norm, "error": r.error, "elapsed": r.elapsed,
+               "hist": list(r.hist), "lsqr_its": list(getattr(r, "lsqr_its", []))}
     else:
         from .asynchronous import am_solve
         for blk in blocks:

@@ -195,13 +195,48 @@ class GpuBlock:
                 self.lsqr_semi.get_converged_reason())
 
     # -- global asynchronous minimization (AMAM-global)
-    def setup_global_async_minimization(self, s: int, opts: Options | None = None, prefix: str | None = None):
+    MINIMIZATIONS = ("lsqr", "rtr")
+
+    def setup_global_async_minimization(self, s: int, opts: Options | None = None, prefix: str | None = None,
+                                        minimization: str | None = None):
         """AMAM-global_prime.c:238-330: S over the block's rows and neighbour planes,
         this block's rows of R, the replicated R -- every block's rows, zero until
         that block's first message arrives (MatZeroEntries(R)) --, the global b and
-        the outer LSQR over the nb row blocks in block order."""
+        the outer LSQR over the nb row blocks in block order.
+
+        minimization "rtr" (-msplit_minimization rtr) is the reference's outer_solver
+        (utils.c:972-996) instead of outer_solver_norm_equation: each block forms
+        G_b = R_b^T R_b and c_b = R_b^T b_b in one pass over its rows (msp_dense_gram) and
+        publishes those s(s+1) doubles newest-value; every block sums the newest parts in
+        block order (zeros before a block's first message: R_j = 0 gives G_j = 0) and runs
+        the outer KSP (lsqr, the same options) on G alpha = c.  No replicated R or b: a
+        block holds its own rows only, whatever the block count."""
         L = self.layout
         self.setup_minimization(s)
+        if minimization is None:
+            o = opts if opts is not None else self.opts
+            minimization = o.get_string("msplit_minimization", "lsqr").lower() if o is not None else "lsqr"
+        if minimization not in self.MINIMIZATIONS:
+            raise ValueError(f"-msplit_minimization {minimization}: expected one of {self.MINIMIZATIONS}")
+        self.minimization = minimization
+        pfx = prefix if prefix is not None else f"outer{L.b + 1}_"
+        if minimization == "rtr":
+            self.Gc = DenseMat(self.ctx, self.s, self.s + 1)              # [R_b^T R_b | R_b^T b_b]
+            self.Gc_rep = []
+            for j in range(L.nb):                                         # newest part of every block
+                if j == L.b:
+                    self.Gc_rep.append(self.Gc)
+                else:
+                    G = DenseMat(self.ctx, self.s, self.s + 1)
+                    G.zero_entries()
+                    self.Gc_rep.append(G)
+            self.Gsum = DenseMat(self.ctx, self.s, self.s + 1)
+            self.G_op = self.Gsum.view(0, self.s)                         # R_transpose_R
+            self.c_rhs = self.Gsum.column_vec(self.s)                     # vec_R_transpose_b_block_jacobi
+            self.lsqr_glob = initializeOuterKSP(self.ctx, pfx, opts if opts is not None else self.opts)
+            self.lsqr_glob.set_operators([self.G_op])
+            self.alpha_glob = Vec(self.ctx, self.s)
+            return
         self.R_rep, self.b_all = [], []
         for j in range(L.nb):
             if j == L.b:
@@ -221,10 +256,15 @@ class GpuBlock:
             A.mult(ones, bj)
             self.b_all.append(bj)
             del A, ones
-        self.lsqr_glob = initializeOuterKSP(self.ctx, prefix if prefix is not None else f"outer{L.b + 1}_",
-                                            opts if opts is not None else self.opts)
+        self.lsqr_glob = initializeOuterKSP(self.ctx, pfx, opts if opts is not None else self.opts)
         self.lsqr_glob.set_operators(self.R_rep)
         self.alpha_glob = Vec(self.ctx, self.s)
+
+    def bcast_cap(self) -> int:
+        """Doubles one block publishes per minimization: its rows of R, or its Gram part."""
+        if getattr(self, "minimization", "lsqr") == "rtr":
+            return self.s * (self.s + 1)
+        return self.R.shape[0] * self.R.shape[1]
 
     def global_async_minimize(self, bcast):
         """AMAM-global_prime.c:415-440: R_i = A_block S, send it (comm_async_test_and_send_min),
@@ -232,6 +272,17 @@ class GpuBlock:
         alpha = LSQR(R, b) over the replicated R (outer_solver_norm_equation,
         utils.c:1061-1078), x_minimized = S alpha into x_i and the neighbour planes."""
         self.form_R()
+        if self.minimization == "rtr":                 # outer_solver, utils.c:972-996
+            self.R.gram(self.b, self.Gc)               # MatTransposeMatMult + MatMultTranspose (:978-979)
+            bcast.publish_dense(self.Gc)
+            for j, G in enumerate(self.Gc_rep):
+                if j != self.layout.b:
+                    bcast.fetch_dense(j, G)
+            DenseMat.sum(self.Gc_rep, self.Gsum)       # block order
+            self.lsqr_glob.solve([self.c_rhs], self.alpha_glob)   # KSPSolve(outer_ksp, R^T b, alpha) (:982)
+            self.apply_alpha(self.alpha_glob)          # MatMult(S, alpha, x_minimized) (:993)
+            return (self.lsqr_glob.get_residual_norm(), self.lsqr_glob.get_iteration_number(),
+                    self.lsqr_glob.get_converged_reason())
         bcast.publish_dense(self.R)
         for j, R in enumerate(self.R_rep):
             if j != self.layout.b:

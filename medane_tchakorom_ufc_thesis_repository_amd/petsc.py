@@ -429,6 +429,37 @@ class DenseMat:
     def mult_transpose(self, u: Vec, out: Vec):                      # MatMultTranspose (local rows)
         call("msp_dense_mult_transpose", self.h, u.h, out.h)
 
+    def gram(self, b: Vec, out: "DenseMat"):
+        """out = [R^T R | R^T b] over this block's rows (msp_dense_gram; MatTransposeMatMult + MatMultTranspose
+        of outer_solver, utils.c:978-979); out is s x (s+1)."""
+        call("msp_dense_gram", self.h, b.h, out.h)
+
+    def view(self, col0: int, ncols: int) -> "DenseMat":
+        """Columns [col0, col0+ncols) sharing this block's storage (msp_dense_create_view)."""
+        V = DenseMat.__new__(DenseMat)
+        h = C.c_void_p()
+        call("msp_dense_create_view", self.h, int(col0), int(ncols), C.byref(h))
+        V.ctx, V.h, V.shape, V.lda = self.ctx, h, (self.shape[0], int(ncols)), self.lda
+        V._base = self                                              # keep the storage alive
+        return V
+
+    def column_vec(self, j: int) -> "Vec":
+        """Column j as a Vec over this block's storage (msp_vec_create_with_array)."""
+        v = Vec(self.ctx, self.shape[0], device_ptr=self.device_ptr() + 8 * self.lda * int(j))
+        v._base = self
+        return v
+
+    def device_ptr(self) -> int:
+        p = C.c_void_p()
+        call("msp_dense_get_array", self.h, C.byref(p))
+        return p.value
+
+    @staticmethod
+    def sum(parts, out: "DenseMat"):
+        """out = sum of parts in order, elementwise from 0.0 (msp_dense_sum)."""
+        arr = (C.c_void_p * len(parts))(*[p.h.value for p in parts])
+        call("msp_dense_sum", len(parts), arr, out.h)
+
     def destroy(self):
         if getattr(self, "h", None) and self.h.value:
             call("msp_dense_destroy", C.byref(self.h))

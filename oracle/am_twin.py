@@ -527,14 +527,19 @@ def amam_semi_local_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, ou
 
 
 def amam_global_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100,
-                           max_iterations=100000, strict=False, peclet=None):
+                           max_iterations=100000, strict=False, peclet=None, minimization="lsqr"):
     """AMAM with global minimization (asynchronous-multisplitting-asynchronous-
     minimization-global_prime.c:370-470), round-robin: s asynchronous inner steps,
     each followed by a second receive and S_i(:,k) = [neighbour planes | x_i];
     R_i = A_block S_i is broadcast, every other block's newest R rows are taken
     (zeros before the first), alpha = LSQR(R, b) over all nb row blocks in block
     order, x_minimized = S_i alpha replaces x_i and the view of the neighbour
-    planes, the local test is ||b_i - A_block x_minimized||, one detection step."""
+    planes, the local test is ||b_i - A_block x_minimized||, one detection step.
+
+    minimization "rtr": outer_solver (utils.c:972-996) -- block i broadcasts
+    [R_i^T R_i | R_i^T b_i] (the oracle's orc_dense_gram) instead of its rows; the
+    newest parts are summed elementwise in block order from 0.0 and the outer LSQR
+    (same options) solves R^T R alpha = R^T b."""
     mode = po.REDUCE_DBR
     blocks, N, rows, plane = _blocks_ext(po, dim, nx, ny, nz, nb, peclet)
     net = Slots()
@@ -545,7 +550,10 @@ def amam_global_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer:
     outer = dict(outer, reduce_mode=mode)
     published = [None] * nb                                 # newest R rows each block sent
     for blk in blocks:
-        blk["Rrep"] = [np.zeros((rows, s), order="F") for _ in range(nb)]
+        if minimization == "rtr":
+            blk["Rrep"] = [np.zeros((s, s + 1), order="F") for _ in range(nb)]
+        else:
+            blk["Rrep"] = [np.zeros((rows, s), order="F") for _ in range(nb)]
         blk["taken"] = [0] * nb
     versions = [0] * nb
     b_all = [blk["rhs_b"] for blk in blocks]
@@ -576,6 +584,8 @@ def amam_global_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer:
                 blk["steps"] += 1
             R = np.asfortranarray(np.stack([blk["Aext"].mult(np.ascontiguousarray(S[:, k])) for k in range(s)],
                                            axis=1))
+            if minimization == "rtr":
+                R = po.dense_gram(R, blk["rhs_b"], mode)    # [R_i^T R_i | R_i^T b_i]
             blk["Rrep"][bi] = R
             published[bi] = R.copy()                        # comm_async_test_and_send_min
             versions[bi] += 1
@@ -583,7 +593,13 @@ def amam_global_roundrobin(po, dim, nx, ny, nz, nb, s, rtol, inner: dict, outer:
                 if j != bi and versions[j] > blk["taken"][j]:
                     blk["Rrep"][j] = published[j].copy()
                     blk["taken"][j] = versions[j]
-            alpha, lr = po.lsqr(blk["Rrep"], b_all, **outer)
+            if minimization == "rtr":
+                G = np.zeros((s, s + 1), order="F")
+                for part in blk["Rrep"]:                    # block order, from 0.0
+                    G = G + part
+                alpha, lr = po.lsqr([np.asfortranarray(G[:, :s])], [np.ascontiguousarray(G[:, s])], **outer)
+            else:
+                alpha, lr = po.lsqr(blk["Rrep"], b_all, **outer)
             lsqr_its.append(lr["its"])
             _apply_ext(blk, po.dense_mult(S, alpha), rows)
             ln = po.norm2(blk["Aext"].residual(blk["rhs_b"], _ext_col(blk, rows)), mode)

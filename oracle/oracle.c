@@ -820,6 +820,31 @@ void orc_dense_mult(int64_t n, int s, const double *S, int64_t lda, const double
   }
 }
 
+/* outer_solver (src/utils/utils.c:972-996): MatTransposeMatMult(R, R, .., R_transpose_R) and
+ * MatMultTranspose(R, b, vec_R_transpose_b) over one block's rows, as Gc = [R^T R | R^T b]
+ * (s x (s+1), column-major, leading dimension ldg).  R is MATMPIDENSE on a one-rank block
+ * communicator, so PETSc 3.22.1 runs the SeqDense kernels: BLASgemm_("T", "N") and dgemv 'T',
+ * whose reference (f2cblaslapack) loops are, per entry, TEMP = TEMP + A(L,I)*B(L,J) over the
+ * rows in order from zero and C(I,J) = ALPHA*TEMP with ALPHA = 1 (exact): ORC_REDUCE_SEQ.
+ * ORC_REDUCE_DBR: each entry is the device order's dot (dbr_dot), so G(i,j) = G(j,i). */
+void orc_dense_gram(int mode, int64_t n, int s, const double *R, int64_t lda, const double *b, double *Gc,
+                    int64_t ldg) {
+  for (int j = 0; j <= s; ++j) {
+    const double *cj = j < s ? R + (int64_t)j * lda : b;
+    for (int i = 0; i < s; ++i) {
+      const double *ci = R + (int64_t)i * lda;
+      double v;
+      if (mode == ORC_REDUCE_DBR) {
+        v = dbr_dot(n, ci, cj);
+      } else {
+        v = 0.0;
+        for (int64_t l = 0; l < n; ++l) v = v + ci[l] * cj[l];
+      }
+      Gc[i + (int64_t)j * ldg] = v;
+    }
+  }
+}
+
 /* VecNorm of an s-vector (one rank holds it whole: sequential) */
 static double ls_snorm(int s, const double *v) {
   double t = 0.0;

@@ -201,6 +201,12 @@ int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R
  * (reference dgemv 'N': per row, columns in order, starting from 0). */
 void orc_dense_mult(int64_t n, int s, const double *S, int64_t lda, const double *alpha, double *y);
 
+/* outer_solver's normal equations (utils.c:972-996) over one block's rows: Gc = [R^T R | R^T b],
+ * s x (s+1) column-major with leading dimension ldg.  SEQ: the SeqDense BLAS order (dgemm 'T','N',
+ * dgemv 'T': one running sum per entry over the rows); DBR: each entry the device's dot order. */
+void orc_dense_gram(int mode, int64_t n, int s, const double *R, int64_t lda, const double *b, double *Gc,
+                    int64_t ldg);
+
 /* --- SMSM, global minimization ------------------------------------------- */
 typedef struct {
   int dim, nx, ny, nz, nb;

@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
         L.orc_lsqr_solve.argtypes = [C.c_int, P(C.c_int64), C.c_int, P(dp), P(C.c_int64), P(dp), dp,
                                      P(LsqrOpts), P(LsqrResult), dp, C.c_int]
         L.orc_dense_mult.argtypes = [C.c_int64, C.c_int, dp, C.c_int64, dp, dp]
+        L.orc_dense_gram.argtypes = [C.c_int, C.c_int64, C.c_int, dp, C.c_int64, dp, dp, C.c_int64]
         L.orc_smsm_solve.argtypes = [P(SMSMProblem), P(GmresOpts), P(LsqrOpts), P(SMResult), dp, C.c_int,
                                      P(C.c_int), P(C.c_int), P(C.c_int), dp]
         _lib = L
@@ -339,6 +340,16 @@ def lsqr(R_blocks, b_blocks, hist_cap=None, **opts):
            "orc_lsqr_solve")
     return x, {"its": r.its, "reason": r.reason, "rnorm": r.rnorm, "arnorm": r.arnorm, "anorm": r.anorm,
                "hist": hist[:min(r.nhist, cap)].copy()}
+
+
+def dense_gram(R, b, mode=REDUCE_SEQ) -> np.ndarray:
+    """[R^T R | R^T b] (s x (s+1)) over one block's rows (orc_dense_gram; outer_solver, utils.c:978-979)."""
+    R = np.asfortranarray(R, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    n, s = R.shape
+    G = np.zeros((s, s + 1), order="F")
+    lib().orc_dense_gram(mode, n, s, _dp(R), max(n, 1), _dp(b), _dp(G), s)
+    return G
 
 
 def dense_mult(S, alpha) -> np.ndarray:

@@ -9,7 +9,13 @@ typedef struct {
   msp_vec *b, *x;
   PetscInt restart;
   PetscReal haptol, breakdowntol;
+  PetscInt reduction; /* -msplit_reduction dbr|seq: MSP_REDUCE_DBR (default) or PETSc's own order */
 } KSP_MSplit;
+
+/* -msplit_reduction: the device reduction order (include/msplit.h msp_ctx_set_reduction).  "seq" is
+ * the parity mode -- every dot, norm and MDot summed in PETSc's Seq order, so iteration counts and
+ * residual histories are the reference's bit for bit -- at a fraction of the speed (bench.py seq_mode). */
+static const char *const MSplitReductions[] = {"dbr", "seq", "MSplitReduction", "MSPLIT_REDUCTION_", NULL};
 
 #define MSPCall(e) do { int _rc = (e); PetscCheck(!_rc, PETSC_COMM_SELF, _rc, "%s", msp_get_last_error()); } while (0)
 
@@ -29,6 +35,7 @@ static PetscErrorCode KSPSetUp_MSplitGMRES(KSP ksp)
   PetscCall(MatGetRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &nr, &ia, &ja, &done));
   PetscCall(MatSeqAIJGetArrayRead(Ad, &aa));
   if (!ms->ctx) MSPCall(msp_ctx_create(0, NULL, &ms->ctx));   /* device = local rank % ndev in practice */
+  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
   MSPCall(msp_mat_destroy(&ms->A));
   MSPCall(msp_mat_create_csr(ms->ctx, (int32_t)nr, (int32_t)nr, ia, ja, aa, &ms->A));
   PetscCall(MatSeqAIJRestoreArrayRead(Ad, &aa));
@@ -90,6 +97,8 @@ static PetscErrorCode KSPSetFromOptions_MSplitGMRES(KSP ksp, PetscOptionItems *P
   PetscOptionsHeadBegin(PetscOptionsObject, "KSP MSplit GMRES Options");
   PetscCall(PetscOptionsInt("-ksp_gmres_restart", "Krylov directions", NULL, ms->restart, &ms->restart, NULL));
   PetscCall(PetscOptionsReal("-ksp_gmres_haptol", "happy breakdown tolerance", NULL, ms->haptol, &ms->haptol, NULL));
+  PetscCall(PetscOptionsEnum("-msplit_reduction", "device reduction order (seq: PETSc's, bitwise)", NULL,
+                             MSplitReductions, (PetscEnum)ms->reduction, (PetscEnum *)&ms->reduction, NULL));
   PetscCall(PetscOptionsReal("-ksp_gmres_breakdown_tolerance", "restart breakdown tolerance", NULL, ms->breakdowntol,
                              &ms->breakdowntol, NULL));
   PetscOptionsHeadEnd();
@@ -137,6 +146,7 @@ typedef struct {
   msp_lsqr *lsqr;
   msp_vec *b, *x;
   PetscBool exact_norm;
+  PetscInt reduction; /* -msplit_reduction, as for msplitgmres */
 } KSP_MSplitLSQR;
 
 static PetscErrorCode KSPSetUp_MSplitLSQR(KSP ksp)
@@ -155,6 +165,7 @@ static PetscErrorCode KSPSetUp_MSplitLSQR(KSP ksp)
   PetscCall(MatGetSize(Al, &m, &n));
   PetscCall(MatDenseGetLDA(Al, &lda));
   if (!ms->ctx) MSPCall(msp_ctx_create(0, NULL, &ms->ctx));
+  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
   MSPCall(msp_dense_destroy(&ms->R));
   MSPCall(msp_dense_create(ms->ctx, m, (int32_t)n, &ms->R));
   PetscCall(MatDenseGetArrayRead(Al, &a));
@@ -213,6 +224,8 @@ static PetscErrorCode KSPSetFromOptions_MSplitLSQR(KSP ksp, PetscOptionItems *Pe
   KSP_MSplitLSQR *ms = (KSP_MSplitLSQR *)ksp->data;
   PetscFunctionBegin;
   PetscOptionsHeadBegin(PetscOptionsObject, "KSP MSplit LSQR Options");
+  PetscCall(PetscOptionsEnum("-msplit_reduction", "device reduction order (seq: PETSc's, bitwise)", NULL,
+                             MSplitReductions, (PetscEnum)ms->reduction, (PetscEnum *)&ms->reduction, NULL));
   PetscCall(PetscOptionsBool("-ksp_lsqr_exact_mat_norm", "exact Frobenius norm of the operator", NULL,
                              ms->exact_norm, &ms->exact_norm, NULL));
   PetscOptionsHeadEnd();

@@ -40,6 +40,12 @@ static PetscErrorCode MSplitContext(msp_ctx **ctx)
     PetscInt dev = 0;
     PetscCall(PetscOptionsGetInt(NULL, NULL, "-msplit_device", &dev, NULL));
     MSPCall(msp_ctx_create((int)dev, NULL, &g_ctx));
+    /* -msplit_reduction seq: VecDot/VecNorm/VecMDot of the drivers' outer tests in PETSc's order too */
+    const char *const red[] = {"dbr", "seq"};
+    PetscInt  r   = 0;
+    PetscBool set = PETSC_FALSE;
+    PetscCall(PetscOptionsGetEList(NULL, NULL, "-msplit_reduction", red, 2, &r, &set));
+    if (set) MSPCall(msp_ctx_set_reduction(g_ctx, (int)r));
   }
   *ctx = g_ctx;
   PetscFunctionReturn(PETSC_SUCCESS);

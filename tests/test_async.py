@@ -294,26 +294,39 @@ class _Block:
             self.halo[hoff:hoff + cnt] = by_id[nbr].x[nbr_off:nbr_off + cnt]
 
     # global asynchronous minimization (AMAM-global), oracle arithmetic
-    def setup_global_async_minimization(self, s, outer):
+    def setup_global_async_minimization(self, s, outer, minimization="lsqr"):
         L, po = self.layout, self.po
         self.s, self.outer = s, dict(outer, reduce_mode=po.REDUCE_DBR)
+        self.minimization = minimization
         self.S = np.zeros((self.lo + L.nrows + self.hi, s), order="F")
-        self.R_rep = [np.zeros((L.nrows, s), order="F") for _ in range(L.nb)]
+        shape = (s, s + 1) if minimization == "rtr" else (L.nrows, s)
+        self.R_rep = [np.zeros(shape, order="F") for _ in range(L.nb)]
         self.b_all = [am_twin._block_rows(po, L.dim, L.nx, L.ny, L.nz, L.nb, j, L.peclet).mult(
             np.ones(L.nrows * L.nb)) for j in range(L.nb)]
 
     def store_column(self, k):
         self.S[:, k] = np.concatenate([self.halo[:self.lo], self.x, self.halo[self.lo:self.lo + self.hi]])
 
+    def bcast_cap(self):
+        return self.R_rep[0].size
+
     def global_async_minimize(self, bcast):
         L, po = self.layout, self.po
         R = np.stack([self.A_ext.mult(np.ascontiguousarray(self.S[:, k])) for k in range(self.s)], axis=1)
+        if self.minimization == "rtr":                # outer_solver: the block's Gram part travels
+            R = po.dense_gram(R, self.b_all[L.b], po.REDUCE_DBR)
         self.R_rep[L.b] = np.asfortranarray(R)
         bcast.publish(self.R_rep[L.b])
         for j in range(L.nb):
             if j != L.b:
                 bcast.fetch(j, self.R_rep[j])
-        alpha, r = po.lsqr(self.R_rep, self.b_all, **self.outer)
+        if self.minimization == "rtr":
+            G = np.zeros((self.s, self.s + 1), order="F")
+            for part in self.R_rep:
+                G = G + part
+            alpha, r = po.lsqr([np.asfortranarray(G[:, :self.s])], [np.ascontiguousarray(G[:, self.s])], **self.outer)
+        else:
+            alpha, r = po.lsqr(self.R_rep, self.b_all, **self.outer)
         xe = po.dense_mult(self.S, alpha)
         self.x = xe[self.lo:self.lo + L.nrows].copy()
         self.halo[:self.lo] = xe[:self.lo]
@@ -435,22 +448,31 @@ def test_am_multiprocess_gloo_terminates(world, problem):
     assert len({o[2] for o in out}) == 1                             # same phase tag at the verdict
 
 
+@pytest.mark.parametrize("minimization", ["lsqr", "rtr"])
 @pytest.mark.parametrize("dim,nx,ny,nz,nb,s,max_it,peclet", [(3, 8, 8, 8, 2, 4, 5, None),
                                                                (3, 6, 6, 9, 3, 3, 3, None),
                                                                (2, 24, 20, 1, 2, 4, 5, (0.5, 0.25, 0.0))])
-def test_amam_global_roundrobin_host_matches_twin(oracle, dim, nx, ny, nz, nb, s, max_it, peclet):
-    """The product driver (am_solve, variant amam_global: msp_abcast broadcast of R,
-    C detection) over CPU test-double blocks, round-robin in one process, against
-    the twin's independent restatement of the loop: bit for bit."""
+def test_amam_global_roundrobin_host_matches_twin(oracle, dim, nx, ny, nz, nb, s, max_it, peclet, minimization):
+    """The product driver (am_solve, variant amam_global: msp_abcast broadcast of R -- or, with the
+    reference's outer_solver ("rtr"), of each block's [R^T R | R^T b] --, C detection) over CPU test-double
+    blocks, round-robin in one process, against the twin's independent restatement of the loop: bit for bit."""
     from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
     from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm
     from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
     inner = dict(restart=30, max_it=max_it, rtol=1e-20)
     blocks = [_Block(block_layout(dim, nx, ny, nz, nb, b, peclet), oracle, inner) for b in range(nb)]
     for blk in blocks:
-        blk.setup_global_async_minimization(s, OUTER)
+        blk.setup_global_async_minimization(s, OUTER, minimization)
     res = am_solve(blocks, LocalComm(), rtol=1e-6, record=True, variant="amam_global", s=s)
-    tw = am_twin.amam_global_roundrobin(oracle, dim, nx, ny, nz, nb, s, 1e-6, inner, OUTER, peclet=peclet)
+    tw = am_twin.amam_global_roundrobin(oracle, dim, nx, ny, nz, nb, s, 1e-6, inner, OUTER, peclet=peclet,
+                                        minimization=minimization)
+    # every block stopped on its local test (||b_i - A_block x_min|| <= rtol/sqrt(nb) ||b||, AMAM-global_prime.c:436-458)
+    thr = 1e-6 / np.sqrt(nb) * res.norm0
+    last = {}
+    for b, it, ln, state, tag in res.trace:
+        last[b] = ln
+    assert all(v <= thr for v in last.values())
+    assert res.final_norm <= 1e-4 * res.norm0
     assert res.norm0 == tw["norm0"] and res.iterations == tw["iterations"] and res.inner_its == tw["inner_its"]
     assert res.trace == tw["trace"]
     assert np.array_equal(np.concatenate([blk.x for blk in blocks]), tw["x"])
@@ -467,21 +489,23 @@ def _global_worker(rank, world, port, problem, q):
     from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        dim, nx, ny, nz, s, rtol, max_it = problem
+        dim, nx, ny, nz, s, rtol, max_it = problem[:7]
+        minimization = problem[7] if len(problem) > 7 else "lsqr"
         blk = _Block(block_layout(dim, nx, ny, nz, world, rank), po, dict(restart=30, max_it=max_it, rtol=1e-20))
-        blk.setup_global_async_minimization(s, OUTER)
+        blk.setup_global_async_minimization(s, OUTER, minimization)
         res = am_solve([blk], TorchComm(), rtol=rtol, max_iterations=20000, variant="amam_global", s=s)
         q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.error))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("minimization", ["lsqr", "rtr"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_amam_global_multiprocess_gloo_terminates(world):
-    """One process per block, truly asynchronous (R broadcast through shared
+def test_amam_global_multiprocess_gloo_terminates(world, minimization):
+    """One process per block, truly asynchronous (R -- or the Gram part -- broadcast through shared
     memory while the others compute): the detection terminates every block
     in the same phase, with one global final residual."""
-    out = _run(world, (3, 6, 6, 12, 3, 1e-6, 5), _global_worker)
+    out = _run(world, (3, 6, 6, 12, 3, 1e-6, 5, minimization), _global_worker)
     assert all(o[3] == out[0][3] for o in out)
     assert all(o[4] == out[0][4] for o in out)
     assert out[0][4] <= 1e-2 * out[0][3]

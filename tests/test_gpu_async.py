@@ -150,14 +150,18 @@ def test_amam_semi_local_convdiff_gpu_bitwise_vs_twin(ctx, oracle):
     assert res.final_norm == tw["final_norm"] and res.error == tw["error"]
 
 
+@pytest.mark.parametrize("minimization", ["lsqr", "rtr"])
 @pytest.mark.parametrize("dim,nx,ny,nz,nb,s,max_it,peclet", [(2, 24, 20, 1, 2, 4, 5, None),
                                                                (3, 8, 8, 8, 2, 4, 5, None),
                                                                (3, 6, 6, 9, 3, 3, 3, None),
                                                                (3, 8, 8, 8, 4, 4, 5, PE)])
-def test_amam_global_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s, max_it, peclet, monkeypatch):
+def test_amam_global_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz, nb, s, max_it, peclet, monkeypatch,
+                                                    minimization):
     """AMAM-global (configs[3]/[4]'s algorithm): R rows broadcast through msp_abcast,
     LSQR over the replicated R, x_minimized into x_i and the neighbour view (one
-    device buffer per block on the 3-block case, two otherwise)."""
+    device buffer per block on the 3-block case, two otherwise).  "rtr": the reference's
+    outer_solver (utils.c:972-996) -- [R_i^T R_i | R_i^T b_i] broadcast, summed in block
+    order, LSQR on the normal equations."""
     if nb == 3:
         monkeypatch.setenv("MSPLIT_ABCAST_NBUF", "1")
     opts = Options(" ".join(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 "
@@ -165,10 +169,11 @@ def test_amam_global_gpu_roundrobin_bitwise_vs_twin(ctx, oracle, dim, nx, ny, nz
     comm = LocalComm()
     blocks = make_blocks(ctx, dim, nx, ny, nz, nb, range(nb), opts, comm, peclet)
     for blk in blocks:
-        blk.setup_global_async_minimization(s)
+        blk.setup_global_async_minimization(s, minimization=minimization)
     res = am_solve(blocks, comm, rtol=1e-6, record=True, variant="amam_global", s=s)
     tw = am_twin.amam_global_roundrobin(oracle, dim, nx, ny, nz, nb, s, 1e-6,
-                                        dict(restart=30, max_it=max_it, rtol=1e-20), OUTER, peclet=peclet)
+                                        dict(restart=30, max_it=max_it, rtol=1e-20), OUTER, peclet=peclet,
+                                        minimization=minimization)
     assert res.norm0 == tw["norm0"] and res.iterations == tw["iterations"] and res.inner_its == tw["inner_its"]
     assert res.trace == tw["trace"]
     assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), tw["x"])

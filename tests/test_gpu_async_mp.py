@@ -117,7 +117,8 @@ def _am_worker(rank, world, port, problem, q):
     from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Options
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        variant, dim, nx, ny, nz, s, max_it, rtol = problem
+        variant, dim, nx, ny, nz, s, max_it, rtol = problem[:8]
+        minimization = problem[8] if len(problem) > 8 else "lsqr"
         b = rank
         opts = Options(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 -inner{b + 1}_pc_type none "
                        f"-outer{b + 1}_ksp_type lsqr -outer{b + 1}_ksp_convergence_test default "
@@ -127,7 +128,7 @@ def _am_worker(rank, world, port, problem, q):
         comm = TorchComm()
         (blk,) = make_blocks(ctx, dim, nx, ny, nz, world, [rank], opts, comm)
         if variant == "amam_global":
-            blk.setup_global_async_minimization(s)
+            blk.setup_global_async_minimization(s, minimization=minimization)
         res = am_solve([blk], comm, rtol=rtol, max_iterations=20000, variant=variant, s=s)
         q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.transport))
     finally:
@@ -136,7 +137,9 @@ def _am_worker(rank, world, port, problem, q):
 
 @pytest.mark.parametrize("world,problem,nbuf", [(2, ("am", 3, 8, 8, 16, 0, 5, 1e-6), "2"),
                                                 (2, ("amam_global", 3, 8, 8, 16, 4, 5, 1e-6), "2"),
-                                                (3, ("amam_global", 3, 8, 8, 18, 4, 5, 1e-6), "1")])
+                                                (3, ("amam_global", 3, 8, 8, 18, 4, 5, 1e-6), "1"),
+                                                (2, ("amam_global", 3, 8, 8, 16, 4, 5, 1e-6, "rtr"), "2"),
+                                                (3, ("amam_global", 3, 8, 8, 18, 4, 5, 1e-6, "rtr"), "1")])
 def test_am_processes_device_transport(world, problem, nbuf, monkeypatch):
     """One process per block, truly asynchronous, planes (and for AMAM-global the
     R rows, with two or one HBM buffers) through HBM slots opened by IPC: the
