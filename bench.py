@@ -101,6 +101,10 @@ def parse():
     p.add_argument("--amam-mesh", type=int, default=None, help="AMAM: nx = ny (1024; 512 with --peclet)")
     p.add_argument("--amam-planes", type=int, default=None, help="AMAM: z-planes per GPU (128; 64 with --peclet)")
     p.add_argument("--amam-its", type=int, default=2, help="AMAM: outer iterations per block per step")
+    p.add_argument("--minimization", default="lsqr", choices=["lsqr", "rtr"],
+                   help="AMAM: the replicated-R LSQR (outer_solver_norm_equation, utils.c:1061-1078; default) or "
+                        "the reference's normal equations (outer_solver, utils.c:972-996: each block publishes "
+                        "[R^T R | R^T b], s(s+1) doubles, instead of its rows of R)")
     p.add_argument("--operator", default="csr", choices=["csr", "matfree"],
                    help="the assembled operator (the reference's MatMult, default) or the same operator applied "
                         "matrix-free (bitwise the same products, no matrix traffic; gmres, and A_ii for smsm)")
@@ -466,7 +470,7 @@ def main():
         o = Options(kspopts)
         L = block_layout(3, n, n, nz, world, rank, args.peclet)
         blk = GpuBlock(ctx, L, o, comm, prefix="inner1_")
-        blk.setup_global_async_minimization(args.s, o, prefix="outer1_")
+        blk.setup_global_async_minimization(args.s, o, prefix="outer1_", minimization=args.minimization)
         rows = L.nrows
         amres = []
 
@@ -479,7 +483,9 @@ def main():
                     f"{world} z-slab block(s) of {n}x{n}x{args.amam_planes} (one per MI355X; "
                     f"{'configs[4]' if args.peclet else 'configs[3]'} per-GPU block), s = {args.s} inner GMRES("
                     f"{args.restart}) steps of max_it {args.inner_max_it}, {args.amam_its} outer iterations per block "
-                    f"per step, LSQR max_it {args.outer_max_it} over the replicated R, HBM mailboxes (xGMI)")
+                    f"per step, LSQR max_it {args.outer_max_it} "
+                    + ("over the replicated R" if args.minimization == "lsqr" else
+                       "on R^T R (outer_solver: Gram parts broadcast)") + ", HBM mailboxes (xGMI)")
         keep = amres
     else:
         step, workload, kspopts, rows, (blk, mini, lsqr_its) = build_smsm(ctx, args, comm, world, rank)

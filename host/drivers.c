@@ -175,6 +175,11 @@ typedef struct {
   msp_vec *ball[64];
   msp_lsqr *lsqr;
   msp_vec *alpha;
+  /* -msplit_minimization rtr (outer_solver, utils.c:972-996): Gram parts [R_j^T R_j | R_j^T b_j] (own = Gc),
+   * their block-ordered sum Gsum, its R^T R view (the outer KSP's operator) and R^T b column */
+  int rtr;
+  msp_dense *Gc, *Gsum, *Gop;
+  msp_vec *crhs;
 } msd_block;
 
 static int ksp_from_options(msp_ksp *k, const msd_options *o, const char *p, msp_ksp_opts *ko) {
@@ -660,6 +665,29 @@ static int amam_setup_block(msp_ctx *ctx, const msd_problem *p, const msd_option
   const msd_layout *L = &B->L;
   CK(msp_dense_create(ctx, B->lo + B->n + B->hi, p->s, &B->S));
   CK(msp_dense_create(ctx, B->n, p->s, &B->R));
+  char prefix[32];
+  snprintf(prefix, sizeof(prefix), "outer%d_", L->b + 1);
+  B->rtr = p->rtr;
+  if (B->rtr) { /* no replicated R, no global b: Gram parts of s(s+1) doubles per block */
+    for (int j = 0; j < p->nb; ++j) {
+      CK(msp_dense_create(ctx, p->s, p->s + 1, &B->Rrep[j]));
+      CK(msp_dense_zero_entries(B->Rrep[j]));
+    }
+    B->Gc = B->Rrep[L->b];
+    CK(msp_dense_create(ctx, p->s, p->s + 1, &B->Gsum));
+    CK(msp_dense_create_view(B->Gsum, 0, p->s, &B->Gop));
+    double *gd;
+    int64_t lda;
+    CK(msp_dense_get_array(B->Gsum, &gd));
+    CK(msp_dense_get_info(B->Gsum, NULL, NULL, &lda));
+    CK(msp_vec_create_with_array(ctx, p->s, gd + (int64_t)p->s * lda, &B->crhs));
+    CK(msp_lsqr_create(ctx, &B->lsqr));
+    CK(lsqr_from_options(B->lsqr, o, prefix));
+    CK(msp_lsqr_set_operators(B->lsqr, 1, &B->Gop));
+    CK(msp_lsqr_set_comm(B->lsqr, NULL));
+    CK(msp_vec_create(ctx, p->s, &B->alpha));
+    return MSP_SUCCESS;
+  }
   for (int j = 0; j < p->nb; ++j) {
     if (j == L->b) {
       B->Rrep[j] = B->R;
@@ -684,8 +712,6 @@ static int amam_setup_block(msp_ctx *ctx, const msd_problem *p, const msd_option
     msp_mat_destroy(&Aj);
     B->ball[j] = bj;
   }
-  char prefix[32];
-  snprintf(prefix, sizeof(prefix), "outer%d_", L->b + 1);
   CK(msp_lsqr_create(ctx, &B->lsqr));
   CK(lsqr_from_options(B->lsqr, o, prefix));
   CK(msp_lsqr_set_operators(B->lsqr, p->nb, B->Rrep));
@@ -696,10 +722,13 @@ static int amam_setup_block(msp_ctx *ctx, const msd_problem *p, const msd_option
 
 static void amam_free_block(msd_block *B, int nb) {
   for (int j = 0; j < nb; ++j) {
-    if (j == B->L.b) continue;
+    if (j == B->L.b && !B->rtr) continue;
     msp_dense_destroy(&B->Rrep[j]);
     msp_vec_destroy(&B->ball[j]);
   }
+  msp_vec_destroy(&B->crhs);
+  msp_dense_destroy(&B->Gop);
+  msp_dense_destroy(&B->Gsum);
   msp_lsqr_destroy(&B->lsqr);
   msp_vec_destroy(&B->alpha);
 }
@@ -707,6 +736,15 @@ static void amam_free_block(msd_block *B, int nb) {
 static int amam_minimize(msd_block *B, int nb) { /* global_async_minimize, AMAM-global_prime.c:415-440 */
   int32_t done;
   CK(msp_mat_matmult_dense(B->A_ext, B->S, B->R)); /* R_i = A_block S */
+  if (B->rtr) {                                     /* outer_solver, utils.c:972-996 */
+    CK(msp_dense_gram(B->R, B->b, B->Gc));          /* MatTransposeMatMult + MatMultTranspose (:978-979) */
+    CK(msp_abcast_publish_dense(B->bc, B->Gc, &done));
+    for (int j = 0; j < nb; ++j)
+      if (j != B->L.b) CK(msp_abcast_fetch_dense(B->bc, j, B->Rrep[j], &done));
+    CK(msp_dense_sum(nb, (const msp_dense *const *)B->Rrep, B->Gsum)); /* block order */
+    CK(msp_lsqr_solve(B->lsqr, &B->crhs, B->alpha)); /* KSPSolve(outer_ksp, R^T b, alpha) (:982) */
+    return apply_alpha(B, B->alpha);
+  }
   CK(msp_abcast_publish_dense(B->bc, B->R, &done)); /* comm_async_test_and_send_min */
   for (int j = 0; j < nb; ++j)                      /* comm_async_probe_and_receive_min */
     if (j != B->L.b) CK(msp_abcast_fetch_dense(B->bc, j, B->Rrep[j], &done));
@@ -744,8 +782,8 @@ int msd_amam_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options 
   for (int i = 0; i < R.nlocal; ++i) CK(amam_setup_block(ctx, p, o, R.blk[i]));
   CK(sum_over_blocks(&R, norm0_sq, &res->norm0));
   /* the largest block of R any block broadcasts: block 0's replicated R (asynchronous.py) */
-  int64_t cap = 0;
-  for (int j = 0; j < p->nb; ++j) {
+  int64_t cap = p->rtr ? (int64_t)p->s * (p->s + 1) : 0;
+  for (int j = 0; j < p->nb && !p->rtr; ++j) {
     msd_layout Lj;
     CK(msd_layout_make(p->dim, p->nx, p->ny, p->nz, p->nb, j, p->peclet, &Lj));
     const int64_t c = (Lj.r1 - Lj.r0) * (int64_t)p->s;

@@ -45,7 +45,7 @@ static int usage(void) {
   fprintf(stderr, "usage: msplit_driver <synchronous-multisplitting | "
                   "synchronous-multisplitting-synchronous-minimization-global | asynchronous-multisplitting | "
                   "asynchronous-multisplitting-asynchronous-minimization-global> "
-                  "-m M -n N [-s S] [-rtol R] [-dim 3 -p P] [-peclet px,py,pz] [-nb B] [-msplit_reduction dbr|seq] [-json] ...\n");
+                  "-m M -n N [-s S] [-rtol R] [-dim 3 -p P] [-peclet px,py,pz] [-nb B] [-msplit_reduction dbr|seq] [-msplit_minimization lsqr|rtr] [-json] ...\n");
   return 2;
 }
 
@@ -78,6 +78,9 @@ int main(int argc, char **argv) {
   p.nb = world > 1 ? world : (int)msd_opt_int(o, NULL, "nb", 2);
   p.matfree = !strcmp(msd_opt_str(o, NULL, "msplit_operator", "csr"), "matfree");
   p.async_host = !strcmp(msd_opt_str(o, NULL, "msplit_async_transport", "device"), "host");
+  const char *mini = msd_opt_str(o, NULL, "msplit_minimization", "lsqr");
+  if (strcmp(mini, "lsqr") && strcmp(mini, "rtr")) return usage();
+  p.rtr = !strcmp(mini, "rtr");
   const char *pe = msd_opt_str(o, NULL, "peclet", NULL);
   if (pe && sscanf(pe, "%lf,%lf,%lf", &p.peclet[0], &p.peclet[1], &p.peclet[2]) != 3) return usage();
   if (msd_opt_int(o, NULL, "npb", 1) != 1) {

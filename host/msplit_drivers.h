@@ -77,6 +77,7 @@ typedef struct {
   int max_outer;
   int matfree;             /* -msplit_operator matfree: A_ii without storage */
   int async_host;          /* -msplit_async_transport host: shared-memory staging instead of HBM slots */
+  int rtr;                 /* -msplit_minimization rtr: AMAM-global through outer_solver's normal equations */
 } msd_problem;
 
 int msd_sm_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const msd_transport *t, msd_result *r);

@@ -100,20 +100,24 @@ AMAM = "asynchronous-multisplitting-asynchronous-minimization-global"
     ["-dim", "3", "-m", "8", "-n", "8", "-p", "12", "-nb", "3", "-s", "4", "-rtol", "1e-6",
      "-peclet", "0.5,0.25,-0.3"] + _inner(3, 5) + _outer(3),
 ])
-def test_c_host_amam_global_matches_python_host(ctx, built, args):
+@pytest.mark.parametrize("minimization", ["lsqr", "rtr"])
+def test_c_host_amam_global_matches_python_host(ctx, built, args, minimization):
     """AMAM-global (configs[3]/[4]'s algorithm) in the C host, blocks round-robin in one process: the same
-    per-block iteration counts, final residual and error as the Python host, to the last bit."""
+    per-block iteration counts, final residual and error as the Python host, to the last bit; with the
+    replicated-R LSQR and with the reference's outer_solver (-msplit_minimization rtr)."""
+    args = args + ["-msplit_minimization", minimization]
     c = _run([AMAM] + args)
     py = drivers.run([AMAM] + args + ["-json"])
     assert c["iterations"] == py["iterations"]
     assert c["final_norm"] == py["final_norm"] and c["error"] == py["error"]
 
 
-def test_c_host_mpi_amam_global_terminates(ctx, built):
-    """One block per MPI rank (both on the one GPU): the R rows travel between the processes' HBM through the
-    msp_abcast buffers, the detection ends the run, and the residual meets the tolerance."""
-    r = _run([AMAM, "-dim", "3", "-m", "8", "-n", "8", "-p", "16", "-s", "4", "-rtol", "1e-6"] + _inner(2, 5)
-             + _outer(2), mpi=2)
+@pytest.mark.parametrize("minimization", ["lsqr", "rtr"])
+def test_c_host_mpi_amam_global_terminates(ctx, built, minimization):
+    """One block per MPI rank (both on the one GPU): the R rows (or Gram parts) travel between the processes' HBM
+    through the msp_abcast buffers, the detection ends the run, and the residual meets the tolerance."""
+    r = _run([AMAM, "-dim", "3", "-m", "8", "-n", "8", "-p", "16", "-s", "4", "-rtol", "1e-6",
+              "-msplit_minimization", minimization] + _inner(2, 5) + _outer(2), mpi=2)
     assert len(r["iterations"]) == 1 and r["final_norm"] < 1e-4 * r["norm0"]
 
 
