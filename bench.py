@@ -119,6 +119,9 @@ def parse():
     p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--no-seq-mode", action="store_true",
                    help="N=1: skip the seq_mode measurement (one configs[1] step in PETSc's reduction order)")
+    p.add_argument("--no-assembled", action="store_true",
+                   help="N=1: skip the assembled_csr_operator measurement (the GMRES step with the operator handed "
+                        "over as host CSR arrays, msp_mat_create_csr)")
     p.add_argument("--require-rccl", action="store_true",
                    help="N>1: exit non-zero when the library communicator could not be created over RCCL and the "
                         "run would fall back to the host transport (for the driver's scaling runs)")
@@ -354,6 +357,47 @@ def check_step(ksp, x, ref):
     return not bad, bad
 
 
+def assembled_operator_step(ctx, args, b, ref):
+    """The GMRES step with the operator handed over as host CSR arrays through msp_mat_create_csr -- the path
+    the PETSc plugin's MatAssemblyEnd / KSPSetUp take for the reference's assembled AIJ (poisson3DMatrix,
+    utils.c:30-121, cut by MatCreateSubMatrix, :450-478).  The arrays are the assembled 256^3 operator
+    (downloaded from a device assembly: the same rows, columns and values); the library recognises the box
+    stencil and attaches the z-march SpMV.  Timed over the same steps and checked against the oracle record."""
+    import torch
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Mat, Options, Vec
+    n = args.mesh
+    A0 = Mat.box_stencil(ctx, 3, n, n, n)
+    rp, col, val = A0.get_csr()
+    A0.destroy()
+    N = n * n * n
+    t0 = time.perf_counter()
+    A = Mat.from_csr(ctx, N, N, rp, col, val)
+    create_s = time.perf_counter() - t0
+    del rp, col, val
+    ksp = KSP(ctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options(f"-ksp_type gmres -ksp_gmres_restart {args.restart} -pc_type none "
+                                 f"-ksp_norm_type unpreconditioned -ksp_rtol {args.rtol} -ksp_max_it {args.max_it}"))
+    ksp.set_initial_guess_nonzero(False)
+    x = Vec(ctx, N)
+    ksp.solve(b, x)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    its = 0
+    for _ in range(args.steps):
+        ksp.solve(b, x)
+        its += ksp.get_iteration_number()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t1
+    ok = check_step(ksp, x, ref["dbr"])[0] if ref is not None else None
+    out = {"operator": "host CSR arrays through msp_mat_create_csr (the PETSc plugin's path)",
+           "spmv_kernel": A.spmv_kernel(), "matrix_storage": A.get_storage(), "value": float(N) * its / dt,
+           "unit": "DOF-updates/s", "ms_per_step": 1e3 * dt / args.steps, "steps": args.steps,
+           "create_s": create_s, "verified": ok}
+    A.destroy()
+    return out
+
+
 def seq_mode_step(ctx, ksp, b, x, ref):
     """One configs[1] step with every reduction in PETSc's sequential order (MSP_REDUCE_SEQ, the parity
     mode -msplit_reduction seq selects), timed and checked against the PETSc-order oracle record."""
@@ -554,6 +598,8 @@ def main():
     if world == 1 and variant == "gmres" and rank == 0:
         if not args.no_seq_mode and ref is not None:
             extras["seq_mode"] = seq_mode_step(ctx, ksp, b, x, ref)
+        if not args.no_assembled and args.operator == "csr" and args.peclet is None:
+            extras["assembled_csr_operator"] = assembled_operator_step(ctx, args, b, ref)
         # release the headline's objects, then the two side measurements
         del ksp, A, b, x, ones
         if not args.no_spmv512:      # before the SMSM block's ~30 GB come and go
@@ -620,7 +666,8 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    failed = verified is False or (extras.get("seq_mode") or {}).get("verified") is False
+    failed = (verified is False or (extras.get("seq_mode") or {}).get("verified") is False
+              or (extras.get("assembled_csr_operator") or {}).get("verified") is False)
     if variant == "smsm":
         mini.close()
     if world > 1:
