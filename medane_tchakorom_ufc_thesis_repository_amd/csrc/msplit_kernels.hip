@@ -1508,6 +1508,116 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
   }
 }
 
+// The GMRES step's MatMult of a box stencil fused with the VecMDot after it.  Workgroup c owns
+// DBR chunk c and computes W = A (sc x) for its rows in the DBR lane layout (lane t: rows
+// c*4096 + j*512 + 2t, +1), so W never leaves the registers before the dots: the MDot
+// reads the nv basis vectors but not W (8 bytes per row less).  The chunk's x window
+// [c*4096 - nx, c*4096 + 4096 + nx) -- every x-+1 and y-+1 neighbour of its rows -- is staged
+// in LDS; x(z-+1) are coalesced loads.  A row adds v[e] * (x[r + delta_e] * sc) for the
+// neighbours its presence byte names, e = 0..6 in column order from 0.0: the march kernels'
+// terms in their order, so W is bitwise k_spmv_box_march's, and each dot is dot_chunk's.
+// Neighbours are read at their global index, so unlike the march this needs no edge check.
+template <bool D2, int VAR, bool NTY>
+__global__ __launch_bounds__(kT) void k_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, const uint8_t* __restrict__ mask,
+                                                      const double* __restrict__ dval, const double* __restrict__ x,
+                                                      const double* __restrict__ sdev, double* __restrict__ y, Vecs V,
+                                                      int nv, double* __restrict__ partial, int64_t nchunks,
+                                                      const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sx = reinterpret_cast<double*>(smem);  // window of kChunk + 2 nx doubles
+  __shared__ double red[MSK_MAX_GROUP][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t c = blockIdx.x, c0 = c * kChunk, lo = c0 - nx;
+  const int64_t base = c0 + 2 * t;
+  const bool full = (c + 1) * kChunk <= n;
+  const int wlen = kChunk + 2 * nx;
+  if ((nx & 1) == 0 && lo >= 0 && lo + wlen <= n) {  // 16-byte aligned interior window
+    const double2* x2 = reinterpret_cast<const double2*>(x + lo);
+    for (int i = t; i < wlen / 2; i += kT) reinterpret_cast<double2*>(sx)[i] = x2[i];
+  } else {
+    for (int i = t; i < wlen; i += kT) {
+      const int64_t r = lo + i;
+      sx[i] = r >= 0 && r < n ? x[r] : 0.0;
+    }
+  }
+  const double sc = *sdev;
+  double v[7];
+  march_values<D2>(dval, v);
+  uint32_t m[2 * kIters];
+  double xm[2 * kIters], xp[2 * kIters];
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {  // presence bytes and the -+plane neighbours, issued before the LDS wait
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t r = base + j * (2 * kT) + q;
+      const uint32_t mr = r < n ? (uint32_t)mask[r] : 0u;
+      m[2 * j + q] = mr;
+      xm[2 * j + q] = (mr & 1u) ? x[r - P] : 0.0;
+      xp[2 * j + q] = (mr & 64u) ? x[r + P] : 0.0;
+    }
+  }
+  __syncthreads();
+  double wr[2 * kIters];
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = j * (2 * kT) + 2 * t + q + nx;  // the row's place in the window
+      const uint32_t mr = m[2 * j + q];
+      const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], sx[e], sx[e + 1], sx[e + nx], xp[2 * j + q]};
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 7; ++k)
+        if (mr & (1u << k)) s = s + v[k] * (xq[k] * sc);
+      wr[2 * j + q] = s;
+    }
+    const int64_t r = base + j * (2 * kT);
+    if (full) {
+      if constexpr (NTY) {
+        dx2 o;
+        o.x = wr[2 * j];
+        o.y = wr[2 * j + 1];
+        __builtin_nontemporal_store(o, reinterpret_cast<dx2*>(y + r));
+      } else {
+        *reinterpret_cast<double2*>(y + r) = make_double2(wr[2 * j], wr[2 * j + 1]);
+      }
+    } else {
+      if (r < n) y[r] = wr[2 * j];
+      if (r + 1 < n) y[r + 1] = wr[2 * j + 1];
+    }
+  }
+  // VecMDot of W against the nv basis vectors, this chunk (dot_chunk's order)
+  if (full) {
+    int g = 0;
+#pragma unroll 1
+    for (; g + 4 <= nv; g += 4) dot_group_full<4, VAR>(wr, V, base, 0, nv, g, red, lane, wv);
+    switch (nv - g) {
+      case 3: dot_group_full<3, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 2: dot_group_full<2, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 1: dot_group_full<1, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      default: break;
+    }
+  } else {
+#pragma unroll 1
+    for (int vi = 0; vi < nv; ++vi) {
+      const double* __restrict__ yv = vec_at(V, vi);
+      const double sv = vec_scale(V, vi);
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < kIters; ++j) {
+        const int64_t e = base + j * (2 * kT);
+        if (e < n) acc = acc + wr[2 * j] * (yv[e] * sv);
+        if (e + 1 < n) acc = acc + wr[2 * j + 1] * (yv[e + 1] * sv);
+      }
+      acc = wave_butterfly(acc);
+      if (lane == 0) red[vi][wv] = acc;
+    }
+  }
+  __syncthreads();
+  if (t < nv) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+}
+
 // The presence byte of each row of a box stencil in the ELL layout (8 codes per row):
 // bit e set when the row holds neighbour e (march_code).  Built once at assembly.
 template <bool D2>
@@ -2148,6 +2258,28 @@ extern "C" int msk_spmv_mdot(int32_t nrows, const int32_t* rowptr, const int32_t
   if (vec_var()) { if (g2) MSK_SMD(1, 2); else MSK_SMD(1, 4); }
   else { if (g2) MSK_SMD(0, 2); else MSK_SMD(0, 4); }
 #undef MSK_SMD
+  return (int)hipGetLastError();
+}
+
+extern "C" int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval,
+                                 const double* x, const double* sdev, double* y, const Vecs* V, int nv, double* partial,
+                                 int64_t nchunks, const int* stop, hipStream_t s) {
+  if (n <= 0 || nchunks <= 0) return 0;
+  if (nx < 2 || nx > 2048 || P < nx || nv < 1 || nv > MSK_MAX_GROUP || dv_flags_bad()) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
+  const dim3 g((unsigned)nchunks), b(kT);
+  const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
+#define MSK_BSM(D, VAR_, NT_) \
+  k_box_spmv_mdot<D, VAR_, NT_><<<g, b, lds, s>>>(nx, P, n, mask, dval, x, sdev, y, *V, nv, partial, nchunks, stop)
+#define MSK_BSM2(D)                                              \
+  do {                                                           \
+    if (vec_var()) { if (nty) MSK_BSM(D, 1, true); else MSK_BSM(D, 1, false); } \
+    else { if (nty) MSK_BSM(D, 0, true); else MSK_BSM(D, 0, false); }           \
+  } while (0)
+  if (d2) MSK_BSM2(true);
+  else MSK_BSM2(false);
+#undef MSK_BSM2
+#undef MSK_BSM
   return (int)hipGetLastError();
 }
 

@@ -1241,6 +1241,24 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
   msp_ctx* c = A->ctx;
   const int64_t n = A->nrows;
   const int64_t nch = nchunks_of(n);
+  if (c->reduce == MSP_REDUCE_DBR && A->dv_on && box_march(A) && A->march_nx <= 2048 && nv >= 1 &&
+      nv <= MSPI_MAX_GROUP && nch > 0 && (msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT)) {
+    int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
+    if (rc) return rc;
+    {
+      // the march's bytes (presence byte, x, W written) and MDot's nv basis vectors; W is not re-read
+      KTimer kt(c, MSP_KERNEL_SPMVDOT, march_bytes(A, false, false) + 8.0 * (double)n * nv);
+      Vecs vg = {};
+      vg.base = base;
+      vg.stride = stride;
+      vg.scale = scale;
+      const int64_t P = (int64_t)A->march_nx * A->march_ny;
+      KCHK(msk_box_spmv_mdot(A->march_nx, P, n, A->march_d2, A->march_mask, A->dv_val, x, sdev, y, &vg, nv,
+                             c->partial, nch, stop, c->stream));
+    }
+    KCHK(msk_dot_stage2(c->partial, nch, nv, out_dev, stop, c->stream));
+    return MSP_SUCCESS;
+  }
   if (c->reduce == MSP_REDUCE_SEQ || A->matfree || A->compressed || A->csr_released || A->nrows != A->ncols ||
       A->lds_cap512 <= 0 || nv < 1 ||
       nv > MSPI_MAX_GROUP ||

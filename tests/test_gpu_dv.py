@@ -299,10 +299,10 @@ def test_ell_xcd_block_order_bitwise(ctx, oracle, flags, nz):
 
 
 
-MARCH_OFF, MARCH_NOXCD = 268435456, 536870912
+MARCH_OFF, MARCH_NOXCD, BOX_MDOT = 268435456, 536870912, 1073741824
 
 
-@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF])
+@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF, BOX_MDOT])
 @pytest.mark.parametrize("shape", [(256, 16, 40), (512, 3, 17), (256, 1, 1), (256, 5, 16), (768, 2, 33),
                                    (256, 40, 7), (256, 100, 40), (37, 11, 9), (64, 64, 64), (100, 30, 20),
                                    (300, 7, 5), (1, 1, 9), (16, 16, 1), (2, 3, 50), (129, 2, 3)])
@@ -400,7 +400,7 @@ def test_box_march_lines_bitwise(ctx, oracle, lines, zt, shape, mode):
     assert np.array_equal(xv.get_array(), xo)
 
 
-@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF])
+@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF, BOX_MDOT])
 @pytest.mark.parametrize("shape", [(256, 64), (100, 37), (1024, 9), (33, 7), (1, 50), (300, 1), (512, 40)])
 @pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 0.0)])
 def test_box_march_2d_bitwise(ctx, oracle, flags, shape, peclet):
@@ -473,8 +473,9 @@ def _gmres_vs_oracle(ctx, oracle, A, O, b, restart=30, max_it=30):
     assert np.array_equal(xv.get_array(), xo)
 
 
+@pytest.mark.parametrize("flags", [0, BOX_MDOT])
 @pytest.mark.parametrize("case", ["3d_256", "3d_ragged", "2d_configs0_block", "3d_convdiff", "3d_dropped"])
-def test_assembled_box_takes_the_march(ctx, oracle, case):
+def test_assembled_box_takes_the_march(ctx, oracle, case, flags):
     """An operator the caller assembles (the reference's poisson3DMatrix / poisson2DMatrix rows cut to a block by
     MatCreateSubMatrix, utils.c:30-121, :247-293, :450-478) handed to msp_mat_create_csr -- the path the PETSc
     plugin's MatAssemblyEnd takes -- is recognised as a box stencil and runs the z-march SpMV: MatMult, MatResidual
@@ -505,7 +506,9 @@ def test_assembled_box_takes_the_march(ctx, oracle, case):
     assert A.spmv_kernel() == "k_spmv_box_march"
     _products(ctx, A, O, np.random.default_rng(SEED))
     b = O.mult(np.ones(n)) if case == "3d_256" else O.mult(r.uniform(-1, 1, n))
-    _gmres_vs_oracle(ctx, oracle, A, O, b, max_it=30 if case == "3d_256" else 45)
+    from test_gpu_kernels import tuning
+    with tuning(flags):     # BOX_MDOT: the GMRES MatMult fused with the VecMDot (k_box_spmv_mdot)
+        _gmres_vs_oracle(ctx, oracle, A, O, b, max_it=30 if case == "3d_256" else 45)
 
 
 @pytest.mark.parametrize("wrap", ["x_minus", "x_plus", "y_minus", "y_plus", "x_minus_2d"])
