@@ -53,7 +53,8 @@ KERNEL_NAMES = {"mdot": "k_dot_stage1+2 (VecMDot, DBR)",
                 "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy",
                 "spmm": "k_spmm (MatMatMult R = A S)", "dgemv": "k_dense_gemv (LSQR R v - alpha u + norm; S alpha)",
                 "dgemvt": "k_scaled_dot (LSQR scale + R^T u)",
-                "spmvdot": "k_spmv_mdot (GMRES MatMult fused with VecMDot stage 1)"}
+                "spmvdot": "k_box_spmv_mdot_march (GMRES MatMult of the box stencil fused with VecMDot stage 1: "
+                           "W not re-read)"}
 SPMV_NAMES = {"dv": "k_spmv_ell (MatMult/MatResidual, DV storage: one byte per entry)",
               "csr": "k_spmv_lds8 (MatMult/MatResidual, CSR storage)",
               "matfree": "k_stencil_spmv (MatMult/MatResidual, matrix-free)"}

@@ -74,7 +74,10 @@ enum {
   MSK_TUNE_ELL_MARCH_OFF = 268435456, // box-stencil DV SpMV: the row-parallel ELL kernel (default: the z-march
                                       // kernel for every 3D box stencil with lo = hi = 0)
   MSK_TUNE_ELL_MARCH_NOXCD = 536870912, // z-march kernel: identity block order (default: XCD-contiguous runs)
-  MSK_TUNE_GM_BOX_MDOT = 1073741824   // GMRES on a box stencil: MatMult fused with the VecMDot (k_box_spmv_mdot)
+  MSK_TUNE_GM_BOX_MDOT_OFF = 1073741824, // GMRES on a box stencil: separate MatMult and VecMDot kernels (default:
+                                         // fused, k_box_spmv_mdot[_march]: W not re-read, +2.6-2.8 % per step)
+  MSK_TUNE_BOX_MDOT_NOXCD = 524288, // k_box_spmv_mdot_march: tiles in plane order (default: XCD-contiguous eighths)
+  MSK_TUNE_BOX_MDOT_FLAT = 32  // k_box_spmv_mdot: one plane per workgroup even where planes hold whole chunks (no z-march)
 };
 
 extern "C" {

@@ -1618,6 +1618,134 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot(int32_t nx, int64_t P, int
   if (t < nv) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
 }
 
+// The same fused step marching in z: when a plane holds a whole number of DBR chunks (P % 4096 == 0),
+// chunk c + P/4096 is chunk c's tile one plane up, so workgroup w takes tile w % cpp through zt
+// planes.  The lane's own x rows of planes z-1, z, z+1 stay in registers (xm, xc, xp); per plane
+// only x(z+1), the two halo lines of the window and the presence bytes are loaded, the window's
+// own rows are written to LDS from xc.  W and every dot are the unmarched kernel's, bit for bit.
+template <int VAR, bool NTY>
+__global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
+                                                            const uint8_t* __restrict__ mask,
+                                                            const double* __restrict__ dval,
+                                                            const double* __restrict__ x,
+                                                            const double* __restrict__ sdev, double* __restrict__ y,
+                                                            Vecs V, int nv, double* __restrict__ partial,
+                                                            int64_t nchunks, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sx = reinterpret_cast<double*>(smem);  // window of plane z: kChunk + 2 nx doubles
+  __shared__ double red[MSK_MAX_GROUP][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t cpp = P / kChunk;
+  int64_t tile, zg;
+  if (xcd) {  // XCD x (workgroups x, x+8, ...) takes a contiguous eighth of the plane's tiles: neighbouring tiles
+              // share their halo lines through that XCD's L2
+    const int64_t per = cpp / 8, slot = blockIdx.x / 8;
+    tile = (blockIdx.x % 8) * per + slot % per;
+    zg = slot / per;
+  } else {
+    tile = blockIdx.x % cpp;
+    zg = blockIdx.x / cpp;
+  }
+  const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
+  const double sc = *sdev;
+  double v[7];
+  march_values<false>(dval, v);
+  const int nh = nx / 2;  // double2 per halo line
+  double xm[2 * kIters], xc[2 * kIters], xp[2 * kIters];
+  {
+    const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * t;
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double2 a = *reinterpret_cast<const double2*>(x + b0 + j * (2 * kT));
+      xc[2 * j] = a.x;
+      xc[2 * j + 1] = a.y;
+      if (z0 > 0) {
+        const double2 m2 = *reinterpret_cast<const double2*>(x + b0 - P + j * (2 * kT));
+        xm[2 * j] = m2.x;
+        xm[2 * j + 1] = m2.y;
+      } else {
+        xm[2 * j] = xm[2 * j + 1] = 0.0;
+      }
+    }
+  }
+  for (int32_t z = z0; z < z1; ++z) {
+    const int64_t c = (int64_t)z * cpp + tile, c0 = c * kChunk, base = c0 + 2 * t;
+    uint32_t m[kIters];
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {  // plane z+1, the presence bytes: issued before the LDS turn-around
+      if (z + 1 < nz) {
+        const double2 p2 = *reinterpret_cast<const double2*>(x + base + P + j * (2 * kT));
+        xp[2 * j] = p2.x;
+        xp[2 * j + 1] = p2.y;
+      } else {
+        xp[2 * j] = xp[2 * j + 1] = 0.0;
+      }
+      m[j] = *reinterpret_cast<const uint16_t*>(mask + base + j * (2 * kT));
+    }
+    double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0);
+    const bool hasl = t < nh && c0 - nx >= 0, hash = t < nh && c0 + kChunk + nx <= (int64_t)nz * P;
+    if (hasl) hl = *reinterpret_cast<const double2*>(x + c0 - nx + 2 * t);
+    if (hash) hh = *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * t);
+    __syncthreads();  // the previous plane's window reads (and its partial writes) are done
+#pragma unroll
+    for (int j = 0; j < kIters; ++j)
+      *reinterpret_cast<double2*>(sx + nx + j * (2 * kT) + 2 * t) = make_double2(xc[2 * j], xc[2 * j + 1]);
+    if (t < nh) {
+      *reinterpret_cast<double2*>(sx + 2 * t) = hl;
+      *reinterpret_cast<double2*>(sx + nx + kChunk + 2 * t) = hh;
+    }
+    for (int i = t + kT; i < nh; i += kT) {  // nx > 512: the rest of the halo lines
+      *reinterpret_cast<double2*>(sx + 2 * i) =
+          c0 - nx >= 0 ? *reinterpret_cast<const double2*>(x + c0 - nx + 2 * i) : make_double2(0.0, 0.0);
+      *reinterpret_cast<double2*>(sx + nx + kChunk + 2 * i) =
+          c0 + kChunk + nx <= (int64_t)nz * P ? *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * i)
+                                              : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    double wr[2 * kIters];
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int e = j * (2 * kT) + 2 * t + q + nx;
+        const uint32_t mr = (m[j] >> (8 * q)) & 255u;
+        const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], xc[2 * j + q], sx[e + 1], sx[e + nx],
+                              xp[2 * j + q]};
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+          if (mr & (1u << k)) s = s + v[k] * (xq[k] * sc);
+        wr[2 * j + q] = s;
+      }
+      if constexpr (NTY) {
+        dx2 o;
+        o.x = wr[2 * j];
+        o.y = wr[2 * j + 1];
+        __builtin_nontemporal_store(o, reinterpret_cast<dx2*>(y + base + j * (2 * kT)));
+      } else {
+        *reinterpret_cast<double2*>(y + base + j * (2 * kT)) = make_double2(wr[2 * j], wr[2 * j + 1]);
+      }
+    }
+    int g = 0;
+#pragma unroll 1
+    for (; g + 4 <= nv; g += 4) dot_group_full<4, VAR>(wr, V, base, 0, nv, g, red, lane, wv);
+    switch (nv - g) {
+      case 3: dot_group_full<3, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 2: dot_group_full<2, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 1: dot_group_full<1, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      default: break;
+    }
+    __syncthreads();
+    if (t < nv) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+#pragma unroll
+    for (int i = 0; i < 2 * kIters; ++i) {
+      xm[i] = xc[i];
+      xc[i] = xp[i];
+    }
+  }
+}
+
 // The presence byte of each row of a box stencil in the ELL layout (8 codes per row):
 // bit e set when the row holds neighbour e (march_code).  Built once at assembly.
 template <bool D2>
@@ -2269,6 +2397,27 @@ extern "C" int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const
   const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
   const dim3 g((unsigned)nchunks), b(kT);
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
+  if (!d2 && P % kChunk == 0 && n % P == 0 && (nx & 1) == 0 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_FLAT)) {
+    // whole chunks per plane: march zt planes per workgroup (MSPLIT_BOXMDOT_ZT overrides the depth, A/B)
+    static const int zenv = [] {
+      const char* e = getenv("MSPLIT_BOXMDOT_ZT");
+      return e ? atoi(e) : 0;
+    }();
+    const int32_t nz = (int32_t)(n / P);
+    const int32_t zt = zenv > 0 ? zenv : 2;
+    const int64_t grid = (P / kChunk) * ((nz + zt - 1) / zt);
+    if (grid > INT32_MAX) return (int)hipErrorInvalidValue;
+    // XCD-contiguous eighths from 32 tiles per plane (SMSM's 512^2 planes: +1.9 % over plane order, same box);
+    // smaller planes in plane order (256^2: +1.4 % over the eighths; profiles/r03/boxmdot/xcd/)
+    const int xcd = (P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD);
+#define MSK_BSMM(VAR_, NT_)                                                                                       \
+  k_box_spmv_mdot_march<VAR_, NT_><<<dim3((unsigned)grid), b, lds, s>>>(nx, P, nz, zt, xcd, mask, dval, x, sdev, y, *V, nv, \
+                                                                        partial, nchunks, stop)
+    if (vec_var()) { if (nty) MSK_BSMM(1, true); else MSK_BSMM(1, false); }
+    else { if (nty) MSK_BSMM(0, true); else MSK_BSMM(0, false); }
+#undef MSK_BSMM
+    return (int)hipGetLastError();
+  }
 #define MSK_BSM(D, VAR_, NT_) \
   k_box_spmv_mdot<D, VAR_, NT_><<<g, b, lds, s>>>(nx, P, n, mask, dval, x, sdev, y, *V, nv, partial, nchunks, stop)
 #define MSK_BSM2(D)                                              \

@@ -1242,7 +1242,7 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
   const int64_t n = A->nrows;
   const int64_t nch = nchunks_of(n);
   if (c->reduce == MSP_REDUCE_DBR && A->dv_on && box_march(A) && A->march_nx <= 2048 && nv >= 1 &&
-      nv <= MSPI_MAX_GROUP && nch > 0 && (msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT)) {
+      nv <= MSPI_MAX_GROUP && nch > 0 && !(msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT_OFF)) {
     int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
     if (rc) return rc;
     {

@@ -299,13 +299,14 @@ def test_ell_xcd_block_order_bitwise(ctx, oracle, flags, nz):
 
 
 
-MARCH_OFF, MARCH_NOXCD, BOX_MDOT = 268435456, 536870912, 1073741824
+MARCH_OFF, MARCH_NOXCD, BOX_SEPARATE, BOX_FLAT, BOX_NOXCD = 268435456, 536870912, 1073741824, 32, 524288
 
 
-@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF, BOX_MDOT])
+@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF, BOX_SEPARATE, BOX_FLAT, BOX_NOXCD])
 @pytest.mark.parametrize("shape", [(256, 16, 40), (512, 3, 17), (256, 1, 1), (256, 5, 16), (768, 2, 33),
                                    (256, 40, 7), (256, 100, 40), (37, 11, 9), (64, 64, 64), (100, 30, 20),
-                                   (300, 7, 5), (1, 1, 9), (16, 16, 1), (2, 3, 50), (129, 2, 3)])
+                                   (300, 7, 5), (1, 1, 9), (16, 16, 1), (2, 3, 50), (129, 2, 3),
+                                   (256, 16, 7), (1024, 4, 9), (2048, 2, 5), (64, 128, 6), (256, 512, 5)])
 @pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 0.3)])
 def test_box_march_bitwise(ctx, oracle, flags, shape, peclet):
     """The z-march SpMV of box stencils (the default for 3D boxes; MSK_TUNE_ELL_MARCH_NOXCD: identity workgroup
@@ -400,7 +401,7 @@ def test_box_march_lines_bitwise(ctx, oracle, lines, zt, shape, mode):
     assert np.array_equal(xv.get_array(), xo)
 
 
-@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF, BOX_MDOT])
+@pytest.mark.parametrize("flags", [0, MARCH_NOXCD, MARCH_OFF, BOX_SEPARATE])
 @pytest.mark.parametrize("shape", [(256, 64), (100, 37), (1024, 9), (33, 7), (1, 50), (300, 1), (512, 40)])
 @pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 0.0)])
 def test_box_march_2d_bitwise(ctx, oracle, flags, shape, peclet):
@@ -473,7 +474,7 @@ def _gmres_vs_oracle(ctx, oracle, A, O, b, restart=30, max_it=30):
     assert np.array_equal(xv.get_array(), xo)
 
 
-@pytest.mark.parametrize("flags", [0, BOX_MDOT])
+@pytest.mark.parametrize("flags", [0, BOX_SEPARATE, BOX_FLAT])
 @pytest.mark.parametrize("case", ["3d_256", "3d_ragged", "2d_configs0_block", "3d_convdiff", "3d_dropped"])
 def test_assembled_box_takes_the_march(ctx, oracle, case, flags):
     """An operator the caller assembles (the reference's poisson3DMatrix / poisson2DMatrix rows cut to a block by
@@ -507,7 +508,7 @@ def test_assembled_box_takes_the_march(ctx, oracle, case, flags):
     _products(ctx, A, O, np.random.default_rng(SEED))
     b = O.mult(np.ones(n)) if case == "3d_256" else O.mult(r.uniform(-1, 1, n))
     from test_gpu_kernels import tuning
-    with tuning(flags):     # BOX_MDOT: the GMRES MatMult fused with the VecMDot (k_box_spmv_mdot)
+    with tuning(flags):     # 0: the GMRES MatMult fused with the VecMDot (k_box_spmv_mdot); BOX_SEPARATE: two kernels
         _gmres_vs_oracle(ctx, oracle, A, O, b, max_it=30 if case == "3d_256" else 45)
 
 

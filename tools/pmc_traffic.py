@@ -21,6 +21,8 @@ from collections import defaultdict
 
 
 def classify(name: str):
+    if "spmv_mdot" in name:     # the GMRES MatMult fused with VecMDot (k_box_spmv_mdot[_march], k_spmv_mdot)
+        return "spmvdot"
     if "k_maxpy" in name:
         return "maxpy"
     if "k_dot_stage1" in name:
@@ -106,6 +108,10 @@ def main():
                 alg = sum(8.0 * N * (nv + k) for nv in nvs) / m
         elif cls == "norm":
             alg = 8.0 * N
+        elif cls == "spmvdot" and m % 30 == 0:
+            # one GMRES(30) solve in dispatch order: the Arnoldi step it reads nv = it + 1 basis vectors; the
+            # march's bytes (presence byte, x, W written) plus those vectors, W not re-read
+            alg = sum(17.0 * N + 8.0 * N * ((i % 30) + 1) for i in range(m)) / m
         elif cls == "spmv":
             als = [spmv_alg(nm, a.n) for nm, _ in F[:m]]
             if all(als):
