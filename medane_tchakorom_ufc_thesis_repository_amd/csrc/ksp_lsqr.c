@@ -285,18 +285,30 @@ int msp_lsqr_solve(msp_lsqr *l, msp_vec *const *b, msp_vec *x) {
   if ((rc = gather(l, l->gloc, l->gall, s)) || (rc = mspi_ls_first(c, d, l->o.exact_norm ? l->fall : NULL)))
     return rc;
 
+  /* Deferred VecScale (DBR order): U1 *= 1/beta is applied where U1 is read -- in the R^T U1 dots and, as U, in
+   * the next step's R V - alpha U -- instead of being written back: the same roundings, one N-vector write per
+   * step less (SEQ mode re-reads the scaled U1 for its sequential sums, so it keeps the write). */
+  static int write_back = -1; /* MSPLIT_LSQR_SCALE_WRITE=1: the round-2 write-back (same-box A/B) */
+  if (write_back < 0) {
+    const char *e = getenv("MSPLIT_LSQR_SCALE_WRITE");
+    write_back = e && e[0] == '1';
+  }
+  const int defer = !seq && !write_back;
   const int nsteps = l->o.max_it > 0 ? l->o.max_it : 1; /* the do-while runs at least once */
   for (int i = 0; i < nsteps; ++i) {
     double **U = l->U + (i & 1 ? nloc : 0);
     double **U1 = l->U + (i & 1 ? 0 : nloc);
+    /* U of step 0 is the scaled b (written by the first dots); later it is the previous U1, stored unscaled,
+     * whose scale 1/beta is still in st->uscale until this step's beta replaces it */
+    const double *usc = defer && i > 0 ? &d.st->uscale : NULL;
     for (int k = 0; k < nloc; ++k)
-      if ((rc = mspi_dense_gemv(c, l->R[k]->d, l->R[k]->lda, s, l->R[k]->nrows, d.V, &d.st->nalpha, U[k], U1[k],
-                                l->partial, l->gloc + k, stop)))
+      if ((rc = mspi_dense_gemv(c, l->R[k]->d, l->R[k]->lda, s, l->R[k]->nrows, d.V, &d.st->nalpha, U[k], usc,
+                                U1[k], l->partial, l->gloc + k, stop)))
         return rc;
     if (seq && (rc = seq_chain(l, U1, 0, NULL, 1, 0, l->gloc, 1))) return rc;
     if ((rc = gather(l, l->gloc, l->gall, 1)) || (rc = mspi_ls_beta(c, d))) return rc;
     for (int k = 0; k < nloc; ++k)
-      if ((rc = mspi_dense_scaled_dots(c, U1[k], U1[k], &d.st->uscale, l->R[k]->d, l->R[k]->lda, s,
+      if ((rc = mspi_dense_scaled_dots(c, U1[k], defer ? NULL : U1[k], &d.st->uscale, l->R[k]->d, l->R[k]->lda, s,
                                        l->R[k]->nrows, l->partial, l->gloc + k * s, stop)))
         return rc;
     if (seq && (rc = seq_chain(l, NULL, 1, U1, s, 0, l->gloc, s))) return rc;

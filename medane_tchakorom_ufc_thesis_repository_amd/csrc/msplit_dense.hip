@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -73,7 +74,7 @@ __device__ __forceinline__ double wave_butterfly(double v) {
 template <bool AXPY, bool NORM, bool FULL, int VEC, int G, bool NTS>
 __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t lda, int nc,
                                           const double* __restrict__ coef, double nal, const double* __restrict__ U,
-                                          double* __restrict__ y, int64_t base, int64_t n, double& sq) {
+                                          double usc, double* __restrict__ y, int64_t base, int64_t n, double& sq) {
   double u[2 * kIters];
 #pragma unroll
   for (int j = 0; j < 2 * kIters; ++j) u[j] = 0.0;
@@ -127,10 +128,10 @@ __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t 
     const int64_t e = base + j * (2 * kT);
     double r0 = u[2 * j], r1 = u[2 * j + 1];
     if (FULL) {
-      if (AXPY && nal != 0.0) {
+      if (AXPY && nal != 0.0) {  // U stored unscaled: its value is U * usc, the rounding VecScale stored
         const double2 q = *reinterpret_cast<const double2*>(U + e);
-        r0 = r0 + nal * q.x;
-        r1 = r1 + nal * q.y;
+        r0 = r0 + nal * (q.x * usc);
+        r1 = r1 + nal * (q.y * usc);
       }
       st2<NTS>(y + e, r0, r1);
       if (NORM) {
@@ -139,12 +140,12 @@ __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t 
       }
     } else {
       if (e < n) {
-        if (AXPY && nal != 0.0) r0 = r0 + nal * U[e];
+        if (AXPY && nal != 0.0) r0 = r0 + nal * (U[e] * usc);
         y[e] = r0;
         if (NORM) acc = acc + r0 * r0;
       }
       if (e + 1 < n) {
-        if (AXPY && nal != 0.0) r1 = r1 + nal * U[e + 1];
+        if (AXPY && nal != 0.0) r1 = r1 + nal * (U[e + 1] * usc);
         y[e + 1] = r1;
         if (NORM) acc = acc + r1 * r1;
       }
@@ -156,16 +157,19 @@ __device__ __forceinline__ void gemv_body(const double* __restrict__ A, int64_t 
 template <bool AXPY, bool NORM, int VEC, int G, bool NTS>
 __global__ __launch_bounds__(kT) void k_dense_gemv(const double* __restrict__ A, int64_t lda, int nc,
                                                    const double* __restrict__ coef, const double* __restrict__ naldev,
-                                                   const double* __restrict__ U, double* __restrict__ y, int64_t n,
+                                                   const double* __restrict__ U, const double* __restrict__ uscdev,
+                                                   double* __restrict__ y, int64_t n,
                                                    double* __restrict__ partial, const int* __restrict__ stop) {
   if (stopped(stop)) return;
   const int t = threadIdx.x;
   const int64_t c = blockIdx.x;
   const int64_t base = c * kChunk + 2 * t;
   const double nal = AXPY ? *naldev : 0.0;
+  const double usc = uscdev ? *uscdev : 1.0;  // x * 1.0 == x: no scale leaves U as stored
   double sq = 0.0;
-  if (VEC && (c + 1) * kChunk <= n) gemv_body<AXPY, NORM, true, VEC, G, NTS>(A, lda, nc, coef, nal, U, y, base, n, sq);
-  else gemv_body<AXPY, NORM, false, VEC, 1, NTS>(A, lda, nc, coef, nal, U, y, base, n, sq);
+  if (VEC && (c + 1) * kChunk <= n)
+    gemv_body<AXPY, NORM, true, VEC, G, NTS>(A, lda, nc, coef, nal, U, usc, y, base, n, sq);
+  else gemv_body<AXPY, NORM, false, VEC, 1, NTS>(A, lda, nc, coef, nal, U, usc, y, base, n, sq);
   if (NORM) {
     __shared__ double red[4];
     sq = wave_butterfly(sq);
@@ -205,7 +209,8 @@ __global__ __launch_bounds__(kT) void k_scaled_dot(const double* win, double* wo
     if (SCALE) {
       wr[2 * j] = wr[2 * j] * sc;
       wr[2 * j + 1] = wr[2 * j + 1] * sc;
-      if (full) {
+      if (!wout) {  // deferred VecScale: the scaled values are only dotted, the next reader rescales
+      } else if (full) {
         st2<NTS>(wout + e, wr[2 * j], wr[2 * j + 1]);
       } else {
         if (e < n) wout[e] = wr[2 * j];
@@ -420,8 +425,8 @@ static bool dense_tuning(int* grp, bool* nts) {
 
 // ===================================================================== internal
 extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc, int64_t n, const double* coef_dev,
-                               const double* nal_dev, const double* U, double* y, double* partial, double* sumsq_dev,
-                               const int* stop) {
+                               const double* nal_dev, const double* U, const double* usc_dev, double* y,
+                               double* partial, double* sumsq_dev, const int* stop) {
   if (n <= 0) {
     if (sumsq_dev) HIPCHK(hipMemsetAsync(sumsq_dev, 0, sizeof(double), c->stream));
     return MSP_SUCCESS;
@@ -436,7 +441,8 @@ extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc,
   bool nts = true;
   if (!dense_tuning(&grp, &nts)) return MSP_ERR_ARG_OUTOFRANGE;
 #define GEMVK(AX, NO, VE, G_, NT_) \
-  k_dense_gemv<AX, NO, VE, G_, NT_><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, y, n, partial, stop)
+  k_dense_gemv<AX, NO, VE, G_, NT_><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, usc_dev, y, n, partial, \
+                                                            stop)
 #define GEMV(AX, NO, VE)                                         \
   do {                                                           \
     if (nts) {                                                   \
@@ -476,7 +482,7 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
     HIPCHK(hipMemsetAsync(out_dev, 0, (size_t)nc * sizeof(double), c->stream));
     return MSP_SUCCESS;
   }
-  KTimer kt(c, MSP_KERNEL_DGEMVT, 8.0 * (double)n * (nc + 1 + (sc_dev ? 1 : 0)));
+  KTimer kt(c, MSP_KERNEL_DGEMVT, 8.0 * (double)n * (nc + 1 + (sc_dev && wout ? 1 : 0)));
   int grp = 4;
   bool nts = true;
   if (!dense_tuning(&grp, &nts)) return MSP_ERR_ARG_OUTOFRANGE;
@@ -485,8 +491,9 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
   for (int g0 = 0; g0 < nc; g0 += kMaxCols) {
     const int g = std::min(kMaxCols, nc - g0);
     const double* Ag = A + (int64_t)g0 * lda;
-    const bool scale = sc_dev && g0 == 0;          // scale once, later groups read the scaled vector
-    const double* src = (sc_dev && g0 > 0) ? wout : win;
+    // scale once, later groups read the scaled vector; without wout (deferred scale) every group rescales win
+    const bool scale = sc_dev && (g0 == 0 || !wout);
+    const double* src = (sc_dev && g0 > 0 && wout) ? wout : win;
     const dim3 gr((unsigned)nch), b(kT);
 #define SDOTK(SC, VE, WO, SD, G_, NT_) \
   k_scaled_dot<SC, VE, G_, NT_><<<gr, b, 0, c->stream>>>(src, WO, SD, Ag, lda, g, n, partial, nch, stop)
@@ -515,6 +522,7 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
 #undef SDOTK
     KCHK((int)hipGetLastError());
     if (mspi_reduce_seq(c)) {  // dgemv 'T' order: each column . w in sequence (msplit_seq.hip)
+      ARGCHK(!sc_dev || wout, MSP_ERR_SUP, "MSP_REDUCE_SEQ reads the scaled vector back: no deferred scale");
       Vecs v = {};
       v.base = Ag;
       v.stride = lda;
@@ -674,7 +682,19 @@ extern "C" int msp_dense_create_view(msp_dense* A, int32_t col0, int32_t ncols, 
 }
 
 // ======================================================================= dense
-static int64_t lda_for(int64_t nrows) { return std::max<int64_t>(512, (nrows + 511) / 512 * 512); }
+// MSPLIT_DENSE_SKEW (doubles, rounded up to 512): extra leading-dimension padding for blocks of at least 2^20
+// rows, so that the columns of a tall block are not an exact power-of-two apart (same-box A/B knob).
+static int64_t lda_skew() {
+  static const int64_t sk = [] {
+    const char* e = getenv("MSPLIT_DENSE_SKEW");
+    return e ? (atoll(e) + 511) / 512 * 512 : (int64_t)0;
+  }();
+  return sk;
+}
+static int64_t lda_for(int64_t nrows) {
+  const int64_t l = std::max<int64_t>(512, (nrows + 511) / 512 * 512);
+  return nrows >= (int64_t(1) << 20) ? l + lda_skew() : l;
+}
 
 extern "C" int msp_dense_create(msp_ctx* c, int64_t nrows, int32_t ncols, msp_dense** out) {
   ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");
@@ -766,8 +786,8 @@ extern "C" int msp_dense_mult(msp_dense* A, const msp_vec* alpha, int64_t row0, 
          (long long)alpha->n, A->ncols);
   ARGCHK(n >= 0 && row0 >= 0 && row0 + n <= A->nrows && yoff >= 0 && yoff + n <= y->n, MSP_ERR_ARG_OUTOFRANGE,
          "dense mult range out of bounds");
-  return mspi_dense_gemv(A->ctx, A->d + row0, A->lda, A->ncols, n, alpha->d, nullptr, nullptr, y->d + yoff, nullptr,
-                         nullptr, nullptr);
+  return mspi_dense_gemv(A->ctx, A->d + row0, A->lda, A->ncols, n, alpha->d, nullptr, nullptr, nullptr, y->d + yoff,
+                         nullptr, nullptr, nullptr);
 }
 
 extern "C" int msp_dense_mult_transpose(msp_dense* A, const msp_vec* u, msp_vec* out) {

@@ -66,12 +66,14 @@ struct msp_dense {
   int view; /* msp_dense_create_view: columns of another block, storage not freed */
 };
 
-/* y = A[:, 0:nc] coef (+ (*nal_dev) U when U != NULL, skipped when *nal_dev == 0);
+/* y = A[:, 0:nc] coef (+ (*nal_dev) U when U != NULL, skipped when *nal_dev == 0); usc_dev != NULL: U is
+ * stored unscaled and its value is U * (*usc_dev) (a deferred VecScale, rounded as the scale would have been);
  * sumsq_dev != NULL: also ||y||^2 (DBR; partial holds nchunks doubles). */
 int mspi_dense_gemv(msp_ctx *ctx, const double *A, int64_t lda, int nc, int64_t n, const double *coef_dev,
-                    const double *nal_dev, const double *U, double *y, double *partial, double *sumsq_dev,
-                    const int *stop);
-/* sc_dev != NULL: wout = win * (*sc_dev) first; out_dev[j] = column_j . w (DBR), j < nc.
+                    const double *nal_dev, const double *U, const double *usc_dev, double *y, double *partial,
+                    double *sumsq_dev, const int *stop);
+/* sc_dev != NULL: w = win * (*sc_dev) first, stored to wout unless wout == NULL (deferred: the next reader
+ * scales); out_dev[j] = column_j . w (DBR), j < nc.
  * partial holds nchunks*32 doubles. */
 int mspi_dense_scaled_dots(msp_ctx *ctx, const double *win, double *wout, const double *sc_dev, const double *A,
                            int64_t lda, int nc, int64_t n, double *partial, double *out_dev, const int *stop);
