@@ -168,7 +168,15 @@ __device__ inline double fold_partials(const double* __restrict__ p, int64_t nch
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double acc = 0.0;
   int64_t i = t;
-  for (; i + 7 * kUT < nchunks; i += 8 * kUT) {  // k_dot_stage2's order: lane t adds p[t], p[t+256], ...
+  // k_dot_stage2's order: lane t adds p[t], p[t+256], ... (16 loads in flight, then 8, then one at a time)
+  for (; i + 15 * kUT < nchunks; i += 16 * kUT) {
+    double q[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) q[u] = p[i + u * kUT];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = acc + q[u];
+  }
+  for (; i + 7 * kUT < nchunks; i += 8 * kUT) {
     double q[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) q[u] = p[i + u * kUT];
@@ -183,24 +191,36 @@ __device__ inline double fold_partials(const double* __restrict__ p, int64_t nch
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// The state, the column h(0..m+1), cc, ss and grs are loaded into LDS by all lanes together with the
+// partials, so the serial recurrence of lane 0 waits for one round of loads, not one per field; the
+// state is stored back at the end.  m = the restart length the arrays are sized for (st->m).
+constexpr int kStW = (int)(sizeof(mspi_gmres_state) / sizeof(int32_t));
+static_assert(sizeof(mspi_gmres_state) % sizeof(int32_t) == 0, "state copied as 32-bit words");
+static_assert(kStW <= kUT, "one word per lane");
+
 __global__ __launch_bounds__(kUT) void k_norm_update(mspi_gmres_dev g, const double* __restrict__ partial,
-                                                     int64_t nchunks) {
-  mspi_gmres_state* st = g.st;
-  if (st->stop) return;  // uniform: every lane reads the same flag
+                                                     int64_t nchunks, int m) {
   __shared__ double red[4];
-  extern __shared__ double lds[];  // hh column (m+2), cc (m+2), ss (m+2)
-  const int t = threadIdx.x;
-  const int it = st->it, m2 = st->m + 2;
-  const double sumsq = fold_partials(partial, nchunks, red);
+  __shared__ mspi_gmres_state lst;
+  extern __shared__ double lds[];  // hh column, cc, ss, grs: m+2 each
+  const int t = threadIdx.x, m2 = m + 2;
   double* lh = lds;
   double* lc = lds + m2;
   double* ls = lds + 2 * m2;
-  for (int j = t; j <= it; j += kUT) {
+  double* lg = lds + 3 * m2;
+  if (t < kStW) reinterpret_cast<int32_t*>(&lst)[t] = reinterpret_cast<const int32_t*>(g.st)[t];
+  for (int j = t; j < m2; j += kUT) {
     lh[j] = g.h[j];
     lc[j] = g.cc[j];
     ls[j] = g.ss[j];
+    lg[j] = g.grs[j];
   }
-  __syncthreads();
+  const double sumsq = fold_partials(partial, nchunks, red);  // its barrier publishes the LDS copies too
+  if (lst.stop) return;                                       // uniform
+  mspi_gmres_dev gl = g;
+  gl.st = &lst;  // converged() and log_res() on the LDS state
+  mspi_gmres_state* st = &lst;
+  const int it = st->it;
   __shared__ int ncol;
   if (t == 0) {
     g.h[it + 1] = sumsq;
@@ -232,7 +252,7 @@ __global__ __launch_bounds__(kUT) void k_norm_update(mspi_gmres_dev g, const dou
         st->scale = (tt != 0.0) ? 1.0 / tt : 1.0;  // VecNormalize of VV(it+1), deferred to its readers
         g.sc[it + 1] = st->scale;
         hh[it + 1] = tt;
-        double hapbnd = fabs(tt / g.grs[it]);
+        double hapbnd = fabs(tt / lg[it]);
         if (hapbnd > st->haptol) hapbnd = st->haptol;
         if (tt < hapbnd) hapend = 1;
         // KSPGMRESUpdateHessenberg on the LDS column
@@ -249,11 +269,11 @@ __global__ __launch_bounds__(kUT) void k_norm_update(mspi_gmres_dev g, const dou
             const double c = hh[it] / r, sn = hh[it + 1] / r;
             g.cc[it] = c;
             g.ss[it] = sn;
-            const double grs = g.grs[it];
+            const double grs = lg[it];
             g.grs[it + 1] = -(sn * grs);
             g.grs[it] = c * grs;
             hh[it] = c * hh[it] + sn * hh[it + 1];
-            res = fabs(g.grs[it + 1]);
+            res = fabs(-(sn * grs));
           }
         } else {
           res = 0.0;
@@ -264,7 +284,7 @@ __global__ __launch_bounds__(kUT) void k_norm_update(mspi_gmres_dev g, const dou
         st->rnorm = res;
         st->res = res;
         if (!st->reason) {
-          converged(g, st->its, res);
+          converged(gl, st->its, res);
           if (hapend && !st->reason) st->reason = MSP_DIVERGED_BREAKDOWN;
         }
       }
@@ -272,16 +292,17 @@ __global__ __launch_bounds__(kUT) void k_norm_update(mspi_gmres_dev g, const dou
     if (!done) {
       const int itn = st->it;
       if (!st->reason && itn < st->m && st->its < st->max_it) {
-        log_res(g, res);
+        log_res(gl, res);
       } else {
         st->stop = 1;
-        if (itn && (st->reason || st->its >= st->max_it)) log_res(g, res);
+        if (itn && (st->reason || st->its >= st->max_it)) log_res(gl, res);
       }
     }
   }
   __syncthreads();
   double* col = &HHD(0, it);
   for (int j = t; j < ncol; j += kUT) col[j] = lh[j];
+  if (t < kStW) const_cast<int32_t*>(reinterpret_cast<const int32_t*>(g.st))[t] = reinterpret_cast<int32_t*>(&lst)[t];
 }
 
 // KSPGMRESBuildSoln(GRS(0), x, x, ksp, it - 1): back-solve in place (nrs
@@ -338,8 +359,8 @@ extern "C" int mspi_gm_iter_update(msp_ctx* ctx, mspi_gmres_dev g) {
 }
 
 extern "C" int mspi_gm_norm_update(msp_ctx* ctx, mspi_gmres_dev g, const double* partial, int64_t nchunks, int m) {
-  const size_t lds = (size_t)3 * (m + 2) * sizeof(double);
-  k_norm_update<<<1, kUT, lds, mspi_stream(ctx)>>>(g, partial, nchunks);
+  const size_t lds = (size_t)4 * (m + 2) * sizeof(double);
+  k_norm_update<<<1, kUT, lds, mspi_stream(ctx)>>>(g, partial, nchunks, m);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     mspi_set_error(MSP_ERR_LIB, "k_norm_update: %s", hipGetErrorString(e));

@@ -298,15 +298,26 @@ __global__ __launch_bounds__(kT) void k_dot_stage1_op(EllOp op, Vecs V, int64_t 
 }
 
 // Stage 2: workgroup v folds the nchunks partials of vector v the same way.
+template <bool HS>
 __global__ __launch_bounds__(kT) void k_dot_stage2(const double* __restrict__ partial, int64_t nchunks,
                                                    double* __restrict__ out, const int* __restrict__ stop) {
-  if (stopped(stop)) return;
+  // the stop flag (HS: stop is not null) is read together with the partials and tested after the
+  // (convergent) butterfly, so a running cycle waits for one round of loads, not two
+  bool skip = false;
+  if constexpr (HS) skip = *stop != 0;
   __shared__ double red[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const double* p = partial + blockIdx.x * nchunks;
   double acc = 0.0;
   int64_t i = t;
-  // 8 loads in flight per lane, added in the same order (lane t: p[t], p[t+256], ...)
+  // 16, then 8 loads in flight per lane, added in the same order (lane t: p[t], p[t+256], ...)
+  for (; i + 15 * kT < nchunks; i += 16 * kT) {
+    double q[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) q[u] = p[i + u * kT];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = acc + q[u];
+  }
   for (; i + 7 * kT < nchunks; i += 8 * kT) {
     double q[8];
 #pragma unroll
@@ -316,6 +327,7 @@ __global__ __launch_bounds__(kT) void k_dot_stage2(const double* __restrict__ pa
   }
   for (; i < nchunks; i += kT) acc = acc + p[i];
   acc = wave_butterfly(acc);
+  if (skip) return;  // uniform
   if (lane == 0) red[wv] = acc;
   __syncthreads();
   if (t == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
@@ -488,7 +500,7 @@ __global__ __launch_bounds__(kT) void k_maxpy_chunk(const double* win, double* w
   if (nvdev) nv = *nvdev;
   if (nv <= 0) return;
   const int t = threadIdx.x;
-  const int64_t c = blockIdx.x;
+  const int64_t c = (VAR & 64) ? (int64_t)gridDim.x - 1 - blockIdx.x : blockIdx.x;  // 64: top chunks first
   const int64_t base = c * kChunk + 2 * t;
   double sq = 0.0;
   if ((c + 1) * kChunk <= n) maxpy_chunk_body<ACCUM, NORM, true, VAR>(win, wout, V, A, adev, negate, nv, base, n, sq);
@@ -1638,8 +1650,8 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t cpp = P / kChunk;
   int64_t tile, zg;
-  if (xcd) {  // XCD x (workgroups x, x+8, ...) takes a contiguous eighth of the plane's tiles: neighbouring tiles
-              // share their halo lines through that XCD's L2
+  if (xcd & 1) {  // XCD x (workgroups x, x+8, ...) takes a contiguous eighth of the plane's tiles: neighbouring
+                  // tiles share their halo lines through that XCD's L2
     const int64_t per = cpp / 8, slot = blockIdx.x / 8;
     tile = (blockIdx.x % 8) * per + slot % per;
     zg = slot / per;
@@ -1647,6 +1659,7 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     tile = blockIdx.x % cpp;
     zg = blockIdx.x / cpp;
   }
+  if (xcd & 2) zg = (nz + zt - 1) / zt - 1 - zg;  // top plane groups first
   const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
   const double sc = *sdev;
   double v[7];
@@ -2071,7 +2084,8 @@ extern "C" int msk_maxpy_op(const EllOp* op, double* wout, const Vecs* V, int nv
 #if MSK_IN(MSK_PART_DOT)
 extern "C" int msk_dot_stage2(const double* partial, int64_t nchunks, int nv, double* out, const int* stop,
                               hipStream_t s) {
-  k_dot_stage2<<<dim3(nv), dim3(kT), 0, s>>>(partial, nchunks, out, stop);
+  if (stop) k_dot_stage2<true><<<dim3(nv), dim3(kT), 0, s>>>(partial, nchunks, out, stop);
+  else k_dot_stage2<false><<<dim3(nv), dim3(kT), 0, s>>>(partial, nchunks, out, nullptr);
   return (int)hipGetLastError();
 }
 #endif  // part
@@ -2085,6 +2099,15 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
   // unrolled by two unless MSK_TUNE_MAXPY_UNROLL1 (+1.7 % per step: 64-load bursts at one wave per SIMD)
   const int var = vec_var() | ((msk_tuning_flags & MSK_TUNE_MAXPY_TEMPORAL_ST) ? 0 : 4) |
                   ((msk_tuning_flags & MSK_TUNE_MAXPY_HALVES) ? 8 : 0) | ((msk_tuning_flags & MSK_TUNE_MAXPY_UNROLL1) ? 0 : 32);
+  // Top chunk first where a vector outgrows the 256 MiB MALL (n > 2^25): MAXPY then starts on the rows the
+  // fused MatMult+MDot (or the MDot) left in the MALL and ends on those the next one starts with (SMSM's
+  // 512x512x256 block +1.0 %, MAXPY 5.68 -> 5.86 TB/s; at 256^3, where whole vectors fit, -0.7 %; same box,
+  // profiles/r03/rev_ab/).  MSPLIT_MAXPY_REV=0/1 forces either order.
+  static const int rev_env = [] {
+    const char* e = getenv("MSPLIT_MAXPY_REV");
+    return e ? (atoi(e) ? 1 : 0) : -1;
+  }();
+  const int rev = (rev_env < 0 ? n > ((int64_t)1 << 25) : rev_env) ? 64 : 0;
   const unsigned g = (unsigned)((n + kChunk - 1) / kChunk);
 #define MSK_MAXPY_LAUNCH(V_)                                                                                     \
   if (partial)                                                                                                  \
@@ -2105,7 +2128,7 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
     case 32: MSK_MAXPY_LAUNCH(32) break;
     case 33: MSK_MAXPY_LAUNCH(33) break;
     case 36: MSK_MAXPY_LAUNCH(36) break;
-    case 37: MSK_MAXPY_LAUNCH(37) break;
+    case 37: if (rev) { MSK_MAXPY_LAUNCH(101) } else { MSK_MAXPY_LAUNCH(37) } break;
     case 45: MSK_MAXPY_LAUNCH(45) break;
     default: return (int)hipErrorInvalidValue;  // a tuning combination with no kernel: fail, never run another one
   }
@@ -2409,7 +2432,11 @@ extern "C" int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const
     if (grid > INT32_MAX) return (int)hipErrorInvalidValue;
     // XCD-contiguous eighths from 32 tiles per plane (SMSM's 512^2 planes: +1.9 % over plane order, same box);
     // smaller planes in plane order (256^2: +1.4 % over the eighths; profiles/r03/boxmdot/xcd/)
-    const int xcd = (P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD);
+    static const int rev = [] {
+      const char* e = getenv("MSPLIT_BOXMDOT_REV");
+      return e && atoi(e) ? 2 : 0;
+    }();
+    const int xcd = ((P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD)) | rev;
 #define MSK_BSMM(VAR_, NT_)                                                                                       \
   k_box_spmv_mdot_march<VAR_, NT_><<<dim3((unsigned)grid), b, lds, s>>>(nx, P, nz, zt, xcd, mask, dval, x, sdev, y, *V, nv, \
                                                                         partial, nchunks, stop)
