@@ -89,6 +89,9 @@ struct KTimer {
     (void)hipEventRecord(c->pool[ev], c->stream);
     c->recs.push_back({cls, ev, bytes});
   }
+  void set_bytes(double b) {  // the launch turned out to move b algorithmic bytes (this timer's record is the last)
+    if (ev >= 0) c->recs.back().bytes = b;
+  }
   ~KTimer() {
     if (ev >= 0) (void)hipEventRecord(c->pool[ev + 1], c->stream);
   }

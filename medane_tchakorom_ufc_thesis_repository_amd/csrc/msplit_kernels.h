@@ -134,9 +134,10 @@ int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t
                        const int* stop, hipStream_t s);
 // GMRES: y = A (sc*x) for a box stencil with march presence bytes (nx <= 2048; P = the plane, or nx in 2D), fused
 // with the DBR stage 1 of y . V_v (v < nv <= 32) into partial: W in the DBR lane layout, bitwise the march's.
+// *self_out (may be NULL) = 1 when V's last vector is x and its dot came from the march's registers (not re-read).
 int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval,
                       const double* x, const double* sdev, double* y, const Vecs* V, int nv, double* partial,
-                      int64_t nchunks, const int* stop, hipStream_t s);
+                      int64_t nchunks, const int* stop, int* self_out, hipStream_t s);
 // R[:, 0:nc] = A S[:, 0:nc] over DV storage in the ELL layout (W codes per row)
 int msk_spmm_ell(int32_t nrows, int W, const uint8_t* code8, const int32_t* ddelta, const double* dval, int ndict,
                  const double* S, int64_t lds, int nc, double* R, int64_t ldr, hipStream_t s);

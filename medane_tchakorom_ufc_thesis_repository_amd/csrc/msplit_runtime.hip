@@ -1246,15 +1246,18 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
     int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
     if (rc) return rc;
     {
-      // the march's bytes (presence byte, x, W written) and MDot's nv basis vectors; W is not re-read
+      // the march's bytes (presence byte, x, W written) and MDot's nv basis vectors; W is not re-read, and
+      // neither is x when it is the basis' last vector (its dot comes from the march's registers)
       KTimer kt(c, MSP_KERNEL_SPMVDOT, march_bytes(A, false, false) + 8.0 * (double)n * nv);
       Vecs vg = {};
       vg.base = base;
       vg.stride = stride;
       vg.scale = scale;
       const int64_t P = (int64_t)A->march_nx * A->march_ny;
+      int self = 0;
       KCHK(msk_box_spmv_mdot(A->march_nx, P, n, A->march_d2, A->march_mask, A->dv_val, x, sdev, y, &vg, nv,
-                             c->partial, nch, stop, c->stream));
+                             c->partial, nch, stop, &self, c->stream));
+      if (self) kt.set_bytes(march_bytes(A, false, false) + 8.0 * (double)n * (nv - 1));
     }
     KCHK(msk_dot_stage2(c->partial, nch, nv, out_dev, stop, c->stream));
     return MSP_SUCCESS;

@@ -537,3 +537,45 @@ def test_assembled_box_with_wrapped_entry_keeps_ell(ctx, oracle, wrap):
     assert A.spmv_kernel() == "k_spmv_ell"
     _products(ctx, A, O, np.random.default_rng(SEED))
     _gmres_vs_oracle(ctx, oracle, A, O, O.mult(np.random.default_rng(SEED).uniform(-1, 1, n)), max_it=40)
+
+
+_SELF_SCRIPT = r"""
+import hashlib, json, sys
+import numpy as np
+from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, KSP, Mat, Options, Vec
+ctx = Context(0)
+A = Mat.box_stencil(ctx, 3, 64, 64, 32)
+n = A.shape[0]
+b = Vec.from_array(ctx, np.random.default_rng(7).uniform(-1, 1, n))
+ksp = KSP(ctx)
+ksp.set_operators(A)
+ksp.set_from_options(Options("-ksp_type gmres -pc_type none -ksp_norm_type unpreconditioned -ksp_gmres_restart 30 "
+                             "-ksp_max_it 75 -ksp_rtol 1e-30"))
+x = Vec(ctx, n)
+ctx.set_timing(True)
+ksp.solve(b, x)
+ctx.set_timing(False)
+print(json.dumps({"hist": [float(h).hex() for h in ksp.get_residual_history()],
+                  "x": hashlib.sha256(x.get_array().tobytes()).hexdigest(),
+                  "spmvdot": ctx.kernel_stats()["spmvdot"]["launches"]}))
+"""
+
+
+def test_box_mdot_self_dot_from_registers_is_bitwise():
+    """GMRES's basis ends with the vector the MatMult reads (VV(it)); the fused z-march kernel takes that dot from the
+    x rows it holds in registers instead of re-reading the vector.  The same GMRES(30) run with the dot streamed from
+    HBM (MSPLIT_BOXMDOT_SELF=0, read once per process, hence two processes) gives the same history and x bits."""
+    import json
+    import os
+    import subprocess
+    import sys
+    outs = []
+    for self_env in ("1", "0"):
+        env = dict(os.environ, MSPLIT_BOXMDOT_SELF=self_env)
+        r = subprocess.run([sys.executable, "-c", _SELF_SCRIPT], env=env, capture_output=True, text=True, timeout=240,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert outs[0]["spmvdot"] > 0 and outs[1]["spmvdot"] > 0
+    assert len(outs[0]["hist"]) > 75
+    assert outs[0]["hist"] == outs[1]["hist"] and outs[0]["x"] == outs[1]["x"]
