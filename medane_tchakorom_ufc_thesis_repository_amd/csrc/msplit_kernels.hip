@@ -2140,7 +2140,7 @@ extern "C" int msk_maxpy_chunk(const double* win, double* wout, const Vecs* V, i
     case 5: MSK_MAXPY_LAUNCH(5) break;
     case 13: MSK_MAXPY_LAUNCH(13) break;
     case 32: MSK_MAXPY_LAUNCH(32) break;
-    case 33: MSK_MAXPY_LAUNCH(33) break;
+    case 33: if (rev) { MSK_MAXPY_LAUNCH(97) } else { MSK_MAXPY_LAUNCH(33) } break;
     case 36: MSK_MAXPY_LAUNCH(36) break;
     case 37: if (rev) { MSK_MAXPY_LAUNCH(101) } else { MSK_MAXPY_LAUNCH(37) } break;
     case 45: MSK_MAXPY_LAUNCH(45) break;
