@@ -218,6 +218,19 @@ def cpu_baseline(n: int, restart: int, its: int, rtol: float):
     return res
 
 
+def load_ceiling():
+    """The measured streaming ceiling of this MI355X model for the step's access mixes (tools/stream_ceiling.hip:
+    plain 16-byte non-temporal read / copy / MAXPY-mix kernels, profiles/r03/stream_ceiling/), or None."""
+    p = os.path.join(ROOT, "profiles", "r03", "stream_ceiling", "n256.json")
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None
+    return {"read_TBps": max(d["read8_TBps"], d["read16_TBps"]), "copy_TBps": d["copy_TBps"],
+            "maxpy_mix_TBps": max(d["mix15_TBps"], d["mix15_u8_TBps"]),
+            "source": "profiles/r03/stream_ceiling/n256.json (tools/stream_ceiling.hip, 256^3 vectors)"}
+
+
 def load_traffic():
     """HBM bytes per launch of the dominant kernel from the committed PMC summary
     (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
@@ -641,6 +654,7 @@ def main():
             s = stats[dom]
             achieved = (s["bytes"] / s["launches"]) / (s["ms"] / s["launches"] * 1e-3) / 1e9 if s["launches"] else 0
             tr = load_traffic()
+            ceil = load_ceiling()
             traffic = None
             if tr and tr.get("kernel_class") == dom and tr.get("n") == n and variant == "gmres":
                 traffic = tr.get("hbm_bytes_per_launch")
@@ -653,6 +667,9 @@ def main():
                                                   "correction), read from profiles/, not counted in this run"
                                                   if traffic is not None else None),
                                "timed_launches": f"1 in {args.timing_every} per class",
+                               "measured_ceiling": ceil,
+                               "frac_of_measured_read_ceiling": (achieved / (1e3 * ceil["read_TBps"])
+                                                                 if ceil else None),
                                "bytes_per_launch": s["bytes"] / max(s["launches"], 1),
                                "avg_launch_ms": s["ms"] / max(s["launches"], 1)}
             out["kernels"] = {k: {"kernel": names.get(k, k), "launches": v["launches"], "ms_total": v["ms"],
