@@ -81,6 +81,8 @@ def main():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--bench", default=None, help="bench JSON of the same build: algorithmic bytes per launch")
+    ap.add_argument("--x-reread", action="store_true",
+                    help="builds before round 3's register dot: the fused kernel streamed x again for its dot")
     a = ap.parse_args()
     N = a.n ** 3
     fetch = load(a.fetch_dir, "FETCH_SIZE")
@@ -109,9 +111,11 @@ def main():
         elif cls == "norm":
             alg = 8.0 * N
         elif cls == "spmvdot" and m % 30 == 0:
-            # one GMRES(30) solve in dispatch order: the Arnoldi step it reads nv = it + 1 basis vectors; the
-            # march's bytes (presence byte, x, W written) plus those vectors, W not re-read
-            alg = sum(17.0 * N + 8.0 * N * ((i % 30) + 1) for i in range(m)) / m
+            # one GMRES(30) solve in dispatch order: the Arnoldi step it dots W with nv = it + 1 basis vectors; the
+            # march's bytes (presence byte, x, W written) plus those vectors, W not re-read and the last vector
+            # (x itself) dotted from the march's registers (round 3; --x-reread for builds before it)
+            xr = 1 if a.x_reread else 0
+            alg = sum(17.0 * N + 8.0 * N * ((i % 30) + xr) for i in range(m)) / m
         elif cls == "spmv":
             als = [spmv_alg(nm, a.n) for nm, _ in F[:m]]
             if all(als):
