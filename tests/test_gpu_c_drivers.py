@@ -5,6 +5,7 @@ block per MPI rank (MPICH; both ranks share the one GPU, so the transport is
 MPI_Allgather through msp_comm's host path)."""
 import json
 import os
+import signal
 import subprocess
 
 import pytest
@@ -24,10 +25,25 @@ def built():
     return HOST
 
 
-def _run(args, mpi=0):
+# hydra's fork launcher and the loopback interface: no ssh, no lookup of the box's hostname (a box whose name
+# does not resolve would otherwise stall the PMI wire-up)
+MPI_LAUNCH = ["-launcher", "fork", "-iface", "lo"]
+
+
+def _run(args, mpi=0, timeout=150):
+    """Run a C host driver (under mpiexec with mpi ranks); its last JSON line.  The whole process group is
+    killed at the time limit (no rank is left holding the GPU) and the test fails with what it printed."""
     exe = os.path.join(HOST, "msplit_driver_mpi" if mpi else "msplit_driver")
-    cmd = ([MPIEXEC, "-n", str(mpi)] if mpi else []) + [exe] + args + ["-json"]
-    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300).stdout
+    cmd = ([MPIEXEC] + MPI_LAUNCH + ["-n", str(mpi)] if mpi else []) + [exe] + args + ["-json"]
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        raise AssertionError(f"{' '.join(cmd)} did not finish in {timeout} s\nstdout:\n{out[-2000:]}\n"
+                             f"stderr:\n{err[-2000:]}")
+    assert p.returncode == 0, f"{' '.join(cmd)} exited {p.returncode}\nstderr:\n{err[-2000:]}"
     return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
 
 
