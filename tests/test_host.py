@@ -148,3 +148,16 @@ def test_bench_cpu_share_and_topology(monkeypatch):
     assert bench.cpu_threads({"affinity_cpus": 8, "nproc": 256}) == 8
     monkeypatch.setenv("MSPLIT_CPU_THREADS", "5")
     assert bench.cpu_threads({"cgroup_cpu_quota": 16.0}) == 5
+
+
+def test_bench_reads_the_measured_streaming_ceiling():
+    """The roofline's measured ceiling comes from the committed stream_ceiling record (profiles/r03/); the rates
+    are in TB/s, below the 8 TB/s spec, reading at least as fast as the MAXPY mix."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    c = bench.load_ceiling()
+    assert c is not None and c["source"].startswith("profiles/r03/stream_ceiling/")
+    assert 5.0 < c["maxpy_mix_TBps"] <= c["read_TBps"] < bench.HBM_PEAK_GBS / 1e3
+    assert 5.0 < c["copy_TBps"] < bench.HBM_PEAK_GBS / 1e3
