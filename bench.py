@@ -61,14 +61,21 @@ SPMV_NAMES = {"dv": "k_spmv_ell (MatMult/MatResidual, DV storage: one byte per e
 MARCH_NAME = "k_spmv_box_march (MatMult/MatResidual, DV storage: one byte per entry; box stencil marched in z)"
 LINES_NAME = ("k_spmv_box_lines (MatMult/MatResidual, DV storage: one byte per entry; box stencil marched in z "
               "over tiles of four y lines)")
+CHUNK_NAME = ("k_box_march_chunk (MatMult/MatResidual, DV storage: one byte per entry; box stencil marched in z "
+              "over DBR chunk tiles)")
 TUNE_ELL_MARCH_OFF = 268435456
 
 
-def spmv_name(storage, nx):
-    """The kernel the library picks for a box stencil's products (msk_box_march_pick)."""
+def spmv_name(storage, nx, ny=None):
+    """The kernel the library picks for a box stencil's products (msk_spmv_box_march): the chunk-tile march
+    where a plane holds whole 4096-row chunks, else the line or 256-row march."""
     tune = int(os.environ.get("MSPLIT_TUNING", "0") or 0)
+    ny = nx if ny is None else ny
     if storage == "dv" and not tune & TUNE_ELL_MARCH_OFF:
         lines = os.environ.get("MSPLIT_MARCH_LINES", "0")
+        fits = (nx * ny) % 4096 == 0 and nx % 2 == 0 and 2 <= nx <= 2048
+        if fits and (lines == "16" or (lines == "0" and os.environ.get("MSPLIT_MARCH_CHUNK", "1") != "0")):
+            return CHUNK_NAME
         return LINES_NAME if nx % 256 == 0 and lines != "1" else MARCH_NAME
     return SPMV_NAMES[storage]
 

@@ -191,7 +191,8 @@ int msp_mat_get_storage(const msp_mat *A, int *storage, int *ndict);
 /* The kernel family MatMult / MatResidual / the GMRES products launch for A under the current
  * storage and tuning (a static string; MatView-like information, no reference counterpart):
  * "k_spmv_lds8" / "k_spmv_csr" (CSR), "k_spmv_ell" / "k_spmv_dv" (DV storage), "k_spmv_box_march"
- * (DV storage of a box stencil -- generated, or assembled by the caller and recognised by
+ * (the z-march family: k_spmv_box_march, k_spmv_box_lines, k_box_march_chunk, and in GMRES
+ * k_box_spmv_mdot_march; DV storage of a box stencil -- generated, or assembled by the caller and recognised by
  * msp_mat_create_csr: a 7-point (5-point) dictionary with deltas {0, -+1, -+nx, -+nx*ny} and no
  * entry across a line or plane edge), "k_stencil_spmv" (matrix-free), "k_spmv_rows" (row-compressed). */
 int msp_mat_get_spmv_kernel(const msp_mat *A, const char **name);

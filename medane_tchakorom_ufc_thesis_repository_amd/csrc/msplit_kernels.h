@@ -85,7 +85,7 @@ void msk_set_tuning(int flags);
 int msk_get_tuning(void);
 void msk_set_spmv_group(int gb);
 void msk_set_march_z(int z);  // z-march planes per workgroup (0: auto; A/B experiments)
-void msk_set_march_lines(int l);  // z-march tile: 1 = 256 plane rows, 4 = four y lines (0: auto; A/B, tests)
+void msk_set_march_lines(int l);  // z-march tile: 1 = 256 plane rows, 4 = four y lines, 16 = DBR chunk tiles (0: auto; A/B, tests)
 // The CGS block with W = A (sc x) computed in the kernel (op) instead of read from w: stage 1 of
 // W . V_v (v < nv <= 32), and the MAXPY wout = W - sum_j adev_j V_j with the ||wout||^2 partials.
 int msk_dot_stage1_op(const EllOp* op, const Vecs* V, int nv, int64_t n, double* partial, int64_t nchunks,

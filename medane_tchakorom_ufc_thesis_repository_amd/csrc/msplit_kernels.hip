@@ -1520,6 +1520,136 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
   }
 }
 
+// The box march over DBR chunk tiles (planes of whole chunks: P % 4096 == 0), for MatMult, MatResidual
+// and the scaled MatMult on their own: the tiling of k_box_spmv_mdot_march without the dots.  A lane owns
+// 16 rows of the tile (rows 2t, 2t+1 + 512j) and loads x, x(z+1), b and the presence bytes as 16- and
+// 2-byte vectors, so each lane keeps 8 x(z+1) loads and 8 b loads in flight where the line kernels keep
+// one; the tile's window [-nx, 4096+nx) of plane z is in LDS.  Same terms in the same order as
+// k_spmv_box_march: bitwise its products.
+template <int MODE, bool NTY>
+__global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
+                                                        const uint8_t* __restrict__ mask,
+                                                        const double* __restrict__ dval,
+                                                        const double* __restrict__ x,
+                                                        const double* __restrict__ b, double* __restrict__ y,
+                                                        const double* __restrict__ sdev, double* __restrict__ vout,
+                                                        const int* __restrict__ stop) {
+  if (MODE == MSK_SPMV_SCALED && stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sx = reinterpret_cast<double*>(smem);  // window of plane z: kChunk + 2 nx doubles
+  const int t = threadIdx.x;
+  const int64_t cpp = P / kChunk;
+  int64_t tile, zg;
+  if (xcd) {  // XCD-contiguous eighths of the plane's tiles (as k_box_spmv_mdot_march)
+    const int64_t per = cpp / 8, slot = blockIdx.x / 8;
+    tile = (blockIdx.x % 8) * per + slot % per;
+    zg = slot / per;
+  } else {
+    tile = blockIdx.x % cpp;
+    zg = blockIdx.x / cpp;
+  }
+  const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
+  const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
+  double v[7];
+  march_values<false>(dval, v);
+  const int nh = nx / 2;  // double2 per halo line
+  double xm[2 * kIters], xc[2 * kIters], xp[2 * kIters];
+  {
+    const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * t;
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double2 a = *reinterpret_cast<const double2*>(x + b0 + j * (2 * kT));
+      xc[2 * j] = a.x;
+      xc[2 * j + 1] = a.y;
+      if (z0 > 0) {
+        const double2 m2 = *reinterpret_cast<const double2*>(x + b0 - P + j * (2 * kT));
+        xm[2 * j] = m2.x;
+        xm[2 * j + 1] = m2.y;
+      } else {
+        xm[2 * j] = xm[2 * j + 1] = 0.0;
+      }
+    }
+  }
+  for (int32_t z = z0; z < z1; ++z) {
+    const int64_t c0 = ((int64_t)z * cpp + tile) * kChunk, base = c0 + 2 * t;
+    uint32_t m[kIters];
+    double2 bb[kIters];
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {  // plane z+1, b, the presence bytes: issued before the LDS turn-around
+      if (z + 1 < nz) {
+        const double2 p2 = *reinterpret_cast<const double2*>(x + base + P + j * (2 * kT));
+        xp[2 * j] = p2.x;
+        xp[2 * j + 1] = p2.y;
+      } else {
+        xp[2 * j] = xp[2 * j + 1] = 0.0;
+      }
+      m[j] = *reinterpret_cast<const uint16_t*>(mask + base + j * (2 * kT));
+      if constexpr (MODE == MSK_SPMV_RESID) bb[j] = ld_nt(reinterpret_cast<const double2*>(b + base + j * (2 * kT)));
+    }
+    double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0);
+    const bool hasl = t < nh && c0 - nx >= 0, hash = t < nh && c0 + kChunk + nx <= (int64_t)nz * P;
+    if (hasl) hl = *reinterpret_cast<const double2*>(x + c0 - nx + 2 * t);
+    if (hash) hh = *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * t);
+    __syncthreads();  // the previous plane's window reads are done
+#pragma unroll
+    for (int j = 0; j < kIters; ++j)
+      *reinterpret_cast<double2*>(sx + nx + j * (2 * kT) + 2 * t) = make_double2(xc[2 * j], xc[2 * j + 1]);
+    if (t < nh) {
+      *reinterpret_cast<double2*>(sx + 2 * t) = hl;
+      *reinterpret_cast<double2*>(sx + nx + kChunk + 2 * t) = hh;
+    }
+    for (int i = t + kT; i < nh; i += kT) {  // nx > 512: the rest of the halo lines
+      *reinterpret_cast<double2*>(sx + 2 * i) =
+          c0 - nx >= 0 ? *reinterpret_cast<const double2*>(x + c0 - nx + 2 * i) : make_double2(0.0, 0.0);
+      *reinterpret_cast<double2*>(sx + nx + kChunk + 2 * i) =
+          c0 + kChunk + nx <= (int64_t)nz * P ? *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * i)
+                                              : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      double o[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int e = j * (2 * kT) + 2 * t + q + nx;
+        const uint32_t mr = (m[j] >> (8 * q)) & 255u;
+        const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], xc[2 * j + q], sx[e + 1], sx[e + nx],
+                              xp[2 * j + q]};
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+          if (mr & (1u << k)) s = s + v[k] * (MODE == MSK_SPMV_SCALED ? xq[k] * sc : xq[k]);
+        if constexpr (MODE == MSK_SPMV_RESID) s = (q ? bb[j].y : bb[j].x) - s;
+        o[q] = s;
+      }
+      const int64_t r = base + j * (2 * kT);
+      if constexpr (NTY) {
+        dx2 w2;
+        w2.x = o[0];
+        w2.y = o[1];
+        __builtin_nontemporal_store(w2, reinterpret_cast<dx2*>(y + r));
+      } else {
+        *reinterpret_cast<double2*>(y + r) = make_double2(o[0], o[1]);
+      }
+      if (MODE == MSK_SPMV_SCALED && vout) {
+        if constexpr (NTY) {
+          dx2 w2;
+          w2.x = xc[2 * j] * sc;
+          w2.y = xc[2 * j + 1] * sc;
+          __builtin_nontemporal_store(w2, reinterpret_cast<dx2*>(vout + r));
+        } else {
+          *reinterpret_cast<double2*>(vout + r) = make_double2(xc[2 * j] * sc, xc[2 * j + 1] * sc);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * kIters; ++i) {
+      xm[i] = xc[i];
+      xc[i] = xp[i];
+    }
+  }
+}
+
 // The GMRES step's MatMult of a box stencil fused with the VecMDot after it.  Workgroup c owns
 // DBR chunk c and computes W = A (sc x) for its rows in the DBR lane layout (lane t: rows
 // c*4096 + j*512 + 2t, +1), so W never leaves the registers before the dots: the MDot
@@ -2285,14 +2415,58 @@ extern "C" int msk_box_march_pick(int32_t nx, int32_t ny, int32_t nz) {
   return !(f & MSK_TUNE_ELL_MARCH_OFF);
 }
 
+// Whether the chunk-tile march (k_box_march_chunk) takes this box: 3D, planes of whole DBR chunks, nx even
+// and at most 2048 (the LDS window); by default (march lines override 0) unless MSPLIT_MARCH_CHUNK=0, or
+// forced by the override 16.
+static bool march_chunk_ok(int32_t nx, int32_t ny, int d2) {
+  const int64_t P = (int64_t)nx * ny;
+  return !d2 && P % kChunk == 0 && (nx & 1) == 0 && nx >= 2 && nx <= 2048;
+}
+
 extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* mask,
                                   const double* dval, const double* x, const double* b, double* y, int mode,
                                   const double* sdev, double* vout, const int* stop, hipStream_t s) {
   if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad()) return (int)hipErrorInvalidValue;
-  if (msk_march_lines_override != 0 && msk_march_lines_override != 1 && msk_march_lines_override != 4)
+  if (msk_march_lines_override != 0 && msk_march_lines_override != 1 && msk_march_lines_override != 4 &&
+      msk_march_lines_override != 16)
     return (int)hipErrorInvalidValue;
   if (msk_march_lines_override == 4 && nx % kT) return (int)hipErrorInvalidValue;
   if (d2 && msk_march_lines_override == 4) return (int)hipErrorInvalidValue;
+  static const int chunk_env = [] {
+    const char* e = getenv("MSPLIT_MARCH_CHUNK");
+    return e ? atoi(e) : 1;
+  }();
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool chunk_ok = march_chunk_ok(nx, ny, d2) && a16(x) && a16(y) &&
+                        (mode != MSK_SPMV_RESID || a16(b)) && (mode != MSK_SPMV_SCALED || !vout || a16(vout));
+  if (msk_march_lines_override == 16 && !chunk_ok) return (int)hipErrorInvalidValue;
+  if (chunk_ok && (msk_march_lines_override == 16 || (msk_march_lines_override == 0 && chunk_env != 0))) {
+    // depth: the tile-planes dealt to 512 workgroups (two per CU, one wave of the grid; back to back
+    // 256^3 56.6 us at 8 planes against 61-64 at 4, 6, 12, 16; 512x512x256 219.6 us at 32 against 228-234 at
+    // 8-16; profiles/r03/chunk/), or the msk_set_march_z override
+    const int64_t P = (int64_t)nx * ny, cpp = P / kChunk;
+    const int32_t zt = msk_march_z_override > 0
+                           ? msk_march_z_override
+                           : (int32_t)std::max<int64_t>(1, std::min<int64_t>(nz, (cpp * nz + 511) / 512));
+    const int64_t grid = cpp * ((nz + zt - 1) / zt);
+    if (grid > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
+    const int xcd = cpp % 8 == 0 && cpp >= 32 && !(msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD);
+    const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
+    const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
+#define MSK_BMC(M, NT_)                                                                                      \
+  k_box_march_chunk<M, NT_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, mask, dval, x, b, y, \
+                                                                        sdev, vout, stop)
+#define MSK_BMC2(M) \
+  do {              \
+    if (nty) MSK_BMC(M, true); else MSK_BMC(M, false); \
+  } while (0)
+    if (mode == MSK_SPMV_RESID) MSK_BMC2(MSK_SPMV_RESID);
+    else if (mode == MSK_SPMV_SCALED) MSK_BMC2(MSK_SPMV_SCALED);
+    else MSK_BMC2(MSK_SPMV_MULT);
+#undef MSK_BMC2
+#undef MSK_BMC
+    return (int)hipGetLastError();
+  }
   int32_t L, zt;
   int64_t g;
   march_shape(nx, ny, nz, &L, &zt, &g);

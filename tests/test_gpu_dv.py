@@ -579,3 +579,66 @@ def test_box_mdot_self_dot_from_registers_is_bitwise():
     assert outs[0]["spmvdot"] > 0 and outs[1]["spmvdot"] > 0
     assert len(outs[0]["hist"]) > 75
     assert outs[0]["hist"] == outs[1]["hist"] and outs[0]["x"] == outs[1]["x"]
+
+
+@pytest.mark.parametrize("zt", [0, 3])
+@pytest.mark.parametrize("shape", [(256, 16, 40), (512, 8, 2), (64, 64, 33), (2048, 2, 7), (128, 32, 5),
+                                   (256, 256, 3)])
+@pytest.mark.parametrize("mode", ["products", "gmres"])
+def test_box_march_chunk_bitwise(ctx, oracle, zt, shape, mode):
+    """The march over DBR chunk tiles (k_box_march_chunk: planes of whole 4096-row chunks, nx even <= 2048; the
+    default for such boxes), forced with msk_set_march_lines(16), with its 2-plane or a ragged 3-plane depth:
+    MatMult and MatResidual, and GMRES with the MatMult kept apart from the VecMDot (the scaled form with the
+    VecScale output), equal the oracle bit for bit.  XCD-contiguous tiles from 32 tiles per plane (2048 x 2,
+    256 x 256 with 16 tiles per plane: plane order)."""
+    import ctypes
+    from medane_tchakorom_ufc_thesis_repository_amd import _lib
+    from test_gpu_kernels import tuning
+    L = _lib.load()
+    L.msk_set_march_lines.argtypes = [ctypes.c_int]
+    L.msk_set_march_z.argtypes = [ctypes.c_int]
+    nx, ny, nz = shape
+    A = Mat.box_convdiff(ctx, 3, nx, ny, nz, False, False, (0.5, -0.25, 0.3))
+    rp, col, val = A.get_csr()
+    O = oracle.Mat.from_arrays(A.shape[0], A.shape[1], rp, col, val)
+    n = A.shape[0]
+    L.msk_set_march_lines(16)
+    L.msk_set_march_z(zt)
+    try:
+        if mode == "products":
+            _products(ctx, A, O, np.random.default_rng(SEED))
+            return
+        b = O.mult(np.random.default_rng(SEED).uniform(-1, 1, n))
+        o = dict(restart=8, max_it=20, rtol=1e-30)
+        ksp = KSP(ctx)
+        ksp.set_operators(A)
+        ksp.set_from_options(Options(f"-ksp_type gmres -pc_type none -ksp_norm_type unpreconditioned "
+                                     f"-ksp_gmres_restart {o['restart']} -ksp_max_it {o['max_it']} "
+                                     f"-ksp_rtol {o['rtol']}"))
+        xv = Vec(ctx, n)
+        with tuning(BOX_SEPARATE):
+            ksp.solve(Vec.from_array(ctx, b), xv)
+    finally:
+        L.msk_set_march_lines(0)
+        L.msk_set_march_z(0)
+    xo, ro = oracle.gmres(O, b, reduce_mode=oracle.REDUCE_DBR, guess_nonzero=0, **o)
+    assert np.array_equal(ksp.get_residual_history(), ro["hist"])
+    assert np.array_equal(xv.get_array(), xo)
+
+
+def test_box_march_chunk_refused_where_it_does_not_fit(ctx):
+    """msk_set_march_lines(16) on a box whose planes are not whole DBR chunks is an error, not another kernel."""
+    import ctypes
+    from medane_tchakorom_ufc_thesis_repository_amd import _lib
+    from medane_tchakorom_ufc_thesis_repository_amd import MsplitError
+    L = _lib.load()
+    L.msk_set_march_lines.argtypes = [ctypes.c_int]
+    A = Mat.box_convdiff(ctx, 3, 48, 40, 6, False, False, (0.0, 0.0, 0.0))
+    x, y = Vec(ctx, A.shape[0]), Vec(ctx, A.shape[0])
+    x.set(1.0)
+    L.msk_set_march_lines(16)
+    try:
+        with pytest.raises(MsplitError):
+            A.mult(x, y)
+    finally:
+        L.msk_set_march_lines(0)
