@@ -168,6 +168,7 @@ typedef struct {
   msp_amsg *am;
   msp_cvd *cvd;
   int it, inner, tag, state, steps;
+  int rhs_holds_b; /* rhs = b in the rows A_off lists no entry for: later updates recompute the coupled rows only */
   double local_norm;
   /* AMAM-global: the replicated R (own rows = R), the global b, the block's own LSQR */
   msp_abcast *bc;
@@ -285,7 +286,14 @@ static void block_free(msd_block *B) {
   for (size_t i = 0; i < sizeof(v) / sizeof(v[0]); ++i) msp_vec_destroy(&v[i]);
 }
 
-static int update_rhs(msd_block *B) { return msp_mat_residual(B->A_off, B->b, B->halo, B->rhs); } /* utils.c:943-948 */
+/* utils.c:943-948.  The first update writes every row; b is fixed and rhs written nowhere else, so later ones
+ * recompute the coupled rows only (msp_mat_residual_listed: bitwise the full MatResidual). */
+static int update_rhs(msd_block *B) {
+  const int rc = B->rhs_holds_b ? msp_mat_residual_listed(B->A_off, B->b, B->halo, B->rhs)
+                                 : msp_mat_residual(B->A_off, B->b, B->halo, B->rhs);
+  if (!rc) B->rhs_holds_b = 1;
+  return rc;
+}
 
 static int inner_solve(msd_block *B, int *its) { /* inner_solver, utils.c:950-970 */
   B->ko.uirnorm = 1;

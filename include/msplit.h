@@ -210,6 +210,11 @@ int msp_mat_mult(msp_mat *A, const msp_vec *x, msp_vec *y);
 /* MatResidual r = b - A x (utils.c:549, :565, :579, :946;
  * synchronous-multisplitting.c:187). */
 int msp_mat_residual(msp_mat *A, const msp_vec *b, const msp_vec *x, msp_vec *r);
+/* MatResidual on a row-compressed matrix (msp_mat_create_csr_rows) over the rows it lists only:
+ * r_i = b_i - (A x)_i for those rows, every other row of r left as it is.  For updateLocalRHS
+ * (utils.c:943-948) when r already holds b in the unlisted rows -- there b_i - 0 = b_i, so the
+ * result is msp_mat_residual's bit for bit -- without copying b into r again (16 B per row). */
+int msp_mat_residual_listed(msp_mat *A, const msp_vec *b, const msp_vec *x, msp_vec *r);
 
 /* -------------------------------------------------------------------- Vec */
 /* VecCreate/VecSetSizes/VecSetType (utils.c:157-168): zero-initialised, in HBM. */

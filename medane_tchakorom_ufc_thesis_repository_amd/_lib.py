@@ -74,6 +74,7 @@ _SIGS = {
     "msp_mat_get_csr": [_vp, _i32p, _i32p, _dp],
     "msp_mat_mult": [_vp, _vp, _vp],
     "msp_mat_residual": [_vp, _vp, _vp, _vp],
+    "msp_mat_residual_listed": [_vp, _vp, _vp, _vp],
     "msp_vec_create": [_vp, C.c_int64, _P(_vp)],
     "msp_vec_create_with_array": [_vp, C.c_int64, _vp, _P(_vp)],
     "msp_vec_destroy": [_P(_vp)],

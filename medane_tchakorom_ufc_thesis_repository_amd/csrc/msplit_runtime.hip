@@ -1312,6 +1312,23 @@ extern "C" int msp_mat_residual(msp_mat* A, const msp_vec* b, const msp_vec* x, 
   return mspi_residual(A, b->d, x->d, r->d);
 }
 
+extern "C" int msp_mat_residual_listed(msp_mat* A, const msp_vec* b, const msp_vec* x, msp_vec* r) {
+  ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
+  int rc;
+  if ((rc = vec_ok(b, "b")) || (rc = vec_ok(x, "x")) || (rc = vec_ok(r, "r"))) return rc;
+  ARGCHK(A->compressed, MSP_ERR_SUP, "msp_mat_residual_listed needs a row-compressed matrix");
+  ARGCHK(x->n == A->ncols && b->n == A->nrows && r->n == A->nrows, MSP_ERR_ARG_SIZ,
+         "MatResidual sizes: A %d x %d, b %lld, x %lld, r %lld", A->nrows, A->ncols, (long long)b->n,
+         (long long)x->n, (long long)r->n);
+  ARGCHK(x->d != r->d, MSP_ERR_ARG_WRONG, "x and r must be different vectors");
+  msp_ctx* c = A->ctx;
+  // the listed rows' entries and b, their x reads, r written
+  KTimer kt(c, MSP_KERNEL_SPMV,
+            12.0 * (double)A->nnz + 8.0 * (double)A->nlisted * 3.0 + 4.0 * (double)A->nlisted + 8.0 * (double)A->nnz);
+  KCHK(msk_spmv_rows(A->nlisted, A->row_ids, A->rowptr, A->col, A->val, x->d, b->d, r->d, 1, c->stream));
+  return MSP_SUCCESS;
+}
+
 // -------------------------------------------------------------------- Vec
 extern "C" int msp_vec_create(msp_ctx* c, int64_t n, msp_vec** out) {
   ARGCHK(c && out, MSP_ERR_ARG_NULL, "NULL argument");

@@ -18,6 +18,7 @@ with a CPU test double to cover the multi-rank logic on gloo.)
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -56,6 +57,7 @@ class GpuBlock:
         self.b = Vec(ctx, n)
         self.x = Vec(ctx, n)
         self.rhs = Vec(ctx, n)
+        self._rhs_holds_b = False
         self.r = Vec(ctx, n)
         # computeTheRightHandSideWithInitialGuess (utils.c:623-650): b_i = A_block u, u = 1,
         # over the block's full rows in ascending-column order (MatMult_SeqAIJ)
@@ -106,7 +108,11 @@ class GpuBlock:
         return ln * ln
 
     def update_rhs(self):
-        updateLocalRHS(self.A_off, self.halo, self.b, self.rhs)
+        # the first update writes every row (rhs = b - A_off halo); rhs is written nowhere else and b is fixed
+        # at construction, so later updates recompute the coupled rows only (bitwise the full MatResidual)
+        updateLocalRHS(self.A_off, self.halo, self.b, self.rhs,
+                       rhs_holds_b=self._rhs_holds_b and os.environ.get("MSPLIT_RHS_FULL", "0") == "0")
+        self._rhs_holds_b = True                         # A_off is row-compressed (Mat.from_csr_rows)
 
     def solve(self) -> int:
         self.last_its = inner_solver(self.ksp, self.rhs, self.x)

@@ -370,6 +370,11 @@ class Mat:
     def residual(self, b: Vec, x: Vec, r: Vec):                     # MatResidual
         call("msp_mat_residual", self.h, b.h, x.h, r.h)
 
+    def residual_listed(self, b: Vec, x: Vec, r: Vec):
+        """MatResidual over the rows a row-compressed matrix lists; r's other rows are left as they are
+        (msp_mat_residual_listed: bitwise MatResidual when they already hold b)."""
+        call("msp_mat_residual_listed", self.h, b.h, x.h, r.h)
+
     def destroy(self):
         if getattr(self, "h", None) and self.h.value:
             call("msp_mat_destroy", C.byref(self.h))

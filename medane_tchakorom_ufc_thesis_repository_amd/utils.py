@@ -237,6 +237,11 @@ def inner_solver(ksp: KSP, rhs: Vec, x: Vec) -> int:
     return ksp.get_iteration_number()
 
 
-def updateLocalRHS(A_off: Mat, halo: Vec, b_block: Vec, rhs: Vec):
-    """utils.c:943-948: rhs = b_i - A_ij x_j (MatResidual), x_j = the halo."""
-    A_off.residual(b_block, halo, rhs)
+def updateLocalRHS(A_off: Mat, halo: Vec, b_block: Vec, rhs: Vec, rhs_holds_b: bool = False):
+    """utils.c:943-948: rhs = b_i - A_ij x_j (MatResidual), x_j = the halo.  rhs_holds_b: rhs already equals
+    b_i in the rows A_off lists no entry for (b_i - 0 = b_i), so only the coupled rows are recomputed -- the same
+    bits without the 16 B/row copy of b."""
+    if rhs_holds_b:
+        A_off.residual_listed(b_block, halo, rhs)
+    else:
+        A_off.residual(b_block, halo, rhs)
