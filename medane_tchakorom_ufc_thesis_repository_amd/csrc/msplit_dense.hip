@@ -706,7 +706,7 @@ extern "C" int msp_dense_create(msp_ctx* c, int64_t nrows, int32_t ncols, msp_de
   A->ncols = ncols;
   A->lda = lda_for(nrows);
   const size_t bytes = (size_t)(A->lda * ncols + 512) * sizeof(double);
-  if (hipMalloc((void**)&A->d, bytes) != hipSuccess) {
+  if (mspi_big_alloc((void**)&A->d, bytes) != (int)hipSuccess) {
     delete A;
     mspi_ctx_release(c);
     mspi_set_error(MSP_ERR_MEM, "hipMalloc of a %lld x %d dense block failed", (long long)nrows, ncols);

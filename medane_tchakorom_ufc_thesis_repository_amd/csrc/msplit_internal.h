@@ -32,6 +32,8 @@ void mspi_set_error(int code, const char *fmt, ...);
 double *mspi_dev_scratch(msp_ctx *ctx);
 double *mspi_host_scratch(msp_ctx *ctx);
 int mspi_malloc(msp_ctx *ctx, void **p, size_t bytes);
+/* hipMalloc of a large buffer (MSPLIT_ALLOC_CONTIGUOUS: physically contiguous where the driver can) */
+int mspi_big_alloc(void **p, size_t bytes); /* 0 = hipSuccess */
 int mspi_free(msp_ctx *ctx, void *p);
 /* pinned host memory (for per-iteration scalars) */
 int mspi_host_malloc(void **p, size_t bytes);

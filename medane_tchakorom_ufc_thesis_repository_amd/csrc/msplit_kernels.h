@@ -132,6 +132,11 @@ int msk_march_check(int32_t nrows, int32_t nx, int32_t ny, int d2, const uint8_t
 int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* mask, const double* dval,
                        const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
                        const int* stop, hipStream_t s);
+// The chunk-tile march (k_box_march_chunk): whether it takes a box of nx x ny planes; MatMult / MatResidual
+// with the plane below (halo & 1) / above (halo & 2) in the column space (x = the column-space vector).
+int msk_march_chunk_fits(int32_t nx, int32_t ny, int d2);
+int msk_box_march_halo(int32_t nx, int32_t ny, int32_t nz, int halo, const uint8_t* mask, const double* dval,
+                       const double* x, const double* b, double* y, int mode, hipStream_t s);
 // GMRES: y = A (sc*x) for a box stencil with march presence bytes (nx <= 2048; P = the plane, or nx in 2D), fused
 // with the DBR stage 1 of y . V_v (v < nv <= 32) into partial: W in the DBR lane layout, bitwise the march's.
 // *self_out (may be NULL) = 1 when V's last vector is x and its dot came from the march's registers (not re-read).

@@ -1528,7 +1528,7 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
 // k_spmv_box_march: bitwise its products.
 template <int MODE, bool NTY>
 __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
-                                                        const uint8_t* __restrict__ mask,
+                                                        int halo, const uint8_t* __restrict__ mask,
                                                         const double* __restrict__ dval,
                                                         const double* __restrict__ x,
                                                         const double* __restrict__ b, double* __restrict__ y,
@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
       const double2 a = *reinterpret_cast<const double2*>(x + b0 + j * (2 * kT));
       xc[2 * j] = a.x;
       xc[2 * j + 1] = a.y;
-      if (z0 > 0) {
+      if (z0 > 0 || (halo & 1)) {  // halo & 1: the plane below the box is the column space's lo plane
         const double2 m2 = *reinterpret_cast<const double2*>(x + b0 - P + j * (2 * kT));
         xm[2 * j] = m2.x;
         xm[2 * j + 1] = m2.y;
@@ -1576,7 +1576,7 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
     double2 bb[kIters];
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {  // plane z+1, b, the presence bytes: issued before the LDS turn-around
-      if (z + 1 < nz) {
+      if (z + 1 < nz || (halo & 2)) {  // halo & 2: the plane above the box is the hi plane
         const double2 p2 = *reinterpret_cast<const double2*>(x + base + P + j * (2 * kT));
         xp[2 * j] = p2.x;
         xp[2 * j + 1] = p2.y;
@@ -2423,6 +2423,38 @@ static bool march_chunk_ok(int32_t nx, int32_t ny, int d2) {
   return !d2 && P % kChunk == 0 && (nx & 1) == 0 && nx >= 2 && nx <= 2048;
 }
 
+// The chunk-tile march launch (k_box_march_chunk) for a box whose planes hold whole DBR chunks; halo bit 0/1:
+// the column space has the plane below / above the box (x points at the box's first row).
+static int launch_march_chunk(int32_t nx, int32_t ny, int32_t nz, int halo, const uint8_t* mask, const double* dval,
+                              const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
+                              const int* stop, hipStream_t s) {
+  // depth: the tile-planes dealt to 512 workgroups (two per CU, one wave of the grid; back to back
+  // 256^3 56.6 us at 8 planes against 61-64 at 4, 6, 12, 16; 512x512x256 219.6 us at 32 against 228-234 at
+  // 8-16; profiles/r03/chunk/), or the msk_set_march_z override
+  const int64_t P = (int64_t)nx * ny, cpp = P / kChunk;
+  const int32_t zt = msk_march_z_override > 0
+                         ? msk_march_z_override
+                         : (int32_t)std::max<int64_t>(1, std::min<int64_t>(nz, (cpp * nz + 511) / 512));
+  const int64_t grid = cpp * ((nz + zt - 1) / zt);
+  if (grid > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
+  const int xcd = cpp % 8 == 0 && cpp >= 32 && !(msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD);
+  const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
+  const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
+#define MSK_BMC(M, NT_)                                                                                        \
+  k_box_march_chunk<M, NT_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, halo, mask, dval, x, b, \
+                                                                        y, sdev, vout, stop)
+#define MSK_BMC2(M)                                    \
+  do {                                                 \
+    if (nty) MSK_BMC(M, true); else MSK_BMC(M, false); \
+  } while (0)
+  if (mode == MSK_SPMV_RESID) MSK_BMC2(MSK_SPMV_RESID);
+  else if (mode == MSK_SPMV_SCALED) MSK_BMC2(MSK_SPMV_SCALED);
+  else MSK_BMC2(MSK_SPMV_MULT);
+#undef MSK_BMC2
+#undef MSK_BMC
+  return (int)hipGetLastError();
+}
+
 extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t* mask,
                                   const double* dval, const double* x, const double* b, double* y, int mode,
                                   const double* sdev, double* vout, const int* stop, hipStream_t s) {
@@ -2440,33 +2472,8 @@ extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, co
   const bool chunk_ok = march_chunk_ok(nx, ny, d2) && a16(x) && a16(y) &&
                         (mode != MSK_SPMV_RESID || a16(b)) && (mode != MSK_SPMV_SCALED || !vout || a16(vout));
   if (msk_march_lines_override == 16 && !chunk_ok) return (int)hipErrorInvalidValue;
-  if (chunk_ok && (msk_march_lines_override == 16 || (msk_march_lines_override == 0 && chunk_env != 0))) {
-    // depth: the tile-planes dealt to 512 workgroups (two per CU, one wave of the grid; back to back
-    // 256^3 56.6 us at 8 planes against 61-64 at 4, 6, 12, 16; 512x512x256 219.6 us at 32 against 228-234 at
-    // 8-16; profiles/r03/chunk/), or the msk_set_march_z override
-    const int64_t P = (int64_t)nx * ny, cpp = P / kChunk;
-    const int32_t zt = msk_march_z_override > 0
-                           ? msk_march_z_override
-                           : (int32_t)std::max<int64_t>(1, std::min<int64_t>(nz, (cpp * nz + 511) / 512));
-    const int64_t grid = cpp * ((nz + zt - 1) / zt);
-    if (grid > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
-    const int xcd = cpp % 8 == 0 && cpp >= 32 && !(msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD);
-    const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
-    const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
-#define MSK_BMC(M, NT_)                                                                                      \
-  k_box_march_chunk<M, NT_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, mask, dval, x, b, y, \
-                                                                        sdev, vout, stop)
-#define MSK_BMC2(M) \
-  do {              \
-    if (nty) MSK_BMC(M, true); else MSK_BMC(M, false); \
-  } while (0)
-    if (mode == MSK_SPMV_RESID) MSK_BMC2(MSK_SPMV_RESID);
-    else if (mode == MSK_SPMV_SCALED) MSK_BMC2(MSK_SPMV_SCALED);
-    else MSK_BMC2(MSK_SPMV_MULT);
-#undef MSK_BMC2
-#undef MSK_BMC
-    return (int)hipGetLastError();
-  }
+  if (chunk_ok && (msk_march_lines_override == 16 || (msk_march_lines_override == 0 && chunk_env != 0)))
+    return launch_march_chunk(nx, ny, nz, 0, mask, dval, x, b, y, mode, sdev, vout, stop, s);
   int32_t L, zt;
   int64_t g;
   march_shape(nx, ny, nz, &L, &zt, &g);
@@ -2487,6 +2494,29 @@ extern "C" int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, co
   }
 #undef MSK_BML
   return (int)hipGetLastError();
+}
+
+// Whether the chunk-tile march takes a box of nx x ny planes (and MSPLIT_MARCH_CHUNK does not turn it off).
+extern "C" int msk_march_chunk_fits(int32_t nx, int32_t ny, int d2) {
+  static const int chunk_env = [] {
+    const char* e = getenv("MSPLIT_MARCH_CHUNK");
+    return e ? atoi(e) : 1;
+  }();
+  return chunk_env != 0 && march_chunk_ok(nx, ny, d2);
+}
+
+// MatMult / MatResidual of a box stencil whose column space adds the plane below (halo & 1) and / or above
+// (halo & 2) the box -- a block's rows of the block-Jacobi operator with its coupling columns -- over chunk
+// tiles; x is the column-space vector (the lo plane first).  Only boxes k_box_march_chunk takes.
+extern "C" int msk_box_march_halo(int32_t nx, int32_t ny, int32_t nz, int halo, const uint8_t* mask,
+                                  const double* dval, const double* x, const double* b, double* y, int mode,
+                                  hipStream_t s) {
+  if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad() || mode == MSK_SPMV_SCALED) return (int)hipErrorInvalidValue;
+  const double* xo = x + ((halo & 1) ? (int64_t)nx * ny : 0);
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!march_chunk_ok(nx, ny, 0) || !a16(xo) || !a16(y) || (mode == MSK_SPMV_RESID && !a16(b)))
+    return (int)hipErrorInvalidValue;
+  return launch_march_chunk(nx, ny, nz, halo, mask, dval, xo, b, y, mode, nullptr, nullptr, nullptr, s);
 }
 
 extern "C" int msk_march_mask(int32_t nrows, int d2, const uint8_t* code8, uint8_t* mask, hipStream_t s) {

@@ -164,9 +164,24 @@ extern "C" int msp_ctx_get_kernel_stats(msp_ctx* c, int cls, int64_t* launches, 
 extern "C" double* mspi_dev_scratch(msp_ctx* c) { return c->dscratch; }
 extern "C" double* mspi_host_scratch(msp_ctx* c) { return c->hscratch; }
 
+// Device allocation of the large buffers (vectors, the Krylov basis, dense blocks).  MSPLIT_ALLOC_CONTIGUOUS=1
+// (A/B): buffers from 64 MiB up are requested physically contiguous (hipDeviceMallocContiguous), falling back to
+// hipMalloc when the driver cannot.
+extern "C" int mspi_big_alloc(void** p, size_t bytes) {
+  static const int contig = [] {
+    const char* e = getenv("MSPLIT_ALLOC_CONTIGUOUS");
+    return e ? atoi(e) : 0;
+  }();
+  if (contig && bytes >= ((size_t)64 << 20)) {
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return (int)hipSuccess;
+    (void)hipGetLastError();
+  }
+  return (int)hipMalloc(p, bytes);
+}
+
 extern "C" int mspi_malloc(msp_ctx* c, void** p, size_t bytes) {
   (void)c;
-  if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) {
+  if (mspi_big_alloc(p, bytes ? bytes : 16) != (int)hipSuccess) {
     *p = nullptr;
     mspi_set_error(MSP_ERR_MEM, "hipMalloc(%zu bytes) failed", bytes);
     return MSP_ERR_MEM;
@@ -439,6 +454,7 @@ struct msp_mat {
   // its extents, for the z-march SpMV (msk_spmv_box_march); 0 otherwise
   int32_t march_nx = 0, march_ny = 0, march_nz = 0;
   int32_t march_d2 = 0;        // 2D box stencil (five pairs), marched as nx x 1 x ny
+  int32_t march_halo = 0;      // bit 0 / 1: the column space adds the plane below / above the box (chunk march only)
   uint8_t* march_mask = nullptr;  // nrows (+16 pad): the rows' presence bytes (msk_march_mask)
   bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
   uint64_t version = next_version();  // unique per object and bumped when its products' kernels change
@@ -486,6 +502,7 @@ static void dv_free(msp_mat* A) {
   A->march_mask = nullptr;
   A->march_nx = A->march_ny = A->march_nz = 0;
   A->march_d2 = 0;
+  A->march_halo = 0;
 }
 
 // Encode the device CSR of A against the dictionary (host arrays, nd <= 256).
@@ -583,12 +600,16 @@ static int dv_dictionary(int32_t nrows, const int32_t* rowptr, const int32_t* co
 // offset, the encoder names the +P coupling +nx and the march would drop it.  check: verify on the
 // device that no row holds a neighbour across a line or plane edge (k_march_check), for matrices
 // the caller assembled; a failed check leaves the matrix on the row-parallel ELL kernel.
-static int march_attach(msp_mat* A, int32_t nx, int32_t ny, int32_t nz, int d2, bool check) {
+static int march_attach(msp_mat* A, int32_t nx, int32_t ny, int32_t nz, int d2, bool check, int halo = 0) {
   msp_ctx* c = A->ctx;
   const int nd = d2 ? 5 : 7;
+  const int64_t P = (int64_t)nx * ny;
+  const int64_t ext = P * (((halo & 1) ? 1 : 0) + ((halo & 2) ? 1 : 0));
   if (A->ndict != nd || A->dv_w != 8 || nx <= 1 || (!d2 && ny <= 1) || nz < 1 ||
-      (int64_t)nx * ny * nz != (int64_t)A->nrows || A->ncols != A->nrows)
+      (int64_t)nx * ny * nz != (int64_t)A->nrows || (int64_t)A->ncols != (int64_t)A->nrows + ext)
     return MSP_SUCCESS;
+  // with coupling planes in the column space only the chunk-tile march reads them (3D, whole-chunk planes)
+  if (halo && (d2 || !msk_march_chunk_fits(nx, ny, d2))) return MSP_SUCCESS;
   if (hipMalloc((void**)&A->march_mask, (size_t)A->nrows + 16) != hipSuccess) {
     A->march_mask = nullptr;
     mspi_set_error(MSP_ERR_MEM, "hipMalloc of the march presence bytes failed");
@@ -614,6 +635,7 @@ static int march_attach(msp_mat* A, int32_t nx, int32_t ny, int32_t nz, int d2, 
   A->march_ny = d2 ? 1 : ny;
   A->march_nz = nz;
   A->march_d2 = d2;
+  A->march_halo = halo;
   return MSP_SUCCESS;
 }
 
@@ -867,7 +889,8 @@ extern "C" int msp_mat_create_box_convdiff(msp_ctx* c, int dim, int32_t nx, int3
       return rc;
     }
     // the presence bytes the march kernels read instead of the codes (2D: marched as nx x 1 x ny)
-    if (!lo && !hi && (rc = march_attach(A, nx, dim == 3 ? ny : 1, dim == 3 ? nz : ny, dim == 2, false))) {
+    if ((rc = march_attach(A, nx, dim == 3 ? ny : 1, dim == 3 ? nz : ny, dim == 2, false,
+                           (lo ? 1 : 0) | (hi ? 2 : 0)))) {
       msp_mat_destroy(&A);
       return rc;
     }
@@ -976,7 +999,12 @@ static double dv_bytes(const msp_mat* A, bool resid, bool vout) {
 
 // DV products of a box stencil take the z-march kernel when the tuning policy picks it
 static bool box_march(const msp_mat* A) {
-  return A->march_nx > 0 && msk_box_march_pick(A->march_nx, A->march_ny, A->march_nz);
+  return A->march_nx > 0 && A->march_halo == 0 && msk_box_march_pick(A->march_nx, A->march_ny, A->march_nz);
+}
+
+// a box with coupling planes in its column space: MatMult / MatResidual / MatMatMult by the chunk-tile march
+static bool box_march_halo(const msp_mat* A) {
+  return A->march_nx > 0 && A->march_halo != 0 && msk_box_march_pick(A->march_nx, A->march_ny, A->march_nz);
 }
 
 // the march reads one presence byte per row instead of the codes
@@ -1136,6 +1164,25 @@ extern "C" void mspi_graph_destroy(void* exec) {
 extern "C" int mspi_mat_spmm_dv(msp_mat* A, const double* S, int64_t lds, int nc, int64_t srows, double* R,
                                 int64_t ldr) {
   if (!A->dv_on || !A->dv_w) return MSP_ERR_SUP;
+  const bool bm = box_march(A), bh = !bm && box_march_halo(A);
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if ((bm || bh) && msk_march_chunk_fits(A->march_nx, A->march_ny, A->march_d2) && a16(S) && a16(R) &&
+      lds % 2 == 0 && ldr % 2 == 0) {
+    // a box stencil: column by column through the chunk-tile march (each R(r, q) the same CSR-order row sum as
+    // the ELL SpMM's), presence bytes and S's columns read once per column, R written
+    KTimer kt(A->ctx, MSP_KERNEL_SPMM, (double)nc * (march_bytes(A, false, false)));
+    for (int q = 0; q < nc; ++q) {
+      const double* sq = S + (int64_t)q * lds;
+      double* rq = R + (int64_t)q * ldr;
+      if (bm)
+        KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->march_mask, A->dv_val, sq,
+                                nullptr, rq, MSK_SPMV_MULT, nullptr, nullptr, nullptr, A->ctx->stream));
+      else
+        KCHK(msk_box_march_halo(A->march_nx, A->march_ny, A->march_nz, A->march_halo, A->march_mask, A->dv_val, sq,
+                                nullptr, rq, MSK_SPMV_MULT, A->ctx->stream));
+    }
+    return MSP_SUCCESS;
+  }
   // codes once, S's columns read once, R written
   KTimer kt(A->ctx, MSP_KERNEL_SPMM, (double)A->dv_w * A->nrows + 8.0 * nc * ((double)srows + A->nrows));
   KCHK(msk_spmm_ell(A->nrows, A->dv_w, A->dv_code, A->dv_delta, A->dv_val, A->ndict, S, lds, nc, R, ldr,
@@ -1154,7 +1201,7 @@ extern "C" int msp_mat_get_spmv_kernel(const msp_mat* A, const char** name) {
   ARGCHK(A && name, MSP_ERR_ARG_NULL, "NULL argument");
   if (A->matfree) *name = "k_stencil_spmv";
   else if (A->compressed) *name = "k_spmv_rows";
-  else if (A->dv_on && box_march(A)) *name = "k_spmv_box_march";
+  else if (A->dv_on && (box_march(A) || box_march_halo(A))) *name = "k_spmv_box_march";
   else if (A->dv_on) *name = A->dv_w ? "k_spmv_ell" : "k_spmv_dv";
   else *name = A->lds_cap > 0 ? "k_spmv_lds8" : "k_spmv_csr";
   return MSP_SUCCESS;
@@ -1180,13 +1227,16 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
     return MSP_SUCCESS;
   }
   if (A->dv_on) {
-    const bool bm = box_march(A);
-    KTimer kt(c, MSP_KERNEL_SPMV, bm ? march_bytes(A, resid, false) : dv_bytes(A, resid, false));
+    const bool bm = box_march(A), bh = !bm && box_march_halo(A);
+    KTimer kt(c, MSP_KERNEL_SPMV, bm || bh ? march_bytes(A, resid, false) : dv_bytes(A, resid, false));
     if (bm) {
       KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->march_mask, A->dv_val, x, b, y,
                               resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
       return MSP_SUCCESS;
     }
+    if (bh && msk_box_march_halo(A->march_nx, A->march_ny, A->march_nz, A->march_halo, A->march_mask, A->dv_val, x, b,
+                                 y, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, c->stream) == 0)
+      return MSP_SUCCESS;  // (a vector not 16-byte aligned: the row-parallel kernel below)
     KCHK(msk_spmv_dv(A->nrows, A->rowptr, A->dv_len, A->dv_code, A->dv_delta, A->dv_val, A->ndict, A->dv_mb, A->dv_w, x, b,
                      y, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, A->plane, c->stream));
     return MSP_SUCCESS;
@@ -1340,7 +1390,7 @@ extern "C" int msp_vec_create(msp_ctx* c, int64_t n, msp_vec** out) {
   v->owned = 1;
   // pad to 512 doubles so every vector is 4 KiB aligned and double2 loads stay in bounds
   const size_t bytes = (size_t)((n + 511) / 512 * 512 + 512) * sizeof(double);
-  if (hipMalloc((void**)&v->d, bytes) != hipSuccess) {
+  if (mspi_big_alloc((void**)&v->d, bytes) != (int)hipSuccess) {
     delete v;
     mspi_ctx_release(c);
     mspi_set_error(MSP_ERR_MEM, "hipMalloc of a %lld-entry vector failed", (long long)n);

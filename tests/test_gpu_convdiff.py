@@ -77,8 +77,10 @@ def _smsm_opts(nb):
     return Options(inner + " " + outer)
 
 
-@pytest.mark.parametrize("dim,nx,ny,nz,nb,s", [(3, 8, 8, 8, 2, 4), (2, 24, 20, 1, 3, 5)])
+@pytest.mark.parametrize("dim,nx,ny,nz,nb,s", [(3, 8, 8, 8, 2, 4), (2, 24, 20, 1, 3, 5), (3, 64, 64, 12, 3, 4)])
 def test_smsm_convdiff_bitwise_vs_oracle(ctx, oracle, dim, nx, ny, nz, nb, s):
+    """SMSM-global on convection-diffusion blocks, bitwise the oracle; 64 x 64 planes (whole DBR chunks): the
+    blocks' A_ext with coupling planes take the chunk-tile march for R = A S and the global residual."""
     P = (0.5, 0.25, -0.3)
     rtol = 1e-8
     comm = LocalComm()
