@@ -32,7 +32,7 @@ void mspi_set_error(int code, const char *fmt, ...);
 double *mspi_dev_scratch(msp_ctx *ctx);
 double *mspi_host_scratch(msp_ctx *ctx);
 int mspi_malloc(msp_ctx *ctx, void **p, size_t bytes);
-/* hipMalloc of a large buffer (MSPLIT_ALLOC_CONTIGUOUS: physically contiguous where the driver can) */
+/* hipMalloc of a large buffer, physically contiguous from 64 MiB where the driver can (MSPLIT_ALLOC_CONTIGUOUS=0: plain) */
 int mspi_big_alloc(void **p, size_t bytes); /* 0 = hipSuccess */
 int mspi_free(msp_ctx *ctx, void *p);
 /* pinned host memory (for per-iteration scalars) */
