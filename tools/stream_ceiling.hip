@@ -8,11 +8,12 @@
 //   fill     : y = c
 // Prints one JSON object: TB/s per kernel (bytes the kernel requests / time per launch, HIP events).
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/stream_ceiling.hip -o tools/stream_ceiling
-//   tools/stream_ceiling <n> <reps>
+//   tools/stream_ceiling <n> <reps> [contig]   (contig: buffers physically contiguous, as the library allocates them)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                    \
@@ -106,18 +107,24 @@ int main(int argc, char** argv) {
     fprintf(stderr, "n must be a positive multiple of %d\n", kChunk);
     return 2;
   }
+  const bool contig = argc > 3 && std::string(argv[3]) == "contig";
+  auto alloc = [&](double** p, size_t bytes) {
+    if (contig && hipExtMallocWithFlags((void**)p, bytes, hipDeviceMallocContiguous) == hipSuccess) return;
+    (void)hipGetLastError();
+    CK(hipMalloc(p, bytes));
+  };
   const int KMAX = 16;
   const int64_t stride = n;
   double *V, *x, *y, *out;
-  CK(hipMalloc(&V, sizeof(double) * stride * KMAX));
-  CK(hipMalloc(&x, sizeof(double) * n));
-  CK(hipMalloc(&y, sizeof(double) * n));
+  alloc(&V, sizeof(double) * stride * KMAX);
+  alloc(&x, sizeof(double) * n);
+  alloc(&y, sizeof(double) * n);
   const unsigned g = (unsigned)(n / kChunk);
   CK(hipMalloc(&out, sizeof(double) * (size_t)g * kT));
   CK(hipMemset(V, 0, sizeof(double) * stride * KMAX));
   CK(hipMemset(x, 0, sizeof(double) * n));
   const double B = 8.0 * (double)n;
-  printf("{\"n\": %lld, \"reps\": %d", (long long)n, reps);
+  printf("{\"n\": %lld, \"reps\": %d, \"contiguous\": %s", (long long)n, reps, contig ? "true" : "false");
   for (int K : {4, 8, 16}) {
     double ms = time_ms([&] { k_read<4><<<g, kT>>>(V, stride, K, out); }, reps);
     printf(", \"read%d_TBps\": %.3f", K, B * K / (ms * 1e-3) / 1e12);
