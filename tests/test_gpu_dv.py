@@ -583,7 +583,7 @@ def test_box_mdot_self_dot_from_registers_is_bitwise():
 
 @pytest.mark.parametrize("zt", [0, 3])
 @pytest.mark.parametrize("shape", [(256, 16, 40), (512, 8, 2), (64, 64, 33), (2048, 2, 7), (128, 32, 5),
-                                   (256, 256, 3)])
+                                   (256, 256, 3), (64, 64, 1), (4096 // 2, 2, 1)])
 @pytest.mark.parametrize("mode", ["products", "gmres"])
 def test_box_march_chunk_bitwise(ctx, oracle, zt, shape, mode):
     """The march over DBR chunk tiles (k_box_march_chunk: planes of whole 4096-row chunks, nx even <= 2048; the
@@ -645,7 +645,7 @@ def test_box_march_chunk_refused_where_it_does_not_fit(ctx):
 
 
 @pytest.mark.parametrize("halo", [1, 2, 3])
-@pytest.mark.parametrize("shape", [(64, 64, 9), (256, 16, 5), (128, 32, 3)])
+@pytest.mark.parametrize("shape", [(64, 64, 9), (256, 16, 5), (128, 32, 3), (64, 64, 1), (512, 8, 2)])
 def test_box_with_coupling_planes_takes_the_chunk_march(ctx, oracle, halo, shape):
     """A block's rows of the block-Jacobi operator with its coupling columns (A_ext: the plane below and / or
     above the block in the column space, utils.c:891-921) marches over chunk tiles when its planes hold whole DBR
