@@ -523,9 +523,9 @@ static int dv_build(msp_mat* A, int nd, const int32_t* delta, const double* val,
   if (!ell && max_block > kMaxDvBlock) return MSP_SUCCESS;
   A->dv_mb = (int32_t)max_block;
   A->dv_w = ell ? W : 0;
-  if (!ell) HIPCHK(hipMalloc((void**)&A->dv_len, (size_t)A->nrows + 16));
+  if (!ell) HIPCHK((hipError_t)mspi_big_alloc((void**)&A->dv_len, (size_t)A->nrows + 16));
   const size_t ncode = ell ? (size_t)W * A->nrows : (size_t)A->nnz;
-  HIPCHK(hipMalloc((void**)&A->dv_code, ncode + 16));
+  HIPCHK((hipError_t)mspi_big_alloc((void**)&A->dv_code, ncode + 16));
   HIPCHK(hipMalloc((void**)&A->dv_delta, 256 * sizeof(int32_t)));
   HIPCHK(hipMalloc((void**)&A->dv_val, 256 * sizeof(double)));
   HIPCHK(hipMemsetAsync(A->dv_code + ncode, 0, 16, c->stream));
@@ -612,7 +612,7 @@ static int march_attach(msp_mat* A, int32_t nx, int32_t ny, int32_t nz, int d2, 
     return MSP_SUCCESS;
   // with coupling planes in the column space only the chunk-tile march reads them (3D, whole-chunk planes)
   if (halo && (d2 || !msk_march_chunk_fits(nx, ny, d2))) return MSP_SUCCESS;
-  if (hipMalloc((void**)&A->march_mask, (size_t)A->nrows + 16) != hipSuccess) {
+  if (mspi_big_alloc((void**)&A->march_mask, (size_t)A->nrows + 16) != (int)hipSuccess) {
     A->march_mask = nullptr;
     mspi_set_error(MSP_ERR_MEM, "hipMalloc of the march presence bytes failed");
     return MSP_ERR_MEM;
@@ -682,9 +682,9 @@ static bool box_dictionary(int32_t nrows, std::vector<int32_t>& dd, std::vector<
 }
 
 static int mat_alloc(msp_ctx* c, msp_mat* A, int64_t nptr, int64_t nnz) {
-  HIPCHK(hipMalloc((void**)&A->rowptr, (size_t)nptr * sizeof(int32_t)));
-  HIPCHK(hipMalloc((void**)&A->col, (size_t)(nnz + 4) * sizeof(int32_t)));
-  HIPCHK(hipMalloc((void**)&A->val, (size_t)(nnz + 2) * sizeof(double)));
+  HIPCHK((hipError_t)mspi_big_alloc((void**)&A->rowptr, (size_t)nptr * sizeof(int32_t)));
+  HIPCHK((hipError_t)mspi_big_alloc((void**)&A->col, (size_t)(nnz + 4) * sizeof(int32_t)));
+  HIPCHK((hipError_t)mspi_big_alloc((void**)&A->val, (size_t)(nnz + 2) * sizeof(double)));
   HIPCHK(hipMemsetAsync(A->col + nnz, 0, 4 * sizeof(int32_t), c->stream));
   HIPCHK(hipMemsetAsync(A->val + nnz, 0, 2 * sizeof(double), c->stream));
   return MSP_SUCCESS;
