@@ -270,8 +270,8 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
       rc = mspi_maxpy_norm_update(c, k->tmp, VV(k, it + 1), it + 1, k->basis, k->stride, sc, k->n, k->g, it,
                                   k->o.restart, stop);
   }
-  /* KSPGMRESBuildSoln: back-solve (one lane), then x += sum nrs_j VV(j) */
-  if (!rc) rc = mspi_gm_build(c, k->g);
+  /* KSPGMRESBuildSoln: back-solve (one lane, H staged in LDS), then x += sum nrs_j VV(j) */
+  if (!rc) rc = mspi_gm_build(c, k->g, (int)k->o.restart);
   if (!rc) rc = mspi_maxpy_accum_basis(c, x, &k->g.st->nbuild, k->basis, k->stride, sc, k->n, k->g.grs, K);
   return rc;
 }

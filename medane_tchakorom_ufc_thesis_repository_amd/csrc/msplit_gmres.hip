@@ -333,6 +333,58 @@ __global__ void k_build(mspi_gmres_dev g) {
   st->nbuild = it + 1;
 }
 
+// The same back-solve with H(0..it, 0..it) and GRS staged in LDS by all lanes first, so lane 0's serial loop
+// reads LDS instead of one dependent HBM/L2 load per term; the same statements in the same order (bitwise
+// k_build).  m: the restart the arrays are sized for (H has m+1 columns of m+2 entries).
+__global__ __launch_bounds__(kUT) void k_build_lds(mspi_gmres_dev g, int m) {
+  __shared__ mspi_gmres_state lst;
+  extern __shared__ double lds[];  // H: (m+1) x (m+2), then GRS: m+2
+  const int t = threadIdx.x, m2 = m + 2;
+  double* lh = lds;
+  double* lg = lds + (size_t)(m + 1) * m2;
+  if (t < kStW) reinterpret_cast<int32_t*>(&lst)[t] = reinterpret_cast<const int32_t*>(g.st)[t];
+  for (int i = t; i < (m + 1) * m2; i += kUT) lh[i] = g.hh[i];
+  for (int i = t; i < m2; i += kUT) lg[i] = g.grs[i];
+  __syncthreads();
+  mspi_gmres_state* st = &lst;
+  __shared__ int nw;  // GRS entries to write back
+  if (t == 0) {
+    nw = 0;
+    st->nbuild = 0;
+    const int it = st->it - 1;
+    if (!st->skip_build && it >= 0) {
+#define LHH(a, b) lh[(b) * m2 + (a)]
+      double* nrs = lg;
+      bool ok = true;
+      if (LHH(it, it) != 0.0) {
+        nrs[it] = lg[it] / LHH(it, it);
+      } else {
+        st->reason = MSP_DIVERGED_BREAKDOWN;
+        ok = false;
+      }
+      for (int ii = 1; ok && ii <= it; ++ii) {
+        const int k = it - ii;
+        double tt = lg[k];
+#pragma unroll 8
+        for (int j = k + 1; j <= it; ++j) tt = tt - LHH(k, j) * nrs[j];  // the LDS reads of 8 terms issued together
+        if (LHH(k, k) == 0.0) {
+          st->reason = MSP_DIVERGED_BREAKDOWN;
+          ok = false;
+          nw = it + 1;
+          break;
+        }
+        nrs[k] = tt / LHH(k, k);
+      }
+#undef LHH
+      nw = it + 1;
+      if (ok) st->nbuild = it + 1;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < nw; i += kUT) g.grs[i] = lg[i];
+  if (t < kStW) const_cast<int32_t*>(reinterpret_cast<const int32_t*>(g.st))[t] = reinterpret_cast<int32_t*>(&lst)[t];
+}
+
 }  // namespace
 
 // ctx stream accessor lives in msplit_runtime.hip
@@ -369,8 +421,10 @@ extern "C" int mspi_gm_norm_update(msp_ctx* ctx, mspi_gmres_dev g, const double*
   return MSP_SUCCESS;
 }
 
-extern "C" int mspi_gm_build(msp_ctx* ctx, mspi_gmres_dev g) {
-  k_build<<<1, 1, 0, mspi_stream(ctx)>>>(g);
+extern "C" int mspi_gm_build(msp_ctx* ctx, mspi_gmres_dev g, int m) {
+  const size_t lds = ((size_t)(m + 1) * (m + 2) + (m + 2)) * sizeof(double);
+  if (lds <= 48 * 1024) k_build_lds<<<1, kUT, lds, mspi_stream(ctx)>>>(g, m);  // restart <= 75
+  else k_build<<<1, 1, 0, mspi_stream(ctx)>>>(g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     mspi_set_error(MSP_ERR_LIB, "k_build: %s", hipGetErrorString(e));

@@ -129,7 +129,7 @@ typedef struct {
 /* one-lane kernels of the GMRES recurrence */
 int mspi_gm_cycle_start(msp_ctx *ctx, mspi_gmres_dev g, const double *sumsq_dev);
 int mspi_gm_iter_update(msp_ctx *ctx, mspi_gmres_dev g);
-int mspi_gm_build(msp_ctx *ctx, mspi_gmres_dev g);
+int mspi_gm_build(msp_ctx *ctx, mspi_gmres_dev g, int m); /* m: the restart H and GRS are sized for */
 /* fold the ||w||^2 partials (stage-2 DBR) and run the Hessenberg update, one launch */
 int mspi_gm_norm_update(msp_ctx *ctx, mspi_gmres_dev g, const double *partial, int64_t nchunks, int m);
 /* CGS VecMAXPY + ||w||^2 partials, then mspi_gm_norm_update (h(it+1) = ||w||^2) */
