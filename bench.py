@@ -130,6 +130,9 @@ def parse():
     p.add_argument("--no-assembled", action="store_true",
                    help="N=1: skip the assembled_csr_operator measurement (the GMRES step with the operator handed "
                         "over as host CSR arrays, msp_mat_create_csr)")
+    p.add_argument("--no-verify-ranks", action="store_true",
+                   help="N>1: skip the post-timing multi-rank check (SMSM-global on a small box, one block per "
+                        "rank over the same communicator, bitwise against tests/golden/smsm_ranks.json)")
     p.add_argument("--require-rccl", action="store_true",
                    help="N>1: exit non-zero when the library communicator could not be created over RCCL and the "
                         "run would fall back to the host transport (for the driver's scaling runs)")
@@ -365,6 +368,52 @@ def golden_configs1(args, n):
     return json.load(open(GOLDEN))
 
 
+def verify_ranks(ctx, comm, world, rank):
+    """The N > 1 line's check, after the timed loop: SMSM-global on the small box of
+    tests/golden/smsm_ranks.json, one z-slab block per rank over the SAME library communicator the
+    timed steps used (RCCL on the driver's node: grouped ncclSend/ncclRecv planes, ncclAllGather of the
+    residual sums and LSQR partials), compared bit for bit with the single-process oracle's record for
+    this world size (outer history, LSQR counts, final residual, SHA-256 of this rank's block of x).
+    Returns (ok, mismatch list, seconds); every rank gets the all-ranks verdict."""
+    import hashlib
+    import numpy as np
+    import torch.distributed as dist
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import make_smsm, smsm_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Options
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "smsm_ranks.json")
+    if not os.path.exists(path):
+        return None, ["no record"], 0.0
+    g = json.load(open(path))
+    ref = g["worlds"].get(str(world))
+    if ref is None:
+        return None, [f"no record for {world} ranks"], 0.0
+    P, inn, out = g["problem"], g["inner"], g["outer"]
+    opts = " ".join(f"-inner{b + 1}_ksp_type gmres -inner{b + 1}_ksp_gmres_restart {inn['restart']} "
+                    f"-inner{b + 1}_ksp_max_it {inn['max_it']} -inner{b + 1}_ksp_rtol {inn['rtol']} "
+                    f"-inner{b + 1}_ksp_atol {inn['abstol']} -inner{b + 1}_pc_type none "
+                    f"-outer{b + 1}_ksp_type lsqr -outer{b + 1}_ksp_convergence_test default "
+                    f"-outer{b + 1}_ksp_lsqr_exact_mat_norm -outer{b + 1}_ksp_atol {out['abstol']} "
+                    f"-outer{b + 1}_ksp_max_it {out['max_it']} -outer{b + 1}_ksp_rtol {out['rtol']} "
+                    f"-outer{b + 1}_pc_type none" for b in range(world))
+    t0 = time.perf_counter()
+    nz = P["planes_per_block"] * world
+    blocks, mini = make_smsm(ctx, 3, P["nx"], P["ny"], nz, world, [rank], P["s"], Options(f"{opts} -s {P['s']}"),
+                             comm)
+    res = smsm_solve(blocks, comm, P["s"], mini, rtol=P["rtol"], max_outer=P["outer_its"])
+    xs = hashlib.sha256(np.ascontiguousarray(blocks[0].x.get_array(), np.float64).tobytes()).hexdigest()
+    mini.close()
+    got = {"outer_its": res.outer_its, "norm0_hex": float(res.norm0).hex(),
+           "hist_hex": [float(h).hex() for h in res.hist], "lsqr_its": [int(v) for v in res.lsqr_its],
+           "final_norm_hex": float(res.final_norm).hex()}
+    bad = [k for k in got if got[k] != ref[k]]
+    if xs != ref["x_block_sha256"][rank]:
+        bad.append("x_block_sha256")
+    allbad = [None] * world
+    dist.all_gather_object(allbad, bad)
+    mismatch = [f"rank {r}: {k}" for r, b in enumerate(allbad) for k in b]
+    return not mismatch, mismatch, time.perf_counter() - t0
+
+
 def check_step(ksp, x, ref):
     """Compare one GMRES step's result (iteration count, reason, every history entry as hex,
     SHA-256 of x) with a committed oracle record; outside any timed region."""
@@ -581,7 +630,7 @@ def main():
     stats = ctx.kernel_stats() if timing else {}
 
     # the result of the last timed step against the committed oracle record (outside the timed region)
-    verified, mismatch = None, []
+    verified, mismatch, ref_ranks = None, [], None
     ref = golden_configs1(args, n) if variant == "gmres" and world == 1 else None
     if ref is not None:
         verified, mismatch = check_step(ksp, x, ref["dbr"])
@@ -612,6 +661,14 @@ def main():
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed_max, updates = float(tmax[0]), float(t[1])
+        if not args.no_verify_ranks:
+            # collective on every rank, after the timed loop and outside it
+            verified, vmis, vsec = verify_ranks(ctx, comm, world, rank)
+            ref_ranks = {"reference": "tests/golden/smsm_ranks.json (oracle/oracle.c orc_smsm_solve, DBR order)",
+                         "checked": f"SMSM-global on a small box, {world} z-slab blocks, one per rank over this "
+                                    f"run's library communicator ({transport}): outer history (hex), LSQR counts, "
+                                    "final residual, SHA-256 of every rank's block of x",
+                         "mismatch": vmis, "seconds": round(vsec, 3)}
     else:
         elapsed_max, updates = elapsed, my_updates
 
@@ -642,6 +699,8 @@ def main():
                           "parallelism": f"{world} z-slab block(s), one per GPU",
                           "transport": transport},
                "verified": verified}
+        if ref_ranks is not None:
+            out["verification"] = ref_ranks
         if ref is not None:
             out["verification"] = {"reference": "tests/golden/configs1_seq.json['dbr'] (oracle/oracle.c, DBR order)",
                                    "checked": "iterations, reason, every residual-history entry (hex), SHA-256 of x",

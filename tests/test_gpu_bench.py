@@ -1,6 +1,7 @@
 """bench.py's own checks on the GPU box: the N > 1 line names its transport, --require-rccl refuses a run
-that fell back to the host transport, and the N = 1 step verifies its result against the committed oracle
-record (tests/golden/configs1_seq.json)."""
+that fell back to the host transport, the N = 1 step verifies its result against the committed oracle
+record (tests/golden/configs1_seq.json), and the N > 1 line carries the multi-rank check against
+tests/golden/smsm_ranks.json."""
 import json
 import os
 import socket
@@ -43,6 +44,18 @@ def test_two_rank_rehearsal_reports_host_transport():
     assert r.returncode == 0, r.stderr[-3000:]
     out = _json(r.stdout)
     assert out["n_gpus"] == 2 and out["config"]["transport"] == "host"
+    # the post-timing multi-rank check: SMSM-global over the same communicator, bitwise the oracle record
+    assert out["verified"] is True and out["verification"]["mismatch"] == [], out.get("verification")
+    assert "smsm_ranks.json" in out["verification"]["reference"]
+
+
+def test_three_rank_rehearsal_is_verified():
+    """Three ranks (an interior block with two neighbours): the multi-rank check reproduces the oracle's
+    three-block record bit for bit on every rank."""
+    r = _launch(3, ["--backend", "gloo"] + SMALL)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json(r.stdout)
+    assert out["n_gpus"] == 3 and out["verified"] is True, out.get("verification")
 
 
 def test_require_rccl_refuses_host_transport():

@@ -226,3 +226,17 @@ def test_configs1_seq_fixture_is_consistent():
     assert np.all(np.diff(hs) <= 0) and np.all(np.diff(hd) <= 0)
     assert not np.array_equal(hs, hd)                      # the two orders really differ
     assert float(np.max(np.abs(hd - hs) / np.abs(hs))) == g["dbr_vs_seq"]["max_rel_dev_hist"]
+
+
+def test_smsm_ranks_record_matches_oracle(oracle):
+    """tests/golden/smsm_ranks.json (bench.py's N > 1 check) is what the oracle computes now, for 2 and 3
+    blocks; the generator's own function rebuilds the records."""
+    import importlib.util
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_smsm_ranks", os.path.join(here, "golden", "make_smsm_ranks.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    rec = json.load(open(os.path.join(here, "golden", "smsm_ranks.json")))
+    assert sorted(rec["worlds"]) == [str(n) for n in range(2, 9)]
+    for nb in (2, 3):
+        assert gen.record(nb) == rec["worlds"][str(nb)]
