@@ -48,13 +48,14 @@ sys.path.insert(0, ROOT)
 METRIC = "DOF-updates/s on 3D 7-pt Poisson GMRES; achieved HBM GB/s vs peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 KERNEL_NAMES = {"mdot": "k_dot_stage1+2 (VecMDot, DBR)",
-                "maxpy": "k_maxpy_chunk (VecMAXPY, CGS update + fused ||w||^2, and BuildSoln)",
+                "maxpy": "k_box_maxpy_march (VecMAXPY, CGS update with W = A(sc x) recomputed on the z-march + "
+                         "fused ||w||^2) and k_maxpy_chunk (BuildSoln)",
                 "norm": "k_dot_stage1<1,self>+stage2 (VecNorm)",
                 "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy",
                 "spmm": "k_spmm (MatMatMult R = A S)", "dgemv": "k_dense_gemv (LSQR R v - alpha u + norm; S alpha)",
                 "dgemvt": "k_scaled_dot (LSQR scale + R^T u)",
                 "spmvdot": "k_box_spmv_mdot_march (GMRES MatMult of the box stencil fused with VecMDot stage 1: "
-                           "W not re-read)"}
+                           "W not stored)"}
 SPMV_NAMES = {"dv": "k_spmv_ell (MatMult/MatResidual, DV storage: one byte per entry)",
               "csr": "k_spmv_lds8 (MatMult/MatResidual, CSR storage)",
               "matfree": "k_stencil_spmv (MatMult/MatResidual, matrix-free)"}

@@ -256,7 +256,15 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
       rc = mspi_maxpy_norm_update_op(k->A, VV(k, it), sc + it, VV(k, it + 1), it + 1, k->basis, k->stride, sc, k->g,
                                      k->o.restart, stop);
   }
-  for (int it = 0; it < K && !rc && !opfuse; ++it) {
+  /* box stencils: W is not stored; the MAXPY recomputes its rows from VV(it) (which it streams anyway) */
+  const int wfree = !opfuse && k->o.restart <= MSPI_MAX_GROUP && mspi_gm_wfree(k->A);
+  for (int it = 0; it < K && !rc && wfree; ++it) {
+    rc = mspi_spmv_mdot(k->A, VV(k, it), sc + it, NULL, it + 1, k->basis, k->stride, sc, k->g.h, stop);
+    if (!rc)
+      rc = mspi_maxpy_norm_update_march(k->A, VV(k, it), sc + it, VV(k, it + 1), it + 1, k->basis, k->stride, sc,
+                                        k->g, k->o.restart, stop);
+  }
+  for (int it = 0; it < K && !rc && !opfuse && !wfree; ++it) {
     /* W = A (sc[it] VV(it))  (KSP_PCApplyBAorAB with PCNONE on the normalised VV(it)),
      * CGS: h = VecMDot(W, VV(0..it)) -- one fused launch where the operator allows */
     rc = mspi_spmv_mdot(k->A, VV(k, it), sc + it, k->tmp, it + 1, k->basis, k->stride, sc, k->g.h, stop);

@@ -140,6 +140,12 @@ int mspi_maxpy_norm_update(msp_ctx *ctx, const double *win, double *wout, int nv
 int mspi_spmv_scaled(msp_mat *A, const double *x, const double *sdev, double *vout, double *y, const int *stop);
 int mspi_spmv_mdot(msp_mat *A, const double *x, const double *sdev, double *y, int nv, const double *base,
                    int64_t stride, const double *scale, double *out_dev, const int *stop);
+/* the W-free step for box stencils: mspi_spmv_mdot(.., y = NULL, ..) then mspi_maxpy_norm_update_march, which
+   recomputes W = A (sdev[0] x) (x = VV(it), the basis' last vector) -- bitwise the stored-W step */
+int mspi_gm_wfree(const msp_mat *A);
+int mspi_maxpy_norm_update_march(msp_mat *A, const double *x, const double *sdev, double *wout, int nv,
+                                 const double *base, int64_t stride, const double *scale, mspi_gmres_dev g, int m,
+                                 const int *stop);
 int mspi_mdot_basis(msp_ctx *ctx, const double *w, int nv, const double *base, int64_t stride, const double *scale,
                     int64_t n, double *out_dev, const int *stop);
 int mspi_maxpy_norm_basis(msp_ctx *ctx, const double *win, double *wout, int nv, const double *base, int64_t stride,
@@ -173,6 +179,7 @@ uint64_t mspi_ctx_epoch(const msp_ctx *ctx);
 int msk_get_tuning(void);
 /* bumped by every launch-shape override (msk_set_march_z / _lines / msk_set_spmv_group) */
 int msk_get_shape_epoch(void);
+int msk_get_gm_wfree(void);
 int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
 /* ---- HBM mailboxes shared between processes (msplit_ipc.hip) ---- */
 #define MSPI_IPC_HANDLE_BYTES 64

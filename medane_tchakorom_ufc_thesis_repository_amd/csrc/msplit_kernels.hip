@@ -1861,6 +1861,7 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
           if (mr & (1u << k)) s = s + v[k] * (xq[k] * sc);
         wr[2 * j + q] = s;
       }
+      if (!y) continue;  // uniform: W is recomputed by the MAXPY after (k_box_maxpy_march), not stored
       if constexpr (NTY) {
         dx2 o;
         o.x = wr[2 * j];
@@ -1895,6 +1896,192 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     }
     __syncthreads();
     if (t < nv) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+#pragma unroll
+    for (int i = 0; i < 2 * kIters; ++i) {
+      xm[i] = xc[i];
+      xc[i] = xp[i];
+    }
+  }
+}
+
+// One vector group of the CGS MAXPY over a full chunk, u += sum_q a_q (V_{g+q} * s_q) in chunk_group's
+// arithmetic (group_sum left to right; G == 1: s + u), a_q = -adev[g + q].  SELF: the group's last vector is
+// x itself, whose 16 values of this chunk the caller holds in xs (the march registers): not read again.
+template <int G, int VAR, bool SELF>
+__device__ __forceinline__ void march_maxpy_group(double (&u)[2 * kIters], const Vecs& V,
+                                                  const double* __restrict__ adev, int g, int64_t base,
+                                                  const double (&xs)[2 * kIters]) {
+  double a[G], sv[G];
+  const double* vp[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    a[q] = -adev[g + q];
+    vp[q] = vec_at(V, g + q);
+    sv[q] = vec_scale(V, g + q);
+  }
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    double p0[G], p1[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      if (SELF && q == G - 1) {
+        p0[q] = xs[2 * j] * sv[q];
+        p1[q] = xs[2 * j + 1] * sv[q];
+      } else {
+        const double2* pv = reinterpret_cast<const double2*>(vp[q] + base + j * (2 * kT));
+        const double2 v = (VAR & 1) ? ld_nt(pv) : *pv;
+        p0[q] = v.x * sv[q];
+        p1[q] = v.y * sv[q];
+      }
+    }
+    const double s0 = group_sum<G>(a, p0), s1 = group_sum<G>(a, p1);
+    if constexpr (G == 1) {
+      u[2 * j] = s0 + u[2 * j];
+      u[2 * j + 1] = s1 + u[2 * j + 1];
+    } else {
+      u[2 * j] = u[2 * j] + s0;
+      u[2 * j + 1] = u[2 * j + 1] + s1;
+    }
+  }
+}
+
+// The GMRES step's CGS VecMAXPY for a box stencil whose fused MatMult+MDot (k_box_spmv_mdot_march, y = null)
+// did not store W: this kernel recomputes W = A (sc x) for its rows on the same chunk tiles, with the same
+// terms in the same order (bitwise that kernel's W), then wout = W - sum_j h_j VV(j) in k_maxpy_chunk's
+// grouping (the nv & 3 leading vectors, then groups of four), the last basis vector being x itself, taken
+// from the march registers.  It stores wout and the DBR partial of ||wout||^2 per chunk exactly as
+// k_maxpy_chunk<false, true, .> does.  Bytes per row: the presence byte, x once (+ the tile's halo lines),
+// nv - 1 basis vectors and wout, against 8 (nv + 2) for k_maxpy_chunk plus the 8 the MatMult spent storing W.
+// xcd & 1: XCD-contiguous eighths of each plane's tiles; xcd & 2: top plane groups first.
+template <int VAR, bool NTY>
+__global__ __launch_bounds__(kT) void k_box_maxpy_march(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
+                                                        const uint8_t* __restrict__ mask,
+                                                        const double* __restrict__ dval,
+                                                        const double* __restrict__ x,
+                                                        const double* __restrict__ sdev, double* __restrict__ wout,
+                                                        Vecs V, int nv, const double* __restrict__ adev,
+                                                        double* __restrict__ partial, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sx = reinterpret_cast<double*>(smem);  // window of plane z: kChunk + 2 nx doubles
+  __shared__ double red[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t cpp = P / kChunk;
+  int64_t tile, zg;
+  if (xcd & 1) {
+    const int64_t per = cpp / 8, slot = blockIdx.x / 8;
+    tile = (blockIdx.x % 8) * per + slot % per;
+    zg = slot / per;
+  } else {
+    tile = blockIdx.x % cpp;
+    zg = blockIdx.x / cpp;
+  }
+  if (xcd & 2) zg = (nz + zt - 1) / zt - 1 - zg;
+  const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
+  const double sc = *sdev;
+  double v[7];
+  march_values<false>(dval, v);
+  const int nh = nx / 2;
+  double xm[2 * kIters], xc[2 * kIters], xp[2 * kIters];
+  {
+    const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * t;
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double2 a = *reinterpret_cast<const double2*>(x + b0 + j * (2 * kT));
+      xc[2 * j] = a.x;
+      xc[2 * j + 1] = a.y;
+      if (z0 > 0) {
+        const double2 m2 = *reinterpret_cast<const double2*>(x + b0 - P + j * (2 * kT));
+        xm[2 * j] = m2.x;
+        xm[2 * j + 1] = m2.y;
+      } else {
+        xm[2 * j] = xm[2 * j + 1] = 0.0;
+      }
+    }
+  }
+  const int jrem = nv & 3;
+  for (int32_t z = z0; z < z1; ++z) {
+    const int64_t c = (int64_t)z * cpp + tile, c0 = c * kChunk, base = c0 + 2 * t;
+    uint32_t m[kIters];
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      if (z + 1 < nz) {
+        const double2 p2 = *reinterpret_cast<const double2*>(x + base + P + j * (2 * kT));
+        xp[2 * j] = p2.x;
+        xp[2 * j + 1] = p2.y;
+      } else {
+        xp[2 * j] = xp[2 * j + 1] = 0.0;
+      }
+      m[j] = *reinterpret_cast<const uint16_t*>(mask + base + j * (2 * kT));
+    }
+    double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0);
+    const bool hasl = t < nh && c0 - nx >= 0, hash = t < nh && c0 + kChunk + nx <= (int64_t)nz * P;
+    if (hasl) hl = *reinterpret_cast<const double2*>(x + c0 - nx + 2 * t);
+    if (hash) hh = *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * t);
+    __syncthreads();  // the previous plane's window reads (and its red reads) are done
+#pragma unroll
+    for (int j = 0; j < kIters; ++j)
+      *reinterpret_cast<double2*>(sx + nx + j * (2 * kT) + 2 * t) = make_double2(xc[2 * j], xc[2 * j + 1]);
+    if (t < nh) {
+      *reinterpret_cast<double2*>(sx + 2 * t) = hl;
+      *reinterpret_cast<double2*>(sx + nx + kChunk + 2 * t) = hh;
+    }
+    for (int i = t + kT; i < nh; i += kT) {
+      *reinterpret_cast<double2*>(sx + 2 * i) =
+          c0 - nx >= 0 ? *reinterpret_cast<const double2*>(x + c0 - nx + 2 * i) : make_double2(0.0, 0.0);
+      *reinterpret_cast<double2*>(sx + nx + kChunk + 2 * i) =
+          c0 + kChunk + nx <= (int64_t)nz * P ? *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * i)
+                                              : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    double u[2 * kIters];
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int e = j * (2 * kT) + 2 * t + q + nx;
+        const uint32_t mr = (m[j] >> (8 * q)) & 255u;
+        const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], xc[2 * j + q], sx[e + 1], sx[e + nx],
+                              xp[2 * j + q]};
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+          if (mr & (1u << k)) s = s + v[k] * (xq[k] * sc);
+        u[2 * j + q] = s;
+      }
+    }
+    // u -= sum_j h_j VV(j): leading nv & 3 vectors, then groups of four; VV(nv - 1) = x from xc
+    if (nv <= 3) {
+      if (jrem == 3) march_maxpy_group<3, VAR, true>(u, V, adev, 0, base, xc);
+      else if (jrem == 2) march_maxpy_group<2, VAR, true>(u, V, adev, 0, base, xc);
+      else march_maxpy_group<1, VAR, true>(u, V, adev, 0, base, xc);
+    } else {
+      if (jrem == 3) march_maxpy_group<3, VAR, false>(u, V, adev, 0, base, xc);
+      else if (jrem == 2) march_maxpy_group<2, VAR, false>(u, V, adev, 0, base, xc);
+      else if (jrem == 1) march_maxpy_group<1, VAR, false>(u, V, adev, 0, base, xc);
+#pragma unroll 1
+      for (int g = jrem; g + 4 < nv; g += 4) march_maxpy_group<4, VAR, false>(u, V, adev, g, base, xc);
+      march_maxpy_group<4, VAR, true>(u, V, adev, nv - 4, base, xc);
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double r0 = u[2 * j], r1 = u[2 * j + 1];
+      if constexpr (NTY) {
+        dx2 o;
+        o.x = r0;
+        o.y = r1;
+        __builtin_nontemporal_store(o, reinterpret_cast<dx2*>(wout + base + j * (2 * kT)));
+      } else {
+        *reinterpret_cast<double2*>(wout + base + j * (2 * kT)) = make_double2(r0, r1);
+      }
+      acc = acc + r0 * r0;
+      acc = acc + r1 * r1;
+    }
+    acc = wave_butterfly(acc);
+    if (lane == 0) red[wv] = acc;
+    __syncthreads();
+    if (t == 0) partial[c] = (red[0] + red[1]) + (red[2] + red[3]);
 #pragma unroll
     for (int i = 0; i < 2 * kIters; ++i) {
       xm[i] = xc[i];
@@ -2095,11 +2282,23 @@ extern "C" void msk_set_march_lines(int l) {
   ++msk_shape_epoch;
 }
 extern "C" int msk_get_shape_epoch(void) { return msk_shape_epoch; }
+// The W-free GMRES step for box stencils (k_box_maxpy_march recomputes W; the fused MatMult+MDot does not store
+// it): on unless MSPLIT_GM_WFREE=0; msk_set_gm_wfree switches it (A/B, tests) and re-keys captured cycles.
+__attribute__((visibility("hidden"))) int msk_gm_wfree = [] {
+  const char* e = getenv("MSPLIT_GM_WFREE");
+  return e ? (atoi(e) ? 1 : 0) : 1;
+}();
+extern "C" void msk_set_gm_wfree(int on) {
+  msk_gm_wfree = on ? 1 : 0;
+  ++msk_shape_epoch;
+}
+extern "C" int msk_get_gm_wfree(void) { return msk_gm_wfree; }
 #else
 extern __attribute__((visibility("hidden"))) int msk_tuning_flags;
 extern __attribute__((visibility("hidden"))) int msk_spmv_gb_override;
 extern __attribute__((visibility("hidden"))) int msk_march_z_override;
 extern __attribute__((visibility("hidden"))) int msk_march_lines_override;
+extern __attribute__((visibility("hidden"))) int msk_gm_wfree;
 #endif
 
 [[maybe_unused]] static inline XcdMap xcd_map(int32_t nrows, int64_t plane) {
@@ -2683,6 +2882,48 @@ extern "C" int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const
   else MSK_BSM2(false);
 #undef MSK_BSM2
 #undef MSK_BSM
+  return (int)hipGetLastError();
+}
+
+// whether msk_box_spmv_mdot takes its z-march form for this box (the condition above)
+static bool box_mdot_marches(int32_t nx, int64_t P, int64_t n, int d2) {
+  return !d2 && nx >= 2 && nx <= 2048 && P >= nx && P % kChunk == 0 && n > 0 && n % P == 0 && (nx & 1) == 0 &&
+         !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_FLAT) && !dv_flags_bad() && (n / P) <= INT32_MAX;
+}
+
+extern "C" int msk_box_wfree_fits(int32_t nx, int64_t P, int64_t n, int d2) {
+  return msk_gm_wfree && box_mdot_marches(nx, P, n, d2) ? 1 : 0;
+}
+
+extern "C" int msk_box_maxpy_march(int32_t nx, int64_t P, int64_t n, const uint8_t* mask, const double* dval,
+                                   const double* x, const double* sdev, double* wout, const Vecs* V, int nv,
+                                   const double* adev, double* partial, const int* stop, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (!box_mdot_marches(nx, P, n, 0) || nv < 1) return (int)hipErrorInvalidValue;
+  const double* last = V->base ? V->base + (int64_t)(nv - 1) * V->stride : (nv <= MSK_MAX_GROUP ? V->p[nv - 1] : nullptr);
+  if (last != x) return (int)hipErrorInvalidValue;  // the basis must end with x (GMRES: VV(it))
+  static const int zenv = [] {
+    const char* e = getenv("MSPLIT_MAXPY_ZT");
+    return e ? atoi(e) : 0;
+  }();
+  static const int rev_env = [] {
+    const char* e = getenv("MSPLIT_MAXPY_REV");
+    return e ? (atoi(e) ? 1 : 0) : -1;
+  }();
+  const int32_t nz = (int32_t)(n / P);
+  const int32_t zt = zenv > 0 ? zenv : 2;
+  const int64_t grid = (P / kChunk) * ((nz + zt - 1) / zt);
+  if (grid > INT32_MAX) return (int)hipErrorInvalidValue;
+  const int rev = (rev_env < 0 ? n > ((int64_t)1 << 25) : rev_env) ? 2 : 0;
+  const int xcd = ((P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD)) | rev;
+  const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
+  const bool nty = !(msk_tuning_flags & MSK_TUNE_MAXPY_TEMPORAL_ST);
+#define MSK_BMM(VAR_, NT_)                                                                                      \
+  k_box_maxpy_march<VAR_, NT_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, mask, dval, x,  \
+                                                                           sdev, wout, *V, nv, adev, partial, stop)
+  if (vec_var()) { if (nty) MSK_BMM(1, true); else MSK_BMM(1, false); }
+  else { if (nty) MSK_BMM(0, true); else MSK_BMM(0, false); }
+#undef MSK_BMM
   return (int)hipGetLastError();
 }
 

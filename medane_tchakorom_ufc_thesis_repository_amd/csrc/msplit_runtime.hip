@@ -1300,7 +1300,9 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
     {
       // the march's bytes (presence byte, x, W written) and MDot's nv basis vectors; W is not re-read, and
       // neither is x when it is the basis' last vector (its dot comes from the march's registers)
-      KTimer kt(c, MSP_KERNEL_SPMVDOT, march_bytes(A, false, false) + 8.0 * (double)n * nv);
+      // (y = NULL: the W-free step, W not written; mspi_maxpy_norm_update_march recomputes it)
+      const double wb = y ? 0.0 : 8.0 * (double)n;
+      KTimer kt(c, MSP_KERNEL_SPMVDOT, march_bytes(A, false, false) - wb + 8.0 * (double)n * nv);
       Vecs vg = {};
       vg.base = base;
       vg.stride = stride;
@@ -1309,7 +1311,7 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
       int self = 0;
       KCHK(msk_box_spmv_mdot(A->march_nx, P, n, A->march_d2, A->march_mask, A->dv_val, x, sdev, y, &vg, nv,
                              c->partial, nch, stop, &self, c->stream));
-      if (self) kt.set_bytes(march_bytes(A, false, false) + 8.0 * (double)n * (nv - 1));
+      if (self) kt.set_bytes(march_bytes(A, false, false) - wb + 8.0 * (double)n * (nv - 1));
     }
     KCHK(msk_dot_stage2(c->partial, nch, nv, out_dev, stop, c->stream));
     return MSP_SUCCESS;
@@ -1333,6 +1335,40 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
   }
   KCHK(msk_dot_stage2(c->partial, nch, nv, out_dev, stop, c->stream));  // ~4 us, not in the class stats
   return MSP_SUCCESS;
+}
+
+// The W-free GMRES step (DBR order, box stencil taking the fused march): mspi_spmv_mdot is called with
+// y = NULL and mspi_maxpy_norm_update_march recomputes W.  1 when A takes it.
+extern "C" int mspi_gm_wfree(const msp_mat* A) {
+  const msp_ctx* c = A->ctx;
+  if (c->reduce != MSP_REDUCE_DBR || !A->dv_on || !box_march(A) || A->march_d2 ||
+      (msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT_OFF))
+    return 0;
+  return msk_box_wfree_fits(A->march_nx, (int64_t)A->march_nx * A->march_ny, A->nrows, 0);
+}
+
+// VV(it+1) = A (sc x) - sum_j h_j VV(j), x = VV(it) the basis' last vector, with the ||VV(it+1)||^2 partials
+// (k_box_maxpy_march), then the fold + Hessenberg update (k_norm_update) as mspi_maxpy_norm_update.
+extern "C" int mspi_maxpy_norm_update_march(msp_mat* A, const double* x, const double* sdev, double* wout, int nv,
+                                            const double* base, int64_t stride, const double* scale,
+                                            mspi_gmres_dev g, int m, const int* stop) {
+  msp_ctx* c = A->ctx;
+  const int64_t n = A->nrows, nch = nchunks_of(n);
+  if (nch == 0 || nv <= 0 || !mspi_gm_wfree(A)) {
+    mspi_set_error(MSP_ERR_SUP, "W-free MAXPY on an operator that does not take it");
+    return MSP_ERR_SUP;
+  }
+  {
+    // the march's presence byte and x (VV(it), read once: also the basis' last vector), nv - 1 basis vectors, wout
+    KTimer kt(c, MSP_KERNEL_MAXPY, (double)n + 8.0 * (double)A->ncols + 8.0 * (double)n * nv);
+    Vecs vg = {};
+    vg.base = base;
+    vg.stride = stride;
+    vg.scale = scale;
+    KCHK(msk_box_maxpy_march(A->march_nx, (int64_t)A->march_nx * A->march_ny, n, A->march_mask, A->dv_val, x, sdev,
+                             wout, &vg, nv, g.h, c->partial, stop, c->stream));
+  }
+  return mspi_gm_norm_update(c, g, c->partial, nch, m);
 }
 
 static int vec_ok(const msp_vec* v, const char* name) {

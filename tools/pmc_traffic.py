@@ -23,7 +23,7 @@ from collections import defaultdict
 def classify(name: str):
     if "spmv_mdot" in name:     # the GMRES MatMult fused with VecMDot (k_box_spmv_mdot[_march], k_spmv_mdot)
         return "spmvdot"
-    if "k_maxpy" in name:
+    if "k_maxpy" in name or "maxpy_march" in name:  # k_maxpy_chunk, k_box_maxpy_march (the W-free CGS MAXPY)
         return "maxpy"
     if "k_dot_stage1" in name:
         return "norm" if "true>" in name.replace(" ", "") or ", true" in name else "mdot"
@@ -103,7 +103,14 @@ def main():
         rd = sum(2.0 * v for _, v in F[:m]) / m
         wr = sum(v for _, v in W[:m]) / m
         alg = None
-        if cls in ("maxpy", "mdot"):
+        wfree = any("maxpy_march" in nm for nm, _ in F[:m]) or any("maxpy_march" in nm for nm, _ in
+                                                                    per_class_f.get("maxpy", []))
+        if cls == "maxpy" and wfree and m % 31 == 0:
+            # GMRES(30) solves in dispatch order: 30 W-free MAXPYs (presence byte, x once, nv - 1 basis vectors,
+            # wout: N + 8 N (nv + 1), nv = it + 1), then BuildSoln's accumulate over 30 vectors (8 N (30 + 2))
+            alg = sum(8.0 * N * 32 if "maxpy_march" not in nm else N + 8.0 * N * ((i % 31) + 2)
+                      for i, (nm, _) in enumerate(F[:m])) / m
+        elif cls in ("maxpy", "mdot"):
             nvs = [nv_of(nm) for nm, _ in F[:m]]
             if all(nvs):
                 k = 2 if cls == "maxpy" else 1
@@ -114,8 +121,9 @@ def main():
             # one GMRES(30) solve in dispatch order: the Arnoldi step it dots W with nv = it + 1 basis vectors; the
             # march's bytes (presence byte, x, W written) plus those vectors, W not re-read and the last vector
             # (x itself) dotted from the march's registers (round 3; --x-reread for builds before it)
+            # (W-free builds: W is not written either, the MAXPY recomputes it)
             xr = 1 if a.x_reread else 0
-            alg = sum(17.0 * N + 8.0 * N * ((i % 30) + xr) for i in range(m)) / m
+            alg = sum((9.0 if wfree else 17.0) * N + 8.0 * N * ((i % 30) + xr) for i in range(m)) / m
         elif cls == "spmv":
             als = [spmv_alg(nm, a.n) for nm, _ in F[:m]]
             if all(als):
