@@ -2059,8 +2059,13 @@ __global__ __launch_bounds__(kT) void k_box_maxpy_march(int32_t nx, int64_t P, i
       if (jrem == 3) march_maxpy_group<3, VAR, false>(u, V, adev, 0, base, xc);
       else if (jrem == 2) march_maxpy_group<2, VAR, false>(u, V, adev, 0, base, xc);
       else if (jrem == 1) march_maxpy_group<1, VAR, false>(u, V, adev, 0, base, xc);
+      if constexpr ((VAR & 32) != 0) {  // two groups per iteration: 8 vectors' loads in one burst
+#pragma unroll 2
+        for (int g = jrem; g + 4 < nv; g += 4) march_maxpy_group<4, VAR, false>(u, V, adev, g, base, xc);
+      } else {
 #pragma unroll 1
-      for (int g = jrem; g + 4 < nv; g += 4) march_maxpy_group<4, VAR, false>(u, V, adev, g, base, xc);
+        for (int g = jrem; g + 4 < nv; g += 4) march_maxpy_group<4, VAR, false>(u, V, adev, g, base, xc);
+      }
       march_maxpy_group<4, VAR, true>(u, V, adev, nv - 4, base, xc);
     }
     double acc = 0.0;
@@ -2911,17 +2916,25 @@ extern "C" int msk_box_maxpy_march(int32_t nx, int64_t P, int64_t n, const uint8
     return e ? (atoi(e) ? 1 : 0) : -1;
   }();
   const int32_t nz = (int32_t)(n / P);
-  const int32_t zt = zenv > 0 ? zenv : 2;
+  // one plane per workgroup (x(z-+1) loaded per plane, twice the workgroups of the fused kernel's 2-plane march):
+  // 256^3 GMRES step 2.261 -> 2.336e10 over 2 planes, MAXPY 392 -> 368 us (profiles/r03/wfree/ab/)
+  const int32_t zt = zenv > 0 ? zenv : 1;
   const int64_t grid = (P / kChunk) * ((nz + zt - 1) / zt);
   if (grid > INT32_MAX) return (int)hipErrorInvalidValue;
   const int rev = (rev_env < 0 ? n > ((int64_t)1 << 25) : rev_env) ? 2 : 0;
   const int xcd = ((P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD)) | rev;
   const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
   const bool nty = !(msk_tuning_flags & MSK_TUNE_MAXPY_TEMPORAL_ST);
+  // MSPLIT_MAXPY_MARCH_U2=1: the group loop unrolled by two (A/B)
+  static const int u2 = [] {
+    const char* e = getenv("MSPLIT_MAXPY_MARCH_U2");
+    return e ? atoi(e) : 0;
+  }();
 #define MSK_BMM(VAR_, NT_)                                                                                      \
   k_box_maxpy_march<VAR_, NT_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, mask, dval, x,  \
                                                                            sdev, wout, *V, nv, adev, partial, stop)
-  if (vec_var()) { if (nty) MSK_BMM(1, true); else MSK_BMM(1, false); }
+  if (u2 && vec_var() && nty) MSK_BMM(33, true);
+  else if (vec_var()) { if (nty) MSK_BMM(1, true); else MSK_BMM(1, false); }
   else { if (nty) MSK_BMM(0, true); else MSK_BMM(0, false); }
 #undef MSK_BMM
   return (int)hipGetLastError();
