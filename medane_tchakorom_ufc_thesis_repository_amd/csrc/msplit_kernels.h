@@ -146,11 +146,12 @@ int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* m
 // The W-free GMRES step: msk_box_spmv_mdot with y = null (W not stored), then msk_box_maxpy_march, which
 // recomputes W for its rows on the same march tiles (bitwise) and runs the CGS VecMAXPY wout = W - sum_j adev_j
 // VV(j) with the DBR partials of ||wout||^2 (k_maxpy_chunk's arithmetic; V's last vector must be x).
-// msk_box_wfree_fits: 1 when the box takes the march form and the W-free step is on (msk_set_gm_wfree).
+// msk_box_wfree_fits: 1 when msk_box_spmv_mdot takes the box and the W-free step is on (msk_set_gm_wfree); the
+// MAXPY marches where the fused kernel does (planes of whole DBR chunks), else it takes one chunk per workgroup.
 void msk_set_gm_wfree(int on);
 int msk_get_gm_wfree(void);
 int msk_box_wfree_fits(int32_t nx, int64_t P, int64_t n, int d2);
-int msk_box_maxpy_march(int32_t nx, int64_t P, int64_t n, const uint8_t* mask, const double* dval, const double* x,
+int msk_box_maxpy_march(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval, const double* x,
                         const double* sdev, double* wout, const Vecs* V, int nv, const double* adev, double* partial,
                         const int* stop, hipStream_t s);
 // R[:, 0:nc] = A S[:, 0:nc] over DV storage in the ELL layout (W codes per row)

@@ -1715,6 +1715,7 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot(int32_t nx, int64_t P, int
       wr[2 * j + q] = s;
     }
     const int64_t r = base + j * (2 * kT);
+    if (!y) continue;  // uniform: the W-free step (k_box_maxpy recomputes W)
     if (full) {
       if constexpr (NTY) {
         dx2 o;
@@ -2093,6 +2094,166 @@ __global__ __launch_bounds__(kT) void k_box_maxpy_march(int32_t nx, int64_t P, i
       xc[i] = xp[i];
     }
   }
+}
+
+// march_maxpy_group for a ragged last chunk: chunk_group<G, FULL = false>'s guarded loads (rows >= n add 0.0).
+template <int G, bool SELF>
+__device__ __forceinline__ void ragged_maxpy_group(double (&u)[2 * kIters], const Vecs& V,
+                                                   const double* __restrict__ adev, int g, int64_t base, int64_t n,
+                                                   const double (&xs)[2 * kIters]) {
+  double a[G], sv[G];
+  const double* vp[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    a[q] = -adev[g + q];
+    vp[q] = vec_at(V, g + q);
+    sv[q] = vec_scale(V, g + q);
+  }
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    const int64_t e = base + j * (2 * kT);
+    double p0[G], p1[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      if (SELF && q == G - 1) {
+        p0[q] = e < n ? xs[2 * j] * sv[q] : 0.0;
+        p1[q] = e + 1 < n ? xs[2 * j + 1] * sv[q] : 0.0;
+      } else {
+        p0[q] = e < n ? vp[q][e] * sv[q] : 0.0;
+        p1[q] = e + 1 < n ? vp[q][e + 1] * sv[q] : 0.0;
+      }
+    }
+    const double s0 = group_sum<G>(a, p0), s1 = group_sum<G>(a, p1);
+    if constexpr (G == 1) {
+      u[2 * j] = s0 + u[2 * j];
+      u[2 * j + 1] = s1 + u[2 * j + 1];
+    } else {
+      u[2 * j] = u[2 * j] + s0;
+      u[2 * j + 1] = u[2 * j + 1] + s1;
+    }
+  }
+}
+
+// The W-free MAXPY where the fused kernel does not march (k_box_spmv_mdot: one DBR chunk per workgroup, 2D boxes,
+// planes that do not hold whole chunks, a ragged last chunk): W for the chunk's rows exactly as k_box_spmv_mdot
+// computes it (the same window, the same terms in the same order), then k_box_maxpy_march's MAXPY, x's values from
+// the window's own rows; a ragged chunk follows k_maxpy_chunk's guarded path (stores and squares for rows < n).
+template <bool D2, int VAR, bool NTY>
+__global__ __launch_bounds__(kT) void k_box_maxpy(int32_t nx, int64_t P, int64_t n, const uint8_t* __restrict__ mask,
+                                                  const double* __restrict__ dval, const double* __restrict__ x,
+                                                  const double* __restrict__ sdev, double* __restrict__ wout, Vecs V,
+                                                  int nv, const double* __restrict__ adev,
+                                                  double* __restrict__ partial, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sx = reinterpret_cast<double*>(smem);  // window of kChunk + 2 nx doubles
+  __shared__ double red[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t c = blockIdx.x, c0 = c * kChunk, lo = c0 - nx;
+  const int64_t base = c0 + 2 * t;
+  const bool full = (c + 1) * kChunk <= n;
+  const int wlen = kChunk + 2 * nx;
+  if ((nx & 1) == 0 && lo >= 0 && lo + wlen <= n) {
+    const double2* x2 = reinterpret_cast<const double2*>(x + lo);
+    for (int i = t; i < wlen / 2; i += kT) reinterpret_cast<double2*>(sx)[i] = x2[i];
+  } else {
+    for (int i = t; i < wlen; i += kT) {
+      const int64_t r = lo + i;
+      sx[i] = r >= 0 && r < n ? x[r] : 0.0;
+    }
+  }
+  const double sc = *sdev;
+  double v[7];
+  march_values<D2>(dval, v);
+  uint32_t m[2 * kIters];
+  double xm[2 * kIters], xp[2 * kIters];
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t r = base + j * (2 * kT) + q;
+      const uint32_t mr = r < n ? (uint32_t)mask[r] : 0u;
+      m[2 * j + q] = mr;
+      xm[2 * j + q] = (mr & 1u) ? x[r - P] : 0.0;
+      xp[2 * j + q] = (mr & 64u) ? x[r + P] : 0.0;
+    }
+  }
+  __syncthreads();
+  double u[2 * kIters], xs[2 * kIters];
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = j * (2 * kT) + 2 * t + q + nx;
+      const uint32_t mr = m[2 * j + q];
+      const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], sx[e], sx[e + 1], sx[e + nx], xp[2 * j + q]};
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 7; ++k)
+        if (mr & (1u << k)) s = s + v[k] * (xq[k] * sc);
+      u[2 * j + q] = s;
+      xs[2 * j + q] = sx[e];
+    }
+  }
+  const int jrem = nv & 3;
+  double acc = 0.0;
+  if (full) {
+    if (nv <= 3) {
+      if (jrem == 3) march_maxpy_group<3, VAR, true>(u, V, adev, 0, base, xs);
+      else if (jrem == 2) march_maxpy_group<2, VAR, true>(u, V, adev, 0, base, xs);
+      else march_maxpy_group<1, VAR, true>(u, V, adev, 0, base, xs);
+    } else {
+      if (jrem == 3) march_maxpy_group<3, VAR, false>(u, V, adev, 0, base, xs);
+      else if (jrem == 2) march_maxpy_group<2, VAR, false>(u, V, adev, 0, base, xs);
+      else if (jrem == 1) march_maxpy_group<1, VAR, false>(u, V, adev, 0, base, xs);
+#pragma unroll 1
+      for (int g = jrem; g + 4 < nv; g += 4) march_maxpy_group<4, VAR, false>(u, V, adev, g, base, xs);
+      march_maxpy_group<4, VAR, true>(u, V, adev, nv - 4, base, xs);
+    }
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double r0 = u[2 * j], r1 = u[2 * j + 1];
+      if constexpr (NTY) {
+        dx2 o;
+        o.x = r0;
+        o.y = r1;
+        __builtin_nontemporal_store(o, reinterpret_cast<dx2*>(wout + base + j * (2 * kT)));
+      } else {
+        *reinterpret_cast<double2*>(wout + base + j * (2 * kT)) = make_double2(r0, r1);
+      }
+      acc = acc + r0 * r0;
+      acc = acc + r1 * r1;
+    }
+  } else {
+    if (nv <= 3) {
+      if (jrem == 3) ragged_maxpy_group<3, true>(u, V, adev, 0, base, n, xs);
+      else if (jrem == 2) ragged_maxpy_group<2, true>(u, V, adev, 0, base, n, xs);
+      else ragged_maxpy_group<1, true>(u, V, adev, 0, base, n, xs);
+    } else {
+      if (jrem == 3) ragged_maxpy_group<3, false>(u, V, adev, 0, base, n, xs);
+      else if (jrem == 2) ragged_maxpy_group<2, false>(u, V, adev, 0, base, n, xs);
+      else if (jrem == 1) ragged_maxpy_group<1, false>(u, V, adev, 0, base, n, xs);
+#pragma unroll 1
+      for (int g = jrem; g + 4 < nv; g += 4) ragged_maxpy_group<4, false>(u, V, adev, g, base, n, xs);
+      ragged_maxpy_group<4, true>(u, V, adev, nv - 4, base, n, xs);
+    }
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const int64_t e = base + j * (2 * kT);
+      if (e < n) {
+        wout[e] = u[2 * j];
+        acc = acc + u[2 * j] * u[2 * j];
+      }
+      if (e + 1 < n) {
+        wout[e + 1] = u[2 * j + 1];
+        acc = acc + u[2 * j + 1] * u[2 * j + 1];
+      }
+    }
+  }
+  acc = wave_butterfly(acc);
+  if (lane == 0) red[wv] = acc;
+  __syncthreads();
+  if (t == 0) partial[c] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // The presence byte of each row of a box stencil in the ELL layout (8 codes per row):
@@ -2896,17 +3057,39 @@ static bool box_mdot_marches(int32_t nx, int64_t P, int64_t n, int d2) {
          !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_FLAT) && !dv_flags_bad() && (n / P) <= INT32_MAX;
 }
 
+// the boxes msk_box_spmv_mdot takes (marched or not)
+static bool box_mdot_fits(int32_t nx, int64_t P) { return nx >= 2 && nx <= 2048 && P >= nx && !dv_flags_bad(); }
+
 extern "C" int msk_box_wfree_fits(int32_t nx, int64_t P, int64_t n, int d2) {
-  return msk_gm_wfree && box_mdot_marches(nx, P, n, d2) ? 1 : 0;
+  return msk_gm_wfree && n > 0 && box_mdot_fits(nx, P) ? 1 : 0;
 }
 
-extern "C" int msk_box_maxpy_march(int32_t nx, int64_t P, int64_t n, const uint8_t* mask, const double* dval,
+extern "C" int msk_box_maxpy_march(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval,
                                    const double* x, const double* sdev, double* wout, const Vecs* V, int nv,
                                    const double* adev, double* partial, const int* stop, hipStream_t s) {
   if (n <= 0) return 0;
-  if (!box_mdot_marches(nx, P, n, 0) || nv < 1) return (int)hipErrorInvalidValue;
+  if (!box_mdot_fits(nx, P) || nv < 1) return (int)hipErrorInvalidValue;
   const double* last = V->base ? V->base + (int64_t)(nv - 1) * V->stride : (nv <= MSK_MAX_GROUP ? V->p[nv - 1] : nullptr);
   if (last != x) return (int)hipErrorInvalidValue;  // the basis must end with x (GMRES: VV(it))
+  const bool nt = !(msk_tuning_flags & MSK_TUNE_MAXPY_TEMPORAL_ST);
+  if (!box_mdot_marches(nx, P, n, d2)) {  // the unmarched form, one chunk per workgroup (as k_box_spmv_mdot)
+    const int64_t nch = (n + kChunk - 1) / kChunk;
+    if (nch > INT32_MAX) return (int)hipErrorInvalidValue;
+    const size_t ldsu = (size_t)(kChunk + 2 * nx) * sizeof(double);
+#define MSK_BMU(D_, VAR_, NT_)                                                                                      \
+  k_box_maxpy<D_, VAR_, NT_><<<dim3((unsigned)nch), dim3(kT), ldsu, s>>>(nx, P, n, mask, dval, x, sdev, wout, *V, nv, \
+                                                                        adev, partial, stop)
+#define MSK_BMU2(D_)                                                                          \
+  do {                                                                                        \
+    if (vec_var()) { if (nt) MSK_BMU(D_, 1, true); else MSK_BMU(D_, 1, false); }              \
+    else { if (nt) MSK_BMU(D_, 0, true); else MSK_BMU(D_, 0, false); }                        \
+  } while (0)
+    if (d2) MSK_BMU2(true);
+    else MSK_BMU2(false);
+#undef MSK_BMU2
+#undef MSK_BMU
+    return (int)hipGetLastError();
+  }
   static const int zenv = [] {
     const char* e = getenv("MSPLIT_MAXPY_ZT");
     return e ? atoi(e) : 0;
@@ -2924,7 +3107,7 @@ extern "C" int msk_box_maxpy_march(int32_t nx, int64_t P, int64_t n, const uint8
   const int rev = (rev_env < 0 ? n > ((int64_t)1 << 25) : rev_env) ? 2 : 0;
   const int xcd = ((P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD)) | rev;
   const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
-  const bool nty = !(msk_tuning_flags & MSK_TUNE_MAXPY_TEMPORAL_ST);
+  const bool nty = nt;
   // MSPLIT_MAXPY_MARCH_U2=1: the group loop unrolled by two (A/B)
   static const int u2 = [] {
     const char* e = getenv("MSPLIT_MAXPY_MARCH_U2");

@@ -1341,10 +1341,9 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
 // y = NULL and mspi_maxpy_norm_update_march recomputes W.  1 when A takes it.
 extern "C" int mspi_gm_wfree(const msp_mat* A) {
   const msp_ctx* c = A->ctx;
-  if (c->reduce != MSP_REDUCE_DBR || !A->dv_on || !box_march(A) || A->march_d2 ||
-      (msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT_OFF))
+  if (c->reduce != MSP_REDUCE_DBR || !A->dv_on || !box_march(A) || (msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT_OFF))
     return 0;
-  return msk_box_wfree_fits(A->march_nx, (int64_t)A->march_nx * A->march_ny, A->nrows, 0);
+  return msk_box_wfree_fits(A->march_nx, (int64_t)A->march_nx * A->march_ny, A->nrows, A->march_d2);
 }
 
 // VV(it+1) = A (sc x) - sum_j h_j VV(j), x = VV(it) the basis' last vector, with the ||VV(it+1)||^2 partials
@@ -1365,7 +1364,7 @@ extern "C" int mspi_maxpy_norm_update_march(msp_mat* A, const double* x, const d
     vg.base = base;
     vg.stride = stride;
     vg.scale = scale;
-    KCHK(msk_box_maxpy_march(A->march_nx, (int64_t)A->march_nx * A->march_ny, n, A->march_mask, A->dv_val, x, sdev,
+    KCHK(msk_box_maxpy_march(A->march_nx, (int64_t)A->march_nx * A->march_ny, n, A->march_d2, A->march_mask, A->dv_val, x, sdev,
                              wout, &vg, nv, g.h, c->partial, stop, c->stream));
   }
   return mspi_gm_norm_update(c, g, c->partial, nch, m);

@@ -106,14 +106,38 @@ def test_wfree_eager_and_captured(ctx, oracle, timing):
     _check(ctx, oracle, A, b, 30, 70, timing=timing)
 
 
-def test_wfree_not_taken_where_the_march_does_not_fit(ctx, oracle):
-    """Planes that do not hold whole 4096-row chunks keep the stored-W step (the unmarched fused kernel); 2D boxes
-    and odd nx too.  GMRES still equals the oracle."""
+@pytest.mark.parametrize("shape", [(100, 30, 9), (37, 11, 9), (256, 40, 7), (2, 3, 50), (300, 7, 5), (2048, 3, 2),
+                                   (256, 64, 0), (100, 37, 0), (33, 7, 0), (512, 40, 0), (300, 1, 0)])
+@pytest.mark.parametrize("peclet", [None, (0.5, -0.25, 0.3)])
+def test_wfree_unmarched_forms(ctx, oracle, shape, peclet):
+    """Where the fused kernel does not march -- planes that do not hold whole 4096-row chunks, a ragged last chunk
+    (n % 4096 != 0, incl. a single ragged chunk), and 2D boxes (nz = 0 here: nx x ny, marched as nx x 1 x ny) --
+    the W-free MAXPY takes one chunk per workgroup (k_box_maxpy) and still equals the stored-W step and the oracle
+    bit for bit."""
+    nx, ny, nz = shape
+    dim = 2 if nz == 0 else 3
+    if peclet is not None and dim == 2:
+        peclet = (peclet[0], peclet[1], 0.0)
+    if dim == 3:
+        A = Mat.box_stencil(ctx, 3, nx, ny, nz) if peclet is None else Mat.box_convdiff(ctx, 3, nx, ny, nz, False,
+                                                                                        False, peclet)
+    else:
+        A = Mat.box_stencil(ctx, 2, nx, ny) if peclet is None else Mat.box_convdiff(ctx, 2, nx, ny, 1, False, False,
+                                                                                    peclet)
+    n = A.shape[0]
+    assert _L().msk_box_wfree_fits(nx, nx * (ny if dim == 3 else 1), n, 1 if dim == 2 else 0) == 1
+    _check(ctx, oracle, A, np.random.default_rng(SEED).uniform(-1, 1, n), 12, 30)
+
+
+def test_wfree_not_taken(ctx, oracle):
+    """Boxes the fused kernel does not take (nx > 2048, or one-wide lines) keep the stored-W path; with the
+    switch off no box takes it."""
     L = _L()
-    assert L.msk_box_wfree_fits(100, 100 * 30, 100 * 30 * 4, 0) == 0
-    assert L.msk_box_wfree_fits(256, 256 * 16, 256 * 16 * 4, 1) == 0
-    assert L.msk_box_wfree_fits(4095, 4095 * 4096, 4095 * 4096, 0) == 0
-    A = Mat.box_stencil(ctx, 3, 100, 30, 9)
+    assert L.msk_box_wfree_fits(4096, 4096 * 2, 4096 * 2 * 3, 0) == 0
+    assert L.msk_box_wfree_fits(1, 50, 50 * 7, 0) == 0
+    with wfree(0):
+        assert L.msk_box_wfree_fits(256, 256 * 16, 256 * 16 * 4, 0) == 0
+    A = Mat.box_stencil(ctx, 3, 1, 30, 20)
     _check(ctx, oracle, A, np.random.default_rng(SEED).uniform(-1, 1, A.shape[0]), 30, 40)
 
 
