@@ -106,6 +106,7 @@ int main(int argc, char **argv) {
   memset(&t, 0, sizeof(t));
   t.world = world;
   t.rank = rank;
+  const char *tname = "none"; /* the transport that actually carries the exchange and the sums */
 #ifdef MSD_MPI
   t.barrier = mpi_barrier;
   t.bcast = mpi_bcast;
@@ -126,10 +127,18 @@ int main(int argc, char **argv) {
         ok = 0;
       }
     }
+    /* -msplit_require_rccl: a run that would fall back to the host transport stops before any solve, so an
+     * N-GPU measurement can never silently take the MPI path (bench.py --require-rccl) */
+    if (!ok && msd_opt_has(o, NULL, "msplit_require_rccl")) {
+      if (rank == 0) fprintf(stderr, "msplit: -msplit_require_rccl but the RCCL communicator is unavailable\n");
+      MPI_Finalize();
+      return 3;
+    }
     if (!ok && msp_comm_create_host(ctx, world, rank, mpi_allgather, NULL, &t.comm)) {
       fprintf(stderr, "msp_comm_create_host: %s\n", msp_get_last_error());
       return 1;
     }
+    tname = ok ? "rccl" : "host";
   }
 #endif
   msd_result r;
@@ -141,7 +150,8 @@ int main(int argc, char **argv) {
   if (rc == MSP_ERR_ARG_OUTOFRANGE && async) rc = 0; /* stopped at -max_outer: still report */
   if (!rc && rank == 0) {
     if (msd_opt_has(o, NULL, "json")) {
-      printf("{\"program\": \"%s\", \"host\": \"c\", \"ranks\": %d, \"blocks\": %d, ", prog, world, p.nb);
+      printf("{\"program\": \"%s\", \"host\": \"c\", \"ranks\": %d, \"blocks\": %d, \"transport\": \"%s\", ", prog,
+             world, p.nb, tname);
       if (async) {
         printf("\"iterations\": [");
         for (int i = 0; i < r.nlocal; ++i) printf("%s%d", i ? ", " : "", r.iterations[i]);

@@ -76,17 +76,81 @@ def test_c_host_am_matches_python_host(ctx, built):
     assert c["final_norm"] == py["final_norm"] and c["error"] == py["error"]
 
 
-@pytest.mark.parametrize("prog,args", [
-    ("synchronous-multisplitting", ["-m", "32", "-n", "32", "-rtol", "1e-6"] + INNER2),
-    ("synchronous-multisplitting-synchronous-minimization-global", ["-dim", "3", "-m", "8", "-n", "8", "-p", "8",
-                                                                    "-s", "4", "-rtol", "1e-6"] + INNER2 + OUTER2),
-])
-def test_c_host_mpi_two_ranks_equals_one_process(ctx, built, prog, args):
-    """One block per rank over MPI: bitwise the single-process run (ordered sums)."""
-    one = _run([prog] + args)
-    two = _run([prog] + args, mpi=2)
-    assert two["ranks"] == 2 and two["outer_its"] == one["outer_its"]
-    assert two["final_norm"] == one["final_norm"] and two["error"] == one["error"]
+SM = "synchronous-multisplitting"
+SMSM = "synchronous-multisplitting-synchronous-minimization-global"
+INNER_ORC = dict(restart=30, max_it=20, rtol=1e-20, abstol=1e-50)
+OUTER_ORC = dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
+
+
+def _oracle_record(oracle, prog, dim, nx, ny, nz, nb, s, rtol):
+    """The DBR oracle's run of the same problem (orc_sm_solve / orc_smsm_solve: one process, nb blocks)."""
+    inner = dict(INNER_ORC, reduce_mode=oracle.REDUCE_DBR)
+    if prog == SM:
+        return oracle.sm_solve(dim, nx, ny, nz, nb, rtol, inner, max_outer=200)
+    return oracle.smsm_solve(dim, nx, ny, nz, nb, s, rtol, inner, dict(OUTER_ORC, reduce_mode=oracle.REDUCE_DBR),
+                             max_outer=200)
+
+
+def _assert_same_run(got, want, what):
+    """Outer count, every outer-history entry (and LSQR count), norm0 and the final residual, bit for bit; on a
+    mismatch the message names the first outer iteration at which the two runs part."""
+    gh = [float.fromhex(h) for h in got["hist_hex"]]
+    wh = [float(v) for v in want["hist"]]
+    first = next((i for i in range(min(len(gh), len(wh))) if gh[i] != wh[i]), None)
+    if first is None and len(gh) != len(wh):
+        first = min(len(gh), len(wh))
+    detail = (f"{what}: transport {got.get('transport')}, outer_its {got['outer_its']} vs {want['outer_its']}, first "
+              f"diverging outer iteration {first}\n got  hist {gh}\n want hist {wh}\n"
+              f" got  lsqr {got.get('lsqr_its')}\n want lsqr {list(want.get('lsqr_its', []))}")
+    assert first is None and got["outer_its"] == want["outer_its"], detail
+    if "lsqr_its" in want:
+        assert got["lsqr_its"] == [int(v) for v in want["lsqr_its"]], detail
+    assert got["norm0"] == want["norm0"], detail
+
+
+def _problem_args(prog, dim, nx, ny, nz, nb, s, rtol):
+    a = ["-m", str(nx), "-n", str(ny), "-rtol", repr(rtol)] + _inner(nb, 20)
+    if dim == 3:
+        a = ["-dim", "3", "-p", str(nz)] + a
+    if prog == SMSM:
+        a += ["-s", str(s)] + _outer(nb)
+    return [prog] + a
+
+
+# SM and SMSM-global at 2, 3 and 4 ranks, 2D and 3D (24 lines of 32 / 12 planes divide by every world size).  The
+# 3D 8x8x8 SMSM-global case is the one GPUTEST_r03 caught at 5 outer iterations against the oracle's 3.
+MPI_CASES = [(SM, 2, 24, 32, 1, 2, 0, 1e-6), (SMSM, 3, 8, 8, 8, 2, 4, 1e-6),
+             (SMSM, 2, 24, 32, 1, 2, 4, 1e-6), (SM, 3, 8, 8, 12, 3, 0, 1e-6), (SMSM, 3, 8, 8, 12, 3, 4, 1e-6),
+             (SMSM, 2, 24, 32, 1, 3, 3, 1e-6), (SM, 2, 24, 32, 1, 4, 0, 1e-6), (SMSM, 3, 8, 8, 12, 4, 4, 1e-6)]
+
+
+@pytest.mark.parametrize("case", MPI_CASES, ids=lambda c: f"{'smsm' if c[0] == SMSM else 'sm'}-{c[1]}d-{c[5]}ranks")
+def test_c_host_mpi_ranks_equal_oracle(ctx, oracle, built, case):
+    """One block per MPI rank over the host transport (every rank shares the box's one GPU, which RCCL refuses;
+    pinned with -msplit_transport host so the run says which transport it took): the outer history, the LSQR
+    counts and the final residual are the single-process run's and the DBR oracle's, bit for bit
+    (comm.c:126-141, synchronous-multisplitting.c:170-206, SMSM-global.c:288-363)."""
+    prog, dim, nx, ny, nz, nb, s, rtol = case
+    args = _problem_args(prog, dim, nx, ny, nz, nb, s, rtol)
+    want = _oracle_record(oracle, prog, dim, nx, ny, nz, nb, s, rtol)
+    one = _run(args + ["-nb", str(nb)])
+    _assert_same_run(one, want, "one process vs oracle")
+    got = _run(args + ["-msplit_transport", "host"], mpi=nb)
+    assert got["ranks"] == nb and got["transport"] == "host"
+    _assert_same_run(got, want, f"{nb} MPI ranks vs oracle")
+    assert got["final_norm"] == one["final_norm"] and got["error"] == one["error"]
+    if prog == SMSM:
+        assert got["final_norm"] == want["final_norm"]
+
+
+def test_c_host_mpi_require_rccl_refuses_the_host_path(built):
+    """-msplit_require_rccl: two ranks on one GPU cannot get an RCCL communicator, so the run stops (exit 3)
+    before any solve instead of silently measuring the MPI path."""
+    exe = os.path.join(HOST, "msplit_driver_mpi")
+    p = subprocess.run([MPIEXEC] + MPI_LAUNCH + ["-n", "2", exe] + _problem_args(SM, 2, 24, 32, 1, 2, 0, 1e-6)
+                       + ["-msplit_require_rccl", "-json"], capture_output=True, text=True, timeout=150)
+    assert p.returncode != 0 and "require_rccl" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
 
 
 def test_c_host_mpi_am_terminates(ctx, built):
