@@ -337,6 +337,10 @@ int msp_mat_matmult_dense(msp_mat *A, const msp_dense *S, msp_dense *R);
 #define MSP_COMM_ID_BYTES 128
 typedef int (*msp_allgather_fn)(void *user, const double *send, double *recv, int64_t count);
 int msp_comm_get_unique_id(uint8_t id[MSP_COMM_ID_BYTES]);
+/* *ok = 1 when librccl.so.1 loads and exports what msp_comm needs: the readiness test of the ranks that do
+ * not create the id (msp_comm_get_unique_id starts RCCL's bootstrap root -- a thread and a listening socket --
+ * and belongs on rank 0 only). */
+int msp_comm_rccl_available(int32_t *ok);
 int msp_comm_create_rccl(msp_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[MSP_COMM_ID_BYTES],
                          msp_comm **comm);
 int msp_comm_create_host(msp_ctx *ctx, int32_t nranks, int32_t rank, msp_allgather_fn fn, void *user,

@@ -131,6 +131,7 @@ _SIGS = {
     "msp_dense_create_view": [_vp, C.c_int32, C.c_int32, _P(_vp)],
     "msp_mat_matmult_dense": [_vp, _vp, _vp],
     "msp_comm_get_unique_id": [_P(C.c_uint8)],
+    "msp_comm_rccl_available": [_i32p],
     "msp_comm_create_rccl": [_vp, C.c_int32, C.c_int32, _P(C.c_uint8), _P(_vp)],
     "msp_comm_create_host": [_vp, C.c_int32, C.c_int32, ALLGATHER_FN, _vp, _P(_vp)],
     "msp_comm_destroy": [_P(_vp)],

@@ -222,13 +222,18 @@ class LibComm:
                 dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
                 return bool(int(t.item()))
 
-            # readiness before the collective ncclCommInitRank: a rank that cannot load RCCL (or get an id)
-            # must not leave the others blocked inside init, so all ranks agree first
-            err = None
+            # readiness before the collective ncclCommInitRank: a rank that cannot load RCCL (or rank 0 that
+            # cannot get an id) must not leave the others blocked inside init, so all ranks agree first.  Only
+            # rank 0 creates the id (ncclGetUniqueId starts a bootstrap root thread and socket, as in
+            # host/main.c); the others test that the library loads.
+            err, uid = None, None
             try:
-                uid = Comm.unique_id()
+                if self.rank == 0:
+                    uid = Comm.unique_id()
+                elif not Comm.rccl_available():
+                    err = RuntimeError("librccl.so.1 could not be loaded")
             except Exception as e:
-                err, uid = e, None
+                err = e
             ready = agree(err is None)
             if ready:
                 obj = [uid if self.rank == 0 else None]

@@ -205,7 +205,7 @@ int msp_ksp_set_up(msp_ksp *k) {
   const size_t nd = (size_t)((m + 2) * (m + 1) + 5 * (m + 2) + k->hist_cap);
   const size_t st_bytes = (sizeof(mspi_gmres_state) + 63) / 64 * 64;
   int rc = mspi_malloc(k->ctx, (void **)&k->basis, (size_t)mv * (size_t)k->stride * sizeof(double) + 4096);
-  if (!rc) rc = mspi_malloc(k->ctx, (void **)&k->tmp, (size_t)k->stride * sizeof(double) + 4096);
+  /* W (k->tmp) is allocated by the first cycle that stores it (ensure_w): the W-free step never does */
   if (!rc) rc = mspi_malloc(k->ctx, &k->gblock, st_bytes + nd * sizeof(double));
   if (!rc) rc = mspi_host_malloc((void **)&k->hst, sizeof(mspi_gmres_state));
   k->hist = (double *)calloc((size_t)k->hist_cap, sizeof(double));
@@ -238,6 +238,23 @@ int msp_ksp_set_up(msp_ksp *k) {
 
 static double *VV(const msp_ksp *k, int j) { return k->basis + (int64_t)j * k->stride; }
 
+/* Which Arnoldi step a cycle runs: the operator computed inside MDot and MAXPY (opfuse), the W-free step on a box
+ * stencil (wfree), or W stored between the MatMult and the CGS kernels (neither).  The W-free choice follows the
+ * operator and msk_set_gm_wfree, so it is asked again before every solve. */
+static void step_kind(const msp_ksp *k, int *opfuse, int *wfree) {
+  *opfuse = mspi_op_fusable(k->A) && k->o.restart + 1 <= MSPI_MAX_GROUP;
+  *wfree = !*opfuse && k->o.restart <= MSPI_MAX_GROUP && mspi_gm_wfree(k->A);
+}
+
+/* The stored-W step's n-vector, allocated the first time a cycle takes that step (before any graph capture: no
+ * allocation inside a captured cycle) -- 134-537 MB per block that the default W-free step never touches. */
+static int ensure_w(msp_ksp *k) {
+  int opfuse, wfree;
+  step_kind(k, &opfuse, &wfree);
+  if (opfuse || wfree || k->tmp) return MSP_SUCCESS;
+  return mspi_malloc(k->ctx, (void **)&k->tmp, (size_t)k->stride * sizeof(double) + 4096);
+}
+
 /* One KSPGMRESCycle from its initial residual in VV(0): VecNormalize (deferred),
  * up to K Arnoldi steps, BuildSoln(it-1) into x.  Enqueued, no host synchronisation. */
 static int enqueue_cycle(msp_ksp *k, double *x, int K) {
@@ -247,7 +264,8 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
   double *sumsq = &k->g.h[0];
   int rc = mspi_norm2sq(c, VV(k, 0), k->n, sumsq);
   if (!rc) rc = mspi_gm_cycle_start(c, k->g, sumsq);
-  const int opfuse = mspi_op_fusable(k->A) && k->o.restart + 1 <= MSPI_MAX_GROUP;
+  int opfuse, wfree;
+  step_kind(k, &opfuse, &wfree);
   for (int it = 0; it < K && !rc && opfuse; ++it) {
     /* W = A (sc[it] VV(it)) never reaches HBM: MDot and MAXPY each compute their rows of it from the operator's
      * one-byte codes and VV(it) (which both stream anyway), bitwise the separate MatMult's W */
@@ -257,7 +275,6 @@ static int enqueue_cycle(msp_ksp *k, double *x, int K) {
                                      k->o.restart, stop);
   }
   /* box stencils: W is not stored; the MAXPY recomputes its rows from VV(it) (which it streams anyway) */
-  const int wfree = !opfuse && k->o.restart <= MSPI_MAX_GROUP && mspi_gm_wfree(k->A);
   for (int it = 0; it < K && !rc && wfree; ++it) {
     rc = mspi_spmv_mdot(k->A, VV(k, it), sc + it, NULL, it + 1, k->basis, k->stride, sc, k->g.h, stop);
     if (!rc)
@@ -347,6 +364,7 @@ int msp_ksp_solve(msp_ksp *k, const msp_vec *b, msp_vec *x) {
   }
   int rc = mspi_set_device(k->ctx);
   if (!rc) rc = msp_ksp_set_up(k);
+  if (!rc) rc = ensure_w(k);
   if (rc) return rc;
   msp_ctx *c = k->ctx;
   const int guess_zero = !k->o.guess_nonzero;

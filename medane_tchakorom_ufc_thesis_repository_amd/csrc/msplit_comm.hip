@@ -90,6 +90,12 @@ extern "C" int msp_comm_get_unique_id(uint8_t id[MSP_COMM_ID_BYTES]) {
   return MSP_SUCCESS;
 }
 
+extern "C" int msp_comm_rccl_available(int32_t* ok) {
+  ARGCHK(ok, MSP_ERR_ARG_NULL, "ok is NULL");
+  *ok = rccl().ok ? 1 : 0;
+  return MSP_SUCCESS;
+}
+
 extern "C" int msp_comm_create_rccl(msp_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[MSP_COMM_ID_BYTES],
                                     msp_comm** out) {
   ARGCHK(c && id && out, MSP_ERR_ARG_NULL, "NULL argument");

@@ -135,6 +135,8 @@ int msk_spmv_box_march(int32_t nx, int32_t ny, int32_t nz, int d2, const uint8_t
 // The chunk-tile march (k_box_march_chunk): whether it takes a box of nx x ny planes; MatMult / MatResidual
 // with the plane below (halo & 1) / above (halo & 2) in the column space (x = the column-space vector).
 int msk_march_chunk_fits(int32_t nx, int32_t ny, int d2);
+int msk_box_march_halo_fits(int32_t nx, int32_t ny, int32_t nz, int halo, const double *x, const double *b,
+                            const double *y, int mode);
 int msk_box_march_halo(int32_t nx, int32_t ny, int32_t nz, int halo, const uint8_t* mask, const double* dval,
                        const double* x, const double* b, double* y, int mode, hipStream_t s);
 // GMRES: y = A (sc*x) for a box stencil with march presence bytes (nx <= 2048; P = the plane, or nx in 2D), fused

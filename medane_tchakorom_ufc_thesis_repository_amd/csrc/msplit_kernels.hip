@@ -2873,14 +2873,22 @@ extern "C" int msk_march_chunk_fits(int32_t nx, int32_t ny, int d2) {
 // MatMult / MatResidual of a box stencil whose column space adds the plane below (halo & 1) and / or above
 // (halo & 2) the box -- a block's rows of the block-Jacobi operator with its coupling columns -- over chunk
 // tiles; x is the column-space vector (the lo plane first).  Only boxes k_box_march_chunk takes.
+// Whether msk_box_march_halo takes these operands (the caller's choice of kernel, made before the launch so that a
+// launch error is never mistaken for "does not fit"): chunk tiles that fit the plane, 16-byte aligned x (past the
+// lower coupling plane), y and, for MatResidual, b.
+extern "C" int msk_box_march_halo_fits(int32_t nx, int32_t ny, int32_t nz, int halo, const double* x,
+                                       const double* b, const double* y, int mode) {
+  if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad() || mode == MSK_SPMV_SCALED) return 0;
+  const double* xo = x + ((halo & 1) ? (int64_t)nx * ny : 0);
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return march_chunk_ok(nx, ny, 0) && a16(xo) && a16(y) && (mode != MSK_SPMV_RESID || a16(b));
+}
+
 extern "C" int msk_box_march_halo(int32_t nx, int32_t ny, int32_t nz, int halo, const uint8_t* mask,
                                   const double* dval, const double* x, const double* b, double* y, int mode,
                                   hipStream_t s) {
-  if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad() || mode == MSK_SPMV_SCALED) return (int)hipErrorInvalidValue;
+  if (!msk_box_march_halo_fits(nx, ny, nz, halo, x, b, y, mode)) return (int)hipErrorInvalidValue;
   const double* xo = x + ((halo & 1) ? (int64_t)nx * ny : 0);
-  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (!march_chunk_ok(nx, ny, 0) || !a16(xo) || !a16(y) || (mode == MSK_SPMV_RESID && !a16(b)))
-    return (int)hipErrorInvalidValue;
   return launch_march_chunk(nx, ny, nz, halo, mask, dval, xo, b, y, mode, nullptr, nullptr, nullptr, s);
 }
 

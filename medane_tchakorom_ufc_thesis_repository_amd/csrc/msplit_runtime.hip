@@ -1229,16 +1229,23 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
     return MSP_SUCCESS;
   }
   if (A->dv_on) {
-    const bool bm = box_march(A), bh = !bm && box_march_halo(A);
+    const int mode = resid ? MSK_SPMV_RESID : MSK_SPMV_MULT;
+    const bool bm = box_march(A);
+    // a block's A_ext with coupling planes: the chunk march when its operands fit (a vector not 16-byte aligned
+    // takes the row-parallel kernel below), decided before the launch so a launch error is reported, not hidden
+    const bool bh = !bm && box_march_halo(A) &&
+                    msk_box_march_halo_fits(A->march_nx, A->march_ny, A->march_nz, A->march_halo, x, b, y, mode);
     KTimer kt(c, MSP_KERNEL_SPMV, bm || bh ? march_bytes(A, resid, false) : dv_bytes(A, resid, false));
     if (bm) {
       KCHK(msk_spmv_box_march(A->march_nx, A->march_ny, A->march_nz, A->march_d2, A->march_mask, A->dv_val, x, b, y,
-                              resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
+                              mode, nullptr, nullptr, nullptr, c->stream));
       return MSP_SUCCESS;
     }
-    if (bh && msk_box_march_halo(A->march_nx, A->march_ny, A->march_nz, A->march_halo, A->march_mask, A->dv_val, x, b,
-                                 y, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, c->stream) == 0)
-      return MSP_SUCCESS;  // (a vector not 16-byte aligned: the row-parallel kernel below)
+    if (bh) {
+      KCHK(msk_box_march_halo(A->march_nx, A->march_ny, A->march_nz, A->march_halo, A->march_mask, A->dv_val, x, b, y,
+                              mode, c->stream));
+      return MSP_SUCCESS;
+    }
     KCHK(msk_spmv_dv(A->nrows, A->rowptr, A->dv_len, A->dv_code, A->dv_delta, A->dv_val, A->ndict, A->dv_mb, A->dv_w, x, b,
                      y, resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, A->plane, c->stream));
     return MSP_SUCCESS;

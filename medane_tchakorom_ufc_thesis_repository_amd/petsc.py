@@ -494,6 +494,13 @@ class Comm:
         call("msp_comm_get_unique_id", buf)
         return bytes(buf)
 
+    @staticmethod
+    def rccl_available() -> bool:
+        """librccl loads (no bootstrap thread started: the readiness test of the ranks other than 0)."""
+        ok = C.c_int32(0)
+        call("msp_comm_rccl_available", C.byref(ok))
+        return bool(ok.value)
+
     @classmethod
     def rccl(cls, ctx: Context, nranks: int, rank: int, uid: bytes) -> "Comm":
         buf = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)

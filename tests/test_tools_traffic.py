@@ -11,6 +11,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -24,14 +26,17 @@ def _write(d, counter, names):
                         "Counter_Value": 1.0})
 
 
-def test_wfree_accounting(tmp_path):
+@pytest.mark.parametrize("maxpy", ["k_box_maxpy_march", "k_box_maxpy"])
+def test_wfree_accounting(tmp_path, maxpy):
+    """Both W-free MAXPY kernels (marched tiles, and one chunk per workgroup where the fused kernel does not march)
+    land in the maxpy class with the same algorithmic bytes."""
     n = 16
     N = float(n) ** 3
     names = []
     for _cycle in range(2):
         for it in range(30):
             names.append("void msk::k_box_spmv_mdot_march<1, true>(...)")
-            names.append("void msk::k_box_maxpy_march<1, true>(...)")
+            names.append(f"void msk::{maxpy}<1, true>(...)")
         names.append("void msk::k_maxpy_chunk<true, false, 37>(...)")
     _write(str(tmp_path / "f"), "FETCH_SIZE", names)
     _write(str(tmp_path / "w"), "WRITE_SIZE", names)

@@ -20,10 +20,16 @@ import re
 from collections import defaultdict
 
 
+def wfree_maxpy(name: str) -> bool:
+    """The W-free CGS MAXPY: k_box_maxpy_march (marched tiles) and k_box_maxpy (one chunk per workgroup: 2D boxes,
+    planes without whole chunks, a ragged last chunk) -- the same bytes per launch."""
+    return "k_box_maxpy" in name
+
+
 def classify(name: str):
     if "spmv_mdot" in name:     # the GMRES MatMult fused with VecMDot (k_box_spmv_mdot[_march], k_spmv_mdot)
         return "spmvdot"
-    if "k_maxpy" in name or "maxpy_march" in name:  # k_maxpy_chunk, k_box_maxpy_march (the W-free CGS MAXPY)
+    if "k_maxpy" in name or wfree_maxpy(name):  # k_maxpy_chunk; the W-free CGS MAXPY k_box_maxpy[_march]
         return "maxpy"
     if "k_dot_stage1" in name:
         return "norm" if "true>" in name.replace(" ", "") or ", true" in name else "mdot"
@@ -103,12 +109,12 @@ def main():
         rd = sum(2.0 * v for _, v in F[:m]) / m
         wr = sum(v for _, v in W[:m]) / m
         alg = None
-        wfree = any("maxpy_march" in nm for nm, _ in F[:m]) or any("maxpy_march" in nm for nm, _ in
-                                                                    per_class_f.get("maxpy", []))
+        wfree = any(wfree_maxpy(nm) for nm, _ in F[:m]) or any(wfree_maxpy(nm) for nm, _ in
+                                                                per_class_f.get("maxpy", []))
         if cls == "maxpy" and wfree and m % 31 == 0:
             # GMRES(30) solves in dispatch order: 30 W-free MAXPYs (presence byte, x once, nv - 1 basis vectors,
             # wout: N + 8 N (nv + 1), nv = it + 1), then BuildSoln's accumulate over 30 vectors (8 N (30 + 2))
-            alg = sum(8.0 * N * 32 if "maxpy_march" not in nm else N + 8.0 * N * ((i % 31) + 2)
+            alg = sum(8.0 * N * 32 if not wfree_maxpy(nm) else N + 8.0 * N * ((i % 31) + 2)
                       for i, (nm, _) in enumerate(F[:m])) / m
         elif cls in ("maxpy", "mdot"):
             nvs = [nv_of(nm) for nm, _ in F[:m]]
