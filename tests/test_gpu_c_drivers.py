@@ -226,3 +226,40 @@ def test_c_host_configs0_reduction_option_matches_oracle(ctx, oracle, built, red
         assert c["outer_its"] == cap        # the PETSc-order run stagnates just above 1e-3
     py = drivers.run(args + ["-json"])    # the Python host takes the same option
     assert py["outer_its"] == c["outer_its"] and py["hist"] == list(ro["hist"])
+
+
+ISOLVE_CONFIGS0 = ["--np", "2", "--npb", "1", "--m", "256", "--n", "256", "--s", "4", "--rtol", "1e-3",
+                   "--alg", "SMSM_GLOBAL", "--inner-ksp", "gmres", "--inner-rtol", "1e-3", "--inner-max-iters", "20",
+                   "--inner-pc-type", "none", "--outer-ksp", "lsqr", "--outer-rtol", "1e-15",
+                   "--outer-max-iters", "70", "--outer-pc-type", "none", "--other-petsc-options",
+                   "-inner_ksp_gmres_restart 30 -outer_ksp_convergence_test default -outer_ksp_lsqr_exact_mat_norm "
+                   "-outer_ksp_atol 1e-100 -json"]
+
+
+def _isolve(args, launch):
+    env = dict(os.environ, ISOLVE_LAUNCH=launch)
+    p = subprocess.run([os.path.join(HOST, "isolve")] + args, capture_output=True, text=True, env=env, timeout=300,
+                       start_new_session=True)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("launch", ["single", "mpi"])
+def test_isolve_configs0_command_line_equals_explicit_prefixes_and_oracle(ctx, oracle, built, launch):
+    """BASELINE configs[0] as an iSolve command line (iSolve:118-194; --np 2 --alg SMSM_GLOBAL, the campaign's
+    inner/outer options, running_bulk_test_g5k:247-248) through host/isolve: the run is the explicit-prefix C-host
+    run (-inner1_/-inner2_/-outer1_/-outer2_) and the DBR oracle, bit for bit -- outer count, every outer LSQR
+    residual and LSQR count, the final residual -- in one process (-nb 2) and over 2 MPI ranks."""
+    got = _isolve(ISOLVE_CONFIGS0, launch)
+    inner = [a for b in (1, 2) for a in (f"-inner{b}_ksp_type", "gmres", f"-inner{b}_ksp_max_it", "20",
+                                         f"-inner{b}_ksp_rtol", "1e-3", f"-inner{b}_ksp_gmres_restart", "30",
+                                         f"-inner{b}_pc_type", "none")]
+    explicit = _run([SMSM, "-m", "256", "-n", "256", "-s", "4", "-rtol", "1e-3", "-nb", "2"] + inner + OUTER2)
+    assert got["transport"] == ("host" if launch == "mpi" else "none") and got["ranks"] == (2 if launch == "mpi" else 1)
+    assert got["hist_hex"] == explicit["hist_hex"] and got["lsqr_its"] == explicit["lsqr_its"]
+    assert got["outer_its"] == explicit["outer_its"] and got["final_norm"] == explicit["final_norm"]
+    ro = oracle.smsm_solve(2, 256, 256, 1, 2, 4, 1e-3,
+                           dict(restart=30, max_it=20, rtol=1e-3, abstol=1e-50, reduce_mode=oracle.REDUCE_DBR),
+                           dict(OUTER_ORC, reduce_mode=oracle.REDUCE_DBR), max_outer=200)
+    _assert_same_run(got, ro, f"isolve configs[0] ({launch})")
+    assert got["final_norm"] == ro["final_norm"]

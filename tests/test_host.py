@@ -161,3 +161,51 @@ def test_bench_reads_the_measured_streaming_ceiling():
     assert c is not None and c["source"].startswith("profiles/r03/stream_ceiling/")
     assert 5.0 < c["maxpy_mix_TBps"] <= c["read_TBps"] < bench.HBM_PEAK_GBS / 1e3
     assert 5.0 < c["copy_TBps"] < bench.HBM_PEAK_GBS / 1e3
+
+
+def _isolve(args, **env):
+    e = dict(os.environ, ISOLVE_DRYRUN="1", **env)
+    p = subprocess.run([os.path.join(ROOT, "host", "isolve")] + args, capture_output=True, text=True, env=e,
+                       timeout=60)
+    assert p.returncode == 0, p.stderr
+    return p.stdout.splitlines()
+
+
+def test_isolve_maps_every_flag_onto_every_block_prefix():
+    """host/isolve takes iSolve's command line (iSolve:118-194) and, unlike the reference -- whose drivers read
+    inner1_/inner2_ while iSolve writes inner_ (iSolve:349-371, default_run_variables:54,68) -- sets every
+    --inner-* / --outer-* flag and every -inner_* / -outer_* option on each block's prefix."""
+    cmd = _isolve(["--np", "3", "--m", "24", "--n", "32", "--s", "5", "--rtol", "1e-4", "--alg", "SMSM_GLOBAL",
+                   "--inner-ksp", "gmres", "--inner-rtol", "1e-20", "--inner-max-iters", "20", "--inner-pc-type",
+                   "none", "--outer-ksp", "lsqr", "--outer-rtol", "1e-15", "--outer-max-iters", "70",
+                   "--outer-pc-type", "none", "--other-petsc-options",
+                   "-inner_ksp_gmres_restart 30 -outer_ksp_lsqr_exact_mat_norm -outer_ksp_convergence_test default "
+                   "-json"])
+    assert cmd[cmd.index("-n") + 1] == "3" and cmd[cmd.index("-n") + 2].endswith("host/msplit_driver_mpi")
+    assert "synchronous-multisplitting-synchronous-minimization-global" in cmd
+
+    def opt(k):
+        i = cmd.index(k)
+        return cmd[i + 1] if i + 1 < len(cmd) and not cmd[i + 1].startswith("-") else True
+    for b in (1, 2, 3):
+        assert opt(f"-inner{b}_ksp_type") == "gmres" and opt(f"-inner{b}_ksp_rtol") == "1e-20"
+        assert opt(f"-inner{b}_ksp_max_it") == "20" and opt(f"-inner{b}_pc_type") == "none"
+        assert opt(f"-inner{b}_ksp_gmres_restart") == "30"
+        assert opt(f"-outer{b}_ksp_type") == "lsqr" and opt(f"-outer{b}_ksp_max_it") == "70"
+        assert opt(f"-outer{b}_ksp_lsqr_exact_mat_norm") is True
+        assert opt(f"-outer{b}_ksp_convergence_test") == "default"
+    assert opt("-s") == "5" and opt("-rtol") == "1e-4" and opt("-m") == "24" and "-json" in cmd
+    assert not any(c.startswith("-inner_") or c.startswith("-outer_") for c in cmd)
+
+
+def test_isolve_single_process_and_python_variants():
+    cmd = _isolve(["--np", "2", "--alg", "SM"], ISOLVE_LAUNCH="single")
+    assert cmd[0].endswith("host/msplit_driver") and cmd[cmd.index("-nb") + 1] == "2"
+    assert not any(c.startswith("-outer") for c in cmd) and "-s" not in cmd
+    cmd = _isolve(["--np", "4", "--alg", "AMAM_SEMI_LOCAL", "--outer-ksp", "lsqr"])
+    assert cmd[:3] == ["python3", "-m", "medane_tchakorom_ufc_thesis_repository_amd.drivers"]
+    assert cmd[3] == "asynchronous-multisplitting-asynchronous-minimization-semi-local"   # iSolve:56 runs the -local binary
+    assert cmd[cmd.index("-nb") + 1] == "4" and cmd[cmd.index("-outer4_ksp_type") + 1] == "lsqr"
+    p = subprocess.run([os.path.join(ROOT, "host", "isolve"), "--np", "2", "--npb", "2"], capture_output=True,
+                       text=True, env=dict(os.environ, ISOLVE_DRYRUN="1"), timeout=60)
+    assert p.returncode != 0 and "npb" in p.stderr
