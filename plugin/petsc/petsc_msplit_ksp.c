@@ -19,6 +19,31 @@ static const char *const MSplitReductions[] = {"dbr", "seq", "MSplitReduction", 
 
 #define MSPCall(e) do { int _rc = (e); PetscCheck(!_rc, PETSC_COMM_SELF, _rc, "%s", msp_get_last_error()); } while (0)
 
+/* The block's GPU: -msplit_device when given, else the rank's index on its node modulo the devices it sees (one
+ * block per rank, one rank per GPU, as petscmpiexec -n 8 places them on an 8-GPU node).  Shared with
+ * petsc_msplit_vecmat.c. */
+PetscErrorCode MSplitDefaultDevice(int *dev)
+{
+  PetscInt    d   = -1;
+  PetscBool   set = PETSC_FALSE;
+  PetscMPIInt local = 0;
+  MPI_Comm    node;
+  int         ndev = 0;
+
+  PetscFunctionBegin;
+  PetscCall(PetscOptionsGetInt(NULL, NULL, "-msplit_device", &d, &set));
+  if (set) {
+    *dev = (int)d;
+    PetscFunctionReturn(PETSC_SUCCESS);
+  }
+  PetscCallMPI(MPI_Comm_split_type(PETSC_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node));
+  PetscCallMPI(MPI_Comm_rank(node, &local));
+  PetscCallMPI(MPI_Comm_free(&node));
+  MSPCall(msp_get_device_count(&ndev));
+  *dev = ndev > 0 ? (int)(local % ndev) : 0;
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
 static PetscErrorCode KSPSetUp_MSplitGMRES(KSP ksp)
 {
   KSP_MSplit        *ms = (KSP_MSplit *)ksp->data;
@@ -34,7 +59,11 @@ static PetscErrorCode KSPSetUp_MSplitGMRES(KSP ksp)
   PetscCall(MatMPIAIJGetSeqAIJ(A, &Ad, NULL, NULL));          /* or A itself when it is MATSEQAIJ */
   PetscCall(MatGetRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &nr, &ia, &ja, &done));
   PetscCall(MatSeqAIJGetArrayRead(Ad, &aa));
-  if (!ms->ctx) MSPCall(msp_ctx_create(0, NULL, &ms->ctx));   /* device = local rank % ndev in practice */
+  if (!ms->ctx) {
+    int dev;
+    PetscCall(MSplitDefaultDevice(&dev));
+    MSPCall(msp_ctx_create(dev, NULL, &ms->ctx));
+  }
   MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
   MSPCall(msp_mat_destroy(&ms->A));
   MSPCall(msp_mat_create_csr(ms->ctx, (int32_t)nr, (int32_t)nr, ia, ja, aa, &ms->A));
@@ -164,7 +193,11 @@ static PetscErrorCode KSPSetUp_MSplitLSQR(KSP ksp)
   else Al = A;
   PetscCall(MatGetSize(Al, &m, &n));
   PetscCall(MatDenseGetLDA(Al, &lda));
-  if (!ms->ctx) MSPCall(msp_ctx_create(0, NULL, &ms->ctx));
+  if (!ms->ctx) {
+    int dev;
+    PetscCall(MSplitDefaultDevice(&dev));
+    MSPCall(msp_ctx_create(dev, NULL, &ms->ctx));
+  }
   MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
   MSPCall(msp_dense_destroy(&ms->R));
   MSPCall(msp_dense_create(ms->ctx, m, (int32_t)n, &ms->R));
@@ -268,5 +301,22 @@ PetscErrorCode MSplitRegisterAll(void)
   PetscFunctionBegin;
   PetscCall(KSPRegister("msplitgmres", KSPCreate_MSplitGMRES));
   PetscCall(KSPRegister("msplitlsqr", KSPCreate_MSplitLSQR));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+PetscErrorCode MSplitRegisterVecMat(void); /* petsc_msplit_vecmat.c */
+
+/* The entry point PETSc's dynamic-library loader calls: `-dll_append /path/libpetsc_msplit.so` (or
+ * -dll_prepend) makes PetscInitialize open the library and call PetscDLLibraryRegister_<name>, the name being
+ * the file's basename without "lib" and the suffix.  It registers the two KSP types, the VecType and the MatType,
+ * so the reference's executables pick them up through their existing KSPSetFromOptions / MatSetFromOptions /
+ * VecSetFromOptions calls (utils.c:130, :146, :164, :530) with no source change and no relink:
+ *   petscmpiexec -n 2 ./bin/synchronous-multisplitting ... -dll_append libpetsc_msplit.so \
+ *       -inner1_ksp_type msplitgmres -inner2_ksp_type msplitgmres */
+PETSC_EXTERN PetscErrorCode PetscDLLibraryRegister_petsc_msplit(void)
+{
+  PetscFunctionBegin;
+  PetscCall(MSplitRegisterAll());
+  PetscCall(MSplitRegisterVecMat());
   PetscFunctionReturn(PETSC_SUCCESS);
 }

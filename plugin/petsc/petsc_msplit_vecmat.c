@@ -33,13 +33,15 @@
 
 static msp_ctx *g_ctx; /* one context (GPU) per process: the block's GPU */
 
+PetscErrorCode MSplitDefaultDevice(int *dev); /* petsc_msplit_ksp.c: -msplit_device, else node-local rank % ndev */
+
 static PetscErrorCode MSplitContext(msp_ctx **ctx)
 {
   PetscFunctionBegin;
   if (!g_ctx) {
-    PetscInt dev = 0;
-    PetscCall(PetscOptionsGetInt(NULL, NULL, "-msplit_device", &dev, NULL));
-    MSPCall(msp_ctx_create((int)dev, NULL, &g_ctx));
+    int dev = 0;
+    PetscCall(MSplitDefaultDevice(&dev));
+    MSPCall(msp_ctx_create(dev, NULL, &g_ctx));
     /* -msplit_reduction seq: VecDot/VecNorm/VecMDot of the drivers' outer tests in PETSc's order too */
     const char *const red[] = {"dbr", "seq"};
     PetscInt  r   = 0;
@@ -384,7 +386,8 @@ static PetscErrorCode MatCreate_AIJMSplit(Mat A)
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
-/* Call once after PetscInitialize, with MSplitRegisterAll (petsc_msplit_ksp.c). */
+/* Call once after PetscInitialize, with MSplitRegisterAll (petsc_msplit_ksp.c) -- or let -dll_append load the
+ * library, whose PetscDLLibraryRegister_petsc_msplit calls both. */
 PetscErrorCode MSplitRegisterVecMat(void)
 {
   PetscFunctionBegin;
