@@ -6,7 +6,10 @@ Layers:
   csrc/                       HIP kernels for gfx950 + the KSPGMRES host logic in C
   _lib.py / petsc.py          ctypes binding and PETSc-style host objects
   utils.py                    the reference's glue (assembly, split, inner_solver, ...)
-  comm.py / multisplitting.py block exchange (RCCL via torch.distributed) and the SM driver
+  comm.py                     one library communicator per rank (LibComm: RCCL send/recv and all-gathers
+                              on the context's stream; torch.distributed only broadcasts the id)
+  multisplitting.py           the synchronous drivers (SM, SMSM-global/-local/-semi-local)
+  asynchronous.py             the asynchronous drivers (AM, AMAM-*) over HBM mailboxes
 """
 from ._lib import LIB_PATH, MsplitError, load  # noqa: F401
 
