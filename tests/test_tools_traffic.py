@@ -48,3 +48,37 @@ def test_wfree_accounting(tmp_path, maxpy):
     spmvdot = sum(9.0 * N + 8.0 * N * (nv - 1) for nv in range(1, 31)) / 30
     assert t["maxpy"]["launches"] == 62 and abs(t["maxpy"]["alg_bytes_per_launch"] / maxpy - 1) < 1e-12
     assert t["spmvdot"]["launches"] == 60 and abs(t["spmvdot"]["alg_bytes_per_launch"] / spmvdot - 1) < 1e-12
+
+
+def test_smsm_per_kernel_accounting(tmp_path):
+    """--smsm: the SMSM-global outer iteration's kernels on synthetic counters -- the W-free MAXPY and fused
+    MatMult+MDot at Arnoldi steps 1..k of each of the s inner solves, BuildSoln, the LSQR GEMV (8n(s+2)) and
+    x = S alpha (8n(s+1)) told apart by the template's AXPY argument, and the scaled dots (8n(s+1); the solve's
+    first writes U = b / beta, 8n(s+2))."""
+    nx, ny, nz, s, k = 8, 8, 4, 3, 5
+    N = float(nx * ny * nz)
+    names = []
+    for _solve in range(s):
+        for it in range(k):
+            names.append("void msk::k_box_spmv_mdot_march<1, true>(...)")
+            names.append("void msk::k_box_maxpy_march<1, true>(...)")
+        names.append("void msk::k_maxpy_chunk<true, false, 37>(...)")
+    names.append("void k_scaled_dot<true, 2, 4, true>(...)")       # the LSQR start: U = b / beta written
+    for _step in range(4):
+        names.append("void k_dense_gemv<true, true, 2, 4, true>(...)")
+        names.append("void k_scaled_dot<true, 2, 4, true>(...)")
+    names.append("void k_dense_gemv<false, false, 2, 4, true>(...)")
+    _write(str(tmp_path / "f"), "FETCH_SIZE", names)
+    _write(str(tmp_path / "w"), "WRITE_SIZE", names)
+    out = str(tmp_path / "smsm.json")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), str(tmp_path / "f"),
+                    str(tmp_path / "w"), "--smsm", f"{nx},{ny},{nz},{s},{k},4", "--out", out], check=True,
+                   stdout=subprocess.DEVNULL)
+    t = json.load(open(out))["kernels"]
+    close = lambda a, b: abs(a / b - 1) < 1e-12  # noqa: E731
+    assert t["k_box_maxpy_march"]["launches"] == s * k
+    assert close(t["k_box_maxpy_march"]["alg_bytes_per_launch"], sum(N + 8 * N * (nv + 1) for nv in range(1, k + 1)) / k)
+    assert close(t["k_box_spmv_mdot_march"]["alg_bytes_per_launch"], sum(9 * N + 8 * N * (nv - 1) for nv in range(1, k + 1)) / k)
+    assert close(t["k_maxpy_chunk"]["alg_bytes_per_launch"], 8 * N * (k + 2))
+    assert close(t["k_dense_gemv"]["alg_bytes_per_launch"], (4 * 8 * N * (s + 2) + 8 * N * (s + 1)) / 5)
+    assert close(t["k_scaled_dot"]["alg_bytes_per_launch"], (8 * N * (s + 2) + 4 * 8 * N * (s + 1)) / 5)

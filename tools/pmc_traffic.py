@@ -68,6 +68,61 @@ def spmv_alg(name: str, n: int):
     return None
 
 
+def base_name(name: str) -> str:
+    """The kernel's function name: 'void msk::k_dense_gemv<true, ...>(...)' -> 'k_dense_gemv'."""
+    nm = name.split("(")[0].split("<")[0]
+    return nm.split("::")[-1].split()[-1]
+
+
+def tmpl_args(name: str):
+    m = re.search(r"<([^<>]*)>", name)
+    return [a.strip() for a in m.group(1).split(",")] if m else []
+
+
+def smsm_alg(name: str, i: int, rows: float, s: int, k: int, lsqr: int = 70):
+    """Algorithmic bytes of the i-th launch (dispatch order) of this kernel in the SMSM-global per-GPU outer
+    iteration (bench.py --variant smsm, SMSM-global.c:288-363): s inner GMRES solves of exactly k Arnoldi steps
+    (rtol 1e-20) in the W-free step, then R = A S, the LSQR over R (n x s) of `lsqr` steps and x = S alpha, on
+    `rows` rows."""
+    N = rows
+    b = base_name(name)
+    if b == "k_box_maxpy_march" or b == "k_box_maxpy":
+        return N + 8.0 * N * ((i % k) + 2)              # presence byte, x once, nv - 1 basis vectors, wout
+    if b == "k_box_spmv_mdot_march" or b == "k_box_spmv_mdot":
+        return 9.0 * N + 8.0 * N * (i % k)               # presence byte, x, nv - 1 basis vectors (W not stored)
+    if b == "k_maxpy_chunk":
+        return 8.0 * N * (k + 2)                         # BuildSoln: x += sum of k basis vectors
+    if b == "k_dense_gemv":
+        ax = tmpl_args(name)[:1] == ["true"]
+        return 8.0 * N * (s + 2) if ax else 8.0 * N * (s + 1)   # U1 = R V - a U, ||U1||^2 / x = S alpha
+    if b == "k_scaled_dot":   # R^T (U1 / beta), U1 not written back; the solve's first: U = b / beta written
+        return 8.0 * N * (s + 2) if i % (lsqr + 1) == 0 else 8.0 * N * (s + 1)
+    return None
+
+
+def smsm_table(fetch, write, rows, s, k, lsqr=70):
+    """Per kernel: launches, HBM read/write bytes per launch (PMC) and the algorithmic bytes per launch."""
+    per_f, per_w = defaultdict(list), defaultdict(list)
+    for _, (name, v) in sorted(fetch.items()):
+        per_f[base_name(name)].append((name, v))
+    for _, (name, v) in sorted(write.items()):
+        per_w[base_name(name)].append((name, v))
+    out = {}
+    for b in sorted(set(per_f) | set(per_w)):
+        F, W = per_f.get(b, []), per_w.get(b, [])
+        m = min(len(F), len(W))
+        if m == 0:
+            continue
+        rd = sum(2.0 * v for _, v in F[:m]) / m
+        wr = sum(v for _, v in W[:m]) / m
+        als = [smsm_alg(nm, i, rows, s, k, lsqr) for i, (nm, _) in enumerate(F[:m])]
+        alg = sum(als) / m if all(a is not None for a in als) else None
+        out[b] = {"launches": m, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                  "hbm_bytes_per_launch": rd + wr, "alg_bytes_per_launch": alg,
+                  "hbm_over_alg": (rd + wr) / alg if alg else None}
+    return out
+
+
 def load(d, counter):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
@@ -89,10 +144,24 @@ def main():
     ap.add_argument("--bench", default=None, help="bench JSON of the same build: algorithmic bytes per launch")
     ap.add_argument("--x-reread", action="store_true",
                     help="builds before round 3's register dot: the fused kernel streamed x again for its dot")
+    ap.add_argument("--smsm", default=None, metavar="NX,NY,NZ,S,K[,L]",
+                    help="per-kernel table for the SMSM-global per-GPU outer iteration (bench.py --variant smsm): "
+                         "an NX x NY x NZ block, S inner solves of K Arnoldi steps, L LSQR steps (70) over S columns")
     a = ap.parse_args()
     N = a.n ** 3
     fetch = load(a.fetch_dir, "FETCH_SIZE")
     write = load(a.write_dir, "WRITE_SIZE")
+    if a.smsm:
+        f = [int(v) for v in a.smsm.split(",")]
+        nx, ny, nz, s_, k_ = f[:5]
+        l_ = f[5] if len(f) > 5 else 70
+        out = {"workload": f"SMSM-global block {nx}x{ny}x{nz}, s {s_}, inner max_it {k_}, LSQR {l_} steps",
+               "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950), write = WRITE_SIZE x 1024",
+               "kernels": smsm_table(fetch, write, float(nx) * ny * nz, s_, k_, l_)}
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        json.dump(out, open(a.out, "w"), indent=1)
+        print(json.dumps(out, indent=1))
+        return
     # dispatch ids of two runs of the same deterministic command line up per class and order
     per_class_f, per_class_w = defaultdict(list), defaultdict(list)
     for _, (name, v) in sorted(fetch.items()):
