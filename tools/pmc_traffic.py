@@ -70,8 +70,8 @@ def spmv_alg(name: str, n: int):
 
 def base_name(name: str) -> str:
     """The kernel's function name: 'void msk::k_dense_gemv<true, ...>(...)' -> 'k_dense_gemv'."""
-    nm = name.split("(")[0].split("<")[0]
-    return nm.split("::")[-1].split()[-1]
+    nm = name.replace("(anonymous namespace)", "").split("(")[0].split("<")[0].split("::")[-1].split()
+    return nm[-1] if nm else name
 
 
 def tmpl_args(name: str):
