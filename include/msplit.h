@@ -435,12 +435,19 @@ int msp_amsg_send_vec(msp_amsg *am, int32_t dst, const int32_t *ints, int32_t ni
 int msp_amsg_recv_vec(msp_amsg *am, int32_t src, int32_t *ints, int32_t nints, msp_vec *v, int64_t off, int64_t cap,
                       int64_t *n, int32_t *got);
 /* Device slots (the xGMI mailboxes of SURVEY.md section 8e): this rank's
- * outgoing planes live in its own HBM, exported by HIP IPC; *_vec then move a
- * plane HBM -> sender's slot and sender's slot -> receiver's HBM (peer copy over
- * xGMI), with the same sequence words.  Every rank enables before the first
- * send; close_peers (every rank) must precede destroy (which frees the slots). */
+ * outgoing planes live in its own HBM (two buffers per neighbour), exported by
+ * HIP IPC; *_vec then move a plane HBM -> sender's slot and sender's slot ->
+ * receiver's HBM (peer copy over xGMI), both enqueued on the context's stream
+ * with no host wait: the stream itself publishes the plane (and releases the
+ * buffer a receiver copied) once its copy is done.  A send whose previous copy
+ * is not yet published, or whose free buffer the receiver still reads, is
+ * skipped, as comm_async_test_and_send_prime posts a new MPI_Isend only when
+ * MPI_Test reports the previous one done (comm.c:528-535).  Every rank enables
+ * before the first send; close_peers (every rank; it drains the stream) must
+ * precede destroy (which frees the slots).  get_stats: sends posted / skipped. */
 int msp_amsg_enable_device(msp_amsg *am, msp_ctx *ctx);
 int msp_amsg_close_peers(msp_amsg *am);
+int msp_amsg_get_stats(const msp_amsg *am, int64_t *sent, int64_t *skipped);
 
 /* ------------------------------------------- async minimization broadcast */
 /* Newest-value broadcast of each block's rows of R (AMAM-global), in POSIX
@@ -468,8 +475,11 @@ int msp_abcast_fetch_dense(msp_abcast *bc, int32_t src, msp_dense *D, int32_t *g
  * is a peer copy over xGMI; enable on every rank before the first publish,
  * close_peers on every rank before destroy.  nbuf = 2 (a publish fills the
  * buffer readers are not using) or 1 (half the HBM: a publish waits until no
- * reader holds the newest block, and readers skip a block being rewritten). */
+ * reader holds the newest block, and readers skip a block being rewritten);
+ * 0 chooses: 2 while an eighth of the GPU's HBM stays free after them, else 1.
+ * msp_abcast_get_nbuf reports the count in use (0 before enable_device). */
 int msp_abcast_enable_device(msp_abcast *bc, msp_ctx *ctx, int32_t nbuf);
+int msp_abcast_get_nbuf(const msp_abcast *bc, int32_t *nbuf);
 int msp_abcast_close_peers(msp_abcast *bc);
 
 /* ------------------------------------------------- convergence detection */

@@ -161,7 +161,9 @@ _SIGS = {
     "msp_comm_sum_ordered": [_vp, _dp, _dp, C.c_int32],
     "msp_amsg_enable_device": [_vp, _vp],
     "msp_amsg_close_peers": [_vp],
+    "msp_amsg_get_stats": [_vp, _P(C.c_int64), _P(C.c_int64)],
     "msp_abcast_enable_device": [_vp, _vp, C.c_int32],
+    "msp_abcast_get_nbuf": [_vp, _i32p],
     "msp_abcast_close_peers": [_vp],
     "msp_abcast_create": [C.c_char_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32, _P(_vp)],
     "msp_abcast_destroy": [_P(_vp)],

@@ -143,17 +143,13 @@ class AsyncBlock:
 
     def enable_device(self):
         """Device slots / buffers in this block's HBM (xGMI peer copies between GPUs).  The R
-        broadcast takes two buffers, or one when two would not leave a quarter of the free HBM
-        (configs[3] scale: DESIGN.md section 6.5); MSPLIT_ABCAST_NBUF forces 1 or 2."""
+        broadcast takes two buffers, or one when two would not leave an eighth of the GPU's HBM free
+        (the library's rule, msp_abcast_enable_device with nbuf 0; configs[3] scale: DESIGN.md section
+        6.5); MSPLIT_ABCAST_NBUF forces 1 or 2."""
         self.am.enable_device(self.blk.ctx)
         if self.bcast is not None:
             nbuf = int(os.environ.get("MSPLIT_ABCAST_NBUF", "0"))
-            if nbuf not in (1, 2):
-                import torch
-                free, _ = torch.cuda.mem_get_info(self.blk.ctx.device)
-                nbuf = 2 if 2 * 8 * self.bcast_cap <= 0.75 * free else 1
-            self.bcast.enable_device(self.blk.ctx, nbuf)
-            self.bcast_nbuf = nbuf
+            self.bcast_nbuf = self.bcast.enable_device(self.blk.ctx, nbuf if nbuf in (1, 2) else 0)
 
     def close_peers(self):
         self.am.close_peers()

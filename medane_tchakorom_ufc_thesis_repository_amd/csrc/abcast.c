@@ -163,13 +163,22 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
 
 int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   if (!b || !ctx) return berr(MSP_ERR_ARG_NULL, "NULL argument");
-  if (nbuf != 1 && nbuf != 2) return berr(MSP_ERR_ARG_OUTOFRANGE, "nbuf must be 1 or 2");
+  if (nbuf < 0 || nbuf > 2) return berr(MSP_ERR_ARG_OUTOFRANGE, "nbuf must be 0 (auto), 1 or 2");
   if (b->dctx) return MSP_SUCCESS;
+  const size_t buf_bytes = (size_t)(b->cap > 0 ? b->cap : 1) * sizeof(double);
+  if (nbuf == 0) {
+    /* auto: two buffers only while an eighth of the GPU's HBM stays free after them (configs[3]'s replicated-R
+     * rank: one 21.5 GB buffer instead of two, 250 instead of 272 GiB of 288 -- DESIGN.md section 6.5) */
+    size_t fr = 0, tot = 0;
+    int rc = mspi_mem_info(ctx, &fr, &tot);
+    if (rc) return rc;
+    nbuf = fr >= 2 * buf_bytes && fr - 2 * buf_bytes >= tot / 8 ? 2 : 1;
+  }
   b->peer = (double **)calloc((size_t)b->nranks, sizeof(double *));
   b->opened = (uint8_t *)calloc((size_t)b->nranks, 1);
   if (!b->peer || !b->opened) return berr(MSP_ERR_MEM, "allocation failed");
   void *p = NULL;
-  int rc = mspi_dev_alloc(ctx, (size_t)nbuf * (size_t)(b->cap > 0 ? b->cap : 1) * sizeof(double), &p);
+  int rc = mspi_dev_alloc(ctx, (size_t)nbuf * buf_bytes, &p);
   if (rc) return rc;
   b->nbuf_dev = nbuf;
   abc_ipc *e = &b->ipc[b->rank];
@@ -183,6 +192,12 @@ int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   e->pid = (int32_t)getpid();
   e->rawptr = (uint64_t)(uintptr_t)p;
   atomic_store_explicit(&e->ready, 1, memory_order_release);
+  return MSP_SUCCESS;
+}
+
+int msp_abcast_get_nbuf(const msp_abcast *b, int32_t *nbuf) {
+  if (!b || !nbuf) return berr(MSP_ERR_ARG_NULL, "NULL argument");
+  *nbuf = b->dctx ? b->nbuf_dev : 0;
   return MSP_SUCCESS;
 }
 

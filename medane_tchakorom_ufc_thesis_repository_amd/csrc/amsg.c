@@ -20,10 +20,25 @@
  * Iterate payloads are boundary planes: only chain neighbours (|src - dst| = 1,
  * the z-slab blocks) get a data slot of data_cap doubles.  *_vec variants move
  * the plane between HBM and the slot (the region is registered with the HIP
- * runtime, so the copies are DMA transfers).  With device slots enabled
- * (msp_amsg_enable_device) the sequence word stays here but the payload lives
- * in the sender's HBM, exported by HIP IPC: a send is one HBM -> HBM copy into
- * the sender's slot, a receive one copy out of it over xGMI (msplit_ipc.hip).
+ * runtime, so the copies are DMA transfers).
+ *
+ * Device slots (msp_amsg_enable_device): the payload lives in the sender's HBM,
+ * two buffers per neighbour, exported by HIP IPC, and neither end waits for a
+ * copy on the host.  A send claims the buffer that is not the newest, enqueues
+ * the plane's copy into it and, behind the copy on the sender's stream, a
+ * one-lane kernel that publishes (count, buffer) into the shared word `pub`
+ * (a system-scope store into this registered region).  A receive that sees a
+ * newer `pub` marks that buffer as being read, enqueues the copy out of it
+ * (over xGMI) and, behind it, a kernel that clears the mark.  A send whose
+ * previous copy is still unpublished, or whose buffer the receiver still
+ * holds, is skipped -- the reference's comm_async_test_and_send_prime, which
+ * posts a new MPI_Isend only when MPI_Test says the previous one completed
+ * (comm.c:528-535).  The claim / mark handshake is Dekker's (each side stores
+ * its word, then loads the other's, sequentially consistent), so a buffer is
+ * never written while it is read.  When sender and receiver share one stream
+ * (the blocks of a process, run round-robin), stream order already serialises
+ * every copy, so publication and release are immediate host stores: the
+ * schedule, and every result, is that of synchronous copies.
  *
  * Host code only: no GPU is needed for the control messages (the CPU tests use
  * them across processes).
@@ -65,9 +80,20 @@ typedef struct {
   _Atomic int32_t ready;
   int32_t pid;
   uint64_t rawptr; /* valid in the exporting process only */
+  uint64_t stream; /* the exporting context's stream (same process: same stream => stream-ordered copies) */
   uint8_t handle[MSPI_IPC_HANDLE_BYTES];
-  uint8_t pad[128 - 16 - MSPI_IPC_HANDLE_BYTES];
+  uint8_t pad[128 - 24 - MSPI_IPC_HANDLE_BYTES];
 } ipc_entry;
+
+/* device-slot state of one (src, direction) link, in the shared region */
+typedef struct {
+  _Atomic uint64_t pub;         /* (count << 1) | buffer of the newest complete message; 0: none yet (GPU-written) */
+  _Atomic uint64_t claim;       /* (count << 1) | buffer of the sender's latest send; == pub: nothing in flight */
+  _Atomic uint32_t reading[2];  /* the receiver's copy out of buffer b is pending (cleared by its stream) */
+  int32_t ints[2][AMSG_INTS];   /* the tags of the message in buffer b */
+  int64_t n[2];
+  uint8_t pad[128 - 24 - 8 * AMSG_INTS - 16];
+} dslot_state;
 
 struct msp_amsg {
   char name[128];
@@ -82,10 +108,14 @@ struct msp_amsg {
   uint64_t *seen;    /* [src][kind] last sequence number taken by this rank */
   int registered;
   ipc_entry *ipc;    /* [rank] */
+  dslot_state *dst_; /* [src][dir] device-slot states */
+  dslot_state *dst_dev; /* the same words as the GPU addresses them (registered region) */
   msp_ctx *dctx;     /* device slots enabled: the context their copies run on */
-  double *dslots;    /* this rank's 2 x data_cap device slots (dir 0: to rank-1, 1: to rank+1) */
+  uint64_t skey;     /* its stream */
+  double *dslots;    /* this rank's 2 directions x 2 buffers x data_cap device slots (dir 0: to rank-1) */
   double **peer;     /* [src] resolved device slots of src (NULL: not yet) */
   uint8_t *opened;   /* [src] peer[src] came from hipIpcOpenMemHandle */
+  int64_t sent, skipped; /* device-slot sends posted / skipped (previous one in flight, or buffer still read) */
 };
 
 static int aerr(int code, const char *msg) {
@@ -125,7 +155,8 @@ int msp_amsg_create(const char *name, int32_t nranks, int32_t rank, int64_t data
   m->data_bytes = round_up(sizeof(ctrl_slot) + (size_t)data_cap * sizeof(double), 4096);
   const size_t ctrl_bytes = round_up((size_t)nranks * nranks * MSP_AMSG_NKINDS * sizeof(ctrl_slot), 4096);
   const size_t ipc_bytes = round_up((size_t)nranks * sizeof(ipc_entry), 4096);
-  m->bytes = 4096 + ctrl_bytes + (size_t)nranks * 2 * m->data_bytes + ipc_bytes;
+  const size_t dstate_bytes = round_up((size_t)nranks * 2 * sizeof(dslot_state), 4096);
+  m->bytes = 4096 + ctrl_bytes + (size_t)nranks * 2 * m->data_bytes + ipc_bytes + dstate_bytes;
   int fd;
   if (m->owner) {
     shm_unlink(name); /* a stale region of an earlier run */
@@ -158,6 +189,7 @@ int msp_amsg_create(const char *name, int32_t nranks, int32_t rank, int64_t data
   m->ctrl = (ctrl_slot *)(m->base + 4096);
   m->data = m->base + 4096 + ctrl_bytes;
   m->ipc = (ipc_entry *)(m->data + (size_t)nranks * 2 * m->data_bytes);
+  m->dst_ = (dslot_state *)((uint8_t *)m->ipc + ipc_bytes);
   if (m->owner) {
     m->hdr->nranks = nranks;
     m->hdr->data_cap = data_cap;
@@ -186,14 +218,22 @@ int msp_amsg_attached(const msp_amsg *m, int32_t *n) {
   return MSP_SUCCESS;
 }
 
+static int ensure_registered(msp_amsg *m);
+
 int msp_amsg_enable_device(msp_amsg *m, msp_ctx *ctx) {
   if (!m || !ctx) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
   if (m->dctx) return MSP_SUCCESS;
   m->peer = (double **)calloc((size_t)m->nranks, sizeof(double *));
   m->opened = (uint8_t *)calloc((size_t)m->nranks, 1);
   if (!m->peer || !m->opened) return aerr(MSP_ERR_MEM, "allocation failed");
+  /* the GPU publishes and releases through the state words: the region must be mapped for it */
+  int rc = ensure_registered(m);
+  if (rc) return rc;
+  void *dp = NULL;
+  if ((rc = mspi_host_device_ptr(m->dst_, &dp))) return rc;
+  m->dst_dev = (dslot_state *)dp;
   void *p = NULL;
-  int rc = mspi_dev_alloc(ctx, (size_t)2 * (size_t)(m->data_cap > 0 ? m->data_cap : 1) * sizeof(double), &p);
+  rc = mspi_dev_alloc(ctx, (size_t)4 * (size_t)(m->data_cap > 0 ? m->data_cap : 1) * sizeof(double), &p);
   if (rc) return rc;
   ipc_entry *e = &m->ipc[m->rank];
   if ((rc = mspi_ipc_export(p, e->handle))) {
@@ -202,16 +242,31 @@ int msp_amsg_enable_device(msp_amsg *m, msp_ctx *ctx) {
   }
   m->dslots = (double *)p;
   m->dctx = ctx;
+  m->skey = mspi_stream_key(ctx);
   mspi_ctx_retain(ctx);
   e->pid = (int32_t)getpid();
   e->rawptr = (uint64_t)(uintptr_t)p;
+  e->stream = m->skey;
   atomic_store_explicit(&e->ready, 1, memory_order_release);
+  return MSP_SUCCESS;
+}
+
+int msp_amsg_get_stats(const msp_amsg *m, int64_t *sent, int64_t *skipped) {
+  if (!m) return aerr(MSP_ERR_ARG_NULL, "amsg is NULL");
+  if (sent) *sent = m->sent;
+  if (skipped) *skipped = m->skipped;
   return MSP_SUCCESS;
 }
 
 int msp_amsg_close_peers(msp_amsg *m) {
   if (!m) return aerr(MSP_ERR_ARG_NULL, "amsg is NULL");
   if (!m->peer) return MSP_SUCCESS;
+  /* this rank's copies out of the peers' slots (and its publish / release stores) are stream-ordered: let them
+   * finish before the mappings go (the drivers call close_peers on every rank, barrier, then destroy) */
+  if (m->dctx) {
+    int rc = msp_ctx_synchronize(m->dctx);
+    if (rc) return rc;
+  }
   for (int r = 0; r < m->nranks; ++r) {
     if (m->opened[r]) mspi_ipc_close(m->peer[r]);
     m->peer[r] = NULL;
@@ -242,7 +297,7 @@ static int peer_slots(msp_amsg *m, int src, double **out) {
 int msp_amsg_destroy(msp_amsg **pm) {
   if (!pm || !*pm) return MSP_SUCCESS;
   msp_amsg *m = *pm;
-  msp_amsg_close_peers(m);
+  msp_amsg_close_peers(m); /* also drains this rank's stream: no GPU store into the region is left pending */
   if (m->dslots) {
     atomic_store_explicit(&m->ipc[m->rank].ready, 0, memory_order_release);
     mspi_dev_free(m->dslots);
@@ -313,14 +368,6 @@ static int read_slot(msp_amsg *m, int src, int kind, int32_t *ints, int32_t nint
   if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
   uint64_t *seen = m->seen + (size_t)src * MSP_AMSG_NKINDS + kind;
   *got = 0;
-  const double *dsrc = NULL; /* device slots: the payload in src's HBM */
-  if (v && m->dctx) {
-    double *ps = NULL;
-    int rc = peer_slots(m, src, &ps);
-    if (rc) return rc;
-    if (!ps) return MSP_SUCCESS; /* src has not enabled its slots: nothing sent yet */
-    dsrc = ps + (size_t)(m->rank == src - 1 ? 0 : 1) * (size_t)m->data_cap;
-  }
   for (int attempt = 0; attempt < 8; ++attempt) {
     const uint64_t s1 = atomic_load_explicit(&s->seq, memory_order_acquire);
     if ((s1 & 1) || s1 == *seen) return MSP_SUCCESS; /* being written, or nothing new: try next round */
@@ -330,11 +377,7 @@ static int read_slot(msp_amsg *m, int src, int kind, int32_t *ints, int32_t nint
     if (len < 0 || len > m->data_cap) continue;
     if (len) {
       if (len > cap) return aerr(MSP_ERR_ARG_SIZ, "receive buffer smaller than the message");
-      if (dsrc) {
-        const size_t bytes = (size_t)len * sizeof(double);
-        int rc = mspi_d2d_sync(m->dctx, v->d + voff, bytes, dsrc, bytes, bytes, 1);
-        if (rc) return rc;
-      } else if (v) {
+      if (v) {
         int rc = mspi_h2d_sync(v->ctx, v->d + voff, (const double *)(s + 1), (size_t)len * sizeof(double));
         if (rc) return rc;
       } else {
@@ -371,6 +414,90 @@ static int ensure_registered(msp_amsg *m) {
   return MSP_SUCCESS;
 }
 
+/* ------------------------------------------------------------ device slots */
+static dslot_state *dstate(msp_amsg *m, int src, int dir) { return m->dst_ + (size_t)src * 2 + dir; }
+static dslot_state *dstate_dev(msp_amsg *m, int src, int dir) { return m->dst_dev + (size_t)src * 2 + dir; }
+
+/* peer's slots driven by this very stream (the blocks of one process): stream order serialises every copy */
+static int same_stream(msp_amsg *m, int peer) {
+  ipc_entry *e = &m->ipc[peer];
+  return atomic_load_explicit(&e->ready, memory_order_acquire) && e->pid == (int32_t)getpid() && e->stream == m->skey;
+}
+
+static double *slot_buf(double *base, const msp_amsg *m, int dir, int b) {
+  return base + ((size_t)dir * 2 + (size_t)b) * (size_t)m->data_cap;
+}
+
+static int send_vec_device(msp_amsg *m, int dst, const int32_t *ints, int32_t nints, const msp_vec *v, int64_t off,
+                           int64_t n) {
+  const int dir = dst_rank_dir(m, dst);
+  dslot_state *d = dstate(m, m->rank, dir);
+  const uint64_t P = atomic_load_explicit(&d->pub, memory_order_seq_cst);
+  if (atomic_load_explicit(&d->claim, memory_order_relaxed) != P) { /* the previous copy is not published yet */
+    m->skipped++;
+    return MSP_SUCCESS;
+  }
+  const int b = P ? 1 - (int)(P & 1) : 0; /* the buffer that is not the newest */
+  const uint64_t W = ((P >> 1) + 1) << 1 | (uint64_t)b;
+  atomic_store_explicit(&d->claim, W, memory_order_seq_cst);
+  if (atomic_load_explicit(&d->reading[b], memory_order_seq_cst)) { /* the receiver still copies out of b */
+    atomic_store_explicit(&d->claim, P, memory_order_seq_cst);
+    m->skipped++;
+    return MSP_SUCCESS;
+  }
+  memset(d->ints[b], 0, sizeof(d->ints[b]));
+  if (nints) memcpy(d->ints[b], ints, (size_t)nints * sizeof(int32_t));
+  d->n[b] = n;
+  atomic_thread_fence(memory_order_release);
+  int rc;
+  if (n && (rc = mspi_d2d_async(m->dctx, slot_buf(m->dslots, m, dir, b), v->d + off, (size_t)n * sizeof(double)))) {
+    atomic_store_explicit(&d->claim, P, memory_order_seq_cst);
+    return rc;
+  }
+  if (same_stream(m, dst)) atomic_store_explicit(&d->pub, W, memory_order_seq_cst);
+  else if ((rc = mspi_stream_store_u64(m->dctx, (uint64_t *)&dstate_dev(m, m->rank, dir)->pub, W))) return rc;
+  m->sent++;
+  return MSP_SUCCESS;
+}
+
+static int recv_vec_device(msp_amsg *m, int src, int32_t *ints, int32_t nints, msp_vec *v, int64_t voff, int64_t cap,
+                           int64_t *n, int32_t *got) {
+  *got = 0;
+  double *ps = NULL;
+  int rc = peer_slots(m, src, &ps);
+  if (rc) return rc;
+  if (!ps) return MSP_SUCCESS; /* src has not enabled its slots: nothing sent yet */
+  const int dir = m->rank == src - 1 ? 0 : 1; /* src's direction towards this rank */
+  dslot_state *d = dstate(m, src, dir);
+  uint64_t *seen = m->seen + (size_t)src * MSP_AMSG_NKINDS + MSP_AMSG_DATA;
+  const uint64_t P = atomic_load_explicit(&d->pub, memory_order_seq_cst);
+  if (!P || P == *seen) return MSP_SUCCESS; /* nothing newer than the last plane taken */
+  const int b = (int)(P & 1);
+  atomic_store_explicit(&d->reading[b], 1, memory_order_seq_cst);
+  if (atomic_load_explicit(&d->pub, memory_order_seq_cst) != P) { /* a newer one landed: take it next time */
+    atomic_store_explicit(&d->reading[b], 0, memory_order_seq_cst);
+    return MSP_SUCCESS;
+  }
+  int32_t tmp[AMSG_INTS];
+  memcpy(tmp, d->ints[b], sizeof(tmp));
+  const int64_t len = d->n[b];
+  if (len < 0 || len > m->data_cap || len > cap) {
+    atomic_store_explicit(&d->reading[b], 0, memory_order_seq_cst);
+    return aerr(MSP_ERR_ARG_SIZ, "receive buffer smaller than the message");
+  }
+  if (len && (rc = mspi_d2d_async(m->dctx, v->d + voff, slot_buf(ps, m, dir, b), (size_t)len * sizeof(double)))) {
+    atomic_store_explicit(&d->reading[b], 0, memory_order_seq_cst);
+    return rc;
+  }
+  if (same_stream(m, src)) atomic_store_explicit(&d->reading[b], 0, memory_order_seq_cst);
+  else if ((rc = mspi_stream_store_u32(m->dctx, (uint32_t *)&dstate_dev(m, src, dir)->reading[b], 0))) return rc;
+  if (nints) memcpy(ints, tmp, (size_t)nints * sizeof(int32_t));
+  if (n) *n = len;
+  *seen = P;
+  *got = 1;
+  return MSP_SUCCESS;
+}
+
 int msp_amsg_send_vec(msp_amsg *m, int32_t dst, const int32_t *ints, int32_t nints, const msp_vec *v, int64_t off,
                       int64_t n) {
   if (!m || !v) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
@@ -380,22 +507,12 @@ int msp_amsg_send_vec(msp_amsg *m, int32_t dst, const int32_t *ints, int32_t nin
   if (off < 0 || n < 0 || off + n > v->n || n > m->data_cap) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
   ctrl_slot *s = data_at(m, m->rank, dst);
   if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
-  if (!m->dctx && (rc = ensure_registered(m))) return rc;
+  if (m->dctx) return send_vec_device(m, dst, ints, nints, v, off, n);
+  if ((rc = ensure_registered(m))) return rc;
   write_begin(s);
   memset(s->ints, 0, sizeof(s->ints));
   if (nints) memcpy(s->ints, ints, (size_t)nints * sizeof(int32_t));
   s->n = n;
-  if (m->dctx) {
-    double *slot = m->dslots + (size_t)dst_rank_dir(m, dst) * (size_t)m->data_cap;
-    const size_t bytes = (size_t)n * sizeof(double);
-    if (n && (rc = mspi_d2d_sync(m->dctx, slot, bytes, v->d + off, bytes, bytes, 1))) {
-      s->n = 0;
-      write_end(s);
-      return rc;
-    }
-    write_end(s);
-    return MSP_SUCCESS;
-  }
   if (n && (rc = mspi_d2h_sync(v->ctx, (double *)(s + 1), v->d + off, (size_t)n * sizeof(double)))) {
     s->n = 0; /* publish an empty message rather than a partial plane */
     write_end(s);
@@ -412,6 +529,8 @@ int msp_amsg_recv_vec(msp_amsg *m, int32_t src, int32_t *ints, int32_t nints, ms
   if (rc) return rc;
   if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
   if (off < 0 || cap < 0 || off + cap > v->n) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
-  if (!m->dctx && (rc = ensure_registered(m))) return rc;
+  if (!data_at(m, src, m->rank)) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
+  if (m->dctx) return recv_vec_device(m, src, ints, nints, v, off, cap, n, got);
+  if ((rc = ensure_registered(m))) return rc;
   return read_slot(m, src, MSP_AMSG_DATA, ints, nints, NULL, cap, n, got, v, off);
 }

@@ -181,6 +181,8 @@ int msk_get_tuning(void);
 int msk_get_shape_epoch(void);
 int msk_get_gm_wfree(void);
 int mspi_h2d_sync(msp_ctx *ctx, void *dev, const void *host, size_t bytes);
+/* free and total HBM of the context's device (hipMemGetInfo) */
+int mspi_mem_info(msp_ctx *ctx, size_t *free_bytes, size_t *total_bytes);
 /* ---- HBM mailboxes shared between processes (msplit_ipc.hip) ---- */
 #define MSPI_IPC_HANDLE_BYTES 64
 int mspi_dev_alloc(msp_ctx *ctx, size_t bytes, void **p); /* zeroed */
@@ -192,6 +194,13 @@ int mspi_ipc_close(void *p);
 int mspi_d2d_sync(msp_ctx *ctx, void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
                   size_t height);
 /* page-lock a host range (shared-memory mailboxes) for DMA */
+/* the asynchronous device slots (amsg.c): a copy enqueued without waiting, and a word of a registered host region
+ * stored by the stream once the work before it is done (system-scope release) */
+int mspi_d2d_async(msp_ctx *ctx, void *dst, const void *src, size_t bytes);
+int mspi_host_device_ptr(void *host, void **dev);
+uint64_t mspi_stream_key(const msp_ctx *ctx);
+int mspi_stream_store_u64(msp_ctx *ctx, uint64_t *dev_word, uint64_t v);
+int mspi_stream_store_u32(msp_ctx *ctx, uint32_t *dev_word, uint32_t v);
 int mspi_host_register(void *p, size_t bytes);
 int mspi_host_unregister(void *p);
 

@@ -306,8 +306,14 @@ extern "C" int mspi_h2d_sync(msp_ctx* c, void* dev, const void* host, size_t byt
   return MSP_SUCCESS;
 }
 
+extern "C" int mspi_mem_info(msp_ctx* c, size_t* free_bytes, size_t* total_bytes) {
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemGetInfo(free_bytes, total_bytes));
+  return MSP_SUCCESS;
+}
+
 extern "C" int mspi_host_register(void* p, size_t bytes) {
-  HIPCHK(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  HIPCHK(hipHostRegister(p, bytes, hipHostRegisterMapped));  // mapped: the GPU also stores into it (amsg.c)
   return MSP_SUCCESS;
 }
 

@@ -839,6 +839,13 @@ class AsyncMessages:
     def close_peers(self):
         call("msp_amsg_close_peers", self.h)
 
+    def stats(self) -> tuple:
+        """(sends posted, sends skipped) on the device slots: a send is skipped while its previous copy is not yet
+        published or the receiver still reads the free buffer (comm_async_test_and_send_prime's MPI_Test)."""
+        a, b = C.c_int64(), C.c_int64()
+        call("msp_amsg_get_stats", self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
     def recv_vec(self, src: int, nints: int, v: Vec, off: int, cap: int):
         iv = np.zeros(max(nints, 1), np.int32)
         n = C.c_int64()
@@ -888,10 +895,14 @@ class AsyncBroadcast:
              C.byref(got))
         return bool(got.value)
 
-    def enable_device(self, ctx: Context, nbuf: int = 2):
-        """Device buffers: published blocks stay in the sender's HBM (HIP IPC); nbuf 1 halves their HBM."""
+    def enable_device(self, ctx: Context, nbuf: int = 0) -> int:
+        """Device buffers: published blocks stay in the sender's HBM (HIP IPC); nbuf 1 halves their HBM, 0 lets
+        the library choose (two while an eighth of the HBM stays free after them).  Returns the count in use."""
         call("msp_abcast_enable_device", self.h, ctx.h, int(nbuf))
         self._ctx = ctx
+        n = C.c_int32()
+        call("msp_abcast_get_nbuf", self.h, C.byref(n))
+        return n.value
 
     def close_peers(self):
         call("msp_abcast_close_peers", self.h)

@@ -120,10 +120,8 @@ def footprint(args, minimization):
     name = f"/msplit_fp_{os.getpid()}_{uuid.uuid4().hex[:8]}"
     bc = AsyncBroadcast(name + "_R", nb, rank, blk.bcast_cap(), True)
     nbuf = int(os.environ.get("MSPLIT_ABCAST_NBUF", "0"))
-    if nbuf not in (1, 2):                           # the production rule (asynchronous.AsyncBlock.enable_device)
-        free, _ = torch.cuda.mem_get_info(0)
-        nbuf = 2 if 2 * 8 * blk.bcast_cap() <= 0.75 * free else 1
-    bc.enable_device(ctx, nbuf)
+    # the production rule (asynchronous.AsyncBlock.enable_device -> msp_abcast_enable_device with nbuf 0)
+    nbuf = bc.enable_device(ctx, nbuf if nbuf in (1, 2) else 0)
     ctx.synchronize()
     marks["after_broadcast_buffers_GB"] = hbm.used() / 1e9
     blk.reset_halo()
