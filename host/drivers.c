@@ -816,7 +816,7 @@ int msd_amam_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options 
     barrier(&R);
   }
   if (!p->async_host) { /* HBM slots and R buffers, peer copies over xGMI */
-    /* MSPLIT_ABCAST_NBUF = 1 or 2 forces the R-buffer count; otherwise the library's rule (two while an eighth
+    /* MSPLIT_ABCAST_NBUF = 1 or 2 forces the R-buffer count; otherwise the library's rule (two while a quarter
      * of the HBM stays free after them) */
     const char *e = getenv("MSPLIT_ABCAST_NBUF");
     const int nbuf = e && (atoi(e) == 1 || atoi(e) == 2) ? atoi(e) : 0;

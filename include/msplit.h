@@ -476,7 +476,7 @@ int msp_abcast_fetch_dense(msp_abcast *bc, int32_t src, msp_dense *D, int32_t *g
  * close_peers on every rank before destroy.  nbuf = 2 (a publish fills the
  * buffer readers are not using) or 1 (half the HBM: a publish waits until no
  * reader holds the newest block, and readers skip a block being rewritten);
- * 0 chooses: 2 while an eighth of the GPU's HBM stays free after them, else 1.
+ * 0 chooses: 2 while a quarter of the GPU's HBM stays free after them, else 1.
  * msp_abcast_get_nbuf reports the count in use (0 before enable_device). */
 int msp_abcast_enable_device(msp_abcast *bc, msp_ctx *ctx, int32_t nbuf);
 int msp_abcast_get_nbuf(const msp_abcast *bc, int32_t *nbuf);

@@ -143,7 +143,7 @@ class AsyncBlock:
 
     def enable_device(self):
         """Device slots / buffers in this block's HBM (xGMI peer copies between GPUs).  The R
-        broadcast takes two buffers, or one when two would not leave an eighth of the GPU's HBM free
+        broadcast takes two buffers, or one when two would not leave a quarter of the GPU's HBM free
         (the library's rule, msp_abcast_enable_device with nbuf 0; configs[3] scale: DESIGN.md section
         6.5); MSPLIT_ABCAST_NBUF forces 1 or 2."""
         self.am.enable_device(self.blk.ctx)

@@ -167,12 +167,13 @@ int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   if (b->dctx) return MSP_SUCCESS;
   const size_t buf_bytes = (size_t)(b->cap > 0 ? b->cap : 1) * sizeof(double);
   if (nbuf == 0) {
-    /* auto: two buffers only while an eighth of the GPU's HBM stays free after them (configs[3]'s replicated-R
-     * rank: one 21.5 GB buffer instead of two, 250 instead of 272 GiB of 288 -- DESIGN.md section 6.5) */
+    /* auto: two buffers only while a quarter of the GPU's HBM stays free after them -- the run allocates more
+     * afterwards (configs[3]'s replicated-R rank: 100 GB free here, 24 GB of peer blocks and the LSQR's work
+     * still to come; one 21.5 GB buffer instead of two: DESIGN.md section 6.5) */
     size_t fr = 0, tot = 0;
     int rc = mspi_mem_info(ctx, &fr, &tot);
     if (rc) return rc;
-    nbuf = fr >= 2 * buf_bytes && fr - 2 * buf_bytes >= tot / 8 ? 2 : 1;
+    nbuf = fr >= 2 * buf_bytes && fr - 2 * buf_bytes >= tot / 4 ? 2 : 1;
   }
   b->peer = (double **)calloc((size_t)b->nranks, sizeof(double *));
   b->opened = (uint8_t *)calloc((size_t)b->nranks, 1);

@@ -897,7 +897,7 @@ class AsyncBroadcast:
 
     def enable_device(self, ctx: Context, nbuf: int = 0) -> int:
         """Device buffers: published blocks stay in the sender's HBM (HIP IPC); nbuf 1 halves their HBM, 0 lets
-        the library choose (two while an eighth of the HBM stays free after them).  Returns the count in use."""
+        the library choose (two while a quarter of the HBM stays free after them).  Returns the count in use."""
         call("msp_abcast_enable_device", self.h, ctx.h, int(nbuf))
         self._ctx = ctx
         n = C.c_int32()
