@@ -37,6 +37,7 @@ torch.distributed.run, one rank per GPU, RCCL = backend "nccl").
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -128,6 +129,9 @@ def parse():
     p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--no-seq-mode", action="store_true",
                    help="N=1: skip the seq_mode measurement (one configs[1] step in PETSc's reduction order)")
+    p.add_argument("--no-non-stencil", action="store_true",
+                   help="N=1: skip the non_stencil_aij measurement (GMRES on a per-cell-coefficient AIJ in CSR "
+                        "storage, default and fused MatMult+MDot steps)")
     p.add_argument("--no-assembled", action="store_true",
                    help="N=1: skip the assembled_csr_operator measurement (the GMRES step with the operator handed "
                         "over as host CSR arrays, msp_mat_create_csr)")
@@ -469,6 +473,67 @@ def assembled_operator_step(ctx, args, b, ref):
     return out
 
 
+NON_STENCIL_GOLDEN = os.path.join(ROOT, "tests", "golden", "non_stencil_aij.json")
+
+
+def non_stencil_step(ctx, args):
+    """The GMRES step on an assembled AIJ that is not a box stencil: utils.heterogeneous_poisson3d(256)
+    (-div(kappa grad u), 7 points, a per-cell kappa: every row holds its own values, so no dictionary fits and
+    the matrix keeps CSR storage -- the general operator a PETSc user hands over), as host CSR arrays through
+    msp_mat_create_csr; b = A*1, x0 = 0, GMRES(30), 300 iterations.  Timed twice: the default step (CSR MatMult,
+    then the CGS kernels) and the step with the MatMult fused with the VecMDot (k_spmv_mdot: W dotted from
+    registers, not re-read; MSK_TUNE_GM_SPMV_MDOT).  Each is checked against the committed oracle record
+    (tests/golden/non_stencil_aij.json, written by tests/golden/make_non_stencil.py)."""
+    import torch
+    from medane_tchakorom_ufc_thesis_repository_amd import _lib
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import KSP, Mat, Options, Vec
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import heterogeneous_poisson3d
+    n = 256
+    ref = json.load(open(NON_STENCIL_GOLDEN)) if os.path.exists(NON_STENCIL_GOLDEN) else None
+    rp, col, val = heterogeneous_poisson3d(n)
+    N = n ** 3
+    A = Mat.from_csr(ctx, N, N, rp, col, val)
+    nnz = int(rp[-1])
+    del rp, col, val
+    ones = Vec(ctx, N)
+    ones.set(1.0)
+    b = Vec(ctx, N)
+    A.mult(ones, b)
+    ksp = KSP(ctx)
+    ksp.set_operators(A)
+    ksp.set_from_options(Options("-ksp_type gmres -ksp_gmres_restart 30 -pc_type none -ksp_norm_type "
+                                 "unpreconditioned -ksp_rtol 1e-4 -ksp_max_it 300"))
+    ksp.set_initial_guess_nonzero(False)
+    x = Vec(ctx, N)
+    L = _lib.load()
+    L.msk_set_tuning.argtypes = [ctypes.c_int]
+    L.msk_set_tuning.restype = None
+    out = {"operator": "utils.heterogeneous_poisson3d(256): 7-point -div(kappa grad u), per-cell kappa, host CSR "
+                       "through msp_mat_create_csr", "rows": N, "nnz": nnz, "matrix_storage": A.get_storage(),
+           "spmv_kernel": A.spmv_kernel(), "reference": "tests/golden/non_stencil_aij.json['dbr']"}
+    steps = max(1, min(args.steps, 3))
+    for name, flags in (("default", 0), ("fused_matmult_mdot", 2048)):
+        L.msk_set_tuning(flags)
+        try:
+            ksp.solve(b, x)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            its = 0
+            for _ in range(steps):
+                ksp.solve(b, x)
+                its += ksp.get_iteration_number()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            ok, bad = check_step(ksp, x, ref["dbr"]) if ref else (None, ["no record"])
+        finally:
+            L.msk_set_tuning(0)
+        out[name] = {"value": float(N) * its / dt, "unit": "DOF-updates/s", "ms_per_step": 1e3 * dt / steps,
+                     "steps": steps, "verified": ok, "mismatch": bad}
+    out["verified"] = all(out[k]["verified"] for k in ("default", "fused_matmult_mdot"))
+    A.destroy()
+    return out
+
+
 def seq_mode_step(ctx, ksp, b, x, ref):
     """One configs[1] step with every reduction in PETSc's sequential order (MSP_REDUCE_SEQ, the parity
     mode -msplit_reduction seq selects), timed and checked against the PETSc-order oracle record."""
@@ -679,6 +744,8 @@ def main():
             extras["seq_mode"] = seq_mode_step(ctx, ksp, b, x, ref)
         if not args.no_assembled and args.operator == "csr" and args.peclet is None:
             extras["assembled_csr_operator"] = assembled_operator_step(ctx, args, b, ref)
+        if not args.no_non_stencil and args.operator == "csr" and args.peclet is None and n == 256:
+            extras["non_stencil_aij"] = non_stencil_step(ctx, args)
         # release the headline's objects, then the two side measurements
         del ksp, A, b, x, ones
         if not args.no_spmv512:      # before the SMSM block's ~30 GB come and go
@@ -752,7 +819,8 @@ def main():
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     failed = (verified is False or (extras.get("seq_mode") or {}).get("verified") is False
-              or (extras.get("assembled_csr_operator") or {}).get("verified") is False)
+              or (extras.get("assembled_csr_operator") or {}).get("verified") is False
+              or (extras.get("non_stencil_aij") or {}).get("verified") is False)
     if variant == "smsm":
         mini.close()
     if world > 1:

@@ -57,6 +57,47 @@ def poisson3DMatrix_rows(nx, ny, nz, z0, z1):
     return rp, c, v, nxny * nz
 
 
+def _splitmix64(x):
+    z = x + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def heterogeneous_poisson3d(n: int, seed: int = 20251121):
+    """An assembled AIJ operator that is not a box stencil: -div(kappa grad u) on the n^3 grid, 7 points, in
+    the reference's numbering (x fastest, as poisson3DMatrix, utils.c:30-121).  kappa per cell is
+    1 + (h mod 1000) / 1000, h a splitmix64 hash of (cell index + seed); the face between two cells weighs
+    2 ka kb / (ka + kb), a boundary face the cell's own kappa (Dirichlet), the diagonal is the sum of the six
+    face weights in the order z-, y-, x-, x+, y+, z+, the neighbours -weight.  Only IEEE + - * / (no libm), so
+    the arrays are the same bits on every machine.  Almost every row holds its own values, so no (column - row,
+    value) dictionary fits: the matrix keeps CSR storage -- the general AIJ a PETSc user assembles
+    (bench.py non_stencil_aij).  Returns (rowptr int32, col int32, val float64), columns ascending."""
+    N = n * n * n
+    with np.errstate(over="ignore"):
+        h = _splitmix64(np.arange(N, dtype=np.uint64) + np.uint64(seed))
+    kap = (1.0 + (h % np.uint64(1000)).astype(np.float64) * 0.001).reshape(n, n, n)   # [k, j, i]
+
+    def face(axis, side):
+        nb = np.roll(kap, -side, axis=axis)
+        w = 2.0 * kap * nb / (kap + nb)
+        edge = [slice(None)] * 3
+        edge[axis] = -1 if side > 0 else 0
+        w[tuple(edge)] = kap[tuple(edge)]                # boundary face: Dirichlet, the cell's own kappa
+        return w.ravel()
+    P = n * n
+    wzm, wym, wxm = face(0, -1), face(1, -1), face(2, -1)
+    wxp, wyp, wzp = face(2, 1), face(1, 1), face(0, 1)
+    diag = ((((wzm + wym) + wxm) + wxp) + wyp) + wzp
+    g = np.arange(N, dtype=np.int64)
+    i, j, k = g % n, (g // n) % n, g // P
+    cols = np.stack([g - P, g - n, g - 1, g, g + 1, g + n, g + P], axis=1)
+    vals = np.stack([-wzm, -wym, -wxm, diag, -wxp, -wyp, -wzp], axis=1)
+    keep = np.stack([k > 0, j > 0, i > 0, np.ones(N, bool), i < n - 1, j < n - 1, k < n - 1], axis=1)
+    rowptr = np.concatenate([[0], np.cumsum(keep.sum(axis=1))]).astype(np.int32)
+    return rowptr, cols[keep].astype(np.int32), vals[keep]
+
+
 def poisson2DMatrix_rows(m, n, row0, row1):
     """Rows [row0,row1) of poisson2DMatrix (utils.c:247-293): i = Ii / n,
     j = Ii - i*n, diagonal 4.  Returns (rowptr, col, val, ncols)."""

@@ -694,3 +694,22 @@ def test_box_with_coupling_planes_takes_the_chunk_march(ctx, oracle, halo, shape
     R = Rd.get_values()
     for q in range(s):
         assert np.array_equal(R[:, q], O.mult(np.ascontiguousarray(S[:, q])))
+
+
+@pytest.mark.parametrize("flags", [0, 2048])
+@pytest.mark.parametrize("n", [24, 48])
+def test_non_stencil_aij_keeps_csr_and_equals_oracle(ctx, oracle, n, flags):
+    """bench.py's non_stencil_aij operator (utils.heterogeneous_poisson3d: a per-cell kappa, so almost every row
+    holds its own values and no dictionary fits) keeps CSR storage, and MatMult, MatResidual and GMRES(30) through
+    msp_mat_create_csr equal the oracle bit for bit, with the default step (k_spmv_lds8 + the CGS kernels) and with
+    the MatMult fused with the VecMDot (MSPLIT_TUNING 2048, k_spmv_mdot)."""
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import heterogeneous_poisson3d
+    from test_gpu_kernels import tuning
+    rp, col, val = heterogeneous_poisson3d(n)
+    N = n ** 3
+    A = Mat.from_csr(ctx, N, N, rp, col, val)
+    assert A.get_storage() == "csr"
+    O = oracle.Mat.from_arrays(N, N, rp, col, val)
+    _products(ctx, A, O, np.random.default_rng(SEED))
+    with tuning(flags):
+        _gmres_vs_oracle(ctx, oracle, A, O, O.mult(np.ones(N)), max_it=75)

@@ -7,7 +7,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-r04}
 mkdir -p $OUT
 export TMPDIR=/tmp
-NOX="--no-cpu-baseline --no-csr-compare --no-smsm-n1 --no-seq-mode --no-assembled"
+NOX="--no-cpu-baseline --no-csr-compare --no-smsm-n1 --no-seq-mode --no-assembled --no-non-stencil"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run -f csv -- python3 bench.py --steps 3 $NOX > $OUT/bench_trace.json 2> $OUT/trace.err &&
