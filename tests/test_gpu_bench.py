@@ -25,10 +25,14 @@ def _port():
     return p
 
 
-def _launch(n, args, timeout=240):
+def _launch(n, args, timeout=240, rccl_hosts=False):
+    """bench.py --gpus n under torch.distributed.run, as the driver launches it.  rccl_hosts: every rank under its
+    own NCCL_HOSTID (tests/rccl_rank_env.sh), so RCCL accepts n ranks on this box's one GPU."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
-           "--gpus", str(n)] + args
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}"]
+    if rccl_hosts:
+        cmd += ["--no-python", os.path.join(ROOT, "tests", "rccl_rank_env.sh"), sys.executable]
+    cmd += [os.path.join(ROOT, "bench.py"), "--gpus", str(n)] + args
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
 
@@ -78,3 +82,16 @@ def test_single_gpu_line_is_verified():
     assert out["verified"] is True and out["verification"]["mismatch"] == []
     assert out["same_run_csr_storage"]["verified"] is True
     assert out["config"]["transport"] == "none"
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_rccl_multi_rank_line_is_verified(n):
+    """The driver's N > 1 path itself -- torch.distributed.run, the nccl (RCCL) process group, LibComm's library
+    RCCL communicator, --require-rccl -- with n ranks on this box's one GPU, each under its own NCCL_HOSTID (RCCL's
+    socket transport instead of xGMI: correctness, not speed).  The line says transport rccl, and the post-timing
+    SMSM-global check over that communicator reproduces the oracle's n-block record bit for bit on every rank."""
+    r = _launch(n, ["--require-rccl"] + SMALL, rccl_hosts=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json(r.stdout)
+    assert out["n_gpus"] == n and out["config"]["transport"] == "rccl"
+    assert out["verified"] is True and out["verification"]["mismatch"] == [], out.get("verification")

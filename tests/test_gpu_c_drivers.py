@@ -143,6 +143,50 @@ def test_c_host_mpi_ranks_equal_oracle(ctx, oracle, built, case):
         assert got["final_norm"] == want["final_norm"]
 
 
+# RCCL refuses two ranks of one host on one GPU ("Duplicate GPU detected").  With a different NCCL_HOSTID per rank it
+# takes them for separate hosts and connects them over its socket transport on the loopback interface: not xGMI,
+# but msplit_comm.hip's RCCL branch -- grouped ncclSend/ncclRecv of the planes, ncclAllGather of the ordered sums and
+# LSQR partials, all on the context's stream -- runs multi-rank on this one-GPU box.
+RCCL_ENV = ["-env", "NCCL_SOCKET_IFNAME", "lo", "-env", "NCCL_IB_DISABLE", "1"]
+
+
+def _run_rccl(args, nranks, timeout=150):
+    """One rank per block over RCCL (MPMD launch, one NCCL_HOSTID per rank), -msplit_require_rccl: the run stops
+    rather than fall back to the host transport.  Its last JSON line."""
+    exe = os.path.join(HOST, "msplit_driver_mpi")
+    cmd = [MPIEXEC] + MPI_LAUNCH
+    for r in range(nranks):
+        cmd += (([":"] if r else []) + ["-n", "1"] + RCCL_ENV + ["-env", "NCCL_HOSTID", f"msplit-test-rank{r}", exe]
+                + args + ["-msplit_require_rccl", "-json"])
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        raise AssertionError(f"RCCL run did not finish in {timeout} s\nstderr:\n{err[-3000:]}")
+    assert p.returncode == 0, f"RCCL run exited {p.returncode}\nstderr:\n{err[-3000:]}"
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("case", [MPI_CASES[1], MPI_CASES[0], MPI_CASES[4], MPI_CASES[6], MPI_CASES[7]],
+                         ids=lambda c: f"{'smsm' if c[0] == SMSM else 'sm'}-{c[1]}d-{c[5]}ranks")
+def test_c_host_mpi_rccl_ranks_equal_oracle(ctx, oracle, built, case):
+    """The RCCL transport multi-rank (the N > 1 product path; on this box over RCCL's socket transport, see
+    RCCL_ENV): SM and SMSM-global at 2, 3 and 4 ranks, bitwise the DBR oracle and the host-transport run --
+    outer history, LSQR counts, norm0, final residual and error (comm.c:126-141, :252-286)."""
+    prog, dim, nx, ny, nz, nb, s, rtol = case
+    args = _problem_args(prog, dim, nx, ny, nz, nb, s, rtol)
+    want = _oracle_record(oracle, prog, dim, nx, ny, nz, nb, s, rtol)
+    got = _run_rccl(args, nb)
+    assert got["ranks"] == nb and got["transport"] == "rccl"
+    _assert_same_run(got, want, f"{nb} MPI ranks over RCCL vs oracle")
+    host = _run(args + ["-msplit_transport", "host"], mpi=nb)
+    assert got["final_norm"] == host["final_norm"] and got["error"] == host["error"]
+    if prog == SMSM:
+        assert got["final_norm"] == want["final_norm"]
+
+
 def test_c_host_mpi_require_rccl_refuses_the_host_path(built):
     """-msplit_require_rccl: two ranks on one GPU cannot get an RCCL communicator, so the run stops (exit 3)
     before any solve instead of silently measuring the MPI path."""

@@ -32,9 +32,11 @@ def _opts(nb, s):
     return f"{inner} {outer} -s {s}"
 
 
-def _worker(rank, world, port, problem, q, transport="host"):
+def _worker(rank, world, port, problem, q, transport="host", rccl_hosts=False):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if rccl_hosts:  # one NCCL_HOSTID per rank: RCCL takes the ranks sharing this GPU for two hosts (socket transport)
+        os.environ.update(NCCL_HOSTID=f"msplit-test-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     try:
         import torch  # noqa: F401
         import torch.distributed as dist
@@ -70,11 +72,12 @@ def _worker(rank, world, port, problem, q, transport="host"):
         q.put((rank, None, traceback.format_exc() + str(e)))
 
 
-def _run(world, problem, transport="host"):
+def _run(world, problem, transport="host", rccl_hosts=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, problem, q, transport)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, problem, q, transport, rccl_hosts))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
@@ -120,3 +123,29 @@ def test_libcomm_falls_back_when_rccl_is_refused(oracle):
                                                       reduce_mode=oracle.REDUCE_DBR), max_outer=200)
     assert np.array_equal(np.concatenate([o["x"] for o in outs]), ro["x"])
     assert all(o["outer_its"] == ro["outer_its"] for o in outs)
+
+
+@pytest.mark.parametrize("problem,world", [(("smsm", 3, 12, 10, 8, 4, 1e-6), 2), (("sm", 3, 12, 10, 8, 0, 1e-6), 2),
+                                           (("smsm", 3, 8, 8, 12, 3, 1e-6), 3)])
+def test_libcomm_rccl_ranks_bitwise_vs_oracle(oracle, problem, world):
+    """The product's N > 1 path on its RCCL transport: LibComm's library communicator (grouped ncclSend/ncclRecv
+    planes, ncclAllGather of the residual sums and LSQR partials on the context's stream), every rank on this
+    box's one GPU under its own NCCL_HOSTID (RCCL's socket transport on the loopback interface).  Each rank's SM /
+    SMSM-global result is the single-process DBR oracle's bit for bit."""
+    kind, dim, nx, ny, nz, s, rtol = problem
+    outs = _run(world, problem, transport="rccl", rccl_hosts=True)
+    assert all(o["transport"] == "rccl" for o in outs)
+    inner = dict(restart=30, max_it=20, rtol=1e-20, abstol=1e-100, reduce_mode=oracle.REDUCE_DBR)
+    if kind == "smsm":
+        ro = oracle.smsm_solve(dim, nx, ny, nz, world, s, rtol, inner,
+                               dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0,
+                                    reduce_mode=oracle.REDUCE_DBR), max_outer=60)
+    else:
+        ro = oracle.sm_solve(dim, nx, ny, nz, world, rtol, inner, max_outer=200)
+    assert np.array_equal(np.concatenate([o["x"] for o in outs]), ro["x"])
+    for o in outs:
+        assert o["outer_its"] == ro["outer_its"] and o["norm0"] == ro["norm0"]
+        assert np.array_equal(np.array(o["hist"]), ro["hist"])
+        if kind == "smsm":
+            assert o["final_norm"] == ro["final_norm"]
+            assert np.array_equal(np.array(o["lsqr_its"]), ro["lsqr_its"])
