@@ -177,7 +177,14 @@ int msp_mat_get_info(const msp_mat *A, int32_t *nrows, int32_t *ncols, int64_t *
  *                    per-matrix dictionary (<= 256 pairs) and one byte per row
  *                    (its length, <= 255): ~1 byte per entry.  Every
  *                    constant-coefficient stencil fits (7 pairs in 3D).
- * A matrix that fits is given DV at assembly (MSPLIT_MAT_STORAGE=csr in the
+ *   MSP_STORAGE_STENCIL  a 3D box stencil with per-row values (variable
+ *                    coefficients: too many pairs for DV): one presence byte per
+ *                    row and the row's seven values in per-neighbour arrays,
+ *                    57 bytes per row against CSR's 88; taken when the columns of
+ *                    every row are the box's neighbours {0, -+1, -+nx, -+nx*ny}
+ *                    with no entry across a line or plane edge and the planes hold
+ *                    whole 4096-row chunks (the z-march over chunk tiles).
+ * A matrix that fits is given DV (else STENCIL) at assembly (MSPLIT_MAT_STORAGE=csr in the
  * environment keeps CSR); the CSR stays resident for the kernels that need it
  * (MatMatMult, get_csr).  This is MatSetType's choice of format inside one
  * type, like PETSc's AIJ variants, invisible to the caller.  Setting DV on a
@@ -186,6 +193,7 @@ int msp_mat_get_info(const msp_mat *A, int32_t *nrows, int32_t *ncols, int64_t *
 #define MSP_STORAGE_NONE (-1)
 #define MSP_STORAGE_CSR 0
 #define MSP_STORAGE_DV 1
+#define MSP_STORAGE_STENCIL 2
 int msp_mat_set_storage(msp_mat *A, int storage);
 int msp_mat_get_storage(const msp_mat *A, int *storage, int *ndict);
 /* The kernel family MatMult / MatResidual / the GMRES products launch for A under the current
@@ -194,7 +202,8 @@ int msp_mat_get_storage(const msp_mat *A, int *storage, int *ndict);
  * (the z-march family: k_spmv_box_march, k_spmv_box_lines, k_box_march_chunk, and in GMRES
  * k_box_spmv_mdot_march; DV storage of a box stencil -- generated, or assembled by the caller and recognised by
  * msp_mat_create_csr: a 7-point (5-point) dictionary with deltas {0, -+1, -+nx, -+nx*ny} and no
- * entry across a line or plane edge), "k_stencil_spmv" (matrix-free), "k_spmv_rows" (row-compressed). */
+ * entry across a line or plane edge), "k_box_march_chunk_rv" (STENCIL storage; in GMRES fused with the VecMDot,
+ * k_box_spmv_mdot_march with the rows' values), "k_stencil_spmv" (matrix-free), "k_spmv_rows" (row-compressed). */
 int msp_mat_get_spmv_kernel(const msp_mat *A, const char **name);
 /* Free the CSR arrays of a matrix in DV storage (col/val; rowptr too in the
  * ELL layout): 12 bytes per entry of HBM back, e.g. 11.7 GB per GPU for a

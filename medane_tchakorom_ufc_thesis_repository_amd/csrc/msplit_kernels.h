@@ -142,6 +142,14 @@ int msk_box_march_halo(int32_t nx, int32_t ny, int32_t nz, int halo, const uint8
 // GMRES: y = A (sc*x) for a box stencil with march presence bytes (nx <= 2048; P = the plane, or nx in 2D), fused
 // with the DBR stage 1 of y . V_v (v < nv <= 32) into partial: W in the DBR lane layout, bitwise the march's.
 // *self_out (may be NULL) = 1 when V's last vector is x and its dot came from the march's registers (not re-read).
+// The stencil storage (a box stencil whose rows carry their own seven values, rv[e * rvs + row], e in column
+// order): the chunk-tile march products, and the GMRES MatMult fused with VecMDot stage 1 (W stored).
+int msk_box_march_chunk_rv(int32_t nx, int32_t ny, int32_t nz, const uint8_t* mask, const double* rv, int64_t rvs,
+                           const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
+                           const int* stop, hipStream_t s);
+int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval,
+                         const double* rv, int64_t rvs, const double* x, const double* sdev, double* y, const Vecs* V,
+                         int nv, double* partial, int64_t nchunks, const int* stop, int* self_out, hipStream_t s);
 int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval,
                       const double* x, const double* sdev, double* y, const Vecs* V, int nv, double* partial,
                       int64_t nchunks, const int* stop, int* self_out, hipStream_t s);

@@ -1526,10 +1526,15 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
 // 2-byte vectors, so each lane keeps 8 x(z+1) loads and 8 b loads in flight where the line kernels keep
 // one; the tile's window [-nx, 4096+nx) of plane z is in LDS.  Same terms in the same order as
 // k_spmv_box_march: bitwise its products.
-template <int MODE, bool NTY>
+// RV (the stencil storage, MSP_STORAGE_STENCIL): each row's seven values from the per-leg arrays
+// rv[e * rvs + row] (0 where the row has no such neighbour, never added) instead of the dictionary: a box
+// stencil with variable coefficients, 56 value bytes per row read as 16-byte non-temporal vectors, against
+// 88 bytes of CSR (col + val + rowptr).  Same terms, same order: bitwise the CSR kernels' sums.
+template <int MODE, bool NTY, bool RV>
 __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
                                                         int halo, const uint8_t* __restrict__ mask,
                                                         const double* __restrict__ dval,
+                                                        const double* __restrict__ rv, int64_t rvs,
                                                         const double* __restrict__ x,
                                                         const double* __restrict__ b, double* __restrict__ y,
                                                         const double* __restrict__ sdev, double* __restrict__ vout,
@@ -1551,7 +1556,7 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
   const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
   const double sc = MODE == MSK_SPMV_SCALED ? *sdev : 1.0;
   double v[7];
-  march_values<false>(dval, v);
+  if constexpr (!RV) march_values<false>(dval, v);
   const int nh = nx / 2;  // double2 per halo line
   double xm[2 * kIters], xc[2 * kIters], xp[2 * kIters];
   {
@@ -1608,6 +1613,11 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
+      double2 rq[7];
+      if constexpr (RV) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) rq[k] = ld_nt(reinterpret_cast<const double2*>(rv + k * rvs + base + j * (2 * kT)));
+      }
       double o[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -1617,8 +1627,10 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
                               xp[2 * j + q]};
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 7; ++k)
-          if (mr & (1u << k)) s = s + v[k] * (MODE == MSK_SPMV_SCALED ? xq[k] * sc : xq[k]);
+        for (int k = 0; k < 7; ++k) {
+          const double vk = RV ? (q ? rq[k].y : rq[k].x) : v[k];
+          if (mr & (1u << k)) s = s + vk * (MODE == MSK_SPMV_SCALED ? xq[k] * sc : xq[k]);
+        }
         if constexpr (MODE == MSK_SPMV_RESID) s = (q ? bb[j].y : bb[j].x) - s;
         o[q] = s;
       }
@@ -1766,10 +1778,13 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot(int32_t nx, int64_t P, int
 // planes.  The lane's own x rows of planes z-1, z, z+1 stay in registers (xm, xc, xp); per plane
 // only x(z+1), the two halo lines of the window and the presence bytes are loaded, the window's
 // own rows are written to LDS from xc.  W and every dot are the unmarched kernel's, bit for bit.
-template <int VAR, bool NTY>
+// RV: the stencil storage's per-row values (as k_box_march_chunk<.., RV>); W is then stored (y != null):
+// recomputing it in the MAXPY would re-read the 56 value bytes per row to save W's 16.
+template <int VAR, bool NTY, bool RV>
 __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
                                                             const uint8_t* __restrict__ mask,
                                                             const double* __restrict__ dval,
+                                                            const double* __restrict__ rv, int64_t rvs,
                                                             const double* __restrict__ x,
                                                             const double* __restrict__ sdev, double* __restrict__ y,
                                                             Vecs V, int nv, int self, double* __restrict__ partial,
@@ -1794,7 +1809,7 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
   const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
   const double sc = *sdev;
   double v[7];
-  march_values<false>(dval, v);
+  if constexpr (!RV) march_values<false>(dval, v);
   const int nh = nx / 2;  // double2 per halo line
   double xm[2 * kIters], xc[2 * kIters], xp[2 * kIters];
   {
@@ -1850,6 +1865,11 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     double wr[2 * kIters];
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
+      double2 rq[7];
+      if constexpr (RV) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) rq[k] = ld_nt(reinterpret_cast<const double2*>(rv + k * rvs + base + j * (2 * kT)));
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int e = j * (2 * kT) + 2 * t + q + nx;
@@ -1858,8 +1878,10 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
                               xp[2 * j + q]};
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 7; ++k)
-          if (mr & (1u << k)) s = s + v[k] * (xq[k] * sc);
+        for (int k = 0; k < 7; ++k) {
+          const double vk = RV ? (q ? rq[k].y : rq[k].x) : v[k];
+          if (mr & (1u << k)) s = s + vk * (xq[k] * sc);
+        }
         wr[2 * j + q] = s;
       }
       if (!y) continue;  // uniform: W is recomputed by the MAXPY after (k_box_maxpy_march), not stored
@@ -2792,7 +2814,7 @@ static bool march_chunk_ok(int32_t nx, int32_t ny, int d2) {
 // the column space has the plane below / above the box (x points at the box's first row).
 static int launch_march_chunk(int32_t nx, int32_t ny, int32_t nz, int halo, const uint8_t* mask, const double* dval,
                               const double* x, const double* b, double* y, int mode, const double* sdev, double* vout,
-                              const int* stop, hipStream_t s) {
+                              const int* stop, hipStream_t s, const double* rv = nullptr, int64_t rvs = 0) {
   // depth: the tile-planes dealt to 512 workgroups (two per CU, one wave of the grid; back to back
   // 256^3 56.6 us at 8 planes against 61-64 at 4, 6, 12, 16; 512x512x256 219.6 us at 32 against 228-234 at
   // 8-16; profiles/r03/chunk/), or the msk_set_march_z override
@@ -2805,12 +2827,13 @@ static int launch_march_chunk(int32_t nx, int32_t ny, int32_t nz, int halo, cons
   const int xcd = cpp % 8 == 0 && cpp >= 32 && !(msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD);
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
   const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
-#define MSK_BMC(M, NT_)                                                                                        \
-  k_box_march_chunk<M, NT_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, halo, mask, dval, x, b, \
-                                                                        y, sdev, vout, stop)
-#define MSK_BMC2(M)                                    \
-  do {                                                 \
-    if (nty) MSK_BMC(M, true); else MSK_BMC(M, false); \
+#define MSK_BMC(M, NT_, RV_)                                                                                    \
+  k_box_march_chunk<M, NT_, RV_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, halo, mask, dval, rv, \
+                                                                             rvs, x, b, y, sdev, vout, stop)
+#define MSK_BMC2(M)                                                           \
+  do {                                                                        \
+    if (rv) { if (nty) MSK_BMC(M, true, true); else MSK_BMC(M, false, true); } \
+    else { if (nty) MSK_BMC(M, true, false); else MSK_BMC(M, false, false); }  \
   } while (0)
   if (mode == MSK_SPMV_RESID) MSK_BMC2(MSK_SPMV_RESID);
   else if (mode == MSK_SPMV_SCALED) MSK_BMC2(MSK_SPMV_SCALED);
@@ -2890,6 +2913,20 @@ extern "C" int msk_box_march_halo(int32_t nx, int32_t ny, int32_t nz, int halo, 
   if (!msk_box_march_halo_fits(nx, ny, nz, halo, x, b, y, mode)) return (int)hipErrorInvalidValue;
   const double* xo = x + ((halo & 1) ? (int64_t)nx * ny : 0);
   return launch_march_chunk(nx, ny, nz, halo, mask, dval, xo, b, y, mode, nullptr, nullptr, nullptr, s);
+}
+
+// The stencil storage's products (k_box_march_chunk<.., RV>): MatMult, MatResidual or the scaled MatMult of a 3D box
+// (no coupling planes) whose rows carry their own seven values, rv[e * rvs + row].  Only boxes the chunk-tile march
+// takes; every operand 16-byte aligned.
+extern "C" int msk_box_march_chunk_rv(int32_t nx, int32_t ny, int32_t nz, const uint8_t* mask, const double* rv,
+                                      int64_t rvs, const double* x, const double* b, double* y, int mode,
+                                      const double* sdev, double* vout, const int* stop, hipStream_t s) {
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad() || !march_chunk_ok(nx, ny, 0) || !rv || (rvs & 1) ||
+      rvs < (int64_t)nx * ny * nz || !a16(rv) || !a16(x) || !a16(y) || (mode == MSK_SPMV_RESID && !a16(b)) ||
+      (mode == MSK_SPMV_SCALED && vout && !a16(vout)))
+    return (int)hipErrorInvalidValue;
+  return launch_march_chunk(nx, ny, nz, 0, mask, nullptr, x, b, y, mode, sdev, vout, stop, s, rv, rvs);
 }
 
 extern "C" int msk_march_mask(int32_t nrows, int d2, const uint8_t* code8, uint8_t* mask, hipStream_t s) {
@@ -3006,13 +3043,23 @@ extern "C" int msk_spmv_mdot(int32_t nrows, const int32_t* rowptr, const int32_t
 extern "C" int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval,
                                  const double* x, const double* sdev, double* y, const Vecs* V, int nv, double* partial,
                                  int64_t nchunks, const int* stop, int* self_out, hipStream_t s) {
+  return msk_box_spmv_mdot_rv(nx, P, n, d2, mask, dval, nullptr, 0, x, sdev, y, V, nv, partial, nchunks, stop,
+                              self_out, s);
+}
+
+// rv != null: the stencil storage's per-row values (marched form only, W stored)
+extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, const uint8_t* mask, const double* dval,
+                                    const double* rv, int64_t rvs, const double* x, const double* sdev, double* y,
+                                    const Vecs* V, int nv, double* partial, int64_t nchunks, const int* stop,
+                                    int* self_out, hipStream_t s) {
   if (self_out) *self_out = 0;
   if (n <= 0 || nchunks <= 0) return 0;
   if (nx < 2 || nx > 2048 || P < nx || nv < 1 || nv > MSK_MAX_GROUP || dv_flags_bad()) return (int)hipErrorInvalidValue;
+  if (rv && (!y || d2 || P % kChunk || n % P || (nx & 1))) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
   const dim3 g((unsigned)nchunks), b(kT);
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
-  if (!d2 && P % kChunk == 0 && n % P == 0 && (nx & 1) == 0 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_FLAT)) {
+  if (!d2 && P % kChunk == 0 && n % P == 0 && (nx & 1) == 0 && (rv || !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_FLAT))) {
     // whole chunks per plane: march zt planes per workgroup (MSPLIT_BOXMDOT_ZT overrides the depth, A/B)
     static const int zenv = [] {
       const char* e = getenv("MSPLIT_BOXMDOT_ZT");
@@ -3037,11 +3084,17 @@ extern "C" int msk_box_spmv_mdot(int32_t nx, int64_t P, int64_t n, int d2, const
     const double* last = V->base ? V->base + (int64_t)(nv - 1) * V->stride : V->p[nv - 1];
     const int self = self_env != 0 && last == x;
     if (self_out) *self_out = self;
-#define MSK_BSMM(VAR_, NT_)                                                                                       \
-  k_box_spmv_mdot_march<VAR_, NT_><<<dim3((unsigned)grid), b, lds, s>>>(nx, P, nz, zt, xcd, mask, dval, x, sdev, y, *V, nv, \
-                                                                        self, partial, nchunks, stop)
-    if (vec_var()) { if (nty) MSK_BSMM(1, true); else MSK_BSMM(1, false); }
-    else { if (nty) MSK_BSMM(0, true); else MSK_BSMM(0, false); }
+#define MSK_BSMM(VAR_, NT_, RV_)                                                                              \
+  k_box_spmv_mdot_march<VAR_, NT_, RV_><<<dim3((unsigned)grid), b, lds, s>>>(nx, P, nz, zt, xcd, mask, dval, rv, rvs, x, \
+                                                                             sdev, y, *V, nv, self, partial, nchunks,    \
+                                                                             stop)
+    if (rv) {
+      if (vec_var()) { if (nty) MSK_BSMM(1, true, true); else MSK_BSMM(1, false, true); }
+      else { if (nty) MSK_BSMM(0, true, true); else MSK_BSMM(0, false, true); }
+    } else {
+      if (vec_var()) { if (nty) MSK_BSMM(1, true, false); else MSK_BSMM(1, false, false); }
+      else { if (nty) MSK_BSMM(0, true, false); else MSK_BSMM(0, false, false); }
+    }
 #undef MSK_BSMM
     return (int)hipGetLastError();
   }

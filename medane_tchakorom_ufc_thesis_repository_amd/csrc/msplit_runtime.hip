@@ -464,6 +464,11 @@ struct msp_mat {
   int32_t march_d2 = 0;        // 2D box stencil (five pairs), marched as nx x 1 x ny
   int32_t march_halo = 0;      // bit 0 / 1: the column space adds the plane below / above the box (chunk march only)
   uint8_t* march_mask = nullptr;  // nrows (+16 pad): the rows' presence bytes (msk_march_mask)
+  // STENCIL storage (rv_attach): a 3D box stencil whose rows carry their own values; rv_val[e * rv_stride + r] is
+  // row r's entry at neighbour e (column order; 0.0 where the row has none), march_* and march_mask as above
+  double* rv_val = nullptr;
+  int64_t rv_stride = 0;
+  bool rv_on = false;
   bool csr_released = false;   // msp_mat_release_csr: col/val freed (and rowptr in the ELL layout)
   uint64_t version = next_version();  // unique per object and bumped when its products' kernels change
 };
@@ -492,6 +497,13 @@ static int32_t lds_cap_for(int64_t max_block_nnz) {
 static bool dv_default() {
   const char* e = getenv("MSPLIT_MAT_STORAGE");
   return !(e && strcmp(e, "csr") == 0);
+}
+
+static void rv_free(msp_mat* A) {
+  if (A->rv_val) (void)hipFree(A->rv_val);
+  A->rv_val = nullptr;
+  A->rv_stride = 0;
+  A->rv_on = false;
 }
 
 static void dv_free(msp_mat* A) {
@@ -687,6 +699,70 @@ static bool box_dictionary(int32_t nrows, std::vector<int32_t>& dd, std::vector<
   return true;
 }
 
+// The STENCIL storage of an assembled square CSR that no dictionary covers (variable coefficients): when the
+// distinct column offsets of its rows are a 3D box stencil's seven {-P, -nx, -1, 0, 1, nx, P} (box_dictionary on
+// the offsets) and the chunk-tile march takes the box, every row's entries go to per-neighbour value arrays
+// (rv_val[e * stride + r], 0.0 where absent) with one presence byte per row, and the device checks that no row
+// holds a neighbour across a line or plane edge (k_march_check); a failed check keeps CSR.  The products add
+// the present entries in column order from 0.0, as the CSR kernels: bitwise the same.
+static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, const double* val) {
+  msp_ctx* c = A->ctx;
+  const int32_t n = A->nrows;
+  if (A->compressed || A->matfree || n == 0 || A->ncols != n || A->dv_on) return MSP_SUCCESS;
+  std::vector<int32_t> dd;
+  for (int32_t r = 0; r < n; ++r)
+    for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+      const int32_t d = col[k] - r;
+      if (std::find(dd.begin(), dd.end(), d) == dd.end()) {
+        if (dd.size() == 7) return MSP_SUCCESS;  // more than a 7-point stencil's offsets
+        dd.push_back(d);
+      }
+    }
+  std::vector<double> dummy(dd.size(), 0.0);
+  int32_t nx = 0, ny = 0, nz = 0;
+  int d2 = 0;
+  if (!box_dictionary(n, dd, dummy, &nx, &ny, &nz, &d2) || d2 || !msk_march_chunk_fits(nx, ny, 0)) return MSP_SUCCESS;
+  const int64_t stride = ((int64_t)n + 511) / 512 * 512;
+  std::vector<uint8_t> mask((size_t)n + 16, 0);
+  std::vector<double> rv((size_t)7 * stride, 0.0);
+  for (int32_t r = 0; r < n; ++r)
+    for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+      const int e = (int)(std::find(dd.begin(), dd.end(), col[k] - r) - dd.begin());  // dd is in column order now
+      mask[r] |= (uint8_t)(1u << e);
+      rv[(size_t)e * stride + r] = val[k];
+    }
+  if (mspi_big_alloc((void**)&A->march_mask, (size_t)n + 16) != (int)hipSuccess ||
+      mspi_big_alloc((void**)&A->rv_val, (size_t)7 * stride * sizeof(double)) != (int)hipSuccess) {
+    rv_free(A);
+    if (A->march_mask) (void)hipFree(A->march_mask);
+    A->march_mask = nullptr;
+    mspi_set_error(MSP_ERR_MEM, "hipMalloc of the stencil storage failed");
+    return MSP_ERR_MEM;
+  }
+  HIPCHK(hipMemcpyAsync(A->march_mask, mask.data(), (size_t)n + 16, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(A->rv_val, rv.data(), (size_t)7 * stride * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  int* fail = reinterpret_cast<int*>(mspi_dev_scratch(c));
+  HIPCHK(hipMemsetAsync(fail, 0, sizeof(int), c->stream));
+  KCHK(msk_march_check(n, nx, ny, 0, A->march_mask, fail, c->stream));
+  int hfail = 0;
+  HIPCHK(hipMemcpyAsync(&hfail, fail, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));  // also: the host arrays above are read before they go
+  if (hfail) {
+    rv_free(A);
+    (void)hipFree(A->march_mask);
+    A->march_mask = nullptr;
+    return MSP_SUCCESS;
+  }
+  A->rv_stride = stride;
+  A->march_nx = nx;
+  A->march_ny = ny;
+  A->march_nz = nz;
+  A->march_d2 = 0;
+  A->march_halo = 0;
+  A->rv_on = dv_default();
+  return MSP_SUCCESS;
+}
+
 static int mat_alloc(msp_ctx* c, msp_mat* A, int64_t nptr, int64_t nnz) {
   HIPCHK((hipError_t)mspi_big_alloc((void**)&A->rowptr, (size_t)nptr * sizeof(int32_t)));
   HIPCHK((hipError_t)mspi_big_alloc((void**)&A->col, (size_t)(nnz + 4) * sizeof(int32_t)));
@@ -766,6 +842,11 @@ extern "C" int msp_mat_create_csr(msp_ctx* c, int32_t nrows, int32_t ncols, cons
       return rc;
     }
     if (box && (rc = march_attach(A, bx, by, bz, d2, true))) {
+      msp_mat_destroy(&A);
+      return rc;
+    }
+    // no dictionary covers it (variable coefficients): the stencil storage, if it is a box stencil's shape
+    if (!A->dv_on && A->ndict == 0 && (rc = rv_attach(A, rowptr, col, val))) {
       msp_mat_destroy(&A);
       return rc;
     }
@@ -959,6 +1040,7 @@ extern "C" int msp_mat_destroy(msp_mat** pA) {
   if (A->col) (void)hipFree(A->col);
   if (A->val) (void)hipFree(A->val);
   if (A->row_ids) (void)hipFree(A->row_ids);
+  rv_free(A);
   dv_free(A);
   msp_ctx* c = A->ctx;
   delete A;
@@ -1021,15 +1103,24 @@ static double march_bytes(const msp_mat* A, bool resid, bool vout) {
   return rows + 8.0 * (double)A->ncols + 8.0 * rows + (resid ? 8.0 * rows : 0.0) + (vout ? 8.0 * rows : 0.0);
 }
 
+// STENCIL storage: the presence byte and the seven values of every row, x once, y written (b read, vout written)
+static double rv_bytes(const msp_mat* A, bool resid, bool vout) {
+  return 56.0 * (double)A->nrows + march_bytes(A, resid, vout);
+}
+
 extern "C" int msp_mat_set_storage(msp_mat* A, int storage) {
   ARGCHK(A, MSP_ERR_ARG_NULL, "mat is NULL");
-  ARGCHK(storage == MSP_STORAGE_CSR || storage == MSP_STORAGE_DV, MSP_ERR_ARG_OUTOFRANGE, "unknown storage %d",
-         storage);
+  ARGCHK(storage == MSP_STORAGE_CSR || storage == MSP_STORAGE_DV || storage == MSP_STORAGE_STENCIL,
+         MSP_ERR_ARG_OUTOFRANGE, "unknown storage %d", storage);
   ARGCHK(!(A->csr_released && storage == MSP_STORAGE_CSR), MSP_ERR_SUP, "CSR storage released (msp_mat_release_csr)");
   if (storage == MSP_STORAGE_DV)
     ARGCHK(A->ndict > 0, MSP_ERR_SUP, "matrix has no DV storage (more than 256 (col - row, value) pairs, a row "
            "longer than 255, or not an assembled square-block CSR)");
+  if (storage == MSP_STORAGE_STENCIL)
+    ARGCHK(A->rv_val, MSP_ERR_SUP, "matrix has no stencil storage (not a 3D box stencil the chunk march takes, or "
+           "a dictionary covers it)");
   A->dv_on = storage == MSP_STORAGE_DV;
+  A->rv_on = storage == MSP_STORAGE_STENCIL;
   A->version++;
   return MSP_SUCCESS;
 }
@@ -1200,7 +1291,10 @@ extern "C" int mspi_mat_spmm_dv(msp_mat* A, const double* S, int64_t lds, int nc
 
 extern "C" int msp_mat_get_storage(const msp_mat* A, int* storage, int* ndict) {
   ARGCHK(A && storage, MSP_ERR_ARG_NULL, "NULL argument");
-  *storage = A->matfree ? MSP_STORAGE_NONE : (A->dv_on ? MSP_STORAGE_DV : MSP_STORAGE_CSR);
+  *storage = A->matfree ? MSP_STORAGE_NONE
+             : A->dv_on  ? MSP_STORAGE_DV
+             : A->rv_on  ? MSP_STORAGE_STENCIL
+                         : MSP_STORAGE_CSR;
   if (ndict) *ndict = A->ndict;
   return MSP_SUCCESS;
 }
@@ -1209,6 +1303,7 @@ extern "C" int msp_mat_get_spmv_kernel(const msp_mat* A, const char** name) {
   ARGCHK(A && name, MSP_ERR_ARG_NULL, "NULL argument");
   if (A->matfree) *name = "k_stencil_spmv";
   else if (A->compressed) *name = "k_spmv_rows";
+  else if (A->rv_on) *name = "k_box_march_chunk_rv";
   else if (A->dv_on && (box_march(A) || box_march_halo(A))) *name = "k_spmv_box_march";
   else if (A->dv_on) *name = A->dv_w ? "k_spmv_ell" : "k_spmv_dv";
   else *name = A->lds_cap > 0 ? "k_spmv_lds8" : "k_spmv_csr";
@@ -1232,6 +1327,12 @@ static int spmv_impl(msp_mat* A, const double* b, const double* x, double* y, bo
       KCHK(msk_blas1(MSK_SET, y, nullptr, nullptr, 0.0, A->nrows, c->stream));
     }
     KCHK(msk_spmv_rows(A->nlisted, A->row_ids, A->rowptr, A->col, A->val, x, b, y, resid ? 1 : 0, c->stream));
+    return MSP_SUCCESS;
+  }
+  if (A->rv_on) {
+    KTimer kt(c, MSP_KERNEL_SPMV, rv_bytes(A, resid, false));
+    KCHK(msk_box_march_chunk_rv(A->march_nx, A->march_ny, A->march_nz, A->march_mask, A->rv_val, A->rv_stride, x, b, y,
+                                resid ? MSK_SPMV_RESID : MSK_SPMV_MULT, nullptr, nullptr, nullptr, c->stream));
     return MSP_SUCCESS;
   }
   if (A->dv_on) {
@@ -1280,6 +1381,12 @@ extern "C" int mspi_spmv_scaled(msp_mat* A, const double* x, const double* sdev,
                           MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
     return MSP_SUCCESS;
   }
+  if (A->rv_on) {
+    KTimer kt(c, MSP_KERNEL_SPMV, rv_bytes(A, false, vout != nullptr));
+    KCHK(msk_box_march_chunk_rv(A->march_nx, A->march_ny, A->march_nz, A->march_mask, A->rv_val, A->rv_stride, x,
+                                nullptr, y, MSK_SPMV_SCALED, sdev, vout, stop, c->stream));
+    return MSP_SUCCESS;
+  }
   if (A->dv_on) {
     const bool bm = box_march(A);
     KTimer kt(c, MSP_KERNEL_SPMV, bm ? march_bytes(A, false, vout != nullptr) : dv_bytes(A, false, vout != nullptr));
@@ -1306,6 +1413,27 @@ extern "C" int mspi_spmv_mdot(msp_mat* A, const double* x, const double* sdev, d
   msp_ctx* c = A->ctx;
   const int64_t n = A->nrows;
   const int64_t nch = nchunks_of(n);
+  if (c->reduce == MSP_REDUCE_DBR && A->rv_on && y && nv >= 1 && nv <= MSPI_MAX_GROUP && nch > 0 &&
+      !(msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT_OFF)) {
+    // the stencil storage: the chunk-tile march with the rows' values, W stored (the MAXPY reads it), the dots
+    // from the registers; bytes as the march's plus the 56 value bytes per row
+    int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);
+    if (rc) return rc;
+    {
+      KTimer kt(c, MSP_KERNEL_SPMVDOT, rv_bytes(A, false, false) + 8.0 * (double)n * nv);
+      Vecs vg = {};
+      vg.base = base;
+      vg.stride = stride;
+      vg.scale = scale;
+      const int64_t P = (int64_t)A->march_nx * A->march_ny;
+      int self = 0;
+      KCHK(msk_box_spmv_mdot_rv(A->march_nx, P, n, 0, A->march_mask, nullptr, A->rv_val, A->rv_stride, x, sdev, y,
+                                &vg, nv, c->partial, nch, stop, &self, c->stream));
+      if (self) kt.set_bytes(rv_bytes(A, false, false) + 8.0 * (double)n * (nv - 1));
+    }
+    KCHK(msk_dot_stage2(c->partial, nch, nv, out_dev, stop, c->stream));
+    return MSP_SUCCESS;
+  }
   if (c->reduce == MSP_REDUCE_DBR && A->dv_on && box_march(A) && A->march_nx <= 2048 && nv >= 1 &&
       nv <= MSPI_MAX_GROUP && nch > 0 && !(msk_get_tuning() & MSK_TUNE_GM_BOX_MDOT_OFF)) {
     int rc = ensure_partial(c, nch * MSPI_MAX_GROUP);

@@ -339,10 +339,11 @@ class Mat:
         call("msp_mat_get_csr", self.h, _ip(rp), _ip(cl), _dp(vl))
         return rp, cl[: self.nnz], vl[: self.nnz]
 
-    STORAGE = {"none": -1, "csr": 0, "dv": 1}
+    STORAGE = {"none": -1, "csr": 0, "dv": 1, "stencil": 2}
 
     def set_storage(self, storage: str):
-        """Entry storage in HBM (msp_mat_set_storage): 'csr' or 'dv' (one byte per entry); same products."""
+        """Entry storage in HBM (msp_mat_set_storage): 'csr', 'dv' (one byte per entry) or 'stencil' (a box
+        stencil's presence byte and per-row values); same products."""
         call("msp_mat_set_storage", self.h, self.STORAGE[storage])
 
     def get_storage(self) -> str:

@@ -64,19 +64,23 @@ def _splitmix64(x):
     return z ^ (z >> np.uint64(31))
 
 
-def heterogeneous_poisson3d(n: int, seed: int = 20251121):
-    """An assembled AIJ operator that is not a box stencil: -div(kappa grad u) on the n^3 grid, 7 points, in
-    the reference's numbering (x fastest, as poisson3DMatrix, utils.c:30-121).  kappa per cell is
-    1 + (h mod 1000) / 1000, h a splitmix64 hash of (cell index + seed); the face between two cells weighs
-    2 ka kb / (ka + kb), a boundary face the cell's own kappa (Dirichlet), the diagonal is the sum of the six
-    face weights in the order z-, y-, x-, x+, y+, z+, the neighbours -weight.  Only IEEE + - * / (no libm), so
-    the arrays are the same bits on every machine.  Almost every row holds its own values, so no (column - row,
-    value) dictionary fits: the matrix keeps CSR storage -- the general AIJ a PETSc user assembles
-    (bench.py non_stencil_aij).  Returns (rowptr int32, col int32, val float64), columns ascending."""
-    N = n * n * n
+def heterogeneous_poisson3d(nx: int, ny: int | None = None, nz: int | None = None, seed: int = 20251121):
+    """An assembled AIJ operator with variable coefficients: -div(kappa grad u) on the nx x ny x nz grid (ny, nz
+    default to nx), 7 points, in the reference's numbering (x fastest, as poisson3DMatrix, utils.c:30-121).
+    kappa per cell is 1 + (h mod 1000) / 1000, h a splitmix64 hash of (cell index + seed); the face between two
+    cells weighs 2 ka kb / (ka + kb), a boundary face the cell's own kappa (Dirichlet), the diagonal is the sum
+    of the six face weights in the order z-, y-, x-, x+, y+, z+, the neighbours -weight.  Only IEEE + - * / (no
+    libm), so the arrays are the same bits on every machine.  Almost every row holds its own values, so no
+    (column - row, value) dictionary fits: the library stores it as the box stencil it is (MSP_STORAGE_STENCIL,
+    per-row values) when its planes hold whole 4096-row chunks, else as CSR -- the general AIJ a PETSc user
+    assembles (bench.py non_stencil_aij).  Returns (rowptr int32, col int32, val float64), columns ascending."""
+    ny = nx if ny is None else ny
+    nz = nx if nz is None else nz
+    P = nx * ny
+    N = P * nz
     with np.errstate(over="ignore"):
         h = _splitmix64(np.arange(N, dtype=np.uint64) + np.uint64(seed))
-    kap = (1.0 + (h % np.uint64(1000)).astype(np.float64) * 0.001).reshape(n, n, n)   # [k, j, i]
+    kap = (1.0 + (h % np.uint64(1000)).astype(np.float64) * 0.001).reshape(nz, ny, nx)   # [k, j, i]
 
     def face(axis, side):
         nb = np.roll(kap, -side, axis=axis)
@@ -85,15 +89,14 @@ def heterogeneous_poisson3d(n: int, seed: int = 20251121):
         edge[axis] = -1 if side > 0 else 0
         w[tuple(edge)] = kap[tuple(edge)]                # boundary face: Dirichlet, the cell's own kappa
         return w.ravel()
-    P = n * n
     wzm, wym, wxm = face(0, -1), face(1, -1), face(2, -1)
     wxp, wyp, wzp = face(2, 1), face(1, 1), face(0, 1)
     diag = ((((wzm + wym) + wxm) + wxp) + wyp) + wzp
     g = np.arange(N, dtype=np.int64)
-    i, j, k = g % n, (g // n) % n, g // P
-    cols = np.stack([g - P, g - n, g - 1, g, g + 1, g + n, g + P], axis=1)
+    i, j, k = g % nx, (g // nx) % ny, g // P
+    cols = np.stack([g - P, g - nx, g - 1, g, g + 1, g + nx, g + P], axis=1)
     vals = np.stack([-wzm, -wym, -wxm, diag, -wxp, -wyp, -wzp], axis=1)
-    keep = np.stack([k > 0, j > 0, i > 0, np.ones(N, bool), i < n - 1, j < n - 1, k < n - 1], axis=1)
+    keep = np.stack([k > 0, j > 0, i > 0, np.ones(N, bool), i < nx - 1, j < ny - 1, k < nz - 1], axis=1)
     rowptr = np.concatenate([[0], np.cumsum(keep.sum(axis=1))]).astype(np.int32)
     return rowptr, cols[keep].astype(np.int32), vals[keep]
 

@@ -700,9 +700,10 @@ def test_box_with_coupling_planes_takes_the_chunk_march(ctx, oracle, halo, shape
 @pytest.mark.parametrize("n", [24, 48])
 def test_non_stencil_aij_keeps_csr_and_equals_oracle(ctx, oracle, n, flags):
     """bench.py's non_stencil_aij operator (utils.heterogeneous_poisson3d: a per-cell kappa, so almost every row
-    holds its own values and no dictionary fits) keeps CSR storage, and MatMult, MatResidual and GMRES(30) through
-    msp_mat_create_csr equal the oracle bit for bit, with the default step (k_spmv_lds8 + the CGS kernels) and with
-    the MatMult fused with the VecMDot (MSPLIT_TUNING 2048, k_spmv_mdot)."""
+    holds its own values and no dictionary fits) on boxes whose planes do not hold whole 4096-row chunks keeps CSR
+    storage, and MatMult, MatResidual and GMRES(30) through msp_mat_create_csr equal the oracle bit for bit, with
+    the default step (k_spmv_lds8 + the CGS kernels) and with the MatMult fused with the VecMDot (MSPLIT_TUNING
+    2048, k_spmv_mdot)."""
     from medane_tchakorom_ufc_thesis_repository_amd.utils import heterogeneous_poisson3d
     from test_gpu_kernels import tuning
     rp, col, val = heterogeneous_poisson3d(n)
@@ -713,3 +714,57 @@ def test_non_stencil_aij_keeps_csr_and_equals_oracle(ctx, oracle, n, flags):
     _products(ctx, A, O, np.random.default_rng(SEED))
     with tuning(flags):
         _gmres_vs_oracle(ctx, oracle, A, O, O.mult(np.ones(N)), max_it=75)
+
+
+@pytest.mark.parametrize("flags", [0, BOX_SEPARATE])
+@pytest.mark.parametrize("shape", [(64, 64, 16), (128, 32, 9), (64, 64, 2), (2048, 2, 3)])
+def test_variable_coefficient_box_takes_the_stencil_storage(ctx, oracle, shape, flags):
+    """A box stencil with variable coefficients (utils.heterogeneous_poisson3d) whose planes hold whole 4096-row
+    chunks: no dictionary fits, so msp_mat_create_csr gives it the STENCIL storage (a presence byte and the row's
+    seven values per row, k_box_march_chunk_rv; in GMRES the MatMult fused with the VecMDot, W stored).  MatMult,
+    MatResidual and GMRES(30) over 3 restart cycles equal the oracle bit for bit -- with the fused step (0) and
+    with the separate MatMult (BOX_SEPARATE) -- and switching to CSR gives the same products."""
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import heterogeneous_poisson3d
+    from test_gpu_kernels import tuning
+    nx, ny, nz = shape
+    rp, col, val = heterogeneous_poisson3d(nx, ny, nz)
+    N = nx * ny * nz
+    A = Mat.from_csr(ctx, N, N, rp, col, val)
+    assert A.get_storage() == "stencil" and A.spmv_kernel() == "k_box_march_chunk_rv"
+    O = oracle.Mat.from_arrays(N, N, rp, col, val)
+    y, res = _products(ctx, A, O, np.random.default_rng(SEED))
+    with tuning(flags):
+        _gmres_vs_oracle(ctx, oracle, A, O, O.mult(np.ones(N)), max_it=75)
+    A.set_storage("csr")
+    yc, rc = _products(ctx, A, O, np.random.default_rng(SEED))
+    assert np.array_equal(y, yc) and np.array_equal(res, rc)
+    A.set_storage("stencil")
+    assert A.get_storage() == "stencil"
+
+
+@pytest.mark.parametrize("defect", ["dropped", "wrapped", "eighth_offset", "odd_nx"])
+def test_stencil_storage_edge_cases(ctx, oracle, defect):
+    """Entries left out of some rows still take the STENCIL storage (the presence bytes say which neighbours a row
+    holds) and equal the oracle; a row holding a neighbour across a line edge (x-1 at i = 0), an eighth column
+    offset, or a box whose plane rows the chunk march cannot tile (odd nx) keep CSR, still bitwise the oracle."""
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import heterogeneous_poisson3d
+    nx, ny, nz = (64, 64, 6) if defect != "odd_nx" else (3, 4096, 2)
+    rp, col, val = heterogeneous_poisson3d(nx, ny, nz)
+    N = nx * ny * nz
+    rows = np.repeat(np.arange(N), np.diff(rp))
+    if defect == "dropped":
+        keep = (np.random.default_rng(SEED).random(col.size) > 0.2) | (rows == col)
+        rows, col, val = rows[keep], col[keep], val[keep]
+    elif defect in ("wrapped", "eighth_offset"):
+        r0 = 3 * nx * ny + 5 * nx                          # i = 0 of an interior line
+        c_new = r0 - 1 if defect == "wrapped" else r0 + 2
+        rows, col, val = np.append(rows, r0), np.append(col, c_new), np.append(val, -0.25)
+        order = np.lexsort((col, rows))
+        rows, col, val = rows[order], col[order], val[order]
+    rp = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=N))]).astype(np.int32)
+    col = col.astype(np.int32)
+    A = Mat.from_csr(ctx, N, N, rp, col, val)
+    O = oracle.Mat.from_arrays(N, N, rp, col, val)
+    assert A.get_storage() == ("stencil" if defect == "dropped" else "csr")
+    _products(ctx, A, O, np.random.default_rng(SEED))
+    _gmres_vs_oracle(ctx, oracle, A, O, O.mult(np.random.default_rng(SEED).uniform(-1, 1, N)), max_it=40)
