@@ -477,12 +477,13 @@ NON_STENCIL_GOLDEN = os.path.join(ROOT, "tests", "golden", "non_stencil_aij.json
 
 
 def non_stencil_step(ctx, args):
-    """The GMRES step on an assembled AIJ that is not a box stencil: utils.heterogeneous_poisson3d(256)
-    (-div(kappa grad u), 7 points, a per-cell kappa: every row holds its own values, so no dictionary fits and
-    the matrix keeps CSR storage -- the general operator a PETSc user hands over), as host CSR arrays through
-    msp_mat_create_csr; b = A*1, x0 = 0, GMRES(30), 300 iterations.  Timed twice: the default step (CSR MatMult,
-    then the CGS kernels) and the step with the MatMult fused with the VecMDot (k_spmv_mdot: W dotted from
-    registers, not re-read; MSK_TUNE_GM_SPMV_MDOT).  Each is checked against the committed oracle record
+    """The GMRES step on an assembled AIJ no dictionary covers: utils.heterogeneous_poisson3d(256), the 7-point
+    -div(kappa grad u) with a per-cell kappa (every row holds its own values), as host CSR arrays through
+    msp_mat_create_csr -- the general operator a PETSc user hands over; b = A*1, x0 = 0, GMRES(30), 300
+    iterations.  Timed three ways on the same matrix: the storage the library picks (STENCIL: the box stencil's
+    presence byte and each row's seven values, the chunk-tile march, the MatMult fused with the VecMDot with W
+    stored), CSR storage (k_spmv_lds8, then the CGS kernels), and CSR with the MatMult fused with the VecMDot
+    (k_spmv_mdot, MSK_TUNE_GM_SPMV_MDOT).  Each is checked against the committed oracle record
     (tests/golden/non_stencil_aij.json, written by tests/golden/make_non_stencil.py)."""
     import torch
     from medane_tchakorom_ufc_thesis_repository_amd import _lib
@@ -492,7 +493,9 @@ def non_stencil_step(ctx, args):
     ref = json.load(open(NON_STENCIL_GOLDEN)) if os.path.exists(NON_STENCIL_GOLDEN) else None
     rp, col, val = heterogeneous_poisson3d(n)
     N = n ** 3
+    t0 = time.perf_counter()
     A = Mat.from_csr(ctx, N, N, rp, col, val)
+    create_s = time.perf_counter() - t0
     nnz = int(rp[-1])
     del rp, col, val
     ones = Vec(ctx, N)
@@ -508,11 +511,15 @@ def non_stencil_step(ctx, args):
     L = _lib.load()
     L.msk_set_tuning.argtypes = [ctypes.c_int]
     L.msk_set_tuning.restype = None
+    picked = A.get_storage()
     out = {"operator": "utils.heterogeneous_poisson3d(256): 7-point -div(kappa grad u), per-cell kappa, host CSR "
-                       "through msp_mat_create_csr", "rows": N, "nnz": nnz, "matrix_storage": A.get_storage(),
-           "spmv_kernel": A.spmv_kernel(), "reference": "tests/golden/non_stencil_aij.json['dbr']"}
+                       "through msp_mat_create_csr", "rows": N, "nnz": nnz, "matrix_storage": picked,
+           "spmv_kernel": A.spmv_kernel(), "create_s": create_s,
+           "reference": "tests/golden/non_stencil_aij.json['dbr']"}
     steps = max(1, min(args.steps, 3))
-    for name, flags in (("default", 0), ("fused_matmult_mdot", 2048)):
+    variants = [("default", picked, 0), ("csr_storage", "csr", 0), ("csr_fused_matmult_mdot", "csr", 2048)]
+    for name, storage, flags in variants:
+        A.set_storage(storage)
         L.msk_set_tuning(flags)
         try:
             ksp.solve(b, x)
@@ -527,9 +534,11 @@ def non_stencil_step(ctx, args):
             ok, bad = check_step(ksp, x, ref["dbr"]) if ref else (None, ["no record"])
         finally:
             L.msk_set_tuning(0)
-        out[name] = {"value": float(N) * its / dt, "unit": "DOF-updates/s", "ms_per_step": 1e3 * dt / steps,
-                     "steps": steps, "verified": ok, "mismatch": bad}
-    out["verified"] = all(out[k]["verified"] for k in ("default", "fused_matmult_mdot"))
+        out[name] = {"matrix_storage": storage, "value": float(N) * its / dt, "unit": "DOF-updates/s",
+                     "ms_per_step": 1e3 * dt / steps, "steps": steps, "verified": ok, "mismatch": bad}
+    A.set_storage(picked)
+    out["value"] = out["default"]["value"]
+    out["verified"] = all(out[k]["verified"] for k, _, _ in variants)
     A.destroy()
     return out
 
