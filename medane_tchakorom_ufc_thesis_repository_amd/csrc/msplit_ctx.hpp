@@ -58,6 +58,8 @@ struct msp_ctx {
   double* hscratch = nullptr;  // pinned host scalars
   double* partial = nullptr;   // DBR stage-1 partials
   int64_t partial_cap = 0;     // doubles
+  void* seqbuf = nullptr;      // MSP_REDUCE_SEQ's transducers and guesses (msplit_seq.hip)
+  int64_t seqbuf_cap = 0;      // bytes
   uint64_t epoch = 0;          // bumped when a buffer captured graphs point at is reallocated
   int reduce = MSP_REDUCE_DBR;  // MSP_REDUCE_SEQ: PETSc's sequential order (msplit_seq.hip)
   bool timing = false;
@@ -109,6 +111,10 @@ static inline int ensure_partial(msp_ctx* c, int64_t need) {
   c->epoch++;
   return MSP_SUCCESS;
 }
+
+// MSP_REDUCE_SEQ's stage 1 (msplit_seq.hip): the sequential sums in the DBR partial layout
+int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial,
+                    int64_t nchunks, const int* stop);
 
 static inline int64_t nchunks_of(int64_t n) { return (n + MSK_DBR_CHUNK - 1) / MSK_DBR_CHUNK; }
 

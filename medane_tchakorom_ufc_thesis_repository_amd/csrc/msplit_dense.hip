@@ -467,7 +467,7 @@ extern "C" int mspi_dense_gemv(msp_ctx* c, const double* A, int64_t lda, int nc,
   KCHK((int)hipGetLastError());
   if (norm && mspi_reduce_seq(c)) {  // ||y||^2 in PETSc's order (msplit_seq.hip)
     Vecs v = {};
-    KCHK(msk_seq_stage1(y, &v, 1, n, 1, partial, nch, stop, c->stream));
+    KCHK(mspi_seq_stage1(c, y, &v, 1, n, 1, partial, nch, stop));
   }
   if (norm) KCHK(msk_dot_stage2(partial, nch, 1, sumsq_dev, stop, c->stream));
   return MSP_SUCCESS;
@@ -526,7 +526,7 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
       Vecs v = {};
       v.base = Ag;
       v.stride = lda;
-      KCHK(msk_seq_stage1(sc_dev ? wout : win, &v, g, n, 0, partial, nch, stop, c->stream));
+      KCHK(mspi_seq_stage1(c, sc_dev ? wout : win, &v, g, n, 0, partial, nch, stop));
     }
     KCHK(msk_dot_stage2(partial, nch, g, out_dev + g0, stop, c->stream));
   }
@@ -546,7 +546,7 @@ extern "C" int mspi_dense_colsumsq(msp_ctx* c, const double* A, int64_t lda, int
   for (int j = 0; j < nc; ++j) {
     Vecs v = {};
     v.p[0] = A + (int64_t)j * lda;
-    if (mspi_reduce_seq(c)) KCHK(msk_seq_stage1(v.p[0], &v, 1, n, 1, partial, nch, nullptr, c->stream));
+    if (mspi_reduce_seq(c)) KCHK(mspi_seq_stage1(c, v.p[0], &v, 1, n, 1, partial, nch, nullptr));
     else KCHK(msk_dot_stage1(v.p[0], &v, 1, n, partial, nch, 1, nullptr, c->stream));
     KCHK(msk_dot_stage2(partial, nch, 1, out_dev + j, nullptr, c->stream));
   }
@@ -594,10 +594,10 @@ extern "C" int msp_dense_gram(const msp_dense* R, const msp_vec* b, msp_dense* G
         v.stride = R->lda;
         const double* w = j < s ? R->d + (int64_t)j * R->lda : b->d;
         double* dst = out + j * (j + 1) / 2;
-        rc = msk_seq_stage1(w, &v, std::min(j + 1, s), n, 0, dst, 1, nullptr, c->stream);
+        rc = mspi_seq_stage1(c, w, &v, std::min(j + 1, s), n, 0, dst, 1, nullptr);
         if (!rc && j == s) {
           Vecs vb = {};
-          rc = msk_seq_stage1(b->d, &vb, 1, n, 1, dst + s, 1, nullptr, c->stream);
+          rc = mspi_seq_stage1(c, b->d, &vb, 1, n, 1, dst + s, 1, nullptr);
         }
       }
     } else {

@@ -82,6 +82,7 @@ static void ctx_free(msp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->partial) (void)hipFree(c->partial);
+  if (c->seqbuf) (void)hipFree(c->seqbuf);
   if (c->dscratch) (void)hipFree(c->dscratch);
   if (c->hscratch) (void)hipHostFree(c->hscratch);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -227,7 +228,7 @@ extern "C" int mspi_d2h_sync(msp_ctx* c, void* host, const void* dev, size_t byt
 // written in the DBR partial layout).
 static int stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, int64_t nch,
                   const int* stop) {
-  if (c->reduce == MSP_REDUCE_SEQ) return msk_seq_stage1(w, V, nv, n, self, c->partial, nch, stop, c->stream);
+  if (c->reduce == MSP_REDUCE_SEQ) return mspi_seq_stage1(c, w, V, nv, n, self, c->partial, nch, stop);
   return msk_dot_stage1(w, V, nv, n, c->partial, nch, self, stop, c->stream);
 }
 

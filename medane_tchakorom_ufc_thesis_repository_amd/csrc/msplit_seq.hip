@@ -15,17 +15,48 @@
 // and the reference's outer LSQR runs on one rank over the whole of R
 // (SMSM-global.c:136, comm_jacobi_block with one process per block), so its
 // sums run across the row blocks in block order.  oracle/oracle.c's
-// ORC_REDUCE_SEQ restates exactly this.
+// ORC_REDUCE_SEQ restates exactly this: s = fl(s + p_i), s_0 = +0.0, in index
+// order, p_i = x_i * (y_i * sy) (or x_i * x_i).
 //
-// A sequential sum cannot be parallelised without changing its roundings, so
-// this is a parity mode, not a fast path: the products are formed by the
-// whole workgroup into LDS (the loads stay coalesced, and each product is the
-// same IEEE multiplication the DBR kernels do), and one lane adds them in
-// order while the other waves form the next tile.  Results go out in the DBR
-// partial layout -- partial[v*nchunks + 0] = the sum, the other chunks +0.0 --
-// so the unchanged stage 2 (or the fused GMRES norm/Hessenberg update) folds
-// them to exactly the sequential sum: x + (+0.0) == x for every x a sum of
-// products starting at +0.0 can produce.
+// Results go out in the DBR partial layout -- partial[v*nchunks + 0] = the
+// sum, the other chunks +0.0 -- so the unchanged stage 2 (or the fused GMRES
+// norm/Hessenberg update) folds them to exactly the sequential sum: x + (+0.0)
+// == x for every x a sum of products starting at +0.0 can produce.
+//
+// Two engines compute the same bits.
+//
+// The serial engine (k_seq_stage1; MSPLIT_SEQ_ENGINE=serial): the products are
+// formed by the whole workgroup into LDS, and one lane adds them in order
+// while the other waves form the next tile.  16.7 M terms cost ~56 ms: one
+// dependent f64 add per term.
+//
+// The exact parallel engine (default, mspi_seq_stage1).  While the running
+// sum s stays inside one binade [2^e, 2^(e+1)) of one sign, every double it can
+// take is M * u, u = 2^(e-52), M an integer in [2^52, 2^53), and fl(s + p)
+// = (M + inc) * u with inc = floor(p/u) + [frac(p/u) > 1/2], a tie (frac ==
+// 1/2) rounding to the even M.  So a run of terms acts on M as an integer
+// translation whose only dependence on M is M's parity (through ties; after a
+// tie M is even whatever it was), valid while every exact sum stays >= 2^e and
+// every rounded one < 2^(e+1).  A run's "transducer" is therefore, per input
+// parity, the offset D, the lowest exact sum LO and the highest result HI
+// (all in units of u), and transducers of one binade compose associatively.
+// Three passes build and apply them:
+//   1. approximate chunk sums (the DBR stage 1) and their exclusive prefix --
+//      a guess of s at each 4096-term segment, used only to pick the binade;
+//   2. k_seqx_trans: per 64-term sub-segment the transducer in the binade its
+//      guessed start lies in (integer arithmetic on the terms' bits, exact),
+//      and per segment their composition (BAD where the subs disagree);
+//   3. k_seqx_walk, one wave per sum: from s = +0.0, apply up to 64 segment
+//      transducers at once (an ordered wave scan, checked against the actual
+//      M: LO/HI bound the whole run); where a segment does not apply, its sub
+//      transducers; where a sub does not apply, its terms, 64 at a time
+//      (integer prefix of inc, the same checks), and the one term that leaves
+//      the binade, ties, zeros, subnormals and non-finite values by the f64
+//      add itself.
+// Every step either is the f64 add or provably equals it, so the result is the
+// sequential sum bit for bit whatever the guesses were; the guesses only
+// decide how often the walk descends.  GMRES's dots at 256^3 leave their
+// binade in at most a few hundred of 4096 segments.
 #include <hip/hip_runtime.h>
 
 #include "msplit_ctx.hpp"
@@ -115,6 +146,452 @@ __global__ __launch_bounds__(kT) void k_seq_chain(mspi_seq_segs sg, int ncol, in
   }
 }
 
+
+// ------------------------------------------------------------ exact parallel engine
+constexpr int kSeg = MSK_DBR_CHUNK;  // one segment = one DBR chunk (its partial is the guess)
+constexpr int kSub = 64;             // terms per sub-segment (one per lane in the walk)
+constexpr int kSubs = kSeg / kSub;
+constexpr int kPer = kSeg / kT;      // contiguous terms per thread in k_seqx_trans
+constexpr int64_t kM0 = int64_t(1) << 52, kM1 = int64_t(1) << 53;
+constexpr int64_t kLim = int64_t(1) << 56, kBig = int64_t(1) << 60;
+constexpr uint64_t kFrac = (uint64_t(1) << 52) - 1;
+constexpr uint32_t F_NEG = 1, F_BAD = 2, F_ZERO = 4, F_NZERO = 8;
+
+// A run of terms as a map of the state M (s = +-M * 2^(e-52)): for input parity pi, M -> M + d[pi], valid iff
+// M + lo[pi] >= 2^52 (every exact sum >= 2^e) and M + hi[pi] < 2^53 (every result < 2^(e+1)).  F_ZERO: every term
+// is +-0 (identity; F_NZERO: all -0.0, so a -0.0 state stays -0.0); F_BAD: not a translation of one binade.
+struct alignas(16) Tr {  // scalar fields, no arrays: a select between two of them must not become a private index
+  int64_t d0, d1, lo0, lo1, hi0, hi1;
+  int32_t e;
+  uint32_t fl;
+  int64_t pad;
+};
+static_assert(sizeof(Tr) == 64, "Tr is one 64-byte record");
+
+__device__ __forceinline__ Tr tr_ident() {
+  Tr t;
+  t.d0 = t.d1 = 0;
+  t.lo0 = t.lo1 = kBig;
+  t.hi0 = t.hi1 = -kBig;
+  t.e = 0;
+  t.fl = F_ZERO | F_NZERO;
+  t.pad = 0;
+  return t;
+}
+
+__device__ __forceinline__ Tr tr_bad() {
+  Tr t = tr_ident();
+  t.fl = F_BAD;
+  return t;
+}
+
+// field by field (a select of whole records becomes a private-memory copy)
+__device__ __forceinline__ Tr tr_sel(bool c, const Tr& a, const Tr& b) {
+  Tr r;
+  r.d0 = c ? a.d0 : b.d0;
+  r.d1 = c ? a.d1 : b.d1;
+  r.lo0 = c ? a.lo0 : b.lo0;
+  r.lo1 = c ? a.lo1 : b.lo1;
+  r.hi0 = c ? a.hi0 : b.hi0;
+  r.hi1 = c ? a.hi1 : b.hi1;
+  r.e = c ? a.e : b.e;
+  r.fl = c ? a.fl : b.fl;
+  r.pad = 0;
+  return r;
+}
+
+__device__ __forceinline__ Tr tr_load(const Tr* p) {
+  const int4* q = reinterpret_cast<const int4*>(p);
+  const int4 a = q[0], b = q[1], c = q[2], d = q[3];
+  Tr r;
+  r.d0 = (int64_t)(((uint64_t)(uint32_t)a.y << 32) | (uint32_t)a.x);
+  r.d1 = (int64_t)(((uint64_t)(uint32_t)a.w << 32) | (uint32_t)a.z);
+  r.lo0 = (int64_t)(((uint64_t)(uint32_t)b.y << 32) | (uint32_t)b.x);
+  r.lo1 = (int64_t)(((uint64_t)(uint32_t)b.w << 32) | (uint32_t)b.z);
+  r.hi0 = (int64_t)(((uint64_t)(uint32_t)c.y << 32) | (uint32_t)c.x);
+  r.hi1 = (int64_t)(((uint64_t)(uint32_t)c.w << 32) | (uint32_t)c.z);
+  r.e = d.x;
+  r.fl = (uint32_t)d.y;
+  r.pad = 0;
+  return r;
+}
+
+// c ? x1 : x0 as arithmetic on the difference: a select of two loaded fields would be folded into a select of
+// their addresses, and the record would go to private memory
+__device__ __forceinline__ int64_t pick(bool c, int64_t x1, int64_t x0) { return x0 + (c ? x1 - x0 : 0); }
+
+__device__ __forceinline__ int64_t clampb(int64_t v) { return v < -kBig ? -kBig : (v > kBig ? kBig : v); }
+
+// a, then b
+__device__ __forceinline__ Tr tr_comb(const Tr& a, const Tr& b) {
+  if (a.fl & F_ZERO) {
+    Tr r = b;
+    if (!(a.fl & F_NZERO)) r.fl &= ~F_NZERO;
+    return r;
+  }
+  if (b.fl & F_ZERO) return a;
+  Tr r;
+  r.e = a.e;
+  r.pad = 0;
+  r.fl = ((a.fl | b.fl) & F_BAD) | (a.fl & F_NEG);
+  if (a.e != b.e || ((a.fl ^ b.fl) & F_NEG)) r.fl |= F_BAD;
+  // input parity 0 leaves a with parity (a.d0 & 1), input parity 1 with ((1 + a.d1) & 1)
+  const bool q0 = (a.d0 & 1) != 0, q1 = (a.d1 & 1) == 0;
+  int64_t d0 = a.d0 + pick(q0, b.d1, b.d0), d1 = a.d1 + pick(q1, b.d1, b.d0);
+  r.lo0 = clampb(min(a.lo0, a.d0 + pick(q0, b.lo1, b.lo0)));
+  r.lo1 = clampb(min(a.lo1, a.d1 + pick(q1, b.lo1, b.lo0)));
+  r.hi0 = clampb(max(a.hi0, a.d0 + pick(q0, b.hi1, b.hi0)));
+  r.hi1 = clampb(max(a.hi1, a.d1 + pick(q1, b.hi1, b.hi0)));
+  if (d0 > kLim || d0 < -kLim || d1 > kLim || d1 < -kLim) {
+    r.fl |= F_BAD;
+    d0 = d1 = 0;
+  }
+  r.d0 = d0;
+  r.d1 = d1;
+  return r;
+}
+
+// s after the run, or false when the run is not known to be a translation at s
+__device__ __forceinline__ bool tr_apply(const Tr& t, double s, double& out) {
+  if (t.fl & F_ZERO) {
+    out = s == 0.0 ? ((signbit(s) && (t.fl & F_NZERO)) ? -0.0 : 0.0) : s;
+    return true;
+  }
+  if (t.fl & F_BAD) return false;
+  const uint64_t b = (uint64_t)__double_as_longlong(s);
+  const int E = (int)((b >> 52) & 0x7ff);
+  if (E == 0 || E == 0x7ff) return false;
+  if (E - 1023 != t.e || (uint32_t)(b >> 63) != (t.fl & F_NEG)) return false;
+  const int64_t M = (int64_t)((b & kFrac) | (uint64_t(1) << 52));
+  const bool odd = (M & 1) != 0;
+  if (M + pick(odd, t.lo1, t.lo0) < kM0 || M + pick(odd, t.hi1, t.hi0) >= kM1) return false;
+  out = __longlong_as_double((long long)((b & ~kFrac) | (uint64_t)(M + pick(odd, t.d1, t.d0) - kM0)));
+  return true;
+}
+
+// p / 2^(e-52), sign-flipped when the state is negative, as q = floor and the fraction's class c (0: < 1/2,
+// 1: == 1/2, 2: > 1/2), exactly, from p's bits.  False for a non-finite p or |p| >= 2^(e+1).
+__device__ __forceinline__ bool decomp(double p, int e, uint32_t sneg, int64_t& q, int& c) {
+  const uint64_t b = (uint64_t)__double_as_longlong(p);
+  int E = (int)((b >> 52) & 0x7ff);
+  q = 0;
+  c = 0;
+  if (E == 0x7ff) return false;
+  uint64_t m = b & kFrac;
+  if (E) m |= uint64_t(1) << 52;
+  else E = 1;
+  if (m == 0) return true;
+  const int sh = E - 1023 - e;
+  if (sh > 0) return false;
+  const bool neg = (uint32_t)(b >> 63) != sneg;
+  int k = -sh;
+  if (k == 0) {
+    q = neg ? -(int64_t)m : (int64_t)m;
+    return true;
+  }
+  if (k > 63) k = 63;  // m < 2^53 <= the half: the same classes
+  const uint64_t qq = m >> k, rr = m & ((uint64_t(1) << k) - 1), half = uint64_t(1) << (k - 1);
+  if (!neg) {
+    q = (int64_t)qq;
+    c = rr > half ? 2 : (rr == half ? 1 : 0);
+  } else if (rr == 0) {
+    q = -(int64_t)qq;
+  } else {
+    q = -(int64_t)qq - 1;
+    c = rr < half ? 2 : (rr == half ? 1 : 0);
+  }
+  return true;
+}
+
+// append one term to a run whose terms are decomposed in binade (e, sneg) (gok: that guess is usable)
+__device__ __forceinline__ void tr_push(Tr& t, double p, int e, uint32_t sneg, bool gok) {
+  const uint64_t b = (uint64_t)__double_as_longlong(p);
+  if ((b << 1) == 0) {  // +-0: no effect on a nonzero state
+    if (!(b >> 63)) t.fl &= ~F_NZERO;
+    return;
+  }
+  if (t.fl & F_ZERO) {  // the first nonzero term
+    t.fl = sneg ? F_NEG : 0u;
+    t.e = e;
+  }
+  if (!gok) {
+    t.fl |= F_BAD;
+    return;
+  }
+  int64_t q;
+  int c;
+  if (!decomp(p, e, sneg, q, c)) {
+    t.fl |= F_BAD;
+    return;
+  }
+  const int64_t up = c == 2 ? 1 : 0;
+  t.lo0 = min(t.lo0, t.d0 + q);
+  t.lo1 = min(t.lo1, t.d1 + q);
+  t.d0 += q + up + ((c == 1) ? ((t.d0 + q) & 1) : 0);  // a tie rounds the candidate M + d + q to even
+  t.d1 += q + up + ((c == 1) ? ((1 + t.d1 + q) & 1) : 0);
+  t.hi0 = max(t.hi0, t.d0);
+  t.hi1 = max(t.hi1, t.d1);
+}
+
+__device__ __forceinline__ Tr shfl_xor_tr(const Tr& t, int m) {
+  Tr r;
+  r.d0 = __shfl_xor(t.d0, m);
+  r.d1 = __shfl_xor(t.d1, m);
+  r.lo0 = __shfl_xor(t.lo0, m);
+  r.lo1 = __shfl_xor(t.lo1, m);
+  r.hi0 = __shfl_xor(t.hi0, m);
+  r.hi1 = __shfl_xor(t.hi1, m);
+  r.e = __shfl_xor(t.e, m);
+  r.fl = __shfl_xor(t.fl, m);
+  r.pad = 0;
+  return r;
+}
+
+__device__ __forceinline__ Tr shfl_down_tr(const Tr& t, int o) {
+  Tr r;
+  r.d0 = __shfl_down(t.d0, o);
+  r.d1 = __shfl_down(t.d1, o);
+  r.lo0 = __shfl_down(t.lo0, o);
+  r.lo1 = __shfl_down(t.lo1, o);
+  r.hi0 = __shfl_down(t.hi0, o);
+  r.hi1 = __shfl_down(t.hi1, o);
+  r.e = __shfl_down(t.e, o);
+  r.fl = __shfl_down(t.fl, o);
+  r.pad = 0;
+  return r;
+}
+
+__device__ __forceinline__ Tr shfl_up_tr(const Tr& t, int o) {
+  Tr r;
+  r.d0 = __shfl_up(t.d0, o);
+  r.d1 = __shfl_up(t.d1, o);
+  r.lo0 = __shfl_up(t.lo0, o);
+  r.lo1 = __shfl_up(t.lo1, o);
+  r.hi0 = __shfl_up(t.hi0, o);
+  r.hi1 = __shfl_up(t.hi1, o);
+  r.e = __shfl_up(t.e, o);
+  r.fl = __shfl_up(t.fl, o);
+  r.pad = 0;
+  return r;
+}
+
+__device__ __forceinline__ const double* vec_row(const Vecs& V, int v) {
+  return V.base ? V.base + (int64_t)v * V.stride : V.p[v];
+}
+
+// Row v of a (nv rows of K approximate chunk sums) -> its exclusive prefix: the guessed s at each segment start.
+// Any order: a guess only picks the binade the transducers are built in.
+__global__ __launch_bounds__(kT) void k_seqx_prefix(double* __restrict__ a, int64_t K, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  __shared__ double sh[kT];
+  double* row = a + (int64_t)blockIdx.x * K;
+  const int t = threadIdx.x;
+  const int64_t per = (K + kT - 1) / kT, lo = min<int64_t>((int64_t)t * per, K), hi = min<int64_t>(lo + per, K);
+  double sum = 0.0;
+  for (int64_t i = lo; i < hi; ++i) sum += row[i];
+  sh[t] = sum;
+  __syncthreads();
+  if (t == 0) {
+    double run = 0.0;
+    for (int i = 0; i < kT; ++i) {
+      const double v = sh[i];
+      sh[i] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  double run = sh[t];
+  for (int64_t i = lo; i < hi; ++i) {
+    const double v = row[i];
+    row[i] = run;
+    run += v;
+  }
+}
+
+// Workgroup k: segment k of every sum.  Thread t holds terms 16t..16t+15 of the segment (the products staged
+// through LDS from coalesced loads); four threads make a sub-segment's transducer, wave 0 composes the 64 subs.
+__global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w, Vecs V, int nv, int64_t n,
+                                                   int self, const double* __restrict__ pre, Tr* __restrict__ segT,
+                                                   Tr* __restrict__ subT, int64_t K, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  __shared__ double sp[kSeg + kSeg / kPer];  // products, one pad slot per 16: thread t's run at 17t
+  __shared__ double ssum[kSubs];
+  __shared__ Tr str[kSubs];
+  const int t = threadIdx.x, j = t >> 2;
+  const int64_t k = blockIdx.x, c0 = k * kSeg;
+  const int cnt = (int)max<int64_t>(0, min<int64_t>(kPer, n - (c0 + (int64_t)kPer * t)));
+  double xr[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int64_t g = c0 + t + i * kT;
+    xr[i] = g < n ? w[g] : 0.0;
+  }
+  for (int v = 0; v < nv; ++v) {
+    const double* y = self ? nullptr : vec_row(V, v);
+    const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int64_t g = c0 + t + i * kT;
+      const int l = t + i * kT;
+      double p = 0.0;
+      if (g < n) p = y ? xr[i] * (y[g] * sy) : xr[i] * xr[i];
+      sp[l + l / kPer] = p;
+    }
+    __syncthreads();
+    double pr[kPer];
+    double ps = 0.0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      pr[i] = sp[t * (kPer + 1) + i];
+      ps += pr[i];
+    }
+    ps += __shfl_xor(ps, 1);
+    ps += __shfl_xor(ps, 2);
+    if ((t & 3) == 0) ssum[j] = ps;
+    __syncthreads();
+    if (t < kSubs) {  // exclusive prefix of the sub sums (wave 0)
+      const double a = ssum[t];
+      double incl = a;
+#pragma unroll
+      for (int o = 1; o < kSubs; o <<= 1) {
+        const double u = __shfl_up(incl, o);
+        if (t >= o) incl += u;
+      }
+      ssum[t] = incl - a;
+    }
+    __syncthreads();
+    const double G = pre[(int64_t)v * K + k] + ssum[j];
+    const uint64_t gb = (uint64_t)__double_as_longlong(G);
+    const int GE = (int)((gb >> 52) & 0x7ff);
+    const bool gok = GE != 0 && GE != 0x7ff;
+    const int e = GE - 1023;
+    const uint32_t sneg = (uint32_t)(gb >> 63);
+    Tr a = tr_ident();
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+      if (i < cnt) tr_push(a, pr[i], e, sneg, gok);
+    if (!(a.fl & F_ZERO) && (a.d0 > kLim || a.d0 < -kLim || a.d1 > kLim || a.d1 < -kLim)) {
+      a.fl |= F_BAD;
+      a.d0 = a.d1 = 0;
+    }
+    Tr o = shfl_xor_tr(a, 1);
+    if ((t & 1) == 0) a = tr_comb(a, o);
+    o = shfl_xor_tr(a, 2);
+    if ((t & 3) == 0) {
+      a = tr_comb(a, o);
+      subT[((int64_t)v * K + k) * kSubs + j] = a;
+      str[j] = a;
+    }
+    __syncthreads();
+    if (t < kSubs) {  // ordered tree over the 64 subs
+      Tr b = str[t];
+#pragma unroll
+      for (int s = 1; s < kSubs; s <<= 1) {
+        const Tr u = shfl_down_tr(b, s);
+        if ((t & (2 * s - 1)) == 0) b = tr_comb(b, u);
+      }
+      if (t == 0) segT[(int64_t)v * K + k] = b;
+    }
+    __syncthreads();
+  }
+}
+
+// Apply the longest prefix of the lanes' runs (lane order) that is valid at s; returns its length.
+__device__ __forceinline__ int tr_walk(Tr t, double& s, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const Tr u = shfl_up_tr(t, o);
+    if (lane >= o) t = tr_comb(u, t);
+  }
+  double out = 0.0;
+  const bool ok = tr_apply(t, s, out);
+  const uint64_t bad = __ballot(!ok);
+  const int f = bad ? __builtin_ctzll(bad) : 64;
+  const double sn = __shfl(out, f > 0 ? f - 1 : 0);
+  if (f > 0) s = sn;
+  return f;
+}
+
+// The terms of one sub-segment (lane l: term l; act: the term exists), applied to s in order.
+__device__ __forceinline__ void elem_walk(double p, bool act0, double& s, int lane) {
+  const uint64_t am = __ballot(act0);
+  const int cnt = am ? 64 - __builtin_clzll(am) : 0;
+  int i = 0;
+  while (i < cnt) {
+    const bool act = act0 && lane >= i;
+    const uint64_t sb = (uint64_t)__double_as_longlong(s);
+    const int E = (int)((sb >> 52) & 0x7ff);
+    int f;
+    if (E != 0 && E != 0x7ff) {  // a normal state: integer steps in its binade
+      const int e = E - 1023;
+      const uint32_t sneg = (uint32_t)(sb >> 63);
+      const int64_t M = (int64_t)((sb & kFrac) | (uint64_t(1) << 52));
+      int64_t q = 0;
+      int c = 0;
+      bool okd = true;
+      if (act) okd = decomp(p, e, sneg, q, c);
+      const int64_t inc = act && okd ? q + (c == 2 ? 1 : 0) : 0;
+      int64_t D = inc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t u = __shfl_up(D, o);
+        if (lane >= o) D += u;
+      }
+      const bool ok = !act || (okd && c != 1 && M + (D - inc) + q >= kM0 && M + D < kM1);
+      const uint64_t bad = __ballot(!ok);
+      f = bad ? __builtin_ctzll(bad) : 64;
+      const int64_t Df = __shfl(D, f > 0 ? f - 1 : 0);
+      if (f > i) s = __longlong_as_double((long long)((sb & ~kFrac) | (uint64_t)(M + Df - kM0)));
+    } else if (s == 0.0) {  // +-0: zeros keep it (-0.0 only while every term is -0.0)
+      const uint64_t nz = __ballot(act && p != 0.0);
+      f = nz ? __builtin_ctzll(nz) : 64;
+      const uint64_t pz = __ballot(act && lane < f && !signbit(p));
+      if (pz) s = 0.0;
+    } else {  // subnormal or non-finite: term by term
+      f = i;
+    }
+    if (f >= cnt) break;
+    s = s + __shfl(p, f);  // the term that leaves the binade (or a tie, or the first nonzero): the f64 add itself
+    i = f + 1;
+  }
+}
+
+// Wave v: sum v, from +0.0, through the segment transducers, descending where one does not apply.
+__global__ __launch_bounds__(64) void k_seqx_walk(const double* __restrict__ w, Vecs V, int64_t n, int self,
+                                                  const Tr* __restrict__ segT, const Tr* __restrict__ subT,
+                                                  int64_t K, double* __restrict__ partial, int64_t nchunks,
+                                                  const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  const int v = blockIdx.x, lane = threadIdx.x;
+  const double* y = self ? nullptr : vec_row(V, v);
+  const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
+  double s = 0.0;
+  int64_t k = 0;
+  while (k < K) {
+    const bool in = k + lane < K;
+    const Tr ts = tr_load(segT + (int64_t)v * K + (in ? k + lane : 0));
+    k += tr_walk(tr_sel(in, ts, tr_bad()), s, lane);
+    if (k >= K) break;
+    const Tr u = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
+    int j = 0;
+    while (j < kSubs) {
+      j = tr_walk(tr_sel(lane < j, tr_ident(), u), s, lane);
+      if (j >= kSubs) break;
+      const int64_t g = k * kSeg + (int64_t)j * kSub + lane;
+      const bool act = g < n;
+      double p = 0.0;
+      if (act) {
+        const double xi = w[g];
+        p = y ? xi * (y[g] * sy) : xi * xi;
+      }
+      elem_walk(p, act, s, lane);
+      ++j;
+    }
+    ++k;
+  }
+  for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
+}
+
 }  // namespace
 
 extern "C" int msk_seq_stage1(const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial,
@@ -133,4 +610,33 @@ extern "C" int mspi_seq_chain(msp_ctx* c, const mspi_seq_segs* sg, int ncol, int
   k_seq_chain<<<dim3(frob ? 1 : ncol), dim3(kT), 0, c->stream>>>(*sg, ncol, frob, out, m, stop);
   KCHK((int)hipGetLastError());
   return MSP_SUCCESS;
+}
+
+// MSP_REDUCE_SEQ's stage 1: the exact parallel engine (the serial one under MSPLIT_SEQ_ENGINE=serial).
+int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial,
+                    int64_t nchunks, const int* stop) {
+  const char* eng = getenv("MSPLIT_SEQ_ENGINE");
+  const int64_t K = (n + kSeg - 1) / kSeg;
+  if ((eng && (eng[0] == 's' || eng[0] == 'S')) || K == 0)
+    return msk_seq_stage1(w, V, nv, n, self, partial, nchunks, stop, c->stream);
+  if (nv < 1 || nv > MSK_MAX_GROUP || (self && nv != 1) || nchunks < 1) return (int)hipErrorInvalidValue;
+  const int64_t need = (int64_t)nv * K * ((int64_t)sizeof(Tr) * (kSubs + 1) + (int64_t)sizeof(double));
+  if (need > c->seqbuf_cap) {
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return (int)hipErrorUnknown;
+    if (c->seqbuf) (void)hipFree(c->seqbuf);
+    c->seqbuf = nullptr;
+    c->seqbuf_cap = 0;
+    const hipError_t e = hipMalloc(&c->seqbuf, (size_t)need);
+    if (e != hipSuccess) return (int)e;
+    c->seqbuf_cap = need;
+  }
+  Tr* subT = static_cast<Tr*>(c->seqbuf);
+  Tr* segT = subT + (int64_t)nv * K * kSubs;
+  double* pre = reinterpret_cast<double*>(segT + (int64_t)nv * K);
+  int rc = msk_dot_stage1(w, V, nv, n, pre, K, self, stop, c->stream);
+  if (rc) return rc;
+  k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, stop);
+  k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop);
+  k_seqx_walk<<<dim3(nv), dim3(64), 0, c->stream>>>(w, *V, n, self, segT, subT, K, partial, nchunks, stop);
+  return (int)hipGetLastError();
 }

@@ -1,0 +1,188 @@
+"""The exact parallel engine of MSP_REDUCE_SEQ (csrc/msplit_seq.hip, mspi_seq_stage1).
+
+A sequential sum s = fl(s + p_i) is rebuilt from integer translations of the state's mantissa inside one binade
+(transducers composed in a wave scan) and the f64 add itself wherever a step leaves the binade, ties, meets a zero,
+a subnormal or a non-finite value.  Its result must be the sequential sum BIT FOR BIT whatever the data, so these
+inputs are chosen to hit every branch of that argument: dense ties at both mantissa parities, sums that return to
+exactly +0.0, walks that change binade thousands of times, power-of-two boundaries hit exactly, subnormal and
+overflowing sums, +-0.0, inf and NaN, and every length edge of the 64-term sub-segments and 4096-term segments.
+Each is checked against the PETSc-order oracle (orc_dot / orc_norm2 / orc_mdot with ORC_REDUCE_SEQ, the
+reference's f2cblaslapack ddot order) and against the serial engine (MSPLIT_SEQ_ENGINE=serial, one lane adding in
+order) on the same device.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Vec
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20251121
+
+
+@pytest.fixture(scope="module")
+def sctx(ctx):
+    c = Context(0)
+    c.set_reduction("seq")
+    yield c
+
+
+def _bits(v):
+    return np.float64(v).view(np.uint64)
+
+
+def _serial(fn):
+    os.environ["MSPLIT_SEQ_ENGINE"] = "serial"
+    try:
+        return fn()
+    finally:
+        del os.environ["MSPLIT_SEQ_ENGINE"]
+
+
+def _check_dot(sctx, oracle, x, y):
+    xv, yv = Vec.from_array(sctx, x), Vec.from_array(sctx, y)
+    got = xv.dot(yv)
+    ref = oracle.dot(x, y, oracle.REDUCE_SEQ)
+    ser = _serial(lambda: xv.dot(yv))
+    assert _bits(got) == _bits(ref) and _bits(ser) == _bits(ref), (got, ref, ser)
+    return got
+
+
+def _check_norm(sctx, oracle, x):
+    xv = Vec.from_array(sctx, x)
+    got = xv.norm()
+    ref = oracle.norm2(x, oracle.REDUCE_SEQ)
+    ser = _serial(lambda: xv.norm())
+    assert _bits(got) == _bits(ref) and _bits(ser) == _bits(ref), (got, ref, ser)
+
+
+def _ties(n, rng, start):
+    """products p = x * y that are exact halves of the state's ulp: every term a rounding tie"""
+    x = np.ones(n)
+    y = rng.choice([-3.0, -1.0, 1.0, 3.0, 5.0, -5.0, 0.5, -0.5, 2.0], n)
+    x[0], y[0] = start, 1.0
+    return x, y
+
+
+def _cases():
+    rng = np.random.default_rng(SEED)
+    c = {}
+    c["ties_even_start"] = _ties(50_000, rng, 2.0 ** 53)                      # u = 2: +-1, +-3, +-5 tie
+    c["ties_odd_start"] = _ties(50_000, rng, 2.0 ** 52 + 1)                   # u = 1, odd M: +-0.5 tie
+    x = rng.standard_normal(1 << 20)
+    c["random_walk_1M"] = (x, rng.standard_normal(1 << 20))                   # ~33k binade changes
+    a = rng.uniform(-1, 1, 40_000)
+    x = np.repeat(a, 2)
+    y = np.tile([1.0, -1.0], 40_000)
+    c["cancel_to_zero"] = (x, y)                                              # s returns to +0.0 every 2 terms
+    c["quarter_steps"] = (np.full(300_000, 0.25), np.ones(300_000))           # s hits every power of two exactly
+    x = np.full(100_000, 0.125)
+    x[::7] = -0.375
+    c["dyadic_up_down"] = (x, np.ones(100_000))
+    c["all_pos_zero"] = (np.zeros(10_000), rng.uniform(-1, 1, 10_000))
+    c["all_neg_zero"] = (np.full(9_000, -0.0), np.ones(9_000))
+    x = rng.uniform(-1, 1, 70_001)
+    x[rng.random(70_001) < 0.5] = 0.0
+    x[rng.random(70_001) < 0.1] = -0.0
+    c["sparse_zeros"] = (x, rng.uniform(-1, 1, 70_001))
+    x = np.zeros(8_192)
+    x[5000] = 1.5
+    c["one_nonzero_late"] = (x, np.full(8_192, 3.0))
+    c["subnormal_sum"] = (rng.uniform(-1, 1, 20_000) * 1e-160, rng.uniform(0, 1, 20_000) * 1e-160)
+    c["huge_range"] = (np.sign(rng.standard_normal(60_000)) * 10.0 ** rng.uniform(-150, 150, 60_000),
+                       10.0 ** rng.uniform(-150, 150, 60_000))
+    c["overflow_to_inf"] = (np.full(5_000, 1e154), np.full(5_000, 1e154))
+    x = rng.uniform(-1, 1, 12_345)
+    x[6000] = np.inf
+    c["inf_mid"] = (x, np.ones(12_345))
+    x = rng.uniform(-1, 1, 12_345)
+    x[100], x[9000] = np.inf, -np.inf
+    c["inf_minus_inf"] = (x, np.ones(12_345))
+    x = rng.uniform(-1, 1, 4_097)
+    x[4096] = np.nan
+    c["nan_last"] = (x, np.ones(4_097))
+    x = rng.uniform(0.5, 1.0, 200_000)
+    c["drift_positive"] = (x, rng.uniform(-0.2, 1.0, 200_000))
+    big = np.full(30_000, 1e-3)
+    big[0] = 1e16
+    c["small_onto_large"] = (big, np.ones(30_000))                           # terms below half an ulp
+    x = np.full(30_000, 1e-3)
+    x[15_000] = 1e16
+    x[15_001] = -1e16
+    c["large_in_and_out"] = (x, np.ones(30_000))
+    return c
+
+
+CASES = _cases()
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_seq_engine_adversarial_dots(sctx, oracle, name):
+    x, y = CASES[name]
+    _check_dot(sctx, oracle, x, y)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 4095, 4096, 4097, 8191, 8193, 262_144 + 5, 1_000_003])
+def test_seq_engine_lengths(sctx, oracle, n):
+    rng = np.random.default_rng(SEED + n)
+    x, y = rng.uniform(-1, 1, n), rng.uniform(-1, 1, n)
+    _check_dot(sctx, oracle, x, y)
+    _check_norm(sctx, oracle, x)
+
+
+@pytest.mark.parametrize("name", ["random_walk_1M", "huge_range", "subnormal_sum", "all_neg_zero", "inf_mid",
+                                  "quarter_steps"])
+def test_seq_engine_norms(sctx, oracle, name):
+    _check_norm(sctx, oracle, CASES[name][0])
+
+
+def test_seq_engine_mdot_32_mixed(sctx, oracle):
+    """One MDot launch of 32 sums of very different kinds (the walk runs one wave per sum)."""
+    rng = np.random.default_rng(SEED)
+    n = 300_001
+    w = rng.standard_normal(n)
+    V = []
+    for j in range(32):
+        kind = j % 4
+        if kind == 0:
+            V.append(rng.standard_normal(n))
+        elif kind == 1:
+            V.append(np.abs(w) * (1 + j))                       # a positive drift
+        elif kind == 2:
+            v = np.zeros(n)
+            v[rng.integers(0, n, 50)] = rng.standard_normal(50)  # mostly zero terms
+            V.append(v)
+        else:
+            V.append(rng.choice([1.0, -1.0], n) * 0.5 ** rng.integers(0, 4, n))  # short mantissas: ties
+    got = Vec.from_array(sctx, w).mdot([Vec.from_array(sctx, v) for v in V])
+    ref = oracle.mdot(w, V, oracle.REDUCE_SEQ)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+def test_seq_engine_gmres_vectors_256cube(sctx, oracle):
+    """The dots the configs[1] step actually takes: an Arnoldi basis of the 256^3 Laplacian (w = A v_j against
+    v_0..v_j, then ||w||); 16.7 M terms per sum."""
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Mat
+    n = 256
+    A = Mat.box_stencil(sctx, 3, n, n, n)
+    N = n ** 3
+    one = Vec(sctx, N)
+    one.set(1.0)
+    v = Vec(sctx, N)
+    A.mult(one, v)
+    basis = []
+    for j in range(4):
+        nv = v.norm()
+        v.scale(1.0 / nv)
+        basis.append(v.get_array())
+        w = Vec(sctx, N)
+        A.mult(v, w)
+        wh = w.get_array()
+        got = w.mdot([Vec.from_array(sctx, b) for b in basis])
+        ref = oracle.mdot(wh, basis, oracle.REDUCE_SEQ)
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), j
+        for b, h in zip(basis, ref):
+            wh = wh - h * b
+        v = Vec.from_array(sctx, wh)
