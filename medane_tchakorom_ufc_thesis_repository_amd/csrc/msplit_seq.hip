@@ -59,6 +59,9 @@
 // binade in at most a few hundred of 4096 segments.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "msplit_ctx.hpp"
 
 namespace {
@@ -303,36 +306,6 @@ __device__ __forceinline__ bool decomp(double p, int e, uint32_t sneg, int64_t& 
   return true;
 }
 
-// append one term to a run whose terms are decomposed in binade (e, sneg) (gok: that guess is usable)
-__device__ __forceinline__ void tr_push(Tr& t, double p, int e, uint32_t sneg, bool gok) {
-  const uint64_t b = (uint64_t)__double_as_longlong(p);
-  if ((b << 1) == 0) {  // +-0: no effect on a nonzero state
-    if (!(b >> 63)) t.fl &= ~F_NZERO;
-    return;
-  }
-  if (t.fl & F_ZERO) {  // the first nonzero term
-    t.fl = sneg ? F_NEG : 0u;
-    t.e = e;
-  }
-  if (!gok) {
-    t.fl |= F_BAD;
-    return;
-  }
-  int64_t q;
-  int c;
-  if (!decomp(p, e, sneg, q, c)) {
-    t.fl |= F_BAD;
-    return;
-  }
-  const int64_t up = c == 2 ? 1 : 0;
-  t.lo0 = min(t.lo0, t.d0 + q);
-  t.lo1 = min(t.lo1, t.d1 + q);
-  t.d0 += q + up + ((c == 1) ? ((t.d0 + q) & 1) : 0);  // a tie rounds the candidate M + d + q to even
-  t.d1 += q + up + ((c == 1) ? ((1 + t.d1 + q) & 1) : 0);
-  t.hi0 = max(t.hi0, t.d0);
-  t.hi1 = max(t.hi1, t.d1);
-}
-
 __device__ __forceinline__ Tr shfl_xor_tr(const Tr& t, int m) {
   Tr r;
   r.d0 = __shfl_xor(t.d0, m);
@@ -466,13 +439,64 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
     const bool gok = GE != 0 && GE != 0x7ff;
     const int e = GE - 1023;
     const uint32_t sneg = (uint32_t)(gb >> 63);
+    // the lane's run: every term decomposed once, then input parity 0's track; parity 1's differs only through
+    // ties, so it is the same track unless the run holds one (then it is run again from the kept terms)
     Tr a = tr_ident();
+    int64_t qv[kPer];
+    uint32_t cls = 0;  // 2 bits per term: 0 / 1 (tie) / 2 as decomp's class, 3: a +-0 term (no effect)
+    bool bad = false;
 #pragma unroll
-    for (int i = 0; i < kPer; ++i)
-      if (i < cnt) tr_push(a, pr[i], e, sneg, gok);
-    if (!(a.fl & F_ZERO) && (a.d0 > kLim || a.d0 < -kLim || a.d1 > kLim || a.d1 < -kLim)) {
-      a.fl |= F_BAD;
-      a.d0 = a.d1 = 0;
+    for (int i = 0; i < kPer; ++i) {
+      qv[i] = 0;
+      uint32_t ci = 3;
+      if (i < cnt) {
+        const uint64_t b = (uint64_t)__double_as_longlong(pr[i]);
+        if ((b << 1) == 0) {
+          if (!(b >> 63)) a.fl &= ~F_NZERO;
+        } else {
+          if (a.fl & F_ZERO) {
+            a.fl = sneg ? F_NEG : 0u;
+            a.e = e;
+          }
+          int c = 0;
+          if (!gok || !decomp(pr[i], e, sneg, qv[i], c)) bad = true;
+          ci = (uint32_t)c;
+        }
+      }
+      cls |= ci << (2 * i);
+    }
+    if (!(a.fl & F_ZERO)) {
+      bool tie = false;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const uint32_t ci = (cls >> (2 * i)) & 3u;
+        if (ci == 3) continue;
+        const int64_t q = qv[i];
+        a.lo0 = min(a.lo0, a.d0 + q);
+        a.d0 += q + (ci == 2 ? 1 : 0) + (ci == 1 ? ((a.d0 + q) & 1) : 0);
+        a.hi0 = max(a.hi0, a.d0);
+        tie |= ci == 1;
+      }
+      if (tie) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+          const uint32_t ci = (cls >> (2 * i)) & 3u;
+          if (ci == 3) continue;
+          const int64_t q = qv[i];
+          a.lo1 = min(a.lo1, a.d1 + q);
+          a.d1 += q + (ci == 2 ? 1 : 0) + (ci == 1 ? ((1 + a.d1 + q) & 1) : 0);
+          a.hi1 = max(a.hi1, a.d1);
+        }
+      } else {
+        a.d1 = a.d0;
+        a.lo1 = a.lo0;
+        a.hi1 = a.hi0;
+      }
+      if (bad) a.fl |= F_BAD;
+      if (a.d0 > kLim || a.d0 < -kLim || a.d1 > kLim || a.d1 < -kLim) {
+        a.fl |= F_BAD;
+        a.d0 = a.d1 = 0;
+      }
     }
     Tr o = shfl_xor_tr(a, 1);
     if ((t & 1) == 0) a = tr_comb(a, o);
@@ -512,84 +536,121 @@ __device__ __forceinline__ int tr_walk(Tr t, double& s, int lane) {
   return f;
 }
 
-// The terms of one sub-segment (lane l: term l; act: the term exists), applied to s in order.
-__device__ __forceinline__ void elem_walk(double p, bool act0, double& s, int lane) {
-  const uint64_t am = __ballot(act0);
-  const int cnt = am ? 64 - __builtin_clzll(am) : 0;
-  int i = 0;
-  while (i < cnt) {
-    const bool act = act0 && lane >= i;
-    const uint64_t sb = (uint64_t)__double_as_longlong(s);
-    const int E = (int)((sb >> 52) & 0x7ff);
-    int f;
-    if (E != 0 && E != 0x7ff) {  // a normal state: integer steps in its binade
-      const int e = E - 1023;
-      const uint32_t sneg = (uint32_t)(sb >> 63);
-      const int64_t M = (int64_t)((sb & kFrac) | (uint64_t(1) << 52));
-      int64_t q = 0;
-      int c = 0;
-      bool okd = true;
-      if (act) okd = decomp(p, e, sneg, q, c);
-      const int64_t inc = act && okd ? q + (c == 2 ? 1 : 0) : 0;
-      int64_t D = inc;
+constexpr int kWalkT = 256;  // four waves walk one sum redundantly; all four fill a descended segment's terms
+
+// Segment k's terms into LDS (every thread of the workgroup, coalesced), products formed as the serial engine's.
+__device__ __forceinline__ void fill_segment(double* sp, const double* __restrict__ w, const double* __restrict__ y,
+                                             double sy, int64_t n, int64_t k) {
+  const int t = threadIdx.x;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t u = __shfl_up(D, o);
-        if (lane >= o) D += u;
-      }
-      const bool ok = !act || (okd && c != 1 && M + (D - inc) + q >= kM0 && M + D < kM1);
-      const uint64_t bad = __ballot(!ok);
-      f = bad ? __builtin_ctzll(bad) : 64;
-      const int64_t Df = __shfl(D, f > 0 ? f - 1 : 0);
-      if (f > i) s = __longlong_as_double((long long)((sb & ~kFrac) | (uint64_t)(M + Df - kM0)));
-    } else if (s == 0.0) {  // +-0: zeros keep it (-0.0 only while every term is -0.0)
-      const uint64_t nz = __ballot(act && p != 0.0);
-      f = nz ? __builtin_ctzll(nz) : 64;
-      const uint64_t pz = __ballot(act && lane < f && !signbit(p));
-      if (pz) s = 0.0;
-    } else {  // subnormal or non-finite: term by term
-      f = i;
+  for (int r = 0; r < kSeg / kWalkT; ++r) {
+    const int l = t + r * kWalkT;
+    const int64_t g = k * kSeg + l;
+    double p = 0.0;
+    if (g < n) {
+      const double xi = w[g];
+      p = y ? xi * (y[g] * sy) : xi * xi;
     }
-    if (f >= cnt) break;
-    s = s + __shfl(p, f);  // the term that leaves the binade (or a tie, or the first nonzero): the f64 add itself
-    i = f + 1;
+    sp[l] = p;
   }
 }
 
-// Wave v: sum v, from +0.0, through the segment transducers, descending where one does not apply.
-__global__ __launch_bounds__(64) void k_seqx_walk(const double* __restrict__ w, Vecs V, int64_t n, int self,
-                                                  const Tr* __restrict__ segT, const Tr* __restrict__ subT,
-                                                  int64_t K, double* __restrict__ partial, int64_t nchunks,
-                                                  const int* __restrict__ stop) {
+// Wave-uniform: s after the terms [i0, i1) of the LDS segment, added in order by the f64 add (lane 0; broadcast).
+__device__ __forceinline__ double serial_terms(const double* sp, int i0, int i1, double s, int lane) {
+  double a = s;
+  if (lane == 0) {
+    int i = i0;
+    for (; i + 8 <= i1; i += 8) {
+      double q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = sp[i + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a = a + q[u];
+    }
+    for (; i < i1; ++i) a = a + sp[i];
+  }
+  return __shfl(a, 0);
+}
+
+// Workgroup v: sum v, from +0.0.  Windows of 64 segment transducers are composed in a wave scan and the longest
+// prefix valid at s applied; a segment that does not apply is taken sub-segment by sub-segment (each lane applies
+// its own sub's transducer to s, the failing ones' terms are added by the f64 add from LDS); after a descended
+// segment the next one is tried on its own first, so runs of failing segments cost no scans.  All four waves
+// compute the same s (identical inputs and operations), so every decision is uniform across the workgroup.
+__global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__ w, Vecs V, int64_t n, int self,
+                                                      const Tr* __restrict__ segT, const Tr* __restrict__ subT,
+                                                      int64_t K, double* __restrict__ partial, int64_t nchunks,
+                                                      const int* __restrict__ stop, int64_t* __restrict__ stats) {
   if (stopped(stop)) return;
-  const int v = blockIdx.x, lane = threadIdx.x;
+  __shared__ double sp[kSeg];
+  const int v = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const double* y = self ? nullptr : vec_row(V, v);
   const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
+  int64_t n_scan = 0, n_segdesc = 0, n_subser = 0, n_single = 0;
   double s = 0.0;
-  int64_t k = 0;
-  while (k < K) {
-    const bool in = k + lane < K;
-    const Tr ts = tr_load(segT + (int64_t)v * K + (in ? k + lane : 0));
-    k += tr_walk(tr_sel(in, ts, tr_bad()), s, lane);
-    if (k >= K) break;
-    const Tr u = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
-    int j = 0;
-    while (j < kSubs) {
-      j = tr_walk(tr_sel(lane < j, tr_ident(), u), s, lane);
-      if (j >= kSubs) break;
-      const int64_t g = k * kSeg + (int64_t)j * kSub + lane;
-      const bool act = g < n;
-      double p = 0.0;
-      if (act) {
-        const double xi = w[g];
-        p = y ? xi * (y[g] * sy) : xi * xi;
+  for (int64_t kb = 0; kb < K; kb += 64) {
+    const bool in = kb + lane < K;
+    const Tr tw = tr_load(segT + (int64_t)v * K + (in ? kb + lane : 0));
+    const Tr tv = tr_sel(in, tw, tr_bad());
+    int f0 = 0;
+    bool scan = true;
+    while (f0 < 64 && kb + f0 < K) {
+      int f;
+      if (scan) {
+        f = tr_walk(tr_sel(lane < f0, tr_ident(), tv), s, lane);
+        ++n_scan;
+      } else {  // the segment after a descended one, on its own
+        double out = 0.0;
+        const bool ok = tr_apply(tv, s, out);
+        const bool mine = (__ballot(ok) >> f0) & 1;
+        const double sn = __shfl(out, f0);
+        ++n_single;
+        if (mine) {
+          s = sn;
+          f0 += 1;
+          scan = true;
+          continue;
+        }
+        f = f0;
       }
-      elem_walk(p, act, s, lane);
-      ++j;
+      if (f >= 64 || kb + f >= K) break;
+      // segment kb + f does not apply at s: its sub-segments
+      const int64_t k = kb + f;
+      ++n_segdesc;
+      const Tr u = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
+      bool loaded = false;
+      for (int j = 0; j < kSubs; ++j) {
+        double out = 0.0;
+        const bool ok = tr_apply(u, s, out);
+        const bool mine = (__ballot(ok) >> j) & 1;
+        const double sn = __shfl(out, j);
+        if (mine) {
+          s = sn;
+          continue;
+        }
+        if (!loaded) {
+          __syncthreads();  // the previous segment's LDS reads are done
+          fill_segment(sp, w, y, sy, n, k);
+          __syncthreads();
+          loaded = true;
+        }
+        const int64_t c0 = k * kSeg + (int64_t)j * kSub;
+        const int i1 = (int)max<int64_t>(0, min<int64_t>(kSub, n - c0));
+        s = serial_terms(sp, j * kSub, j * kSub + i1, s, lane);
+        ++n_subser;
+      }
+      f0 = f + 1;
+      scan = false;
     }
-    ++k;
   }
-  for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
+  if (t < 64)
+    for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
+  if (stats && t == 0) {
+    stats[v * 4 + 0] = n_scan;
+    stats[v * 4 + 1] = n_segdesc;
+    stats[v * 4 + 2] = n_single;
+    stats[v * 4 + 3] = n_subser;
+  }
 }
 
 }  // namespace
@@ -637,6 +698,20 @@ int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t 
   if (rc) return rc;
   k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, stop);
   k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop);
-  k_seqx_walk<<<dim3(nv), dim3(64), 0, c->stream>>>(w, *V, n, self, segT, subT, K, partial, nchunks, stop);
+  static int64_t* dstats = nullptr;  // MSPLIT_SEQ_STATS=1: per-sum walk counters on stderr (a diagnostic)
+  const char* st = getenv("MSPLIT_SEQ_STATS");
+  const bool want = st && st[0] == '1';
+  if (want && !dstats && hipMalloc((void**)&dstats, 4 * MSK_MAX_GROUP * sizeof(int64_t)) != hipSuccess) dstats = nullptr;
+  k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, partial, nchunks, stop,
+                                                    want ? dstats : nullptr);
+  if (want && dstats) {
+    int64_t h[4 * MSK_MAX_GROUP];
+    if (hipMemcpyAsync(h, dstats, 4 * nv * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+        hipStreamSynchronize(c->stream) == hipSuccess)
+      for (int v = 0; v < nv; ++v)
+        fprintf(stderr, "seqx n=%lld nv=%d v=%d scans=%lld seg_desc=%lld single=%lld sub_serial=%lld\n",
+                (long long)n, nv, v, (long long)h[4 * v], (long long)h[4 * v + 1], (long long)h[4 * v + 2],
+                (long long)h[4 * v + 3]);
+  }
   return (int)hipGetLastError();
 }

@@ -1,0 +1,238 @@
+"""The arithmetic of MSP_REDUCE_SEQ's exact parallel engine (csrc/msplit_seq.hip), restated in Python integers.
+
+The device engine rebuilds a sequential sum s = fl(s + p_i) (the reference's f2cblaslapack ddot order, oracle
+ORC_REDUCE_SEQ) from "transducers": while s stays in one binade [2^e, 2^(e+1)) of one sign it is M * 2^(e-52) with
+M an integer in [2^52, 2^53), and each term adds floor(p / u) plus a rounding bit to M (a tie rounds to even M, so
+the map depends on M's parity).  A run of terms is, per input parity, an offset d with the lowest exact sum lo and
+the highest result hi; runs compose associatively and apply to an actual s only when M + lo >= 2^52 and
+M + hi < 2^53.  This file restates decomp / the lane run / tr_comb / tr_apply exactly as the kernel computes them
+and checks, on the CPU and against the f64 sequential sum itself, that (a) any composition order of the runs
+gives the same map, (b) a walk that applies whatever is valid and adds the rest term by term reproduces the
+sequential sum bit for bit on adversarial inputs (dense ties at both parities, exact powers of two, returns to
++0.0, subnormals, huge ranges, +-inf), whatever the guessed binades were.  The GPU kernels themselves are checked
+against the oracle in tests/test_gpu_seq_engine.py.
+"""
+import math
+import struct
+
+import numpy as np
+import pytest
+
+M0, M1, BIG, LIM = 1 << 52, 1 << 53, 1 << 60, 1 << 56
+FRAC = (1 << 52) - 1
+
+
+def bits(x):
+    return struct.unpack("<Q", struct.pack("<d", x))[0]
+
+
+def fromb(b):
+    return struct.unpack("<d", struct.pack("<Q", b))[0]
+
+
+def decomp(p, e, sneg):
+    """(q, class) of p / 2^(e-52) (sign-flipped for a negative state), or None (non-finite or |p| >= 2^(e+1))."""
+    b = bits(p)
+    E = (b >> 52) & 0x7FF
+    if E == 0x7FF:
+        return None
+    m = b & FRAC
+    if E:
+        m |= 1 << 52
+    else:
+        E = 1
+    if m == 0:
+        return 0, 0
+    sh = E - 1023 - e
+    if sh > 0:
+        return None
+    neg = (b >> 63) != sneg
+    k = min(-sh, 63)
+    if k == 0:
+        return (-m if neg else m), 0
+    qq, rr, half = m >> k, m & ((1 << k) - 1), 1 << (k - 1)
+    if not neg:
+        return qq, (2 if rr > half else (1 if rr == half else 0))
+    if rr == 0:
+        return -qq, 0
+    return -qq - 1, (2 if rr < half else (1 if rr == half else 0))
+
+
+def ident():
+    return dict(d=[0, 0], lo=[BIG, BIG], hi=[-BIG, -BIG], e=0, neg=0, bad=False, zero=True, nzero=True)
+
+
+def run(ps, e, sneg, gok):
+    """The lane run of k_seqx_trans: terms decomposed once, parity 0's track, parity 1's only if a tie occurs."""
+    t = ident()
+    qc = []
+    for p in ps:
+        b = bits(p)
+        if (b << 1) & ((1 << 64) - 1) == 0:
+            if not (b >> 63):
+                t["nzero"] = False
+            qc.append(None)
+            continue
+        if t["zero"]:
+            t.update(zero=False, nzero=False, neg=sneg, e=e)
+        r = decomp(p, e, sneg) if gok else None
+        if r is None:
+            t["bad"] = True
+            r = (0, 0)
+        qc.append(r)
+    if t["zero"]:
+        return t
+    tie = False
+    for pi in (0, 1):
+        if pi == 1 and not tie:
+            t["d"][1], t["lo"][1], t["hi"][1] = t["d"][0], t["lo"][0], t["hi"][0]
+            break
+        for r in qc:
+            if r is None:
+                continue
+            q, c = r
+            t["lo"][pi] = min(t["lo"][pi], t["d"][pi] + q)
+            t["d"][pi] += q + (1 if c == 2 else 0) + (((pi + t["d"][pi] + q) & 1) if c == 1 else 0)
+            t["hi"][pi] = max(t["hi"][pi], t["d"][pi])
+            tie |= c == 1
+    if abs(t["d"][0]) > LIM or abs(t["d"][1]) > LIM:
+        t["bad"] = True
+        t["d"] = [0, 0]
+    return t
+
+
+def comb(a, b):
+    if a["zero"]:
+        r = {k: (list(v) if isinstance(v, list) else v) for k, v in b.items()}
+        if not a["nzero"]:
+            r["nzero"] = False
+        return r
+    if b["zero"]:
+        return a
+    r = dict(e=a["e"], neg=a["neg"], zero=False, nzero=False, d=[0, 0], lo=[0, 0], hi=[0, 0],
+             bad=a["bad"] or b["bad"] or a["e"] != b["e"] or a["neg"] != b["neg"])
+    for pi in (0, 1):
+        ad = a["d"][pi]
+        p2 = (pi + ad) & 1
+        r["d"][pi] = ad + b["d"][p2]
+        r["lo"][pi] = max(-BIG, min(BIG, min(a["lo"][pi], ad + b["lo"][p2])))
+        r["hi"][pi] = max(-BIG, min(BIG, max(a["hi"][pi], ad + b["hi"][p2])))
+    if abs(r["d"][0]) > LIM or abs(r["d"][1]) > LIM:
+        r["bad"] = True
+        r["d"] = [0, 0]
+    return r
+
+
+def apply(t, s):
+    if t["zero"]:
+        if s == 0.0:
+            return -0.0 if (math.copysign(1.0, s) < 0 and t["nzero"]) else 0.0
+        return s
+    if t["bad"]:
+        return None
+    b = bits(s)
+    E = (b >> 52) & 0x7FF
+    if E in (0, 0x7FF) or E - 1023 != t["e"] or (b >> 63) != t["neg"]:
+        return None
+    M = (b & FRAC) | (1 << 52)
+    pi = M & 1
+    if M + t["lo"][pi] < M0 or M + t["hi"][pi] >= M1:
+        return None
+    return fromb((b & ~FRAC & ((1 << 64) - 1)) | (M + t["d"][pi] - M0))
+
+
+def guess(G):
+    b = bits(G)
+    E = (b >> 52) & 0x7FF
+    return E not in (0, 0x7FF), E - 1023, b >> 63
+
+
+def seqsum(ps, s=0.0):
+    for p in ps:
+        s = s + p
+    return s
+
+
+def engine(ps, sub=16, per=4, jitter=1e-9, seed=0):
+    """Sub-segment transducers built from lane runs of `per` terms in the binade of a jittered guess, applied where
+    valid; the rest term by term with the f64 add (the walk's serial sub-segments)."""
+    rng = np.random.default_rng(seed)
+    pre = np.concatenate([[0.0], np.cumsum(ps)])
+    s, i, n, fast = 0.0, 0, len(ps), 0
+    while i < n:
+        j = min(n, i + sub)
+        gok, e, sn = guess(float(pre[i]) * (1.0 + jitter * rng.uniform(-1, 1)))
+        lanes = [run(ps[k:min(k + per, j)], e, sn, gok) for k in range(i, j, per)]
+        t = lanes[0]
+        for u in lanes[1:]:
+            t = comb(t, u)
+        r = apply(t, s)
+        if r is not None:
+            s, fast = r, fast + 1
+        else:
+            s = seqsum(ps[i:j], s)
+        i = j
+    return s, fast
+
+
+def _cases():
+    rng = np.random.default_rng(20251121)
+    tie_terms = [-3.0, -1.0, 1.0, 3.0, 5.0, -5.0, 0.5, -0.5, 2.0]
+    return {
+        "walk": rng.standard_normal(6000) * rng.standard_normal(6000),
+        "ties_even": np.concatenate([[2.0 ** 53], rng.choice(tie_terms, 3000)]),
+        "ties_odd": np.concatenate([[2.0 ** 52 + 1], rng.choice(tie_terms, 3000)]),
+        "quarter": np.full(6000, 0.25),
+        "cancel": np.repeat(rng.uniform(-1, 1, 1500), 2) * np.tile([1.0, -1.0], 1500),
+        "small_on_large": np.concatenate([[1e16], np.full(3000, 1e-3)]),
+        "range": np.sign(rng.standard_normal(4000)) * 10.0 ** rng.uniform(-150, 150, 4000),
+        "drift": rng.uniform(0.5, 1, 4000) * rng.uniform(-0.2, 1, 4000),
+        "subnormal": rng.uniform(-1, 1, 1500) * 1e-160 * rng.uniform(0, 1, 1500) * 1e-160,
+        "neg_zero": np.full(100, -0.0),
+        "inf": np.concatenate([rng.uniform(-1, 1, 500), [np.inf], rng.uniform(-1, 1, 500)]),
+        "overflow": np.full(300, 1e307),
+    }
+
+
+CASES = _cases()
+
+
+@pytest.mark.parametrize("name", list(CASES))
+@pytest.mark.parametrize("jitter", [0.0, 1e-9, 0.3])
+def test_engine_walk_is_the_sequential_sum(name, jitter):
+    ps = [float(v) for v in CASES[name]]
+    ref = seqsum(ps)
+    got, fast = engine(ps, jitter=jitter)
+    assert bits(got) == bits(ref), (got, ref)
+
+
+def test_engine_takes_the_fast_path():
+    """Where the guesses are good the sub-segment maps apply (the walk is not the serial sum in disguise)."""
+    for name in ("walk", "ties_even", "ties_odd", "quarter", "drift", "small_on_large"):
+        ps = [float(v) for v in CASES[name]]
+        _, fast = engine(ps)
+        assert fast > len(ps) // 16 // 4, (name, fast)
+
+
+@pytest.mark.parametrize("name", ["ties_even", "ties_odd", "walk", "drift"])
+def test_composition_is_associative(name):
+    """Left fold, right fold and a balanced tree of 16 lane runs are the same map (the kernel composes in trees
+    and wave scans); it applies to the actual start exactly when the whole run stays in the binade."""
+    ps = [float(v) for v in CASES[name][:256]]
+    s0 = seqsum(ps[:1])
+    gok, e, sn = guess(s0)
+    lanes = [run(ps[1 + 15 * k:1 + 15 * (k + 1)], e, sn, gok) for k in range(16)]
+    left = lanes[0]
+    for u in lanes[1:]:
+        left = comb(left, u)
+    right = lanes[-1]
+    for u in reversed(lanes[:-1]):
+        right = comb(u, right)
+    tree = lanes
+    while len(tree) > 1:
+        tree = [comb(tree[i], tree[i + 1]) for i in range(0, len(tree), 2)]
+    for t in (right, tree[0]):
+        assert {k: t[k] for k in ("d", "lo", "hi", "bad")} == {k: left[k] for k in ("d", "lo", "hi", "bad")}
+    r = apply(left, s0)
+    if r is not None:
+        assert bits(r) == bits(seqsum(ps[1:241], s0))
