@@ -586,7 +586,14 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
   const int v = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const double* y = self ? nullptr : vec_row(V, v);
   const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
-  int64_t n_scan = 0, n_segdesc = 0, n_subser = 0, n_single = 0;
+  int64_t n_scan = 0, n_segdesc = 0, n_subser = 0, n_single = 0, n_fbad = 0, n_fstate = 0, n_fguess = 0, n_frange = 0;
+  int64_t c_scan = 0, c_single = 0, c_serial = 0, c_wait = 0, c_all = stats ? wall_clock64() : 0;  // 100 MHz ticks
+#define TICK(acc, stmt)                     \
+  do {                                      \
+    const int64_t t0_ = stats ? wall_clock64() : 0; \
+    stmt;                                   \
+    if (stats) acc += wall_clock64() - t0_; \
+  } while (0)
   double s = 0.0;
   for (int64_t kb = 0; kb < K; kb += 64) {
     const bool in = kb + lane < K;
@@ -597,7 +604,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
     while (f0 < 64 && kb + f0 < K) {
       int f;
       if (scan) {
-        f = tr_walk(tr_sel(lane < f0, tr_ident(), tv), s, lane);
+        TICK(c_scan, f = tr_walk(tr_sel(lane < f0, tr_ident(), tv), s, lane));
         ++n_scan;
       } else {  // the segment after a descended one, on its own
         double out = 0.0;
@@ -614,42 +621,66 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
         f = f0;
       }
       if (f >= 64 || kb + f >= K) break;
-      // segment kb + f does not apply at s: its sub-segments
+      // segment kb + f does not apply at s: its sub-segments.  Its terms go to LDS now (the loads overlap the
+      // scan over its subs, which skips the leading ones that apply); after the first failing sub, each sub is
+      // tried on its own (lane j applies its map to s) and the failing ones are added term by term.
       const int64_t k = kb + f;
       ++n_segdesc;
       const Tr u = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
-      bool loaded = false;
-      for (int j = 0; j < kSubs; ++j) {
-        double out = 0.0;
-        const bool ok = tr_apply(u, s, out);
-        const bool mine = (__ballot(ok) >> j) & 1;
-        const double sn = __shfl(out, j);
-        if (mine) {
-          s = sn;
-          continue;
-        }
-        if (!loaded) {
-          __syncthreads();  // the previous segment's LDS reads are done
-          fill_segment(sp, w, y, sy, n, k);
-          __syncthreads();
-          loaded = true;
+      __syncthreads();  // the previous segment's LDS reads are done
+      fill_segment(sp, w, y, sy, n, k);
+      int j;
+      TICK(c_scan, j = tr_walk(u, s, lane));
+      ++n_scan;
+      TICK(c_wait, __syncthreads());
+      while (j < kSubs) {
+        if (stats) {  // why this sub-segment did not apply (a diagnostic)
+          const uint64_t sb = (uint64_t)__double_as_longlong(s);
+          const int E = (int)((sb >> 52) & 0x7ff);
+          const uint32_t ufl = __shfl(u.fl, j);
+          const int ue = __shfl(u.e, j);
+          if (ufl & F_BAD) ++n_fbad;
+          else if (E == 0 || E == 0x7ff) ++n_fstate;
+          else if (E - 1023 != ue || (uint32_t)(sb >> 63) != (ufl & F_NEG)) ++n_fguess;
+          else ++n_frange;
         }
         const int64_t c0 = k * kSeg + (int64_t)j * kSub;
         const int i1 = (int)max<int64_t>(0, min<int64_t>(kSub, n - c0));
-        s = serial_terms(sp, j * kSub, j * kSub + i1, s, lane);
+        TICK(c_serial, s = serial_terms(sp, j * kSub, j * kSub + i1, s, lane));
         ++n_subser;
+        const int64_t t1 = stats ? wall_clock64() : 0;
+        for (++j; j < kSubs; ++j) {
+          double out = 0.0;
+          const bool ok = tr_apply(u, s, out);
+          const bool mine = (__ballot(ok) >> j) & 1;
+          const double sn = __shfl(out, j);
+          ++n_single;
+          if (!mine) break;
+          s = sn;
+        }
+        if (stats) c_single += wall_clock64() - t1;
       }
       f0 = f + 1;
       scan = false;
     }
   }
+#undef TICK
   if (t < 64)
     for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
   if (stats && t == 0) {
-    stats[v * 4 + 0] = n_scan;
-    stats[v * 4 + 1] = n_segdesc;
-    stats[v * 4 + 2] = n_single;
-    stats[v * 4 + 3] = n_subser;
+    stats[v * 8 + 0] = n_scan;
+    stats[v * 8 + 1] = n_segdesc;
+    stats[v * 8 + 2] = n_single;
+    stats[v * 8 + 3] = n_subser;
+    stats[v * 8 + 4] = n_fbad;
+    stats[v * 8 + 5] = n_fstate;
+    stats[v * 8 + 6] = n_fguess;
+    stats[v * 8 + 7] = n_frange;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 0] = c_scan;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 1] = c_single;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 2] = c_serial;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 3] = c_wait;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 4] = wall_clock64() - c_all;
   }
 }
 
@@ -701,17 +732,21 @@ int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t 
   static int64_t* dstats = nullptr;  // MSPLIT_SEQ_STATS=1: per-sum walk counters on stderr (a diagnostic)
   const char* st = getenv("MSPLIT_SEQ_STATS");
   const bool want = st && st[0] == '1';
-  if (want && !dstats && hipMalloc((void**)&dstats, 4 * MSK_MAX_GROUP * sizeof(int64_t)) != hipSuccess) dstats = nullptr;
+  if (want && !dstats && hipMalloc((void**)&dstats, 16 * MSK_MAX_GROUP * sizeof(int64_t)) != hipSuccess) dstats = nullptr;
   k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, partial, nchunks, stop,
                                                     want ? dstats : nullptr);
   if (want && dstats) {
-    int64_t h[4 * MSK_MAX_GROUP];
-    if (hipMemcpyAsync(h, dstats, 4 * nv * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+    int64_t h[16 * MSK_MAX_GROUP];
+    if (hipMemcpyAsync(h, dstats, 16 * MSK_MAX_GROUP * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
         hipStreamSynchronize(c->stream) == hipSuccess)
       for (int v = 0; v < nv; ++v)
-        fprintf(stderr, "seqx n=%lld nv=%d v=%d scans=%lld seg_desc=%lld single=%lld sub_serial=%lld\n",
-                (long long)n, nv, v, (long long)h[4 * v], (long long)h[4 * v + 1], (long long)h[4 * v + 2],
-                (long long)h[4 * v + 3]);
+        fprintf(stderr,
+                "seqx n=%lld nv=%d v=%d scans=%lld seg_desc=%lld single=%lld sub_serial=%lld f_bad=%lld f_state=%lld "
+                "f_guess=%lld f_range=%lld us_scan=%lld us_single=%lld us_serial=%lld us_wait=%lld us_all=%lld\n",
+                (long long)n, nv, v, (long long)h[8 * v], (long long)h[8 * v + 1], (long long)h[8 * v + 2],
+                (long long)h[8 * v + 3], (long long)h[8 * v + 4], (long long)h[8 * v + 5], (long long)h[8 * v + 6],
+                (long long)h[8 * v + 7], (long long)h[256 + 8 * v] / 100, (long long)h[256 + 8 * v + 1] / 100,
+                (long long)h[256 + 8 * v + 2] / 100, (long long)h[256 + 8 * v + 3] / 100, (long long)h[256 + 8 * v + 4] / 100);
   }
   return (int)hipGetLastError();
 }
