@@ -389,8 +389,8 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
   if (stopped(stop)) return;
   __shared__ double sp[kSeg + kSeg / kPer];  // products, one pad slot per 16: thread t's run at 17t
   __shared__ double ssum[kSubs];
-  __shared__ Tr str[kSubs];
-  const int t = threadIdx.x, j = t >> 2;
+  __shared__ Tr str[kT / 64];
+  const int t = threadIdx.x, lane = t & 63, j = t >> 2;
   const int64_t k = blockIdx.x, c0 = k * kSeg;
   const int cnt = (int)max<int64_t>(0, min<int64_t>(kPer, n - (c0 + (int64_t)kPer * t)));
   double xr[kPer];
@@ -504,18 +504,15 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
     if ((t & 3) == 0) {
       a = tr_comb(a, o);
       subT[((int64_t)v * K + k) * kSubs + j] = a;
-      str[j] = a;
     }
-    __syncthreads();
-    if (t < kSubs) {  // ordered tree over the 64 subs
-      Tr b = str[t];
 #pragma unroll
-      for (int s = 1; s < kSubs; s <<= 1) {
-        const Tr u = shfl_down_tr(b, s);
-        if ((t & (2 * s - 1)) == 0) b = tr_comb(b, u);
-      }
-      if (t == 0) segT[(int64_t)v * K + k] = b;
+    for (int s = 4; s < 64; s <<= 1) {  // each wave: the ordered tree over its 16 subs (leaders 0, 4, .., 60)
+      const Tr u = shfl_down_tr(a, s);
+      if ((lane & (2 * s - 1)) == 0) a = tr_comb(a, u);
     }
+    if (lane == 0) str[t >> 6] = a;
+    __syncthreads();
+    if (t == 0) segT[(int64_t)v * K + k] = tr_comb(tr_comb(str[0], str[1]), tr_comb(str[2], str[3]));
     __syncthreads();
   }
 }
