@@ -348,6 +348,27 @@ __device__ __forceinline__ Tr shfl_up_tr(const Tr& t, int o) {
   return r;
 }
 
+// wave-uniform copies of lane l's values (v_readlane into scalar registers: no LDS round trip)
+__device__ __forceinline__ int64_t rl64(int64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double rld(double x, int l) { return __longlong_as_double(rl64(__double_as_longlong(x), l)); }
+__device__ __forceinline__ Tr tr_lane(const Tr& t, int l) {
+  Tr r;
+  r.d0 = rl64(t.d0, l);
+  r.d1 = rl64(t.d1, l);
+  r.lo0 = rl64(t.lo0, l);
+  r.lo1 = rl64(t.lo1, l);
+  r.hi0 = rl64(t.hi0, l);
+  r.hi1 = rl64(t.hi1, l);
+  r.e = __builtin_amdgcn_readlane(t.e, l);
+  r.fl = (uint32_t)__builtin_amdgcn_readlane((int)t.fl, l);
+  r.pad = 0;
+  return r;
+}
+
 __device__ __forceinline__ const double* vec_row(const Vecs& V, int v) {
   return V.base ? V.base + (int64_t)v * V.stride : V.p[v];
 }
@@ -528,7 +549,7 @@ __device__ __forceinline__ int tr_walk(Tr t, double& s, int lane) {
   const bool ok = tr_apply(t, s, out);
   const uint64_t bad = __ballot(!ok);
   const int f = bad ? __builtin_ctzll(bad) : 64;
-  const double sn = __shfl(out, f > 0 ? f - 1 : 0);
+  const double sn = rld(out, f > 0 ? f - 1 : 0);
   if (f > 0) s = sn;
   return f;
 }
@@ -556,17 +577,20 @@ __device__ __forceinline__ void fill_segment(double* sp, const double* __restric
 __device__ __forceinline__ double serial_terms(const double* sp, int i0, int i1, double s, int lane) {
   double a = s;
   if (lane == 0) {
-    int i = i0;
-    for (; i + 8 <= i1; i += 8) {
-      double q[8];
+    if (i1 - i0 == kSub) {  // a whole sub-segment: all 64 terms in registers first, then the dependent adds
+      double2 q[kSub / 2];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) q[u] = sp[i + u];
+      for (int u = 0; u < kSub / 2; ++u) q[u] = *reinterpret_cast<const double2*>(sp + i0 + 2 * u);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a = a + q[u];
+      for (int u = 0; u < kSub / 2; ++u) {
+        a = a + q[u].x;
+        a = a + q[u].y;
+      }
+    } else {
+      for (int i = i0; i < i1; ++i) a = a + sp[i];
     }
-    for (; i < i1; ++i) a = a + sp[i];
   }
-  return __shfl(a, 0);
+  return rld(a, 0);
 }
 
 // Workgroup v: sum v, from +0.0.  Windows of 64 segment transducers are composed in a wave scan and the longest
@@ -604,10 +628,8 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
         TICK(c_scan, f = tr_walk(tr_sel(lane < f0, tr_ident(), tv), s, lane));
         ++n_scan;
       } else {  // the segment after a descended one, on its own
-        double out = 0.0;
-        const bool ok = tr_apply(tv, s, out);
-        const bool mine = (__ballot(ok) >> f0) & 1;
-        const double sn = __shfl(out, f0);
+        double sn = 0.0;
+        const bool mine = tr_apply(tr_lane(tv, f0), s, sn);  // wave-uniform: scalar registers
         ++n_single;
         if (mine) {
           s = sn;
@@ -647,10 +669,8 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
         ++n_subser;
         const int64_t t1 = stats ? wall_clock64() : 0;
         for (++j; j < kSubs; ++j) {
-          double out = 0.0;
-          const bool ok = tr_apply(u, s, out);
-          const bool mine = (__ballot(ok) >> j) & 1;
-          const double sn = __shfl(out, j);
+          double sn = 0.0;
+          const bool mine = tr_apply(tr_lane(u, j), s, sn);
           ++n_single;
           if (!mine) break;
           s = sn;
