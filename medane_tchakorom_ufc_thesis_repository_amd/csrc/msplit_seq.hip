@@ -188,6 +188,29 @@ __device__ __forceinline__ Tr tr_bad() {
   return t;
 }
 
+// decomp in f64: a = |p| * 2^(52-e) is exact (ldexp; an underflow only loses bits far below 1/2), its floor and
+// fractional part are exact, and the class is read from the fraction of |p|'s scaled value, never from 1 - f (which
+// can round onto 1/2).  Same (q, class) as decomp for every p.
+__device__ __forceinline__ bool decomp_f(double p, int e, uint32_t sneg, double& q, int& c) {
+  q = 0.0;
+  c = 0;
+  if (!isfinite(p)) return false;
+  const double a = ldexp(fabs(p), 52 - e);
+  if (a >= 9007199254740992.0) return false;  // |p| >= 2^(e+1)
+  const double qa = floor(a), fa = a - qa;
+  const bool neg = (signbit(p) ? 1u : 0u) != sneg;
+  if (!neg) {
+    q = qa;
+    c = fa > 0.5 ? 2 : (fa == 0.5 ? 1 : 0);
+  } else if (fa == 0.0) {
+    q = -qa;
+  } else {
+    q = -qa - 1.0;
+    c = fa < 0.5 ? 2 : (fa == 0.5 ? 1 : 0);
+  }
+  return true;
+}
+
 // field by field (a select of whole records becomes a private-memory copy)
 __device__ __forceinline__ Tr tr_sel(bool c, const Tr& a, const Tr& b) {
   Tr r;
@@ -460,15 +483,16 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
     const bool gok = GE != 0 && GE != 0x7ff;
     const int e = GE - 1023;
     const uint32_t sneg = (uint32_t)(gb >> 63);
-    // the lane's run: every term decomposed once, then input parity 0's track; parity 1's differs only through
-    // ties, so it is the same track unless the run holds one (then it is run again from the kept terms)
+    // the lane's run, in f64 arithmetic on integer values (exact below 2^53; a run that leaves that range cannot
+    // be valid and is marked BAD): every term decomposed once (decomp_f), then input parity 0's track; parity 1's
+    // differs only through ties, so it is the same track unless the run holds one (then it is run again)
     Tr a = tr_ident();
-    int64_t qv[kPer];
+    double qv[kPer];
     uint32_t cls = 0;  // 2 bits per term: 0 / 1 (tie) / 2 as decomp's class, 3: a +-0 term (no effect)
     bool bad = false;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      qv[i] = 0;
+      qv[i] = 0.0;
       uint32_t ci = 3;
       if (i < cnt) {
         const uint64_t b = (uint64_t)__double_as_longlong(pr[i]);
@@ -480,22 +504,24 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
             a.e = e;
           }
           int c = 0;
-          if (!gok || !decomp(pr[i], e, sneg, qv[i], c)) bad = true;
+          if (!gok || !decomp_f(pr[i], e, sneg, qv[i], c)) bad = true;
           ci = (uint32_t)c;
         }
       }
       cls |= ci << (2 * i);
     }
     if (!(a.fl & F_ZERO)) {
+      const double big = (double)kBig;
+      double d0 = 0.0, lo0 = big, hi0 = -big, d1 = 0.0, lo1 = big, hi1 = -big;
       bool tie = false;
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
         const uint32_t ci = (cls >> (2 * i)) & 3u;
         if (ci == 3) continue;
-        const int64_t q = qv[i];
-        a.lo0 = min(a.lo0, a.d0 + q);
-        a.d0 += q + (ci == 2 ? 1 : 0) + (ci == 1 ? ((a.d0 + q) & 1) : 0);
-        a.hi0 = max(a.hi0, a.d0);
+        const double x = d0 + qv[i];
+        lo0 = fmin(lo0, x);
+        d0 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? x - 2.0 * floor(0.5 * x) : 0.0);  // a tie rounds to even
+        hi0 = fmax(hi0, d0);
         tie |= ci == 1;
       }
       if (tie) {
@@ -503,20 +529,27 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
         for (int i = 0; i < kPer; ++i) {
           const uint32_t ci = (cls >> (2 * i)) & 3u;
           if (ci == 3) continue;
-          const int64_t q = qv[i];
-          a.lo1 = min(a.lo1, a.d1 + q);
-          a.d1 += q + (ci == 2 ? 1 : 0) + (ci == 1 ? ((1 + a.d1 + q) & 1) : 0);
-          a.hi1 = max(a.hi1, a.d1);
+          const double x = d1 + qv[i];
+          lo1 = fmin(lo1, x);
+          d1 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? (x + 1.0) - 2.0 * floor(0.5 * (x + 1.0)) : 0.0);
+          hi1 = fmax(hi1, d1);
         }
       } else {
-        a.d1 = a.d0;
-        a.lo1 = a.lo0;
-        a.hi1 = a.hi0;
+        d1 = d0;
+        lo1 = lo0;
+        hi1 = hi0;
       }
-      if (bad) a.fl |= F_BAD;
-      if (a.d0 > kLim || a.d0 < -kLim || a.d1 > kLim || a.d1 < -kLim) {
+      const double lim = 4503599627370496.0;  // 2^52: every offset of a valid run is below this
+      if (bad || fabs(d0) > lim || fabs(d1) > lim || (lo0 < big && fabs(lo0) > lim) ||
+          (lo1 < big && fabs(lo1) > lim) || (hi0 > -big && fabs(hi0) > lim) || (hi1 > -big && fabs(hi1) > lim)) {
         a.fl |= F_BAD;
-        a.d0 = a.d1 = 0;
+      } else {
+        a.d0 = (int64_t)d0;
+        a.d1 = (int64_t)d1;
+        a.lo0 = (int64_t)lo0;
+        a.lo1 = (int64_t)lo1;
+        a.hi0 = (int64_t)hi0;
+        a.hi1 = (int64_t)hi1;
       }
     }
     Tr o = shfl_xor_tr(a, 1);

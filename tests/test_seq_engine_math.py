@@ -62,7 +62,7 @@ def ident():
     return dict(d=[0, 0], lo=[BIG, BIG], hi=[-BIG, -BIG], e=0, neg=0, bad=False, zero=True, nzero=True)
 
 
-def run(ps, e, sneg, gok):
+def run(ps, e, sneg, gok, dec=decomp):
     """The lane run of k_seqx_trans: terms decomposed once, parity 0's track, parity 1's only if a tie occurs."""
     t = ident()
     qc = []
@@ -75,11 +75,11 @@ def run(ps, e, sneg, gok):
             continue
         if t["zero"]:
             t.update(zero=False, nzero=False, neg=sneg, e=e)
-        r = decomp(p, e, sneg) if gok else None
+        r = dec(p, e, sneg) if gok else None
         if r is None:
             t["bad"] = True
             r = (0, 0)
-        qc.append(r)
+        qc.append((int(r[0]), r[1]))
     if t["zero"]:
         return t
     tie = False
@@ -153,7 +153,7 @@ def seqsum(ps, s=0.0):
     return s
 
 
-def engine(ps, sub=16, per=4, jitter=1e-9, seed=0):
+def engine(ps, sub=16, per=4, jitter=1e-9, seed=0, dec=None):
     """Sub-segment transducers built from lane runs of `per` terms in the binade of a jittered guess, applied where
     valid; the rest term by term with the f64 add (the walk's serial sub-segments)."""
     rng = np.random.default_rng(seed)
@@ -162,7 +162,7 @@ def engine(ps, sub=16, per=4, jitter=1e-9, seed=0):
     while i < n:
         j = min(n, i + sub)
         gok, e, sn = guess(float(pre[i]) * (1.0 + jitter * rng.uniform(-1, 1)))
-        lanes = [run(ps[k:min(k + per, j)], e, sn, gok) for k in range(i, j, per)]
+        lanes = [run(ps[k:min(k + per, j)], e, sn, gok, dec or decomp) for k in range(i, j, per)]
         t = lanes[0]
         for u in lanes[1:]:
             t = comb(t, u)
@@ -199,10 +199,11 @@ CASES = _cases()
 
 @pytest.mark.parametrize("name", list(CASES))
 @pytest.mark.parametrize("jitter", [0.0, 1e-9, 0.3])
-def test_engine_walk_is_the_sequential_sum(name, jitter):
+@pytest.mark.parametrize("dec", ["int", "f64"])
+def test_engine_walk_is_the_sequential_sum(name, jitter, dec):
     ps = [float(v) for v in CASES[name]]
     ref = seqsum(ps)
-    got, fast = engine(ps, jitter=jitter)
+    got, fast = engine(ps, jitter=jitter, dec=decomp if dec == "int" else globals()["decomp_f"])
     assert bits(got) == bits(ref), (got, ref)
 
 
@@ -236,3 +237,52 @@ def test_composition_is_associative(name):
     r = apply(left, s0)
     if r is not None:
         assert bits(r) == bits(seqsum(ps[1:241], s0))
+
+
+def decomp_f(p, e, sneg):
+    """k_seqx_trans's f64 decomposition: a = |p| * 2^(52-e) by ldexp, its exact floor and fraction."""
+    if not math.isfinite(p):
+        return None
+    a = math.ldexp(abs(p), 52 - e)
+    if a >= 2.0 ** 53:
+        return None
+    qa = math.floor(a)
+    fa = a - qa
+    neg = (1 if math.copysign(1.0, p) < 0 else 0) != sneg
+    if not neg:
+        return qa, (2 if fa > 0.5 else (1 if fa == 0.5 else 0))
+    if fa == 0.0:
+        return -qa, 0
+    return -qa - 1, (2 if fa < 0.5 else (1 if fa == 0.5 else 0))
+
+
+def test_f64_decomposition_equals_the_integer_one():
+    """The device decomposes terms in f64; it must give decomp's (q, class) for every term the walk can meet,
+    including halves and near-halves of the state's ulp, subnormals, terms far below the ulp and terms at 2^(e+1)."""
+    rng = np.random.default_rng(7)
+    es = [-1022, -1000, -300, -60, -5, 0, 1, 30, 52, 53, 200, 1023]
+    for e in es:
+        u = 2.0 ** (e - 52) if e - 52 >= -1074 else 0.0
+        ps = list(rng.standard_normal(300) * 2.0 ** e)
+        ps += list(rng.standard_normal(300) * 2.0 ** (e - 40))
+        if u:
+            for k in range(1, 60):
+                for m in (1, 3, 5):
+                    h = u * m / 2.0 ** k
+                    ps += [h, -h, math.nextafter(h, 0.0), -math.nextafter(h, 0.0), math.nextafter(h, math.inf)]
+        ps += [2.0 ** e, -(2.0 ** e), 2.0 ** (e + 1) if e < 1023 else math.inf, 5e-324, -5e-324, 2.2e-308,
+               math.nextafter(2.0 ** (e + 1), 0.0) if e < 1023 else 1.0, math.inf, -math.inf, math.nan]
+        for p in ps:
+            for sneg in (0, 1):
+                if p == 0.0:
+                    continue
+                r_int, r_f = decomp(p, e, sneg), decomp_f(p, e, sneg)
+                if r_int is None or r_f is None:
+                    assert r_int is None and r_f is None, (p, e, sneg, r_int, r_f)
+                elif r_int != (int(r_f[0]), r_f[1]):
+                    # the one benign difference: a negative term so far below the ulp that |p| * 2^(52-e)
+                    # underflows to 0.  decomp says (floor -1, fraction > 1/2), decomp_f says (0, 0): the same
+                    # increment (0, the state is unchanged, as the f64 add rounds it), and a lowest exact sum one
+                    # unit higher, which is exact in the only case it decides (s = 2^e: RN(2^e - tiny) = 2^e).
+                    assert r_int == (-1, 2) and r_f == (0, 0) and math.ldexp(abs(p), 52 - e) == 0.0, \
+                        (p, e, sneg, r_int, r_f)
