@@ -297,149 +297,6 @@ __device__ __forceinline__ bool tr_apply(const Tr& t, double s, double& out) {
   return true;
 }
 
-// p / 2^(e-52), sign-flipped when the state is negative, as q = floor and the fraction's class c (0: < 1/2,
-// 1: == 1/2, 2: > 1/2); false for a non-finite p or |p| >= 2^(e+1).  In f64: a = |p| * 2^(52-e) is exact (ldexp;
-// an underflow only loses bits far below 1/2), its floor and fraction are exact, and the class is read from the
-// fraction of |p|'s scaled value, never from 1 - f (which can round onto 1/2).  tests/test_seq_engine_math.py
-// holds it to the integer decomposition of p's bits.
-__device__ __forceinline__ bool decomp_f(double p, int e, uint32_t sneg, double& q, int& c) {
-  q = 0.0;
-  c = 0;
-  if (!isfinite(p)) return false;
-  const double a = ldexp(fabs(p), 52 - e);
-  if (a >= 9007199254740992.0) return false;  // |p| >= 2^(e+1)
-  const double qa = floor(a), fa = a - qa;
-  const bool neg = (signbit(p) ? 1u : 0u) != sneg;
-  if (!neg) {
-    q = qa;
-    c = fa > 0.5 ? 2 : (fa == 0.5 ? 1 : 0);
-  } else if (fa == 0.0) {
-    q = -qa;
-  } else {
-    q = -qa - 1.0;
-    c = fa < 0.5 ? 2 : (fa == 0.5 ? 1 : 0);
-  }
-  return true;
-}
-
-// field by field (a select of whole records becomes a private-memory copy)
-__device__ __forceinline__ Tr tr_sel(bool c, const Tr& a, const Tr& b) {
-  Tr r;
-  r.d0 = c ? a.d0 : b.d0;
-  r.d1 = c ? a.d1 : b.d1;
-  r.lo0 = c ? a.lo0 : b.lo0;
-  r.lo1 = c ? a.lo1 : b.lo1;
-  r.hi0 = c ? a.hi0 : b.hi0;
-  r.hi1 = c ? a.hi1 : b.hi1;
-  r.e = c ? a.e : b.e;
-  r.fl = c ? a.fl : b.fl;
-  r.pad = 0;
-  return r;
-}
-
-__device__ __forceinline__ Tr tr_load(const Tr* p) {
-  const int4* q = reinterpret_cast<const int4*>(p);
-  const int4 a = q[0], b = q[1], c = q[2], d = q[3];
-  Tr r;
-  r.d0 = (int64_t)(((uint64_t)(uint32_t)a.y << 32) | (uint32_t)a.x);
-  r.d1 = (int64_t)(((uint64_t)(uint32_t)a.w << 32) | (uint32_t)a.z);
-  r.lo0 = (int64_t)(((uint64_t)(uint32_t)b.y << 32) | (uint32_t)b.x);
-  r.lo1 = (int64_t)(((uint64_t)(uint32_t)b.w << 32) | (uint32_t)b.z);
-  r.hi0 = (int64_t)(((uint64_t)(uint32_t)c.y << 32) | (uint32_t)c.x);
-  r.hi1 = (int64_t)(((uint64_t)(uint32_t)c.w << 32) | (uint32_t)c.z);
-  r.e = d.x;
-  r.fl = (uint32_t)d.y;
-  r.pad = 0;
-  return r;
-}
-
-// c ? x1 : x0 as arithmetic on the difference: a select of two loaded fields would be folded into a select of
-// their addresses, and the record would go to private memory
-__device__ __forceinline__ int64_t pick(bool c, int64_t x1, int64_t x0) { return x0 + (c ? x1 - x0 : 0); }
-
-__device__ __forceinline__ int64_t clampb(int64_t v) { return v < -kBig ? -kBig : (v > kBig ? kBig : v); }
-
-// a, then b
-__device__ __forceinline__ Tr tr_comb(const Tr& a, const Tr& b) {
-  if (a.fl & F_ZERO) {
-    Tr r = b;
-    if (!(a.fl & F_NZERO)) r.fl &= ~F_NZERO;
-    return r;
-  }
-  if (b.fl & F_ZERO) return a;
-  Tr r;
-  r.e = a.e;
-  r.pad = 0;
-  r.fl = ((a.fl | b.fl) & F_BAD) | (a.fl & F_NEG);
-  if (a.e != b.e || ((a.fl ^ b.fl) & F_NEG)) r.fl |= F_BAD;
-  // input parity 0 leaves a with parity (a.d0 & 1), input parity 1 with ((1 + a.d1) & 1)
-  const bool q0 = (a.d0 & 1) != 0, q1 = (a.d1 & 1) == 0;
-  int64_t d0 = a.d0 + pick(q0, b.d1, b.d0), d1 = a.d1 + pick(q1, b.d1, b.d0);
-  r.lo0 = clampb(min(a.lo0, a.d0 + pick(q0, b.lo1, b.lo0)));
-  r.lo1 = clampb(min(a.lo1, a.d1 + pick(q1, b.lo1, b.lo0)));
-  r.hi0 = clampb(max(a.hi0, a.d0 + pick(q0, b.hi1, b.hi0)));
-  r.hi1 = clampb(max(a.hi1, a.d1 + pick(q1, b.hi1, b.hi0)));
-  if (d0 > kLim || d0 < -kLim || d1 > kLim || d1 < -kLim) {
-    r.fl |= F_BAD;
-    d0 = d1 = 0;
-  }
-  r.d0 = d0;
-  r.d1 = d1;
-  return r;
-}
-
-// s after the run, or false when the run is not known to be a translation at s
-__device__ __forceinline__ bool tr_apply(const Tr& t, double s, double& out) {
-  if (t.fl & F_ZERO) {
-    out = s == 0.0 ? ((signbit(s) && (t.fl & F_NZERO)) ? -0.0 : 0.0) : s;
-    return true;
-  }
-  if (t.fl & F_BAD) return false;
-  const uint64_t b = (uint64_t)__double_as_longlong(s);
-  const int E = (int)((b >> 52) & 0x7ff);
-  if (E == 0 || E == 0x7ff) return false;
-  if (E - 1023 != t.e || (uint32_t)(b >> 63) != (t.fl & F_NEG)) return false;
-  const int64_t M = (int64_t)((b & kFrac) | (uint64_t(1) << 52));
-  const bool odd = (M & 1) != 0;
-  if (M + pick(odd, t.lo1, t.lo0) < kM0 || M + pick(odd, t.hi1, t.hi0) >= kM1) return false;
-  out = __longlong_as_double((long long)((b & ~kFrac) | (uint64_t)(M + pick(odd, t.d1, t.d0) - kM0)));
-  return true;
-}
-
-// p / 2^(e-52), sign-flipped when the state is negative, as q = floor and the fraction's class c (0: < 1/2,
-// 1: == 1/2, 2: > 1/2), exactly, from p's bits.  False for a non-finite p or |p| >= 2^(e+1).
-__device__ __forceinline__ bool decomp(double p, int e, uint32_t sneg, int64_t& q, int& c) {
-  const uint64_t b = (uint64_t)__double_as_longlong(p);
-  int E = (int)((b >> 52) & 0x7ff);
-  q = 0;
-  c = 0;
-  if (E == 0x7ff) return false;
-  uint64_t m = b & kFrac;
-  if (E) m |= uint64_t(1) << 52;
-  else E = 1;
-  if (m == 0) return true;
-  const int sh = E - 1023 - e;
-  if (sh > 0) return false;
-  const bool neg = (uint32_t)(b >> 63) != sneg;
-  int k = -sh;
-  if (k == 0) {
-    q = neg ? -(int64_t)m : (int64_t)m;
-    return true;
-  }
-  if (k > 63) k = 63;  // m < 2^53 <= the half: the same classes
-  const uint64_t qq = m >> k, rr = m & ((uint64_t(1) << k) - 1), half = uint64_t(1) << (k - 1);
-  if (!neg) {
-    q = (int64_t)qq;
-    c = rr > half ? 2 : (rr == half ? 1 : 0);
-  } else if (rr == 0) {
-    q = -(int64_t)qq;
-  } else {
-    q = -(int64_t)qq - 1;
-    c = rr < half ? 2 : (rr == half ? 1 : 0);
-  }
-  return true;
-}
-
 __device__ __forceinline__ Tr shfl_xor_tr(const Tr& t, int m) {
   Tr r;
   r.d0 = __shfl_xor(t.d0, m);
