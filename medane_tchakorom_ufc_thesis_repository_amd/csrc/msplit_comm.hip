@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "msplit_ctx.hpp"
@@ -69,6 +70,11 @@ struct msp_comm {
   double* hsend = nullptr;  // pinned staging (host transport)
   double* hrecv = nullptr;
   int64_t hcap = 0;         // doubles per rank
+  double* dx = nullptr;     // host-transport exchange: [lo | hi] packed planes, then every rank's pair; persistent
+  int64_t dxcap = 0;        // count it was sized for
+  double* dsum = nullptr;   // msp_comm_sum_ordered: [own n | gathered nranks*n] on the device, persistent
+  double* hsum = nullptr;   //                       pinned host mirror of the same
+  int32_t sumcap = 0;       // n it was sized for
 };
 
 #define NCCLCHK(call)                                                                            \
@@ -140,6 +146,9 @@ extern "C" int msp_comm_destroy(msp_comm** pm) {
   if (m->nccl) (void)rccl().comm_destroy(m->nccl);
   if (m->hsend) (void)hipHostFree(m->hsend);
   if (m->hrecv) (void)hipHostFree(m->hrecv);
+  if (m->dx) (void)hipFree(m->dx);
+  if (m->dsum) (void)hipFree(m->dsum);
+  if (m->hsum) (void)hipHostFree(m->hsum);
   msp_ctx* c = m->ctx;
   delete m;
   *pm = nullptr;
@@ -180,6 +189,10 @@ extern "C" int mspi_comm_allgather(msp_comm* m, const double* send, double* recv
   }
   HIPCHK(hipMemcpyAsync(recv, m->hrecv, (size_t)count * m->nranks * sizeof(double), hipMemcpyHostToDevice,
                         c->stream));
+  // the gathered values are on the device before anything else is enqueued: a device-to-host copy of them right
+  // after this host-to-device one has been seen to read the previous contents (one-GPU multi-rank runs), and
+  // this path waits on MPI anyway
+  HIPCHK(hipStreamSynchronize(c->stream));
   return MSP_SUCCESS;
 }
 
@@ -226,11 +239,18 @@ extern "C" int msp_comm_exchange_neighbors(msp_comm* m, const msp_vec* src, int6
     NCCLCHK(rccl().group_end());
     return MSP_SUCCESS;
   }
-  // host transport: [lo plane | hi plane] of every rank, gathered
-  double* pk = nullptr;
-  double* all = nullptr;
-  HIPCHK(hipMallocAsync((void**)&pk, (size_t)2 * count * sizeof(double), c->stream));
-  HIPCHK(hipMallocAsync((void**)&all, (size_t)2 * count * m->nranks * sizeof(double), c->stream));
+  // host transport: [lo plane | hi plane] of every rank, gathered.  Persistent device buffers (no stream-ordered
+  // allocation: one-GPU multi-rank runs saw the planes of a freed-and-reused block), every copy host-synchronised
+  if (count > m->dxcap) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (m->dx) HIPCHK(hipFree(m->dx));
+    m->dx = nullptr;
+    m->dxcap = 0;
+    HIPCHK(hipMalloc((void**)&m->dx, (size_t)2 * count * (1 + (size_t)m->nranks) * sizeof(double)));
+    m->dxcap = count;
+  }
+  double* pk = m->dx;
+  double* all = m->dx + 2 * count;
   const size_t bytes = (size_t)count * sizeof(double);
   int rc = MSP_SUCCESS;
   if (lo) HIPCHK(hipMemcpyAsync(pk, src->d + lo_src, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -242,8 +262,7 @@ extern "C" int msp_comm_exchange_neighbors(msp_comm* m, const msp_vec* src, int6
   if (!rc && hi)  // rank+1 sent its lo plane
     rc = hipMemcpyAsync(dst->d + hi_dst, all + (size_t)(m->rank + 1) * 2 * count, bytes, hipMemcpyDeviceToDevice,
                         c->stream) == hipSuccess ? MSP_SUCCESS : MSP_ERR_LIB;
-  (void)hipFreeAsync(pk, c->stream);
-  (void)hipFreeAsync(all, c->stream);
+  if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = MSP_ERR_LIB;
   if (rc == MSP_ERR_LIB) mspi_set_error(MSP_ERR_LIB, "device copy of a received plane failed");
   return rc;
 }
@@ -258,31 +277,34 @@ extern "C" int msp_comm_sum_ordered(msp_comm* m, const double* in, double* out, 
   if (n == 0) return MSP_SUCCESS;
   msp_ctx* c = m->ctx;
   const size_t per = (size_t)n * sizeof(double);
-  double* d = nullptr;
-  HIPCHK(hipMallocAsync((void**)&d, per * (1 + (size_t)m->nranks), c->stream));
-  HIPCHK(hipMemcpyAsync(d, in, per, hipMemcpyHostToDevice, c->stream));
-  int rc = mspi_comm_allgather(m, d, d + n, n);
-  double* h = (double*)malloc(per * (size_t)m->nranks);
-  if (!rc && !h) {
-    mspi_set_error(MSP_ERR_MEM, "allocation failed");
-    rc = MSP_ERR_MEM;
+  const size_t tot = per * (1 + (size_t)m->nranks);
+  if (n > m->sumcap) {  // persistent buffers: no stream-ordered allocation inside a collective's lifetime
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (m->dsum) HIPCHK(hipFree(m->dsum));
+    if (m->hsum) HIPCHK(hipHostFree(m->hsum));
+    m->dsum = nullptr;
+    m->hsum = nullptr;
+    m->sumcap = 0;
+    HIPCHK(hipMalloc((void**)&m->dsum, tot));
+    HIPCHK(hipHostMalloc((void**)&m->hsum, tot, hipHostMallocDefault));
+    m->sumcap = n;
   }
-  if (!rc && hipMemcpyAsync(h, d + n, per * m->nranks, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
-    mspi_set_error(MSP_ERR_LIB, "copy of the gathered values failed");
-    rc = MSP_ERR_LIB;
+  // the contribution goes up from pinned memory and is on the device before the collective is enqueued, and the
+  // gathered values are read back only after the collective has completed: each side of the all-gather is ordered
+  // by a host synchronisation, not only by the stream (the one-GPU multi-rank runs read a slot of the previous
+  // call's values, or an unwritten one, with stream order alone -- a missing block in one outer residual norm)
+  memcpy(m->hsum, in, per);
+  HIPCHK(hipMemcpyAsync(m->dsum, m->hsum, per, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int rc = mspi_comm_allgather(m, m->dsum, m->dsum + n, n);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpyAsync(m->hsum + n, m->dsum + n, per * m->nranks, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int32_t i = 0; i < n; ++i) {
+    double acc = 0.0;
+    for (int32_t r = 0; r < m->nranks; ++r) acc += m->hsum[n + (size_t)r * n + i];
+    out[i] = acc;
   }
-  (void)hipFreeAsync(d, c->stream);
-  if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) {
-    mspi_set_error(MSP_ERR_LIB, "stream synchronisation failed");
-    rc = MSP_ERR_LIB;
-  }
-  if (!rc) {
-    for (int32_t i = 0; i < n; ++i) {
-      double acc = 0.0;
-      for (int32_t r = 0; r < m->nranks; ++r) acc += h[(size_t)r * n + i];
-      out[i] = acc;
-    }
-  }
-  free(h);
-  return rc;
+  return MSP_SUCCESS;
 }
