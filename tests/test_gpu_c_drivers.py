@@ -30,12 +30,13 @@ def built():
 MPI_LAUNCH = ["-launcher", "fork", "-iface", "lo"]
 
 
-def _run(args, mpi=0, timeout=150):
+def _run(args, mpi=0, timeout=150, env=None):
     """Run a C host driver (under mpiexec with mpi ranks); its last JSON line.  The whole process group is
     killed at the time limit (no rank is left holding the GPU) and the test fails with what it printed."""
     exe = os.path.join(HOST, "msplit_driver_mpi" if mpi else "msplit_driver")
     cmd = ([MPIEXEC] + MPI_LAUNCH + ["-n", str(mpi)] if mpi else []) + [exe] + args + ["-json"]
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True,
+                         env=None if env is None else {**os.environ, **env})
     try:
         out, err = p.communicate(timeout=timeout)
     except subprocess.TimeoutExpired:
@@ -141,6 +142,22 @@ def test_c_host_mpi_ranks_equal_oracle(ctx, oracle, built, case):
     assert got["final_norm"] == one["final_norm"] and got["error"] == one["error"]
     if prog == SMSM:
         assert got["final_norm"] == want["final_norm"]
+
+
+@pytest.mark.parametrize("case", [MPI_CASES[1], MPI_CASES[6]], ids=["smsm-3d-2ranks", "sm-2d-4ranks"])
+def test_c_host_mpi_serialized_equals_oracle(ctx, oracle, built, case):
+    """The same multi-rank runs with every kernel and copy serialised by the HIP runtime (AMD_SERIALIZE_KERNEL=3,
+    AMD_SERIALIZE_COPY=3).  Before round 4's fix the host-transport exchange and ordered sum staged through
+    hipMallocAsync/hipFreeAsync blocks that were reused while a copy was still in flight.  Under serialisation that
+    failed every case from the first outer iteration: this 3D SMSM-global case gave r03's 5 outer iterations
+    against the oracle's 3 (profiles/r04/comm_fix/).  A result that depends on how the runtime overlaps copies and
+    kernels fails here."""
+    prog, dim, nx, ny, nz, nb, s, rtol = case
+    args = _problem_args(prog, dim, nx, ny, nz, nb, s, rtol)
+    want = _oracle_record(oracle, prog, dim, nx, ny, nz, nb, s, rtol)
+    got = _run(args + ["-msplit_transport", "host"], mpi=nb, env={"AMD_SERIALIZE_KERNEL": "3", "AMD_SERIALIZE_COPY": "3"})
+    assert got["ranks"] == nb and got["transport"] == "host"
+    _assert_same_run(got, want, f"{nb} MPI ranks, serialised, vs oracle")
 
 
 # RCCL refuses two ranks of one host on one GPU ("Duplicate GPU detected").  With a different NCCL_HOSTID per rank it
