@@ -747,15 +747,16 @@ int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t 
   if (rc) return rc;
   k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, stop);
   k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop);
-  static int64_t* dstats = nullptr;  // MSPLIT_SEQ_STATS=1: per-sum walk counters on stderr (a diagnostic)
+  // MSPLIT_SEQ_STATS=1: per-sum walk counters on stderr (a diagnostic; its buffer lives for this call only)
   const char* st = getenv("MSPLIT_SEQ_STATS");
-  const bool want = st && st[0] == '1';
-  if (want && !dstats && hipMalloc((void**)&dstats, 16 * MSK_MAX_GROUP * sizeof(int64_t)) != hipSuccess) dstats = nullptr;
+  int64_t* dstats = nullptr;
+  if (st && st[0] == '1' && hipMalloc((void**)&dstats, 16 * MSK_MAX_GROUP * sizeof(int64_t)) != hipSuccess)
+    dstats = nullptr;
   k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, partial, nchunks, stop,
-                                                    want ? dstats : nullptr);
-  if (want && dstats) {
+                                                        dstats);
+  if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];
-    if (hipMemcpyAsync(h, dstats, 16 * MSK_MAX_GROUP * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+    if (hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
         hipStreamSynchronize(c->stream) == hipSuccess)
       for (int v = 0; v < nv; ++v)
         fprintf(stderr,
@@ -764,7 +765,9 @@ int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t 
                 (long long)n, nv, v, (long long)h[8 * v], (long long)h[8 * v + 1], (long long)h[8 * v + 2],
                 (long long)h[8 * v + 3], (long long)h[8 * v + 4], (long long)h[8 * v + 5], (long long)h[8 * v + 6],
                 (long long)h[8 * v + 7], (long long)h[256 + 8 * v] / 100, (long long)h[256 + 8 * v + 1] / 100,
-                (long long)h[256 + 8 * v + 2] / 100, (long long)h[256 + 8 * v + 3] / 100, (long long)h[256 + 8 * v + 4] / 100);
+                (long long)h[256 + 8 * v + 2] / 100, (long long)h[256 + 8 * v + 3] / 100,
+                (long long)h[256 + 8 * v + 4] / 100);
+    (void)hipFree(dstats);
   }
   return (int)hipGetLastError();
 }
