@@ -155,16 +155,18 @@ constexpr int kSeg = MSK_DBR_CHUNK;  // one segment = one DBR chunk (its partial
 constexpr int kSub = 64;             // terms per sub-segment (one per lane in the walk)
 constexpr int kSubs = kSeg / kSub;
 constexpr int kPer = kSeg / kT;      // contiguous terms per thread in k_seqx_trans
-constexpr int64_t kM0 = int64_t(1) << 52, kM1 = int64_t(1) << 53;
-constexpr int64_t kLim = int64_t(1) << 56, kBig = int64_t(1) << 60;
+constexpr double kM0 = 4503599627370496.0, kM1 = 9007199254740992.0;  // 2^52, 2^53
+constexpr double kLim = 4503599627370496.0, kBig = 1152921504606846976.0;  // 2^52 (a valid run's offsets are below), 2^60
 constexpr uint64_t kFrac = (uint64_t(1) << 52) - 1;
 constexpr uint32_t F_NEG = 1, F_BAD = 2, F_ZERO = 4, F_NZERO = 8;
 
 // A run of terms as a map of the state M (s = +-M * 2^(e-52)): for input parity pi, M -> M + d[pi], valid iff
 // M + lo[pi] >= 2^52 (every exact sum >= 2^e) and M + hi[pi] < 2^53 (every result < 2^(e+1)).  F_ZERO: every term
 // is +-0 (identity; F_NZERO: all -0.0, so a -0.0 state stays -0.0); F_BAD: not a translation of one binade.
+// The offsets are integers held in f64: exact below 2^53, and a valid run's are below 2^52 in magnitude (a sum that
+// leaves that range marks the run BAD); +-2^60 stand for "no bound" and stay beyond 2^53 whatever is added to them.
 struct alignas(16) Tr {  // scalar fields, no arrays: a select between two of them must not become a private index
-  int64_t d0, d1, lo0, lo1, hi0, hi1;
+  double d0, d1, lo0, lo1, hi0, hi1;
   int32_t e;
   uint32_t fl;
   int64_t pad;
@@ -173,7 +175,7 @@ static_assert(sizeof(Tr) == 64, "Tr is one 64-byte record");
 
 __device__ __forceinline__ Tr tr_ident() {
   Tr t;
-  t.d0 = t.d1 = 0;
+  t.d0 = t.d1 = 0.0;
   t.lo0 = t.lo1 = kBig;
   t.hi0 = t.hi1 = -kBig;
   t.e = 0;
@@ -228,27 +230,39 @@ __device__ __forceinline__ Tr tr_sel(bool c, const Tr& a, const Tr& b) {
   return r;
 }
 
+__device__ __forceinline__ double dbl(int lo, int hi) {
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
 __device__ __forceinline__ Tr tr_load(const Tr* p) {
   const int4* q = reinterpret_cast<const int4*>(p);
   const int4 a = q[0], b = q[1], c = q[2], d = q[3];
   Tr r;
-  r.d0 = (int64_t)(((uint64_t)(uint32_t)a.y << 32) | (uint32_t)a.x);
-  r.d1 = (int64_t)(((uint64_t)(uint32_t)a.w << 32) | (uint32_t)a.z);
-  r.lo0 = (int64_t)(((uint64_t)(uint32_t)b.y << 32) | (uint32_t)b.x);
-  r.lo1 = (int64_t)(((uint64_t)(uint32_t)b.w << 32) | (uint32_t)b.z);
-  r.hi0 = (int64_t)(((uint64_t)(uint32_t)c.y << 32) | (uint32_t)c.x);
-  r.hi1 = (int64_t)(((uint64_t)(uint32_t)c.w << 32) | (uint32_t)c.z);
+  r.d0 = dbl(a.x, a.y);
+  r.d1 = dbl(a.z, a.w);
+  r.lo0 = dbl(b.x, b.y);
+  r.lo1 = dbl(b.z, b.w);
+  r.hi0 = dbl(c.x, c.y);
+  r.hi1 = dbl(c.z, c.w);
   r.e = d.x;
   r.fl = (uint32_t)d.y;
   r.pad = 0;
   return r;
 }
 
-// c ? x1 : x0 as arithmetic on the difference: a select of two loaded fields would be folded into a select of
-// their addresses, and the record would go to private memory
+// c ? x1 : x0 as integer arithmetic on the bit patterns: a select of two loaded fields would be folded into a
+// select of their addresses, and the record would go to private memory
 __device__ __forceinline__ int64_t pick(bool c, int64_t x1, int64_t x0) { return x0 + (c ? x1 - x0 : 0); }
+__device__ __forceinline__ double pickd(bool c, double x1, double x0) {
+  return __longlong_as_double(pick(c, __double_as_longlong(x1), __double_as_longlong(x0)));
+}
 
-__device__ __forceinline__ int64_t clampb(int64_t v) { return v < -kBig ? -kBig : (v > kBig ? kBig : v); }
+__device__ __forceinline__ double clampb(double v) { return fmin(fmax(v, -kBig), kBig); }
+
+// an integer-valued f64 below 2^53 is odd
+__device__ __forceinline__ bool odd(double x) {
+  const double h = 0.5 * x;
+  return h != floor(h);
+}
 
 // a, then b
 __device__ __forceinline__ Tr tr_comb(const Tr& a, const Tr& b) {
@@ -264,15 +278,15 @@ __device__ __forceinline__ Tr tr_comb(const Tr& a, const Tr& b) {
   r.fl = ((a.fl | b.fl) & F_BAD) | (a.fl & F_NEG);
   if (a.e != b.e || ((a.fl ^ b.fl) & F_NEG)) r.fl |= F_BAD;
   // input parity 0 leaves a with parity (a.d0 & 1), input parity 1 with ((1 + a.d1) & 1)
-  const bool q0 = (a.d0 & 1) != 0, q1 = (a.d1 & 1) == 0;
-  int64_t d0 = a.d0 + pick(q0, b.d1, b.d0), d1 = a.d1 + pick(q1, b.d1, b.d0);
-  r.lo0 = clampb(min(a.lo0, a.d0 + pick(q0, b.lo1, b.lo0)));
-  r.lo1 = clampb(min(a.lo1, a.d1 + pick(q1, b.lo1, b.lo0)));
-  r.hi0 = clampb(max(a.hi0, a.d0 + pick(q0, b.hi1, b.hi0)));
-  r.hi1 = clampb(max(a.hi1, a.d1 + pick(q1, b.hi1, b.hi0)));
-  if (d0 > kLim || d0 < -kLim || d1 > kLim || d1 < -kLim) {
+  const bool q0 = odd(a.d0), q1 = !odd(a.d1);
+  double d0 = a.d0 + pickd(q0, b.d1, b.d0), d1 = a.d1 + pickd(q1, b.d1, b.d0);
+  r.lo0 = clampb(fmin(a.lo0, a.d0 + pickd(q0, b.lo1, b.lo0)));
+  r.lo1 = clampb(fmin(a.lo1, a.d1 + pickd(q1, b.lo1, b.lo0)));
+  r.hi0 = clampb(fmax(a.hi0, a.d0 + pickd(q0, b.hi1, b.hi0)));
+  r.hi1 = clampb(fmax(a.hi1, a.d1 + pickd(q1, b.hi1, b.hi0)));
+  if (fabs(d0) > kLim || fabs(d1) > kLim) {
     r.fl |= F_BAD;
-    d0 = d1 = 0;
+    d0 = d1 = 0.0;
   }
   r.d0 = d0;
   r.d1 = d1;
@@ -290,10 +304,11 @@ __device__ __forceinline__ bool tr_apply(const Tr& t, double s, double& out) {
   const int E = (int)((b >> 52) & 0x7ff);
   if (E == 0 || E == 0x7ff) return false;
   if (E - 1023 != t.e || (uint32_t)(b >> 63) != (t.fl & F_NEG)) return false;
-  const int64_t M = (int64_t)((b & kFrac) | (uint64_t(1) << 52));
-  const bool odd = (M & 1) != 0;
-  if (M + pick(odd, t.lo1, t.lo0) < kM0 || M + pick(odd, t.hi1, t.hi0) >= kM1) return false;
-  out = __longlong_as_double((long long)((b & ~kFrac) | (uint64_t)(M + pick(odd, t.d1, t.d0) - kM0)));
+  const bool od = (b & 1) != 0;  // M's parity is its last fraction bit
+  const double Md = (double)(int64_t)((b & kFrac) | (uint64_t(1) << 52));
+  if (Md + pickd(od, t.lo1, t.lo0) < kM0 || Md + pickd(od, t.hi1, t.hi0) >= kM1) return false;
+  const double Mn = Md + pickd(od, t.d1, t.d0);  // an integer in [2^52, 2^53): its fraction bits are M - 2^52
+  out = __longlong_as_double((long long)((b & ~kFrac) | ((uint64_t)__double_as_longlong(Mn) & kFrac)));
   return true;
 }
 
@@ -348,12 +363,12 @@ __device__ __forceinline__ int64_t rl64(int64_t x, int l) {
 __device__ __forceinline__ double rld(double x, int l) { return __longlong_as_double(rl64(__double_as_longlong(x), l)); }
 __device__ __forceinline__ Tr tr_lane(const Tr& t, int l) {
   Tr r;
-  r.d0 = rl64(t.d0, l);
-  r.d1 = rl64(t.d1, l);
-  r.lo0 = rl64(t.lo0, l);
-  r.lo1 = rl64(t.lo1, l);
-  r.hi0 = rl64(t.hi0, l);
-  r.hi1 = rl64(t.hi1, l);
+  r.d0 = rld(t.d0, l);
+  r.d1 = rld(t.d1, l);
+  r.lo0 = rld(t.lo0, l);
+  r.lo1 = rld(t.lo1, l);
+  r.hi0 = rld(t.hi0, l);
+  r.hi1 = rld(t.hi1, l);
   r.e = __builtin_amdgcn_readlane(t.e, l);
   r.fl = (uint32_t)__builtin_amdgcn_readlane((int)t.fl, l);
   r.pad = 0;
@@ -479,7 +494,7 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
       cls |= ci << (2 * i);
     }
     if (!(a.fl & F_ZERO)) {
-      const double big = (double)kBig;
+      const double big = kBig;
       double d0 = 0.0, lo0 = big, hi0 = -big, d1 = 0.0, lo1 = big, hi1 = -big;
       bool tie = false;
 #pragma unroll
@@ -512,12 +527,12 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
           (lo1 < big && fabs(lo1) > lim) || (hi0 > -big && fabs(hi0) > lim) || (hi1 > -big && fabs(hi1) > lim)) {
         a.fl |= F_BAD;
       } else {
-        a.d0 = (int64_t)d0;
-        a.d1 = (int64_t)d1;
-        a.lo0 = (int64_t)lo0;
-        a.lo1 = (int64_t)lo1;
-        a.hi0 = (int64_t)hi0;
-        a.hi1 = (int64_t)hi1;
+        a.d0 = d0;
+        a.d1 = d1;
+        a.lo0 = lo0;
+        a.lo1 = lo1;
+        a.hi0 = hi0;
+        a.hi1 = hi1;
       }
     }
     Tr o = shfl_xor_tr(a, 1);
