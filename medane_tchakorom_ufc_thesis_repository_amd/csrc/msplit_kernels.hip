@@ -1842,6 +1842,16 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
       }
       m[j] = *reinterpret_cast<const uint16_t*>(mask + base + j * (2 * kT));
     }
+    // RV: the plane's seven value legs for all the lane's rows, issued with x(z+1) before the LDS turn-around (the
+    // kernel runs one workgroup per CU, so the unified register file holds them; loaded after the barrier they
+    // were a second, exposed round trip per plane)
+    double2 rqa[RV ? kIters : 1][7];
+    if constexpr (RV) {
+#pragma unroll
+      for (int j = 0; j < kIters; ++j)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) rqa[j][k] = ld_nt(reinterpret_cast<const double2*>(rv + k * rvs + base + j * (2 * kT)));
+    }
     double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0);
     const bool hasl = t < nh && c0 - nx >= 0, hash = t < nh && c0 + kChunk + nx <= (int64_t)nz * P;
     if (hasl) hl = *reinterpret_cast<const double2*>(x + c0 - nx + 2 * t);
@@ -1865,11 +1875,6 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     double wr[2 * kIters];
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
-      double2 rq[7];
-      if constexpr (RV) {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) rq[k] = ld_nt(reinterpret_cast<const double2*>(rv + k * rvs + base + j * (2 * kT)));
-      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int e = j * (2 * kT) + 2 * t + q + nx;
@@ -1879,7 +1884,7 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
-          const double vk = RV ? (q ? rq[k].y : rq[k].x) : v[k];
+          const double vk = RV ? (q ? rqa[RV ? j : 0][k].y : rqa[RV ? j : 0][k].x) : v[k];
           if (mr & (1u << k)) s = s + vk * (xq[k] * sc);
         }
         wr[2 * j + q] = s;
