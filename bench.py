@@ -561,7 +561,7 @@ def seq_mode_step(ctx, ksp, b, x, ref):
     return {"reduction": "seq (PETSc's order: one running sum per dot/norm/MDot entry)",
             "engine": ("serial (one lane adds in order)" if os.environ.get("MSPLIT_SEQ_ENGINE", "")[:1] in ("s", "S")
                        else "exact parallel (msplit_seq.hip: binade transducers in wave scans, f64 adds where the sum "
-                            "leaves its binade)"),
+                            "leaves its binade; sums below 2^19 terms take the serial engine)"),
             "value": float(x.n) * its / dt, "unit": "DOF-updates/s", "seconds_per_step": dt,
             "gmres_iterations": its, "verified": ok, "mismatch": bad,
             "reference": "tests/golden/configs1_seq.json['seq'] (oracle/oracle.c ORC_REDUCE_SEQ)",

@@ -60,6 +60,7 @@ struct msp_ctx {
   int64_t partial_cap = 0;     // doubles
   void* seqbuf = nullptr;      // MSP_REDUCE_SEQ's transducers and guesses (msplit_seq.hip)
   int64_t seqbuf_cap = 0;      // bytes
+  double* seqacc = nullptr;    // MSP_REDUCE_SEQ chains: two rows of MSK_MAX_GROUP running sums
   uint64_t epoch = 0;          // bumped when a buffer captured graphs point at is reallocated
   int reduce = MSP_REDUCE_DBR;  // MSP_REDUCE_SEQ: PETSc's sequential order (msplit_seq.hip)
   bool timing = false;

@@ -83,6 +83,7 @@ static void ctx_free(msp_ctx* c) {
   for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->partial) (void)hipFree(c->partial);
   if (c->seqbuf) (void)hipFree(c->seqbuf);
+  if (c->seqacc) (void)hipFree(c->seqacc);
   if (c->dscratch) (void)hipFree(c->dscratch);
   if (c->hscratch) (void)hipHostFree(c->hscratch);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);

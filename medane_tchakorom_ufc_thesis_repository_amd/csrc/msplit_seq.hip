@@ -381,7 +381,8 @@ __device__ __forceinline__ const double* vec_row(const Vecs& V, int v) {
 
 // Row v of a (nv rows of K approximate chunk sums) -> its exclusive prefix: the guessed s at each segment start.
 // Any order: a guess only picks the binade the transducers are built in.
-__global__ __launch_bounds__(kT) void k_seqx_prefix(double* __restrict__ a, int64_t K, const int* __restrict__ stop) {
+__global__ __launch_bounds__(kT) void k_seqx_prefix(double* __restrict__ a, int64_t K, const double* __restrict__ acc_in,
+                                                    const int* __restrict__ stop) {
   if (stopped(stop)) return;
   __shared__ double sh[kT];
   double* row = a + (int64_t)blockIdx.x * K;
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(kT) void k_seqx_prefix(double* __restrict__ a, int6
   sh[t] = sum;
   __syncthreads();
   if (t == 0) {
-    double run = 0.0;
+    double run = acc_in ? acc_in[blockIdx.x] : 0.0;  // a chained sum starts where the previous piece ended
     for (int i = 0; i < kT; ++i) {
       const double v = sh[i];
       sh[i] = run;
@@ -616,7 +617,8 @@ __device__ __forceinline__ double serial_terms(const double* sp, int i0, int i1,
 // compute the same s (identical inputs and operations), so every decision is uniform across the workgroup.
 __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__ w, Vecs V, int64_t n, int self,
                                                       const Tr* __restrict__ segT, const Tr* __restrict__ subT,
-                                                      int64_t K, double* __restrict__ partial, int64_t nchunks,
+                                                      int64_t K, const double* __restrict__ acc_in,
+                                                      double* __restrict__ partial, int64_t nchunks,
                                                       const int* __restrict__ stop, int64_t* __restrict__ stats) {
   if (stopped(stop)) return;
   __shared__ double sp[kSeg];
@@ -631,7 +633,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
     stmt;                                   \
     if (stats) acc += wall_clock64() - t0_; \
   } while (0)
-  double s = 0.0;
+  double s = acc_in ? acc_in[v] : 0.0;
   for (int64_t kb = 0; kb < K; kb += 64) {
     const bool in = kb + lane < K;
     const Tr tw = tr_load(segT + (int64_t)v * K + (in ? kb + lane : 0));
@@ -728,23 +730,25 @@ extern "C" int msk_seq_stage1(const double* w, const Vecs* V, int nv, int64_t n,
 
 extern "C" int mspi_reduce_seq(const msp_ctx* c) { return c->reduce == MSP_REDUCE_SEQ; }
 
-extern "C" int mspi_seq_chain(msp_ctx* c, const mspi_seq_segs* sg, int ncol, int frob, double* out, int m,
-                              const int* stop) {
-  ARGCHK(sg && out && sg->nseg >= 1 && sg->nseg <= MSPI_SEQ_MAXSEG && ncol >= 1 && ncol <= m, MSP_ERR_ARG_OUTOFRANGE,
-         "sequential chain over %d segments, %d columns", sg ? sg->nseg : -1, ncol);
-  k_seq_chain<<<dim3(frob ? 1 : ncol), dim3(kT), 0, c->stream>>>(*sg, ncol, frob, out, m, stop);
-  KCHK((int)hipGetLastError());
-  return MSP_SUCCESS;
-}
-
-// MSP_REDUCE_SEQ's stage 1: the exact parallel engine (the serial one under MSPLIT_SEQ_ENGINE=serial).
-int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial,
-                    int64_t nchunks, const int* stop) {
+// Which engine takes a PETSc-order sum of n terms: MSPLIT_SEQ_ENGINE=serial / parallel forces one, else the parallel
+// engine from min_n terms on.  Below that its four launches and the per-segment transducers cost more than the
+// serial adds save (profiles/r04/seq/crossover.jsonl: a dot is 59 us parallel against 22 us serial at n = 1024, and
+// the engines meet between 65 K and 1 M terms, depending on how often the sum changes binade).
+static bool parallel_engine(int64_t n, int64_t min_n) {
   const char* eng = getenv("MSPLIT_SEQ_ENGINE");
+  if (eng && (eng[0] == 's' || eng[0] == 'S')) return false;
+  if (eng && (eng[0] == 'p' || eng[0] == 'P')) return n > 0;
+  return n >= min_n;
+}
+constexpr int64_t kParMinSum = int64_t(1) << 19;    // one dot / norm / MDot
+constexpr int64_t kParMinChain = int64_t(1) << 17;  // an LSQR chain: its total length per sum
+
+// The parallel engine: nv sums of n terms w[i] * (V_v[i] * sy_v) (self: w[i] * w[i]), each from acc_in[v] (device;
+// nullptr: +0.0), into partial's DBR layout.  n > 0.
+static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, const double* acc_in,
+                     double* partial, int64_t nchunks, const int* stop) {
   const int64_t K = (n + kSeg - 1) / kSeg;
-  if ((eng && (eng[0] == 's' || eng[0] == 'S')) || K == 0)
-    return msk_seq_stage1(w, V, nv, n, self, partial, nchunks, stop, c->stream);
-  if (nv < 1 || nv > MSK_MAX_GROUP || (self && nv != 1) || nchunks < 1) return (int)hipErrorInvalidValue;
+  if (nv < 1 || nv > MSK_MAX_GROUP || (self && nv != 1) || nchunks < 1 || K < 1) return (int)hipErrorInvalidValue;
   const int64_t need = (int64_t)nv * K * ((int64_t)sizeof(Tr) * (kSubs + 1) + (int64_t)sizeof(double));
   if (need > c->seqbuf_cap) {
     if (hipStreamSynchronize(c->stream) != hipSuccess) return (int)hipErrorUnknown;
@@ -760,15 +764,15 @@ int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t 
   double* pre = reinterpret_cast<double*>(segT + (int64_t)nv * K);
   int rc = msk_dot_stage1(w, V, nv, n, pre, K, self, stop, c->stream);
   if (rc) return rc;
-  k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, stop);
+  k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, acc_in, stop);
   k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop);
   // MSPLIT_SEQ_STATS=1: per-sum walk counters on stderr (a diagnostic; its buffer lives for this call only)
   const char* st = getenv("MSPLIT_SEQ_STATS");
   int64_t* dstats = nullptr;
   if (st && st[0] == '1' && hipMalloc((void**)&dstats, 16 * MSK_MAX_GROUP * sizeof(int64_t)) != hipSuccess)
     dstats = nullptr;
-  k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, partial, nchunks, stop,
-                                                        dstats);
+  k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
+                                                        stop, dstats);
   if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];
     if (hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
@@ -785,4 +789,79 @@ int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t 
     (void)hipFree(dstats);
   }
   return (int)hipGetLastError();
+}
+
+// MSP_REDUCE_SEQ's stage 1: the exact parallel engine, or the serial one (parallel_engine decides).
+int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial,
+                    int64_t nchunks, const int* stop) {
+  if (!parallel_engine(n, kParMinSum)) return msk_seq_stage1(w, V, nv, n, self, partial, nchunks, stop, c->stream);
+  return seqx_core(c, w, V, nv, n, self, nullptr, partial, nchunks, stop);
+}
+
+
+namespace {
+// the chain's result in the block partial layout: only the last block's slot carries it (a block-order sum of the
+// slots is the chain); frob: one sum, carried by the last block's last column
+__global__ void k_seqx_chain_out(const double* __restrict__ res, int ncol, int frob, int nseg, double* __restrict__ out,
+                                 int m, const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  for (int i = threadIdx.x; i < nseg * ncol; i += blockDim.x) {
+    const int k = i / ncol, j = i % ncol;
+    const bool last = k == nseg - 1 && (!frob || j == ncol - 1);
+    out[(int64_t)k * m + j] = last ? res[frob ? 0 : j] : 0.0;
+  }
+}
+
+__global__ void k_seqx_copy(const double* __restrict__ a, double* __restrict__ b, int n) {
+  if ((int)threadIdx.x < n) b[threadIdx.x] = a ? a[threadIdx.x] : 0.0;
+}
+}  // namespace
+
+static int seqx_piece(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, const double* acc,
+                      double* res, const int* stop) {
+  if (n > 0) return seqx_core(c, w, V, nv, n, self, acc, res, 1, stop);
+  k_seqx_copy<<<1, MSK_MAX_GROUP, 0, c->stream>>>(acc, res, nv);  // an empty piece leaves the sums as they were
+  return (int)hipGetLastError();
+}
+
+// The LSQR sums chained across the row blocks of one process (the reference's LSQR over all of R on one rank,
+// SMSM-global.c:136): column j . y summed over block 0, then block 1, ... as one sequential sum; frob: the squares
+// of column 0 over all blocks, then column 1, ...  The parallel engine runs piece by piece, each starting from the
+// previous piece's exact result (or the serial engine: parallel_engine on the chain's length per sum).
+extern "C" int mspi_seq_chain(msp_ctx* c, const mspi_seq_segs* sg, int ncol, int frob, double* out, int m,
+                              const int* stop) {
+  ARGCHK(sg && out && sg->nseg >= 1 && sg->nseg <= MSPI_SEQ_MAXSEG && ncol >= 1 && ncol <= m && ncol <= MSK_MAX_GROUP,
+         MSP_ERR_ARG_OUTOFRANGE, "sequential chain over %d segments, %d columns", sg ? sg->nseg : -1, ncol);
+  int64_t total = 0;
+  for (int k = 0; k < sg->nseg; ++k) total += sg->n[k];
+  if (!parallel_engine(frob ? total * ncol : total, kParMinChain)) {
+    k_seq_chain<<<dim3(frob ? 1 : ncol), dim3(kT), 0, c->stream>>>(*sg, ncol, frob, out, m, stop);
+    KCHK((int)hipGetLastError());
+    return MSP_SUCCESS;
+  }
+  if (!c->seqacc) HIPCHK(hipMalloc((void**)&c->seqacc, 2 * MSK_MAX_GROUP * sizeof(double)));
+  double* buf[2] = {c->seqacc, c->seqacc + MSK_MAX_GROUP};
+  const double* acc = nullptr;  // +0.0
+  int cur = 0;
+  if (frob) {
+    for (int j = 0; j < ncol; ++j)
+      for (int k = 0; k < sg->nseg; ++k) {
+        Vecs none = {};
+        KCHK(seqx_piece(c, sg->x[k] + (int64_t)j * sg->ldx[k], &none, 1, sg->n[k], 1, acc, buf[cur], stop));
+        acc = buf[cur];
+        cur ^= 1;
+      }
+  } else {
+    for (int k = 0; k < sg->nseg; ++k) {
+      Vecs cols = {};  // column j of block k: x[k] + j*ldx[k]; its products with y[k] are the serial engine's
+      cols.base = sg->x[k];
+      cols.stride = sg->ldx[k];
+      KCHK(seqx_piece(c, sg->y[k], &cols, ncol, sg->n[k], 0, acc, buf[cur], stop));
+      acc = buf[cur];
+      cur ^= 1;
+    }
+  }
+  k_seqx_chain_out<<<1, 256, 0, c->stream>>>(acc, ncol, frob, sg->nseg, out, m, stop);
+  KCHK((int)hipGetLastError());
+  return MSP_SUCCESS;
 }

@@ -94,10 +94,15 @@ def test_seq_gmres_bitwise_vs_petsc_order_oracle(sctx, oracle, case):
     assert np.array_equal(xv.get_array(), xs)
 
 
+@pytest.mark.parametrize("engine", ["auto", "parallel", "serial"])
 @pytest.mark.parametrize("nblk,s", [(1, 4), (2, 4), (3, 20), (4, 7)])
-def test_seq_lsqr_chained_across_blocks(sctx, oracle, nblk, s):
+def test_seq_lsqr_chained_across_blocks(sctx, oracle, nblk, s, engine, monkeypatch):
     """The LSQR over nblk row blocks of one process: every sum runs across the
-    blocks in block order (the oracle's ls_gdot / ls_frobenius SEQ)."""
+    blocks in block order (the oracle's ls_gdot / ls_frobenius SEQ).  Both
+    engines (mspi_seq_chain: the parallel one piece by piece, each block's sum
+    starting from the previous block's exact result)."""
+    if engine != "auto":
+        monkeypatch.setenv("MSPLIT_SEQ_ENGINE", engine)
     sizes = [int(v) for v in RNG.integers(1000, 9000, nblk)]
     Rs = [RNG.standard_normal((m, s)) for m in sizes]
     bs = [RNG.standard_normal(m) for m in sizes]
@@ -113,6 +118,29 @@ def test_seq_lsqr_chained_across_blocks(sctx, oracle, nblk, s):
         assert np.array_equal(lq.get_residual_history(), ro["hist"])
         assert np.array_equal(x.get_array(), xo)
         lq.destroy()
+
+
+@pytest.mark.parametrize("engine", ["auto", "serial"])
+def test_seq_lsqr_chain_long(sctx, oracle, engine, monkeypatch):
+    """Chains long enough (about 2^18 terms per sum) that the default takes the
+    parallel engine, over blocks of uneven length, one of them a single row."""
+    if engine != "auto":
+        monkeypatch.setenv("MSPLIT_SEQ_ENGINE", engine)
+    rng = np.random.default_rng(11)
+    sizes, s = [100_003, 1, 70_000, 95_001], 6
+    Rs = [rng.standard_normal((m, s)) for m in sizes]
+    bs = [rng.standard_normal(m) for m in sizes]
+    lq = LSQR(sctx)
+    lq._set(max_it=25, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=1)
+    lq.set_operators([DenseMat.from_array(sctx, R) for R in Rs])
+    x = Vec(sctx, s)
+    lq.solve([Vec.from_array(sctx, b) for b in bs], x)
+    xo, ro = oracle.lsqr(Rs, bs, reduce_mode=oracle.REDUCE_SEQ, max_it=25, rtol=1e-15, abstol=1e-100,
+                         exact_norm=1, conv_test=1)
+    assert (lq.get_iteration_number(), lq.get_converged_reason()) == (ro["its"], ro["reason"])
+    assert np.array_equal(lq.get_residual_history(), ro["hist"])
+    assert np.array_equal(x.get_array(), xo)
+    lq.destroy()
 
 
 def test_seq_dense_mult_transpose(sctx, oracle):

@@ -8,7 +8,8 @@ exactly +0.0, walks that change binade thousands of times, power-of-two boundari
 overflowing sums, +-0.0, inf and NaN, and every length edge of the 64-term sub-segments and 4096-term segments.
 Each is checked against the PETSc-order oracle (orc_dot / orc_norm2 / orc_mdot with ORC_REDUCE_SEQ, the
 reference's f2cblaslapack ddot order) and against the serial engine (MSPLIT_SEQ_ENGINE=serial, one lane adding in
-order) on the same device.
+order) on the same device.  MSPLIT_SEQ_ENGINE=parallel holds the parallel engine at every length (by default sums
+below 2^19 terms take the serial one).
 """
 import os
 
@@ -33,12 +34,18 @@ def _bits(v):
     return np.float64(v).view(np.uint64)
 
 
+@pytest.fixture(autouse=True)
+def _parallel(monkeypatch):
+    """The engine under test at every length (by default small sums take the serial engine)."""
+    monkeypatch.setenv("MSPLIT_SEQ_ENGINE", "parallel")
+
+
 def _serial(fn):
     os.environ["MSPLIT_SEQ_ENGINE"] = "serial"
     try:
         return fn()
     finally:
-        del os.environ["MSPLIT_SEQ_ENGINE"]
+        os.environ["MSPLIT_SEQ_ENGINE"] = "parallel"
 
 
 def _check_dot(sctx, oracle, x, y):
