@@ -153,12 +153,13 @@ def seqsum(ps, s=0.0):
     return s
 
 
-def engine(ps, sub=16, per=4, jitter=1e-9, seed=0, dec=None):
+def engine(ps, sub=16, per=4, jitter=1e-9, seed=0, dec=None, s0=0.0):
     """Sub-segment transducers built from lane runs of `per` terms in the binade of a jittered guess, applied where
-    valid; the rest term by term with the f64 add (the walk's serial sub-segments)."""
+    valid; the rest term by term with the f64 add (the walk's serial sub-segments).  s0: the exact state the sum
+    starts from (mspi_seq_chain's acc_in: the previous row block's result; the guesses start there too)."""
     rng = np.random.default_rng(seed)
-    pre = np.concatenate([[0.0], np.cumsum(ps)])
-    s, i, n, fast = 0.0, 0, len(ps), 0
+    pre = s0 + np.concatenate([[0.0], np.cumsum(ps)])
+    s, i, n, fast = s0, 0, len(ps), 0
     while i < n:
         j = min(n, i + sub)
         gok, e, sn = guess(float(pre[i]) * (1.0 + jitter * rng.uniform(-1, 1)))
@@ -205,6 +206,19 @@ def test_engine_walk_is_the_sequential_sum(name, jitter, dec):
     ref = seqsum(ps)
     got, fast = engine(ps, jitter=jitter, dec=decomp if dec == "int" else globals()["decomp_f"])
     assert bits(got) == bits(ref), (got, ref)
+
+
+@pytest.mark.parametrize("name", ["walk", "ties_even", "ties_odd", "cancel", "drift", "small_on_large", "range"])
+def test_engine_chained_pieces_are_the_sequential_sum(name):
+    """mspi_seq_chain: a sum cut into pieces (the LSQR's row blocks, empty ones included), each piece walked from
+    the previous piece's exact result, is the one sequential sum."""
+    ps = [float(v) for v in CASES[name]]
+    rng = np.random.default_rng(3)
+    cuts = sorted([0, len(ps)] + [int(c) for c in rng.integers(0, len(ps), 4)] + [len(ps) // 2] * 2)  # one empty piece
+    s = 0.0
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        s, _ = engine(ps[a:b], s0=s)
+    assert bits(s) == bits(seqsum(ps))
 
 
 def test_engine_takes_the_fast_path():
