@@ -305,11 +305,31 @@ __device__ __forceinline__ bool tr_apply(const Tr& t, double s, double& out) {
   if (E == 0 || E == 0x7ff) return false;
   if (E - 1023 != t.e || (uint32_t)(b >> 63) != (t.fl & F_NEG)) return false;
   const bool od = (b & 1) != 0;  // M's parity is its last fraction bit
-  const double Md = (double)(int64_t)((b & kFrac) | (uint64_t(1) << 52));
+  // M in [2^52, 2^53) as an f64: exponent 1075 over M's own fraction bits (no integer conversion)
+  const double Md = __longlong_as_double((long long)((b & kFrac) | (uint64_t(0x433) << 52)));
   if (Md + pickd(od, t.lo1, t.lo0) < kM0 || Md + pickd(od, t.hi1, t.hi0) >= kM1) return false;
   const double Mn = Md + pickd(od, t.d1, t.d0);  // an integer in [2^52, 2^53): its fraction bits are M - 2^52
   out = __longlong_as_double((long long)((b & ~kFrac) | ((uint64_t)__double_as_longlong(Mn) & kFrac)));
   return true;
+}
+
+// tr_apply for a wave-uniform s and a per-lane map, without branches: every lane applies its own map to the same s
+// (the walk's one-record applies: lane j's verdict comes from a ballot and its result from one readlane, instead of
+// fourteen readlanes of lane j's record into scalar registers and a scalar apply).  Same verdict and result as
+// tr_apply wherever that returns true.
+__device__ __forceinline__ bool tr_apply_v(const Tr& t, double s, double& out) {
+  const uint64_t b = (uint64_t)__double_as_longlong(s);
+  const int E = (int)((b >> 52) & 0x7ff);
+  const bool od = (b & 1) != 0;
+  const double Md = __longlong_as_double((long long)((b & kFrac) | (uint64_t(0x433) << 52)));
+  const bool inb = E != 0 && E != 0x7ff && E - 1023 == t.e && (uint32_t)(b >> 63) == (t.fl & F_NEG);
+  const bool rng = Md + pickd(od, t.lo1, t.lo0) >= kM0 && Md + pickd(od, t.hi1, t.hi0) < kM1;
+  const double Mn = Md + pickd(od, t.d1, t.d0);
+  const double ot = __longlong_as_double((long long)((b & ~kFrac) | ((uint64_t)__double_as_longlong(Mn) & kFrac)));
+  const double oz = s == 0.0 ? ((signbit(s) && (t.fl & F_NZERO)) ? -0.0 : 0.0) : s;
+  const bool z = (t.fl & F_ZERO) != 0;
+  out = z ? oz : ot;
+  return z || (!(t.fl & F_BAD) && inb && rng);
 }
 
 __device__ __forceinline__ Tr shfl_xor_tr(const Tr& t, int m) {
@@ -354,27 +374,13 @@ __device__ __forceinline__ Tr shfl_up_tr(const Tr& t, int o) {
   return r;
 }
 
-// wave-uniform copies of lane l's values (v_readlane into scalar registers: no LDS round trip)
+// a wave-uniform copy of lane l's value (v_readlane into scalar registers: no LDS round trip)
 __device__ __forceinline__ int64_t rl64(int64_t x, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ double rld(double x, int l) { return __longlong_as_double(rl64(__double_as_longlong(x), l)); }
-__device__ __forceinline__ Tr tr_lane(const Tr& t, int l) {
-  Tr r;
-  r.d0 = rld(t.d0, l);
-  r.d1 = rld(t.d1, l);
-  r.lo0 = rld(t.lo0, l);
-  r.lo1 = rld(t.lo1, l);
-  r.hi0 = rld(t.hi0, l);
-  r.hi1 = rld(t.hi1, l);
-  r.e = __builtin_amdgcn_readlane(t.e, l);
-  r.fl = (uint32_t)__builtin_amdgcn_readlane((int)t.fl, l);
-  r.pad = 0;
-  return r;
-}
-
 __device__ __forceinline__ const double* vec_row(const Vecs& V, int v) {
   return V.base ? V.base + (int64_t)v * V.stride : V.p[v];
 }
@@ -647,10 +653,11 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
         ++n_scan;
       } else {  // the segment after a descended one, on its own
         double sn = 0.0;
-        const bool mine = tr_apply(tr_lane(tv, f0), s, sn);  // wave-uniform: scalar registers
+        const bool ok = tr_apply_v(tv, s, sn);  // every lane its own segment's map at s; lane f0's is the one
+        const bool mine = ((__ballot(ok) >> f0) & 1) != 0;
         ++n_single;
         if (mine) {
-          s = sn;
+          s = rld(sn, f0);
           f0 += 1;
           scan = true;
           continue;
@@ -688,10 +695,10 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
         const int64_t t1 = stats ? wall_clock64() : 0;
         for (++j; j < kSubs; ++j) {
           double sn = 0.0;
-          const bool mine = tr_apply(tr_lane(u, j), s, sn);
+          const bool ok = tr_apply_v(u, s, sn);  // every lane its own sub's map at s; lane j's is the one
           ++n_single;
-          if (!mine) break;
-          s = sn;
+          if (!((__ballot(ok) >> j) & 1)) break;
+          s = rld(sn, j);
         }
         if (stats) c_single += wall_clock64() - t1;
       }
