@@ -257,7 +257,10 @@ def decomp_f(p, e, sneg):
     """k_seqx_trans's f64 decomposition: a = |p| * 2^(52-e) by ldexp, its exact floor and fraction."""
     if not math.isfinite(p):
         return None
-    a = math.ldexp(abs(p), 52 - e)
+    try:
+        a = math.ldexp(abs(p), 52 - e)
+    except OverflowError:  # the device's ldexp gives inf, which the next test refuses
+        return None
     if a >= 2.0 ** 53:
         return None
     qa = math.floor(a)
