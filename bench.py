@@ -511,13 +511,15 @@ def non_stencil_step(ctx, args):
     L = _lib.load()
     L.msk_set_tuning.argtypes = [ctypes.c_int]
     L.msk_set_tuning.restype = None
+    L.msk_get_tuning.restype = ctypes.c_int
+    saved = int(L.msk_get_tuning())   # MSPLIT_TUNING as the context applied it: restored after every variant
     picked = A.get_storage()
     out = {"operator": "utils.heterogeneous_poisson3d(256): 7-point -div(kappa grad u), per-cell kappa, host CSR "
                        "through msp_mat_create_csr", "rows": N, "nnz": nnz, "matrix_storage": picked,
            "spmv_kernel": A.spmv_kernel(), "create_s": create_s,
            "reference": "tests/golden/non_stencil_aij.json['dbr']"}
     steps = max(1, min(args.steps, 3))
-    variants = [("default", picked, 0), ("csr_storage", "csr", 0), ("csr_fused_matmult_mdot", "csr", 2048)]
+    variants = [("default", picked, saved), ("csr_storage", "csr", saved), ("csr_fused_matmult_mdot", "csr", saved | 2048)]
     for name, storage, flags in variants:
         A.set_storage(storage)
         L.msk_set_tuning(flags)
@@ -533,7 +535,7 @@ def non_stencil_step(ctx, args):
             dt = time.perf_counter() - t0
             ok, bad = check_step(ksp, x, ref["dbr"]) if ref else (None, ["no record"])
         finally:
-            L.msk_set_tuning(0)
+            L.msk_set_tuning(saved)
         out[name] = {"matrix_storage": storage, "value": float(N) * its / dt, "unit": "DOF-updates/s",
                      "ms_per_step": 1e3 * dt / steps, "steps": steps, "verified": ok, "mismatch": bad}
     A.set_storage(picked)

@@ -374,6 +374,40 @@ static int sum_over_blocks(msd_run *R, int (*f)(msd_block *, double *), double *
   return MSP_SUCCESS;
 }
 
+/* Every rank takes the same stop decision at the same outer iteration (synchronous-multisplitting.c:187-206 assumes
+ * it; a rank that stops alone leaves the others waiting in their next collective forever): one msp_comm_agree of
+ * (outer_its, stop) per outer iteration, an error on every rank on a mismatch.  MSPLIT_FAULT_STOP_RANK=r flips rank
+ * r's decision at the first outer iteration (the tests' fault injection; multisplitting.py agree_on_stop). */
+static int agree_on_stop(msd_run *R, int outer_its, int *stop) {
+  const char *f = getenv("MSPLIT_FAULT_STOP_RANK");
+  if (f && atoi(f) == R->t->rank && outer_its == 1) *stop = !*stop;
+  if (R->t->world == 1) return MSP_SUCCESS;
+  int32_t ok = 0;
+  const int rc = msp_comm_agree(R->t->comm, (int64_t)outer_its * 2 + (*stop ? 1 : 0), &ok);
+  if (rc) fprintf(stderr, "msplit: rank %d: %s\n", R->t->rank, msp_get_last_error());
+  return rc;
+}
+
+/* -msplit_dump_x <prefix>: each block's x as raw f64 to <prefix>.<block> (the tests hash it against the oracle's) */
+static int dump_x(msd_run *R, const msd_options *o) {
+  const char *pre = msd_opt_str(o, NULL, "msplit_dump_x", NULL);
+  if (!pre) return MSP_SUCCESS;
+  for (int i = 0; i < R->nlocal; ++i) {
+    msd_block *B = R->blk[i];
+    double *h = (double *)malloc((size_t)(B->n > 0 ? B->n : 1) * sizeof(double));
+    if (!h) return MSP_ERR_MEM;
+    int rc = msp_vec_get_values(B->x, 0, B->n, h);
+    char path[4096];
+    snprintf(path, sizeof(path), "%s.%d", pre, B->L.b);
+    FILE *fp = rc ? NULL : fopen(path, "wb");
+    if (!rc && (!fp || fwrite(h, sizeof(double), (size_t)B->n, fp) != (size_t)B->n)) rc = MSP_ERR_LIB;
+    if (fp) fclose(fp);
+    free(h);
+    if (rc) return rc;
+  }
+  return MSP_SUCCESS;
+}
+
 static int norm0_sq(msd_block *B, double *sq) { return norm_sq(B->b, sq); }
 
 static int setup_run(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const msd_transport *t, msd_run *R,
@@ -432,13 +466,15 @@ int msd_sm_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const
     if (res->outer_its < MSD_HIST_CAP) res->hist[res->outer_its] = norm;
     res->outer_its++;
     res->last_norm = norm;
-    if (norm <= fmax(p->atol, p->rtol * res->norm0)) break;
-    if (res->outer_its >= p->max_outer) break;
+    int stop = norm <= fmax(p->atol, p->rtol * res->norm0) || res->outer_its >= p->max_outer;
+    CK(agree_on_stop(&R, res->outer_its, &stop));
+    if (stop) break;
   }
   barrier(&R);
   res->elapsed = now_s() - t0;
   res->final_norm = res->last_norm;
   CK(sum_over_blocks(&R, error_sq, &res->error));
+  CK(dump_x(&R, o));
   free_run(&R);
   return MSP_SUCCESS;
 }
@@ -536,13 +572,15 @@ int msd_smsm_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options 
     }
     res->outer_its++;
     res->last_norm = norm;
-    if (norm <= fmax(p->atol, p->rtol * res->norm0)) break;
-    if (res->outer_its >= p->max_outer) break;
+    int stop = norm <= fmax(p->atol, p->rtol * res->norm0) || res->outer_its >= p->max_outer;
+    CK(agree_on_stop(&R, res->outer_its, &stop));
+    if (stop) break;
   }
   barrier(&R);
   res->elapsed = now_s() - t0;
   CK(sum_over_blocks(&R, block_residual_sq, &res->final_norm));
   CK(sum_over_blocks(&R, error_sq, &res->error));
+  CK(dump_x(&R, o));
   msp_lsqr_destroy(&lsqr);
   msp_vec_destroy(&alpha);
   free_run(&R);

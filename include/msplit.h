@@ -368,6 +368,12 @@ int msp_comm_exchange_neighbors(msp_comm *comm, const msp_vec *src, int64_t lo_s
 /* out[i] = sum over ranks of in[i] in rank order (host arrays): the outer residual
  * Allreduce of synchronous-multisplitting.c:192, bitwise the same on every rank. */
 int msp_comm_sum_ordered(msp_comm *comm, const double *in, double *out, int32_t n);
+/* The ranks' agreement on the outer loop's control state (no reference counterpart: the reference's drivers
+ * assume it, synchronous-multisplitting.c:187-206, and a disagreement there is a deadlock in the next
+ * collective).  Every rank passes a token (|token| <= 2^53, e.g. outer_its * 2 + stop); all tokens are
+ * gathered; *all_equal = 1 when they match.  When they do not, every rank gets MSP_ERR_ARG_WRONG and an error
+ * text naming the first differing rank, so a transport fault ends the run on every rank instead of hanging it. */
+int msp_comm_agree(msp_comm *comm, int64_t token, int32_t *all_equal);
 
 /* ------------------------------------------------------------------- LSQR */
 /* KSPLSQR options (the outer solver of the minimization variants,

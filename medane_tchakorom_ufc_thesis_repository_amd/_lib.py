@@ -159,6 +159,7 @@ _SIGS = {
     "msp_amsg_recv_vec": [_vp, C.c_int32, _i32p, C.c_int32, _vp, C.c_int64, C.c_int64, _P(C.c_int64), _i32p],
     "msp_comm_exchange_neighbors": [_vp, _vp, C.c_int64, C.c_int64, _vp, C.c_int64, C.c_int64, C.c_int64],
     "msp_comm_sum_ordered": [_vp, _dp, _dp, C.c_int32],
+    "msp_comm_agree": [_vp, C.c_int64, C.POINTER(C.c_int32)],
     "msp_amsg_enable_device": [_vp, _vp],
     "msp_amsg_close_peers": [_vp],
     "msp_amsg_get_stats": [_vp, _P(C.c_int64), _P(C.c_int64)],

@@ -54,6 +54,10 @@ class LocalComm:
     def barrier(self):
         pass
 
+    def agree(self, token: int) -> bool:
+        """Every block is in this process: one loop, one decision."""
+        return True
+
     def lsqr_comm(self, ctx):
         """Every block is in this process: LSQR adds the block partials itself."""
         return None
@@ -139,6 +143,15 @@ class TorchComm:
 
     def barrier(self):
         self.dist.barrier(group=self.group)
+
+    def agree(self, token: int) -> bool:
+        """Every rank holds the same outer-loop token (msp_comm_agree's contract); raises on every rank if not."""
+        got = self.allgather_scalar(float(token))
+        bad = [r for r, v in enumerate(got) if v != got[0]]
+        if bad:
+            raise RuntimeError(f"ranks disagree on the outer loop state: rank 0 holds {int(got[0])}, "
+                               f"rank {bad[0]} {int(got[bad[0]])}")
+        return True
 
     def lsqr_comm(self, ctx):
         """The all-gather of LSQR's block partials (petsc.Comm): with "nccl" an
@@ -296,6 +309,10 @@ class LibComm:
 
     def barrier(self):
         self.dist.barrier(group=self.group)
+
+    def agree(self, token: int) -> bool:
+        """msp_comm_agree over the library communicator (raises petsc's MsplitError on every rank on a mismatch)."""
+        return self.comm.agree(token)
 
     def lsqr_comm(self, ctx):
         return self.comm

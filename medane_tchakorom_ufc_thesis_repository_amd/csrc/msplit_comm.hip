@@ -16,6 +16,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "msplit_ctx.hpp"
 
@@ -75,7 +76,16 @@ struct msp_comm {
   double* dsum = nullptr;   // msp_comm_sum_ordered: [own n | gathered nranks*n] on the device, persistent
   double* hsum = nullptr;   //                       pinned host mirror of the same
   int32_t sumcap = 0;       // n it was sized for
+  // host-synchronised hops around the host transport's all-gather (round 4's fix).  MSPLIT_COMM_HOST_SYNC=0 keeps
+  // the persistent buffers but orders the hops by the stream alone: the diagnostic that separates the two changes
+  // that fix made (profiles/r05/comm_cause/)
+  bool host_sync = true;
 };
+
+static bool comm_host_sync_default() {
+  const char* e = getenv("MSPLIT_COMM_HOST_SYNC");
+  return !(e && e[0] == '0');
+}
 
 #define NCCLCHK(call)                                                                            \
   do {                                                                                           \
@@ -116,6 +126,7 @@ extern "C" int msp_comm_create_rccl(msp_ctx* c, int32_t nranks, int32_t rank, co
   m->ctx = c;
   mspi_ctx_retain(c);
   m->kind = COMM_RCCL;
+  m->host_sync = comm_host_sync_default();
   m->nranks = nranks;
   m->rank = rank;
   m->nccl = nc;
@@ -131,6 +142,7 @@ extern "C" int msp_comm_create_host(msp_ctx* c, int32_t nranks, int32_t rank, ms
   m->ctx = c;
   mspi_ctx_retain(c);
   m->kind = COMM_HOST;
+  m->host_sync = comm_host_sync_default();
   m->nranks = nranks;
   m->rank = rank;
   m->fn = fn;
@@ -189,10 +201,8 @@ extern "C" int mspi_comm_allgather(msp_comm* m, const double* send, double* recv
   }
   HIPCHK(hipMemcpyAsync(recv, m->hrecv, (size_t)count * m->nranks * sizeof(double), hipMemcpyHostToDevice,
                         c->stream));
-  // the gathered values are on the device before anything else is enqueued: a device-to-host copy of them right
-  // after this host-to-device one has been seen to read the previous contents (one-GPU multi-rank runs), and
-  // this path waits on MPI anyway
-  HIPCHK(hipStreamSynchronize(c->stream));
+  // the gathered values are on the device before anything else is enqueued (this path waits on MPI anyway)
+  if (m->host_sync) HIPCHK(hipStreamSynchronize(c->stream));
   return MSP_SUCCESS;
 }
 
@@ -204,6 +214,8 @@ extern "C" int mspi_comm_size(const msp_comm* m, int32_t* nranks, int32_t* rank)
 
 extern "C" int msp_comm_allgather(msp_comm* m, const msp_vec* send, msp_vec* recv, int64_t count) {
   ARGCHK(m && send && recv, MSP_ERR_ARG_NULL, "NULL argument");
+  // the collective runs on the communicator's stream: vectors of another context would be unordered with it
+  ARGCHK(send->ctx == m->ctx && recv->ctx == m->ctx, MSP_ERR_ARG_WRONG, "vectors of another context");
   ARGCHK(count >= 0 && count <= send->n && count * m->nranks <= recv->n, MSP_ERR_ARG_SIZ,
          "allgather of %lld per rank: send %lld, recv %lld", (long long)count, (long long)send->n,
          (long long)recv->n);
@@ -219,6 +231,7 @@ extern "C" int msp_comm_allgather(msp_comm* m, const msp_vec* send, msp_vec* rec
 extern "C" int msp_comm_exchange_neighbors(msp_comm* m, const msp_vec* src, int64_t lo_src, int64_t hi_src,
                                            msp_vec* dst, int64_t lo_dst, int64_t hi_dst, int64_t count) {
   ARGCHK(m && src && dst, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(src->ctx == m->ctx && dst->ctx == m->ctx, MSP_ERR_ARG_WRONG, "vectors of another context");
   const bool lo = m->rank > 0, hi = m->rank < m->nranks - 1;
   ARGCHK(count >= 0, MSP_ERR_ARG_OUTOFRANGE, "negative count");
   ARGCHK((!lo || (lo_src >= 0 && lo_src + count <= src->n && lo_dst >= 0 && lo_dst + count <= dst->n)) &&
@@ -262,19 +275,13 @@ extern "C" int msp_comm_exchange_neighbors(msp_comm* m, const msp_vec* src, int6
   if (!rc && hi)  // rank+1 sent its lo plane
     rc = hipMemcpyAsync(dst->d + hi_dst, all + (size_t)(m->rank + 1) * 2 * count, bytes, hipMemcpyDeviceToDevice,
                         c->stream) == hipSuccess ? MSP_SUCCESS : MSP_ERR_LIB;
-  if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = MSP_ERR_LIB;
+  if (!rc && m->host_sync && hipStreamSynchronize(c->stream) != hipSuccess) rc = MSP_ERR_LIB;
   if (rc == MSP_ERR_LIB) mspi_set_error(MSP_ERR_LIB, "device copy of a received plane failed");
   return rc;
 }
 
-// The outer-residual reduction (the Allreduce over the block roots,
-// synchronous-multisplitting.c:192): out[i] = sum over ranks of in[i], added in
-// rank order from 0.0 on every rank, so every rank holds the same bits whatever
-// the collective's algorithm.  Host arrays; synchronises the context's stream.
-extern "C" int msp_comm_sum_ordered(msp_comm* m, const double* in, double* out, int32_t n) {
-  ARGCHK(m && (n == 0 || (in && out)), MSP_ERR_ARG_NULL, "NULL argument");
-  ARGCHK(n >= 0, MSP_ERR_ARG_OUTOFRANGE, "negative count");
-  if (n == 0) return MSP_SUCCESS;
+// Every rank's n host doubles, gathered into all[r*n + i] on the host (msp_comm_sum_ordered, msp_comm_agree).
+static int gather_host(msp_comm* m, const double* in, double* all, int32_t n) {
   msp_ctx* c = m->ctx;
   const size_t per = (size_t)n * sizeof(double);
   const size_t tot = per * (1 + (size_t)m->nranks);
@@ -289,22 +296,57 @@ extern "C" int msp_comm_sum_ordered(msp_comm* m, const double* in, double* out, 
     HIPCHK(hipHostMalloc((void**)&m->hsum, tot, hipHostMallocDefault));
     m->sumcap = n;
   }
-  // the contribution goes up from pinned memory and is on the device before the collective is enqueued, and the
-  // gathered values are read back only after the collective has completed: each side of the all-gather is ordered
-  // by a host synchronisation, not only by the stream (the one-GPU multi-rank runs read a slot of the previous
-  // call's values, or an unwritten one, with stream order alone -- a missing block in one outer residual norm)
+  // up from pinned memory, the all-gather, back to pinned memory, all on the context's stream; the read-back is
+  // waited for.  With host_sync each hop is also host-synchronised (round 4's fix; see the struct)
   memcpy(m->hsum, in, per);
   HIPCHK(hipMemcpyAsync(m->dsum, m->hsum, per, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (m->host_sync) HIPCHK(hipStreamSynchronize(c->stream));
   int rc = mspi_comm_allgather(m, m->dsum, m->dsum + n, n);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (m->host_sync) HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpyAsync(m->hsum + n, m->dsum + n, per * m->nranks, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  memcpy(all, m->hsum + n, per * m->nranks);
+  return MSP_SUCCESS;
+}
+
+// The outer-residual reduction (the Allreduce over the block roots,
+// synchronous-multisplitting.c:192): out[i] = sum over ranks of in[i], added in
+// rank order from 0.0 on every rank, so every rank holds the same bits whatever
+// the collective's algorithm.  Host arrays; synchronises the context's stream.
+extern "C" int msp_comm_sum_ordered(msp_comm* m, const double* in, double* out, int32_t n) {
+  ARGCHK(m && (n == 0 || (in && out)), MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(n >= 0, MSP_ERR_ARG_OUTOFRANGE, "negative count");
+  if (n == 0) return MSP_SUCCESS;
+  std::vector<double> all((size_t)n * m->nranks);
+  const int rc = gather_host(m, in, all.data(), n);
+  if (rc) return rc;
   for (int32_t i = 0; i < n; ++i) {
     double acc = 0.0;
-    for (int32_t r = 0; r < m->nranks; ++r) acc += m->hsum[n + (size_t)r * n + i];
+    for (int32_t r = 0; r < m->nranks; ++r) acc += all[(size_t)r * n + i];
     out[i] = acc;
   }
+  return MSP_SUCCESS;
+}
+
+// The ranks' agreement on the outer loop's control state (msp_comm_agree, include/msplit.h): every rank's token
+// is gathered; *all_equal = 1 iff all are this rank's, else the first rank that differs is named in the error
+// text and MSP_ERR_ARG_WRONG is returned -- on every rank, since every rank sees the same gathered tokens.
+extern "C" int msp_comm_agree(msp_comm* m, int64_t token, int32_t* all_equal) {
+  ARGCHK(m && all_equal, MSP_ERR_ARG_NULL, "NULL argument");
+  ARGCHK(token >= -(int64_t(1) << 53) && token <= (int64_t(1) << 53), MSP_ERR_ARG_OUTOFRANGE,
+         "token %lld is not exact in a double", (long long)token);
+  *all_equal = 0;
+  std::vector<double> all((size_t)m->nranks);
+  const double mine = (double)token;
+  const int rc = gather_host(m, &mine, all.data(), 1);
+  if (rc) return rc;
+  for (int32_t r = 0; r < m->nranks; ++r)
+    if (all[r] != all[0]) {
+      mspi_set_error(MSP_ERR_ARG_WRONG, "ranks disagree on the outer loop state: rank 0 holds %lld, rank %d %lld",
+                     (long long)all[0], r, (long long)all[r]);
+      return MSP_ERR_ARG_WRONG;
+    }
+  *all_equal = 1;
   return MSP_SUCCESS;
 }

@@ -376,6 +376,20 @@ class SMResult:
     elapsed: float = 0.0
 
 
+def agree_on_stop(comm, outer_its: int, stop: bool) -> bool:
+    """Every rank must take the same stop decision at the same outer iteration, or the next collective of the
+    rank that goes on waits forever for the one that stopped (synchronous-multisplitting.c:187-206 assumes
+    agreement).  One all-gather of (outer_its, stop) per outer iteration (comm.agree, msp_comm_agree) turns a
+    disagreement -- e.g. from a transport fault -- into an error on every rank.  MSPLIT_FAULT_STOP_RANK=r flips
+    rank r's decision at the first outer iteration: the fault injection the tests use."""
+    fault = os.environ.get("MSPLIT_FAULT_STOP_RANK")
+    if fault is not None and int(fault) == comm.rank and outer_its == 1:
+        stop = not stop
+    if comm.world > 1:
+        comm.agree(outer_its * 2 + int(stop))
+    return stop
+
+
 def sm_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_outer: int = 10000,
              monitor=None) -> SMResult:
     """The synchronous multisplitting outer loop (synchronous-multisplitting.c:155-206)."""
@@ -400,9 +414,8 @@ def sm_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_outer: int = 1
         res.outer_its += 1
         if monitor:
             monitor(res.outer_its, norm, its)
-        if norm <= max(atol, rtol * res.norm0):             # (:198)
-            break
-        if res.outer_its >= max_outer:
+        # (:198) and the outer cap, agreed by every rank
+        if agree_on_stop(comm, res.outer_its, norm <= max(atol, rtol * res.norm0) or res.outer_its >= max_outer):
             break
     comm.barrier()
     res.elapsed = time.perf_counter() - t0
@@ -490,9 +503,8 @@ def smsm_solve(blocks, comm, s: int, minimizer, rtol: float, atol: float = 1e-10
         res.outer_its += 1
         if monitor:
             monitor(res.outer_its, norm, its_outer, lits)
-        if norm <= max(atol, rtol * res.norm0):              # (:342)
-            break
-        if res.outer_its >= max_outer:
+        # (:342) and the outer cap, agreed by every rank
+        if agree_on_stop(comm, res.outer_its, norm <= max(atol, rtol * res.norm0) or res.outer_its >= max_outer):
             break
     comm.barrier()
     res.elapsed = time.perf_counter() - t0

@@ -541,6 +541,12 @@ class Comm:
         call("msp_comm_sum_ordered", self.h, _dp(a), _dp(out), a.size)
         return out
 
+    def agree(self, token: int) -> bool:
+        """msp_comm_agree: every rank holds the same token (raises, on every rank, when they do not)."""
+        ok = C.c_int32(0)
+        call("msp_comm_agree", self.h, int(token), C.byref(ok))
+        return bool(ok.value)
+
     def destroy(self):
         if getattr(self, "h", None) and self.h.value:
             call("msp_comm_destroy", C.byref(self.h))

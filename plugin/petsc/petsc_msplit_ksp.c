@@ -1,10 +1,13 @@
 /* petsc_msplit_ksp.c -- KSPType "msplitgmres": KSPGMRES(restart) with PCNONE on the MI355X. */
+#include <stdlib.h>
+
 #include <petsc/private/kspimpl.h>
 #include "msplit.h"
 
 typedef struct {
-  msp_ctx *ctx;
+  msp_ctx *ctx;        /* the process's shared context (MSplitContext): not owned */
   msp_mat *A;
+  PetscBool A_borrowed; /* A is an aijmsplit matrix's own HBM mirror: not destroyed here */
   msp_ksp *ksp;
   msp_vec *b, *x;
   PetscInt restart;
@@ -19,16 +22,49 @@ static const char *const MSplitReductions[] = {"dbr", "seq", "MSplitReduction", 
 
 #define MSPCall(e) do { int _rc = (e); PetscCheck(!_rc, PETSC_COMM_SELF, _rc, "%s", msp_get_last_error()); } while (0)
 
+#if defined(PETSC_USE_64BIT_INDICES)
+#error "the MI355X path takes PetscInt = int32 (msp_mat_create_csr); configure PETSc without --with-64-bit-indices"
+#endif
+
+/* The process's node-local rank, found once where every rank calls collectively (PetscDLLibraryRegister_petsc_msplit
+ * or MSplitRegisterAll, both inside or right after PetscInitialize): the per-object paths below (KSPSetUp of each
+ * block's KSP, the first VECMSPLIT) run at different times on different ranks in the asynchronous drivers, so they
+ * must not call a collective.  -1 until cached; then the launcher's local-rank variable is the fallback. */
+static int g_local_rank = -1;
+
+static PetscErrorCode MSplitCacheLocalRank(void)
+{
+  MPI_Comm    node;
+  PetscMPIInt local = 0;
+
+  PetscFunctionBegin;
+  if (g_local_rank >= 0) PetscFunctionReturn(PETSC_SUCCESS);
+  PetscCallMPI(MPI_Comm_split_type(PETSC_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node));
+  PetscCallMPI(MPI_Comm_rank(node, &local));
+  PetscCallMPI(MPI_Comm_free(&node));
+  g_local_rank = (int)local;
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static int MSplitLocalRankFromEnv(void)
+{
+  const char *vars[] = {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "MV2_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID",
+                        "LOCAL_RANK"};
+  for (size_t i = 0; i < sizeof(vars) / sizeof(vars[0]); ++i) {
+    const char *v = getenv(vars[i]);
+    if (v && *v) return atoi(v);
+  }
+  return 0;
+}
+
 /* The block's GPU: -msplit_device when given, else the rank's index on its node modulo the devices it sees (one
- * block per rank, one rank per GPU, as petscmpiexec -n 8 places them on an 8-GPU node).  Shared with
- * petsc_msplit_vecmat.c. */
+ * block per rank, one rank per GPU, as petscmpiexec -n 8 places them on an 8-GPU node).  Not collective.  Shared
+ * with petsc_msplit_vecmat.c. */
 PetscErrorCode MSplitDefaultDevice(int *dev)
 {
-  PetscInt    d   = -1;
-  PetscBool   set = PETSC_FALSE;
-  PetscMPIInt local = 0;
-  MPI_Comm    node;
-  int         ndev = 0;
+  PetscInt  d    = -1;
+  PetscBool set  = PETSC_FALSE;
+  int       ndev = 0;
 
   PetscFunctionBegin;
   PetscCall(PetscOptionsGetInt(NULL, NULL, "-msplit_device", &d, &set));
@@ -36,11 +72,44 @@ PetscErrorCode MSplitDefaultDevice(int *dev)
     *dev = (int)d;
     PetscFunctionReturn(PETSC_SUCCESS);
   }
-  PetscCallMPI(MPI_Comm_split_type(PETSC_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node));
-  PetscCallMPI(MPI_Comm_rank(node, &local));
-  PetscCallMPI(MPI_Comm_free(&node));
+  const int local = g_local_rank >= 0 ? g_local_rank : MSplitLocalRankFromEnv();
   MSPCall(msp_get_device_count(&ndev));
-  *dev = ndev > 0 ? (int)(local % ndev) : 0;
+  *dev = ndev > 0 ? local % ndev : 0;
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+/* petsc_msplit_vecmat.c: the process's one context (its GPU and stream, shared by every Vec, Mat and KSP of the
+ * plugin, so their work is ordered on one stream), and the HBM mirror of an aijmsplit matrix (NULL otherwise) */
+PetscErrorCode MSplitContext(msp_ctx **ctx);
+PetscErrorCode MSplitMatGetDevice(Mat A, msp_mat **d);
+
+/* The inner operator as a sequential CSR (npb = 1: one rank per block, utils.c:473's MatCreateSubMatrix on the
+ * block's communicator).  MATSEQAIJ and aijmsplit are the CSR itself; MATMPIAIJ on one rank is its diagonal
+ * block, whose off-diagonal block must be empty.  Anything else is refused. */
+static PetscErrorCode MSplitSeqOperator(Mat A, Mat *Ad)
+{
+  PetscBool   seq, mpi, ams;
+  PetscMPIInt size;
+
+  PetscFunctionBegin;
+  PetscCall(PetscObjectTypeCompare((PetscObject)A, MATSEQAIJ, &seq));
+  PetscCall(PetscObjectTypeCompare((PetscObject)A, "aijmsplit", &ams));
+  PetscCall(PetscObjectTypeCompare((PetscObject)A, MATMPIAIJ, &mpi));
+  if (seq || ams) {
+    *Ad = A;
+    PetscFunctionReturn(PETSC_SUCCESS);
+  }
+  PetscCheck(mpi, PetscObjectComm((PetscObject)A), PETSC_ERR_SUP,
+             "msplitgmres: the operator must be MATSEQAIJ, aijmsplit or MATMPIAIJ (got %s)", ((PetscObject)A)->type_name);
+  PetscCallMPI(MPI_Comm_size(PetscObjectComm((PetscObject)A), &size));
+  PetscCheck(size == 1, PetscObjectComm((PetscObject)A), PETSC_ERR_SUP,
+             "msplitgmres: one rank per block (-npb 1); the operator's communicator has %d", (int)size);
+  Mat     Ao;
+  MatInfo info;
+  PetscCall(MatMPIAIJGetSeqAIJ(A, Ad, &Ao, NULL));
+  PetscCall(MatGetInfo(Ao, MAT_LOCAL, &info));
+  PetscCheck(info.nz_used == 0, PETSC_COMM_SELF, PETSC_ERR_SUP,
+             "msplitgmres: the MATMPIAIJ operator couples outside its rank (%g off-diagonal entries)", info.nz_used);
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
@@ -48,6 +117,7 @@ static PetscErrorCode KSPSetUp_MSplitGMRES(KSP ksp)
 {
   KSP_MSplit        *ms = (KSP_MSplit *)ksp->data;
   Mat                A, Ad;
+  msp_mat           *mirror = NULL;
   PetscInt           n, nr;
   const PetscInt    *ia, *ja;
   const PetscScalar *aa;
@@ -55,22 +125,34 @@ static PetscErrorCode KSPSetUp_MSplitGMRES(KSP ksp)
 
   PetscFunctionBegin;
   PetscCall(KSPGetOperators(ksp, &A, NULL));
-  /* npb = 1: the block's operator is one rank's diagonal AIJ block (utils.c:473) */
-  PetscCall(MatMPIAIJGetSeqAIJ(A, &Ad, NULL, NULL));          /* or A itself when it is MATSEQAIJ */
-  PetscCall(MatGetRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &nr, &ia, &ja, &done));
-  PetscCall(MatSeqAIJGetArrayRead(Ad, &aa));
-  if (!ms->ctx) {
-    int dev;
-    PetscCall(MSplitDefaultDevice(&dev));
-    MSPCall(msp_ctx_create(dev, NULL, &ms->ctx));
+  PetscCall(MSplitSeqOperator(A, &Ad));
+  if (!ms->ctx) PetscCall(MSplitContext(&ms->ctx));
+  if (!ms->A_borrowed) MSPCall(msp_mat_destroy(&ms->A));
+  ms->A = NULL;
+  PetscCall(MSplitMatGetDevice(Ad, &mirror));
+  if (mirror) { /* aijmsplit: its MatAssemblyEnd already put the CSR in HBM -- no second upload */
+    ms->A          = mirror;
+    ms->A_borrowed = PETSC_TRUE;
+    PetscCall(MatGetLocalSize(Ad, &nr, NULL));
+  } else {
+    PetscCall(MatGetRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &nr, &ia, &ja, &done));
+    PetscCheck(done, PETSC_COMM_SELF, PETSC_ERR_SUP, "msplitgmres: MatGetRowIJ could not give the CSR");
+    PetscCall(MatSeqAIJGetArrayRead(Ad, &aa));
+    MSPCall(msp_mat_create_csr(ms->ctx, (int32_t)nr, (int32_t)nr, ia, ja, aa, &ms->A));
+    ms->A_borrowed = PETSC_FALSE;
+    PetscCall(MatSeqAIJRestoreArrayRead(Ad, &aa));
+    PetscCall(MatRestoreRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &n, &ia, &ja, &done));
   }
-  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
-  MSPCall(msp_mat_destroy(&ms->A));
-  MSPCall(msp_mat_create_csr(ms->ctx, (int32_t)nr, (int32_t)nr, ia, ja, aa, &ms->A));
-  PetscCall(MatSeqAIJRestoreArrayRead(Ad, &aa));
-  PetscCall(MatRestoreRowIJ(Ad, 0, PETSC_FALSE, PETSC_FALSE, &n, &ia, &ja, &done));
   if (!ms->ksp) MSPCall(msp_ksp_create(ms->ctx, &ms->ksp));
   MSPCall(msp_ksp_set_operators(ms->ksp, ms->A));
+  if (ms->b) {
+    int64_t have = 0;
+    MSPCall(msp_vec_get_size(ms->b, &have));
+    if (have != (int64_t)nr) { /* KSPSetOperators with an operator of another size */
+      MSPCall(msp_vec_destroy(&ms->b));
+      MSPCall(msp_vec_destroy(&ms->x));
+    }
+  }
   if (!ms->b) {
     MSPCall(msp_vec_create(ms->ctx, nr, &ms->b));
     MSPCall(msp_vec_create(ms->ctx, nr, &ms->x));
@@ -90,6 +172,19 @@ static PetscErrorCode KSPSolve_MSplitGMRES(KSP ksp)
   KSPConvergedDefaultCtx *cctx = (KSPConvergedDefaultCtx *)ksp->cnvP;
 
   PetscFunctionBegin;
+  if (ms->A_borrowed) { /* an aijmsplit operator re-assembled since KSPSetUp has a new HBM mirror: follow it */
+    Mat      A, Ad;
+    msp_mat *mirror = NULL;
+    PetscCall(KSPGetOperators(ksp, &A, NULL));
+    PetscCall(MSplitSeqOperator(A, &Ad));
+    PetscCall(MSplitMatGetDevice(Ad, &mirror));
+    PetscCheck(mirror, PETSC_COMM_SELF, PETSC_ERR_ARG_WRONGSTATE, "msplitgmres: the aijmsplit operator lost its mirror");
+    if (mirror != ms->A) {
+      ms->A = mirror;
+      MSPCall(msp_ksp_set_operators(ms->ksp, ms->A));
+    }
+  }
+  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction)); /* the shared context: this KSP's order */
   MSPCall(msp_ksp_get_default_opts(&o));
   o.restart       = (int32_t)ms->restart;
   o.max_it        = (int32_t)ksp->max_it;
@@ -141,8 +236,8 @@ static PetscErrorCode KSPDestroy_MSplitGMRES(KSP ksp)
   msp_vec_destroy(&ms->b);
   msp_vec_destroy(&ms->x);
   msp_ksp_destroy(&ms->ksp);
-  msp_mat_destroy(&ms->A);
-  msp_ctx_destroy(&ms->ctx);
+  if (!ms->A_borrowed) msp_mat_destroy(&ms->A);
+  ms->ctx = NULL; /* shared, not owned */
   PetscCall(PetscFree(ksp->data));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
@@ -170,7 +265,7 @@ PetscErrorCode KSPCreate_MSplitGMRES(KSP ksp)
  * rank per block, as the reference runs it); it is copied to HBM at KSPSetUp
  * (the drivers call KSPSetOperators every outer iteration, SMSM-global.c:331). */
 typedef struct {
-  msp_ctx *ctx;
+  msp_ctx *ctx; /* the process's shared context: not owned */
   msp_dense *R;
   msp_lsqr *lsqr;
   msp_vec *b, *x;
@@ -193,12 +288,7 @@ static PetscErrorCode KSPSetUp_MSplitLSQR(KSP ksp)
   else Al = A;
   PetscCall(MatGetSize(Al, &m, &n));
   PetscCall(MatDenseGetLDA(Al, &lda));
-  if (!ms->ctx) {
-    int dev;
-    PetscCall(MSplitDefaultDevice(&dev));
-    MSPCall(msp_ctx_create(dev, NULL, &ms->ctx));
-  }
-  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
+  if (!ms->ctx) PetscCall(MSplitContext(&ms->ctx));
   MSPCall(msp_dense_destroy(&ms->R));
   MSPCall(msp_dense_create(ms->ctx, m, (int32_t)n, &ms->R));
   PetscCall(MatDenseGetArrayRead(Al, &a));
@@ -224,6 +314,7 @@ static PetscErrorCode KSPSolve_MSplitLSQR(KSP ksp)
   double             rnorm;
 
   PetscFunctionBegin;
+  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
   MSPCall(msp_lsqr_get_default_opts(&o));
   o.max_it     = (int32_t)ksp->max_it;
   o.rtol       = ksp->rtol;
@@ -273,7 +364,7 @@ static PetscErrorCode KSPDestroy_MSplitLSQR(KSP ksp)
   msp_vec_destroy(&ms->x);
   msp_lsqr_destroy(&ms->lsqr);
   msp_dense_destroy(&ms->R);
-  msp_ctx_destroy(&ms->ctx);
+  ms->ctx = NULL; /* shared, not owned */
   PetscCall(PetscFree(ksp->data));
   PetscFunctionReturn(PETSC_SUCCESS);
 }
@@ -299,6 +390,7 @@ PetscErrorCode KSPCreate_MSplitLSQR(KSP ksp)
 PetscErrorCode MSplitRegisterAll(void)
 {
   PetscFunctionBegin;
+  PetscCall(MSplitCacheLocalRank()); /* collective on PETSC_COMM_WORLD: every rank is here */
   PetscCall(KSPRegister("msplitgmres", KSPCreate_MSplitGMRES));
   PetscCall(KSPRegister("msplitlsqr", KSPCreate_MSplitLSQR));
   PetscFunctionReturn(PETSC_SUCCESS);

@@ -35,7 +35,9 @@ static msp_ctx *g_ctx; /* one context (GPU) per process: the block's GPU */
 
 PetscErrorCode MSplitDefaultDevice(int *dev); /* petsc_msplit_ksp.c: -msplit_device, else node-local rank % ndev */
 
-static PetscErrorCode MSplitContext(msp_ctx **ctx)
+/* The process's one context, shared by every Vec, Mat and KSP of the plugin (petsc_msplit_ksp.c): one stream
+ * orders all of their work.  It lives until the process ends. */
+PetscErrorCode MSplitContext(msp_ctx **ctx)
 {
   PetscFunctionBegin;
   if (!g_ctx) {
@@ -383,6 +385,18 @@ static PetscErrorCode MatCreate_AIJMSplit(Mat A)
   A->ops->destroy     = MatDestroy_AIJMSplit;
   PetscCall(PetscFree(A->defaultvectype));
   PetscCall(PetscStrallocpy(VECMSPLIT, &A->defaultvectype)); /* MatCreateVecs -> VECMSPLIT */
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+/* The HBM mirror of an aijmsplit matrix (made at its MatAssemblyEnd), or NULL for any other Mat: msplitgmres
+ * runs on it instead of uploading the CSR again (petsc_msplit_ksp.c KSPSetUp_MSplitGMRES). */
+PetscErrorCode MSplitMatGetDevice(Mat A, msp_mat **d)
+{
+  PetscBool is;
+  PetscFunctionBegin;
+  *d = NULL;
+  PetscCall(PetscObjectTypeCompare((PetscObject)A, MATAIJMSPLIT, &is));
+  if (is && A->spptr) *d = MMS(A)->d;
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 

@@ -17,7 +17,7 @@ def pytest_configure(config):
 # memory-heavy per-GPU AMAM blocks run last, so that under `pytest -x` one host-side failure there can no longer
 # hide the device parity record collected before it.
 _LATE = ["test_gpu_amam_configs.py", "test_gpu_async_mp.py", "test_gpu_libcomm_mp.py", "test_gpu_bench.py",
-         "test_gpu_c_host.py", "test_gpu_c_drivers.py"]
+         "test_gpu_c_host.py", "test_gpu_c_drivers.py", "test_gpu_nb8.py"]
 
 
 def pytest_collection_modifyitems(session, config, items):

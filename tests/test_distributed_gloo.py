@@ -241,3 +241,48 @@ def test_smsm_gloo_matches_oracle(oracle, world, problem):
         assert np.array_equal(np.array(lits), ref["lsqr_its"])
         assert fnorm == ref["final_norm"]
     assert np.array_equal(np.concatenate([o[7] for o in out]), ref["x"])
+
+
+def _fault_worker(rank, world, port, problem, q):
+    """sm_solve with rank 1's stop decision flipped at the first outer iteration (MSPLIT_FAULT_STOP_RANK)."""
+    os.environ["MSPLIT_FAULT_STOP_RANK"] = "1"
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import TorchComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import sm_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.utils import block_layout
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        dim, nx, ny, nz, rtol = problem
+        blk = OracleBlock(block_layout(dim, nx, ny, nz, world, rank), po)
+        try:
+            sm_solve([blk], TorchComm(), rtol=rtol, max_outer=300)
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_stop_disagreement_is_an_error_on_every_rank_not_a_hang():
+    """The ranks agree on (outer iteration, stop) once per outer iteration (multisplitting.agree_on_stop,
+    msp_comm_agree).  One rank injected to stop alone at the first outer iteration: every rank raises, naming
+    the disagreement, instead of the others blocking in their next collective (round 4's pre-fix hang)."""
+    out = _run(3, (3, 8, 8, 9, 1e-6), _fault_worker)
+    assert [r for r, _ in out] == [0, 1, 2]
+    assert all("disagree" in msg for _, msg in out), out
+
+
+def test_smsm_eight_ranks_gloo_matches_oracle(oracle):
+    """nb = 8 (the driver's scaling world size), one rank per block over gloo, bitwise the oracle."""
+    problem = (3, 6, 6, 16, 3, 1e-6)
+    out = _run(8, problem, _smsm_worker)
+    ref = oracle.smsm_solve(3, 6, 6, 16, 8, 3, 1e-6, dict(INNER, reduce_mode=oracle.REDUCE_DBR),
+                            dict(OUTER, reduce_mode=oracle.REDUCE_DBR), max_outer=100)
+    for rank, outer, norm0, hist, its, lits, fnorm, x in out:
+        assert outer == ref["outer_its"] and norm0 == ref["norm0"]
+        assert np.array_equal(np.array(hist), ref["hist"])
+        assert np.array_equal(np.array(lits), ref["lsqr_its"])
+        assert fnorm == ref["final_norm"]
+    assert np.array_equal(np.concatenate([o[7] for o in out]), ref["x"])

@@ -84,13 +84,14 @@ def test_single_gpu_line_is_verified():
     assert out["config"]["transport"] == "none"
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_rccl_multi_rank_line_is_verified(n):
     """The driver's N > 1 path itself -- torch.distributed.run, the nccl (RCCL) process group, LibComm's library
     RCCL communicator, --require-rccl -- with n ranks on this box's one GPU, each under its own NCCL_HOSTID (RCCL's
     socket transport instead of xGMI: correctness, not speed).  The line says transport rccl, and the post-timing
-    SMSM-global check over that communicator reproduces the oracle's n-block record bit for bit on every rank."""
-    r = _launch(n, ["--require-rccl"] + SMALL, rccl_hosts=True)
+    SMSM-global check over that communicator reproduces the oracle's n-block record bit for bit on every rank.
+    n = 8 is the driver's scaling world size: the first time its exact launch runs is here, not on the 8-GPU node."""
+    r = _launch(n, ["--require-rccl"] + SMALL, rccl_hosts=True, timeout=240 if n < 8 else 480)
     assert r.returncode == 0, r.stderr[-3000:]
     out = _json(r.stdout)
     assert out["n_gpus"] == n and out["config"]["transport"] == "rccl"

@@ -324,3 +324,19 @@ def test_isolve_configs0_command_line_equals_explicit_prefixes_and_oracle(ctx, o
                            dict(OUTER_ORC, reduce_mode=oracle.REDUCE_DBR), max_outer=200)
     _assert_same_run(got, ro, f"isolve configs[0] ({launch})")
     assert got["final_norm"] == ro["final_norm"]
+
+
+@pytest.mark.parametrize("prog", [SM, SMSM])
+def test_c_host_mpi_stop_disagreement_exits_instead_of_hanging(built, prog):
+    """Every rank agrees on (outer iteration, stop) once per outer iteration through msp_comm_agree.  With rank 1
+    injected to stop alone at the first outer iteration (MSPLIT_FAULT_STOP_RANK=1), the run exits non-zero on
+    every rank within seconds, naming the disagreement -- round 4's pre-fix corruption hung such a run until its
+    150 s limit (profiles/r04/comm_fix/)."""
+    exe = os.path.join(HOST, "msplit_driver_mpi")
+    args = _problem_args(prog, 3, 8, 8, 12, 2, 4, 1e-6)
+    p = subprocess.run([MPIEXEC] + MPI_LAUNCH + ["-n", "2", "-env", "MSPLIT_FAULT_STOP_RANK", "1", exe] + args
+                       + ["-msplit_transport", "host", "-json"], capture_output=True, text=True, timeout=120,
+                       start_new_session=True)
+    assert p.returncode != 0
+    assert "disagree" in p.stderr, p.stderr[-2000:]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

@@ -76,7 +76,34 @@ def _smsm_opts(nb, s):
     return Options(f"{inner} {outer} -s {s}")
 
 
-C3_OUTER_ITS = 5   # tools/configs_run.py c3 (profiles/r01/configs/), the DBR order
+C3_OUTER_ITS = 5   # tools/configs_run.py c3 (profiles/r01/configs/), the DBR order: the GPU's own count (the
+                   # single-threaded-order oracle at 512^3 needs more memory and hours than either box gives a
+                   # test); configs[2]'s arithmetic itself is pinned to the oracle at 64^3 - 256^3 below
+C2_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs2_smsm.json")
+
+
+@pytest.mark.parametrize("cube", [64, 128, 256])
+def test_configs2_options_bitwise_oracle_record(ctx, cube):
+    """configs[2]'s exact options -- SMSM-global, 2 z-slab blocks, s 20, inner GMRES(30) max_it 20 rtol 1e-20,
+    outer LSQR max_it 70 rtol 1e-15 with the exact matrix norm and the default test, -rtol 1e-4 (SMSM-global.c:
+    288-363, running_bulk_test_g5k:230, :247-248) -- on cubes up to 256^3, bit for bit the committed DBR oracle
+    record (tests/golden/configs2_smsm.json, written by tests/golden/make_configs2.py: 256^3 takes the 8-thread
+    oracle 13 minutes): outer count, norm0, every outer LSQR residual, LSQR counts and reasons, every inner count,
+    the final residual and the SHA-256 of x."""
+    import hashlib
+    import json
+    rec = json.load(open(C2_GOLDEN))["cubes"][str(cube)]
+    comm = LocalComm()
+    blocks, mini = make_smsm(ctx, 3, cube, cube, cube, 2, range(2), 20, _smsm_opts(2, 20), comm)
+    res = smsm_solve(blocks, comm, 20, mini, rtol=1e-4, max_outer=40)
+    x = np.concatenate([blk.x.get_array() for blk in blocks])
+    mini.close()
+    assert res.outer_its == rec["outer_its"] and float(res.norm0).hex() == rec["norm0_hex"]
+    assert [float(h).hex() for h in res.hist] == rec["hist_hex"]
+    assert [int(v) for v in res.lsqr_its] == rec["lsqr_its"] and [int(v) for v in res.lsqr_reason] == rec["lsqr_reason"]
+    assert np.array(res.inner_its).tolist() == rec["inner_its"]
+    assert float(res.final_norm).hex() == rec["final_norm_hex"]
+    assert hashlib.sha256(np.ascontiguousarray(x, np.float64).tobytes()).hexdigest() == rec["x_sha256"]
 
 
 def _c3_run(ctx):

@@ -1,4 +1,5 @@
 """CPU tests of the boundary and the host logic (no compute calls)."""
+import glob
 import os
 import subprocess
 
@@ -209,3 +210,70 @@ def test_isolve_single_process_and_python_variants():
     p = subprocess.run([os.path.join(ROOT, "host", "isolve"), "--np", "2", "--npb", "2"], capture_output=True,
                        text=True, env=dict(os.environ, ISOLVE_DRYRUN="1"), timeout=60)
     assert p.returncode != 0 and "npb" in p.stderr
+
+
+def _split_top(args: str):
+    """The comma-separated items of an argument or parameter list, at parenthesis depth 0."""
+    items, depth, cur = [], 0, ""
+    for ch in args:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        if ch == "," and depth == 0:
+            items.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        items.append(cur)
+    return [i.strip() for i in items]
+
+
+def _header_arity():
+    import re
+    txt = open(os.path.join(ROOT, "include", "msplit.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(?:int\s+|const char\s*\*\s*|void\s+)(msp_\w+)\s*\(([^;{]*?)\)\s*;", txt, flags=re.S):
+        params = _split_top(m.group(2))
+        out[m.group(1)] = 0 if params in ([], ["void"]) else len(params)
+    return out
+
+
+def _calls(src: str):
+    """(name, argument count, line) of every msp_* call in a C source."""
+    import re
+    src = re.sub(r"/\*.*?\*/", lambda m: "\n" * m.group(0).count("\n"), src, flags=re.S)
+    for m in re.finditer(r"\b(msp_\w+)\s*\(", src):
+        i, depth = m.end(), 1
+        while depth:
+            depth += {"(": 1, ")": -1}.get(src[i], 0)
+            i += 1
+        yield m.group(1), len(_split_top(src[m.end():i - 1])), src.count("\n", 0, m.start()) + 1
+
+
+def test_plugin_calls_match_the_c_abi():
+    """plugin/petsc/*.c cannot be compiled here (no PETSc in the image), so its use of the C ABI is checked as text:
+    every msp_* function it calls is declared in include/msplit.h and called with the declared argument count."""
+    decl = _header_arity()
+    assert len(decl) > 80
+    seen = 0
+    for fn in glob.glob(os.path.join(ROOT, "plugin", "petsc", "*.c")):
+        for name, nargs, line in _calls(open(fn).read()):
+            assert name in decl, f"{os.path.basename(fn)}:{line}: {name} is not declared in include/msplit.h"
+            assert nargs == decl[name], (f"{os.path.basename(fn)}:{line}: {name} called with {nargs} arguments, "
+                                         f"declared with {decl[name]}")
+            seen += 1
+    assert seen > 40
+
+
+def test_plugin_device_choice_is_not_collective_per_object():
+    """The node-local rank is found once, in the registration every rank runs inside PetscInitialize; the
+    per-object paths (each block's KSPSetUp, the first VECMSPLIT) never call a collective."""
+    src = open(os.path.join(ROOT, "plugin", "petsc", "petsc_msplit_ksp.c")).read()
+    body = src[src.index("PetscErrorCode MSplitDefaultDevice(int *dev)"):]
+    body = body[:body.index("\n}\n")]
+    assert "MPI_Comm_split_type" not in body and "MPI_" not in body
+    reg = src[src.index("PetscErrorCode MSplitRegisterAll(void)"):]
+    assert "MSplitCacheLocalRank()" in reg[:reg.index("\n}\n")]

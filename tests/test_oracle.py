@@ -240,3 +240,26 @@ def test_smsm_ranks_record_matches_oracle(oracle):
     assert sorted(rec["worlds"]) == [str(n) for n in range(2, 9)]
     for nb in (2, 3):
         assert gen.record(nb) == rec["worlds"][str(nb)]
+    assert gen.record(8) == rec["worlds"]["8"]              # nb = 8: the driver's scaling world size
+
+
+def test_configs2_record_matches_oracle(oracle):
+    """tests/golden/configs2_smsm.json (configs[2]'s options, pinned on the GPU at 64^3 - 256^3) is what the oracle
+    computes now: the generator's own function rebuilds the 64^3 record (the 256^3 one takes 13 minutes)."""
+    import importlib.util
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_configs2", os.path.join(here, "golden", "make_configs2.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    rec = json.load(open(os.path.join(here, "golden", "configs2_smsm.json")))
+    assert sorted(rec["cubes"], key=int) == ["32", "64", "128", "256"]
+    oracle.set_threads(min(8, os.cpu_count() or 1))
+    try:
+        got = gen.record(64)
+    finally:
+        oracle.set_threads(1)
+    got.pop("seconds")
+    want = dict(rec["cubes"]["64"])
+    want.pop("seconds")
+    assert got == want
+    assert rec["cubes"]["256"]["outer_its"] == 4 and all(r == -3 for r in rec["cubes"]["256"]["lsqr_reason"])
