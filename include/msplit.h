@@ -488,13 +488,19 @@ int msp_abcast_publish_dense(msp_abcast *bc, const msp_dense *D, int32_t *publis
 int msp_abcast_fetch_dense(msp_abcast *bc, int32_t src, msp_dense *D, int32_t *got);
 /* device buffers: the published blocks stay in the sender's HBM (HIP IPC), a fetch
  * is a peer copy over xGMI; enable on every rank before the first publish,
- * close_peers on every rank before destroy.  nbuf = 2 (a publish fills the
- * buffer readers are not using) or 1 (half the HBM: a publish waits until no
- * reader holds the newest block, and readers skip a block being rewritten);
- * 0 chooses: 2 while a quarter of the GPU's HBM stays free after them, else 1.
- * msp_abcast_get_nbuf reports the count in use (0 before enable_device). */
+ * close_peers on every rank before destroy.  Neither end waits on the host: a
+ * publish enqueues its copy and the stream publishes the block behind it; a
+ * fetch enqueues the peer copy into D and the stream releases the source's
+ * buffer behind it (D is ready in stream order).  A publish whose previous copy
+ * is still unpublished, or whose buffer a reader still holds, is skipped
+ * (published = 0).  nbuf = 2 (a publish fills the buffer readers are not using)
+ * or 1 (half the HBM: readers skip a block being rewritten); 0 chooses: 2 while
+ * a quarter of the GPU's HBM stays free after them, else 1.  At most 512 ranks.
+ * msp_abcast_get_nbuf reports the count in use (0 before enable_device);
+ * msp_abcast_get_stats the device publishes enqueued and skipped. */
 int msp_abcast_enable_device(msp_abcast *bc, msp_ctx *ctx, int32_t nbuf);
 int msp_abcast_get_nbuf(const msp_abcast *bc, int32_t *nbuf);
+int msp_abcast_get_stats(const msp_abcast *bc, int64_t *sent, int64_t *skipped);
 int msp_abcast_close_peers(msp_abcast *bc);
 
 /* ------------------------------------------------- convergence detection */

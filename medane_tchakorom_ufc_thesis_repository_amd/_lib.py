@@ -165,6 +165,7 @@ _SIGS = {
     "msp_amsg_get_stats": [_vp, _P(C.c_int64), _P(C.c_int64)],
     "msp_abcast_enable_device": [_vp, _vp, C.c_int32],
     "msp_abcast_get_nbuf": [_vp, _i32p],
+    "msp_abcast_get_stats": [_vp, _P(C.c_int64), _P(C.c_int64)],
     "msp_abcast_close_peers": [_vp],
     "msp_abcast_create": [C.c_char_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32, _P(_vp)],
     "msp_abcast_destroy": [_P(_vp)],

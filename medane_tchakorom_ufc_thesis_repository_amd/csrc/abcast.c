@@ -18,7 +18,21 @@
  * "previous send not complete".  Payloads move HBM <-> the registered region
  * by DMA, or, with device buffers enabled (msp_abcast_enable_device), stay in
  * the sender's HBM (HIP IPC): a publish is one HBM -> HBM copy, a fetch one
- * peer copy over xGMI; the lock words stay in shared memory.
+ * peer copy over xGMI.
+ *
+ * Device buffers never wait on the host (the R rows of configs[3] are 21.5 GB
+ * per block).  A publish claims the buffer that is not the newest (the only
+ * one with a single buffer), enqueues the copy into it and, behind the copy on
+ * the sender's stream, a one-lane kernel that publishes (count, buffer) into
+ * the source's shared word `pub`.  A fetch marks the newest buffer as being
+ * read by this rank, enqueues the peer copy out of it, and its stream clears
+ * the mark behind the copy.  Claim and mark are Dekker's handshake (each side
+ * stores its word, then loads the other's), so a buffer is never written while
+ * a reader's pending copy reads it: a publish whose previous copy is still
+ * unpublished, or whose buffer a reader still holds, is skipped -- the
+ * reference's MPI_Test of the previous Isend (comm.c:288-351).  Ranks of one
+ * process on one stream (round-robin) publish and release at once: stream
+ * order already serialises their copies (as amsg.c's planes).
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -58,9 +72,21 @@ typedef struct {
   _Atomic int32_t ready;
   int32_t pid;
   uint64_t rawptr; /* valid in the exporting process only */
+  uint64_t stream; /* the exporting context's stream (same process and stream: copies ordered by the stream) */
   uint8_t handle[MSPI_IPC_HANDLE_BYTES];
-  uint8_t pad[128 - 16 - MSPI_IPC_HANDLE_BYTES];
+  uint8_t pad[128 - 24 - MSPI_IPC_HANDLE_BYTES];
 } abc_ipc;
+
+/* device-buffer state of one source, in the shared region (GPU-written words: pub, reading) */
+typedef struct {
+  _Atomic uint64_t pub;   /* (count << 1) | buffer of the newest complete payload; 0: none yet */
+  _Atomic uint64_t claim; /* (count << 1) | buffer of the source's latest publish; == pub: nothing in flight */
+  int64_t nrows[2], ncols[2];
+  int32_t nbuf;           /* the source's device buffers (1 or 2) */
+  uint8_t pad[128 - 16 - 32 - 4];
+} abc_dline;
+
+#define ABC_MAX_DEVICE_RANKS 512 /* the reading words are nranks x 2 x nranks */
 
 struct msp_abcast {
   char name[128];
@@ -73,6 +99,13 @@ struct msp_abcast {
   uint64_t *seen;  /* [src] version last fetched */
   int registered;
   abc_ipc *ipc;    /* [rank] exported device buffers */
+  abc_dline *dl;   /* [src] device-buffer state */
+  _Atomic uint32_t *reading;  /* [src][buffer][reader]: reader's copy out of src's buffer pending */
+  uint8_t *dstate_dev;        /* the same region as the GPU addresses it (dl first) */
+  size_t dstate_off;          /* offset of dl in the region */
+  uint64_t skey;              /* this rank's stream */
+  uint64_t *dseen; /* [src] the pub word of the last payload fetched (device buffers) */
+  int64_t sent, skipped;      /* device publishes enqueued / skipped */
   msp_ctx *dctx;   /* device buffers enabled */
   double *dbufs;   /* this rank's nbuf_dev x cap device buffers */
   int nbuf_dev;    /* 2, or 1 where HBM is short: a publish then waits out the readers of the newest block */
@@ -86,6 +119,8 @@ static int berr(int code, const char *msg) {
 }
 
 static size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static int ensure_registered(msp_abcast *b);
 
 static double *buf_at(msp_abcast *b, int src, int k) {
   return (double *)(b->bufs + ((size_t)src * 2 + (size_t)k) * b->buf_bytes);
@@ -107,7 +142,11 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
   b->buf_bytes = round_up((size_t)(cap > 0 ? cap : 1) * sizeof(double), 4096);
   const size_t lines_bytes = round_up((size_t)nranks * sizeof(src_line), 4096);
   const size_t ipc_bytes = round_up((size_t)nranks * sizeof(abc_ipc), 4096);
-  b->bytes = 4096 + lines_bytes + (size_t)nranks * 2 * b->buf_bytes + ipc_bytes;
+  const size_t dl_bytes = round_up((size_t)nranks * sizeof(abc_dline), 4096);
+  const size_t rd_bytes =
+      nranks <= ABC_MAX_DEVICE_RANKS ? round_up((size_t)nranks * 2 * (size_t)nranks * sizeof(uint32_t), 4096) : 0;
+  b->dstate_off = 4096 + lines_bytes + (size_t)nranks * 2 * b->buf_bytes + ipc_bytes;
+  b->bytes = b->dstate_off + dl_bytes + rd_bytes;
   int fd;
   if (b->owner) {
     shm_unlink(name);
@@ -140,6 +179,8 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
   b->lines = (src_line *)(b->base + 4096);
   b->bufs = b->base + 4096 + lines_bytes;
   b->ipc = (abc_ipc *)(b->bufs + (size_t)nranks * 2 * b->buf_bytes);
+  b->dl = (abc_dline *)(b->base + b->dstate_off);
+  b->reading = rd_bytes ? (_Atomic uint32_t *)((uint8_t *)b->dl + dl_bytes) : NULL;
   if (b->owner) {
     h->nranks = nranks;
     h->cap = cap;
@@ -152,7 +193,10 @@ int msp_abcast_create(const char *name, int32_t nranks, int32_t rank, int64_t ca
     return berr(MSP_ERR_ARG_WRONG, "shared-memory region not initialised by the owner, or different sizes");
   }
   b->seen = (uint64_t *)calloc((size_t)nranks, sizeof(uint64_t));
-  if (!b->seen) {
+  b->dseen = (uint64_t *)calloc((size_t)nranks, sizeof(uint64_t));
+  if (!b->seen || !b->dseen) {
+    free(b->seen);
+    free(b->dseen);
     munmap(b->base, b->bytes);
     free(b);
     return berr(MSP_ERR_MEM, "allocation failed");
@@ -165,6 +209,7 @@ int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   if (!b || !ctx) return berr(MSP_ERR_ARG_NULL, "NULL argument");
   if (nbuf < 0 || nbuf > 2) return berr(MSP_ERR_ARG_OUTOFRANGE, "nbuf must be 0 (auto), 1 or 2");
   if (b->dctx) return MSP_SUCCESS;
+  if (!b->reading) return berr(MSP_ERR_SUP, "device buffers take at most 512 ranks");
   const size_t buf_bytes = (size_t)(b->cap > 0 ? b->cap : 1) * sizeof(double);
   if (nbuf == 0) {
     /* auto: two buffers only while a quarter of the GPU's HBM stays free after them -- the run allocates more
@@ -178,8 +223,14 @@ int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   b->peer = (double **)calloc((size_t)b->nranks, sizeof(double *));
   b->opened = (uint8_t *)calloc((size_t)b->nranks, 1);
   if (!b->peer || !b->opened) return berr(MSP_ERR_MEM, "allocation failed");
+  /* the streams publish and release through the state words: the region must be mapped for the GPU */
+  int rc = ensure_registered(b);
+  if (rc) return rc;
+  void *dp = NULL;
+  if ((rc = mspi_host_device_ptr(b->dl, &dp))) return rc;
+  b->dstate_dev = (uint8_t *)dp;
   void *p = NULL;
-  int rc = mspi_dev_alloc(ctx, (size_t)nbuf * buf_bytes, &p);
+  rc = mspi_dev_alloc(ctx, (size_t)nbuf * buf_bytes, &p);
   if (rc) return rc;
   b->nbuf_dev = nbuf;
   abc_ipc *e = &b->ipc[b->rank];
@@ -189,10 +240,20 @@ int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   }
   b->dbufs = (double *)p;
   b->dctx = ctx;
+  b->skey = mspi_stream_key(ctx);
   mspi_ctx_retain(ctx);
+  b->dl[b->rank].nbuf = nbuf;
   e->pid = (int32_t)getpid();
   e->rawptr = (uint64_t)(uintptr_t)p;
+  e->stream = b->skey;
   atomic_store_explicit(&e->ready, 1, memory_order_release);
+  return MSP_SUCCESS;
+}
+
+int msp_abcast_get_stats(const msp_abcast *b, int64_t *sent, int64_t *skipped) {
+  if (!b) return berr(MSP_ERR_ARG_NULL, "abcast is NULL");
+  if (sent) *sent = b->sent;
+  if (skipped) *skipped = b->skipped;
   return MSP_SUCCESS;
 }
 
@@ -205,6 +266,12 @@ int msp_abcast_get_nbuf(const msp_abcast *b, int32_t *nbuf) {
 int msp_abcast_close_peers(msp_abcast *b) {
   if (!b) return berr(MSP_ERR_ARG_NULL, "abcast is NULL");
   if (!b->peer) return MSP_SUCCESS;
+  /* this rank's copies out of the peers' buffers, and its publish / release stores, are stream-ordered: let them
+   * finish before the mappings go */
+  if (b->dctx) {
+    int rc = msp_ctx_synchronize(b->dctx);
+    if (rc) return rc;
+  }
   for (int r = 0; r < b->nranks; ++r) {
     if (b->opened[r]) mspi_ipc_close(b->peer[r]);
     b->peer[r] = NULL;
@@ -245,6 +312,7 @@ int msp_abcast_destroy(msp_abcast **pb) {
   munmap(b->base, b->bytes);
   if (b->owner) shm_unlink(b->name);
   free(b->seen);
+  free(b->dseen);
   msp_ctx *c = b->dctx;
   free(b);
   *pb = NULL;
@@ -290,29 +358,113 @@ static int copy_in(const abc_view *v, const double *srcp) {
   return rc;
 }
 
+/* ------------------------------------------------------------ device buffers */
+static _Atomic uint32_t *reading_at(msp_abcast *b, int src, int k, int reader) {
+  return b->reading + ((size_t)src * 2 + (size_t)k) * (size_t)b->nranks + (size_t)reader;
+}
+
+static uint8_t *dev_addr(msp_abcast *b, const void *host_word) {
+  return b->dstate_dev + ((const uint8_t *)host_word - (const uint8_t *)b->dl);
+}
+
+/* peer's buffers driven by this very stream (the blocks of one process): stream order serialises every copy */
+static int same_stream(msp_abcast *b, int peer) {
+  abc_ipc *e = &b->ipc[peer];
+  return atomic_load_explicit(&e->ready, memory_order_acquire) && e->pid == (int32_t)getpid() && e->stream == b->skey;
+}
+
+static int all_same_stream(msp_abcast *b) {
+  for (int r = 0; r < b->nranks; ++r)
+    if (r != b->rank && !same_stream(b, r)) return 0;
+  return 1;
+}
+
+static int publish_device(msp_abcast *b, const abc_view *v, int32_t *published) {
+  abc_dline *d = &b->dl[b->rank];
+  const uint64_t P = atomic_load_explicit(&d->pub, memory_order_seq_cst);
+  if (atomic_load_explicit(&d->claim, memory_order_relaxed) != P) { /* the previous copy is not published yet */
+    b->skipped++;
+    return MSP_SUCCESS;
+  }
+  const int k = b->nbuf_dev == 1 ? 0 : (P ? 1 - (int)(P & 1) : 0); /* the buffer that is not the newest */
+  const uint64_t W = (((P >> 1) + 1) << 1) | (uint64_t)k;
+  atomic_store_explicit(&d->claim, W, memory_order_seq_cst);
+  for (int r = 0; r < b->nranks; ++r)
+    if (r != b->rank && atomic_load_explicit(reading_at(b, b->rank, k, r), memory_order_seq_cst)) {
+      atomic_store_explicit(&d->claim, P, memory_order_seq_cst); /* a reader still copies out of it */
+      b->skipped++;
+      return MSP_SUCCESS;
+    }
+  d->nrows[k] = v->nrows;
+  d->ncols[k] = v->ncols;
+  atomic_thread_fence(memory_order_release);
+  const size_t rowb = (size_t)v->nrows * sizeof(double);
+  int rc = mspi_d2d_async2d(b->dctx, b->dbufs + (size_t)k * (size_t)b->cap, rowb, v->p, (size_t)v->ld * sizeof(double),
+                            rowb, (size_t)v->ncols);
+  if (rc) {
+    atomic_store_explicit(&d->claim, P, memory_order_seq_cst);
+    return rc;
+  }
+  if (all_same_stream(b)) atomic_store_explicit(&d->pub, W, memory_order_seq_cst);
+  else if ((rc = mspi_stream_store_u64(b->dctx, (uint64_t *)dev_addr(b, &d->pub), W))) return rc;
+  b->sent++;
+  *published = 1;
+  return MSP_SUCCESS;
+}
+
+static int fetch_device(msp_abcast *b, int32_t src, const abc_view *v, int32_t *got) {
+  double *pbuf = NULL;
+  int rc = peer_bufs(b, src, &pbuf);
+  if (rc) return rc;
+  if (!pbuf) return MSP_SUCCESS; /* src has not enabled its buffers: nothing sent yet */
+  abc_dline *d = &b->dl[src];
+  const int one = d->nbuf == 1; /* one buffer: the source rewrites the newest itself */
+  const uint64_t P = atomic_load_explicit(&d->pub, memory_order_seq_cst);
+  if (!P || P == b->dseen[src]) return MSP_SUCCESS; /* nothing newer than the last block taken */
+  if (one && atomic_load_explicit(&d->claim, memory_order_seq_cst) != P) return MSP_SUCCESS; /* being rewritten */
+  const int k = (int)(P & 1);
+  _Atomic uint32_t *mark = reading_at(b, src, k, b->rank);
+  atomic_store_explicit(mark, 1u, memory_order_seq_cst);
+  if (atomic_load_explicit(&d->pub, memory_order_seq_cst) != P ||
+      (one && atomic_load_explicit(&d->claim, memory_order_seq_cst) != P)) { /* moved on: take it next time */
+    atomic_store_explicit(mark, 0u, memory_order_seq_cst);
+    return MSP_SUCCESS;
+  }
+  if (d->nrows[k] != v->nrows || d->ncols[k] != v->ncols) {
+    atomic_store_explicit(mark, 0u, memory_order_seq_cst);
+    return berr(MSP_ERR_ARG_SIZ, "received block has a different shape");
+  }
+  const size_t rowb = (size_t)v->nrows * sizeof(double);
+  if ((rc = mspi_d2d_async2d(b->dctx, v->p, (size_t)v->ld * sizeof(double), pbuf + (size_t)k * (size_t)b->cap, rowb,
+                             rowb, (size_t)v->ncols))) {
+    atomic_store_explicit(mark, 0u, memory_order_seq_cst);
+    return rc;
+  }
+  if (same_stream(b, src)) atomic_store_explicit(mark, 0u, memory_order_seq_cst);
+  else if ((rc = mspi_stream_store_u32(b->dctx, (uint32_t *)dev_addr(b, (const void *)mark), 0u))) return rc;
+  b->dseen[src] = P;
+  *got = 1;
+  return MSP_SUCCESS;
+}
+
+/* ------------------------------------------------------------ publish / fetch */
 static int publish(msp_abcast *b, const abc_view *v, int32_t *published) {
   *published = 0;
   if (b->dctx && !v->ctx) return berr(MSP_ERR_ARG_WRONG, "device buffers enabled: publish a dense block in HBM");
   if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
     return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
   if (v->nrows * (int64_t)v->ncols > b->cap) return berr(MSP_ERR_ARG_SIZ, "payload larger than the broadcast slot");
-  int rc = (v->ctx && !b->dctx) ? ensure_registered(b) : MSP_SUCCESS;
+  if (b->dctx) return publish_device(b, v, published);
+  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
   if (rc) return rc;
   src_line *L = &b->lines[b->rank];
   const int32_t newest = atomic_load_explicit(&L->newest, memory_order_acquire);
-  /* the buffer that is not the newest; with one device buffer, the newest itself (free of readers) */
-  const int w = (b->dctx && b->nbuf_dev == 1) ? 0 : (newest == 0 ? 1 : 0);
+  const int w = newest == 0 ? 1 : 0; /* the buffer that is not the newest */
   uint32_t expect = 0;
   if (!atomic_compare_exchange_strong_explicit(&L->lock[w], &expect, ABC_WRITER, memory_order_acq_rel,
                                                memory_order_relaxed))
     return MSP_SUCCESS; /* a reader still holds it: the previous send has not completed */
-  if (b->dctx) {
-    const size_t rowb = (size_t)v->nrows * sizeof(double);
-    rc = mspi_d2d_sync(b->dctx, b->dbufs + (size_t)w * (size_t)b->cap, rowb, v->p, (size_t)v->ld * sizeof(double),
-                       rowb, (size_t)v->ncols);
-  } else {
-    rc = copy_out(v, buf_at(b, b->rank, w));
-  }
+  rc = copy_out(v, buf_at(b, b->rank, w));
   if (rc) {
     atomic_store_explicit(&L->lock[w], 0u, memory_order_release);
     return rc;
@@ -332,13 +484,9 @@ static int fetch(msp_abcast *b, int32_t src, const abc_view *v, int32_t *got) {
   if (src < 0 || src >= b->nranks || src == b->rank) return berr(MSP_ERR_ARG_OUTOFRANGE, "source rank out of range");
   if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
     return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
-  int rc = (v->ctx && !b->dctx) ? ensure_registered(b) : MSP_SUCCESS;
+  if (b->dctx) return fetch_device(b, src, v, got);
+  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
   if (rc) return rc;
-  double *pbuf = NULL;
-  if (b->dctx) {
-    if ((rc = peer_bufs(b, src, &pbuf))) return rc;
-    if (!pbuf) return MSP_SUCCESS; /* src has not enabled its buffers: nothing sent yet */
-  }
   src_line *L = &b->lines[src];
   for (int attempt = 0; attempt < 64; ++attempt) {
     const int32_t k = atomic_load_explicit(&L->newest, memory_order_acquire);
@@ -356,13 +504,7 @@ static int fetch(msp_abcast *b, int32_t src, const abc_view *v, int32_t *got) {
       atomic_fetch_sub_explicit(&L->lock[k], 1u, memory_order_release);
       return berr(MSP_ERR_ARG_SIZ, "received block has a different shape");
     }
-    if (pbuf) {
-      const size_t rowb = (size_t)v->nrows * sizeof(double);
-      rc = mspi_d2d_sync(b->dctx, v->p, (size_t)v->ld * sizeof(double), pbuf + (size_t)k * (size_t)b->cap, rowb, rowb,
-                         (size_t)v->ncols);
-    } else {
-      rc = copy_in(v, buf_at(b, src, k));
-    }
+    rc = copy_in(v, buf_at(b, src, k));
     atomic_fetch_sub_explicit(&L->lock[k], 1u, memory_order_release);
     if (rc) return rc;
     b->seen[src] = ver;

@@ -19,6 +19,14 @@
  * all-gathers of 1 and s doubles per block.  The host enqueues steps in
  * chunks and reads the state back once per chunk; steps past the end return
  * at once on the device's stop flag.
+ *
+ * The DBR default (round 5) takes both products in ONE pass over R:
+ *   ONEPASS  U1 = R V - alpha U, ||U1||^2 and R^T U1 partials  (one pass over R and U)
+ *   gather block partials (1 + s doubles), beta, V1 = (R^T U1) * (1/beta) - beta V, the rest (one lane)
+ * 8*n*(s+3) bytes and one all-gather per block and step.  R^T U1 is taken from the unscaled U1 and
+ * multiplied by 1/beta after the sum -- one rounding that differs from PETSc's order (VecScale first),
+ * restated by the oracle's DBR mode (orc_lsqr_opts.onepass).  MSP_REDUCE_SEQ keeps PETSc's order;
+ * MSPLIT_LSQR_ONEPASS=0 the two passes.
  */
 #include <math.h>
 #include <stdlib.h>
@@ -173,11 +181,12 @@ static int lsqr_setup(msp_lsqr *l) {
       goto fail;
   }
   const int64_t nch = nchunks(l->maxn) > 0 ? nchunks(l->maxn) : 1;
-  if ((rc = mspi_malloc(l->ctx, (void **)&l->partial, (size_t)nch * 32 * sizeof(double)))) goto fail;
-  if ((rc = mspi_malloc(l->ctx, (void **)&l->gloc, (size_t)l->nloc * s * sizeof(double)))) goto fail;
+  const int64_t pw = s + 1 > 32 ? s + 1 : 32; /* partials per chunk: the one-pass step's 1 + s */
+  if ((rc = mspi_malloc(l->ctx, (void **)&l->partial, (size_t)nch * pw * sizeof(double)))) goto fail;
+  if ((rc = mspi_malloc(l->ctx, (void **)&l->gloc, (size_t)l->nloc * (s + 1) * sizeof(double)))) goto fail;
   if ((rc = mspi_malloc(l->ctx, (void **)&l->floc, (size_t)l->nloc * s * sizeof(double)))) goto fail;
   if (l->comm) {
-    if ((rc = mspi_malloc(l->ctx, (void **)&l->gall, (size_t)l->nblk * s * sizeof(double)))) goto fail;
+    if ((rc = mspi_malloc(l->ctx, (void **)&l->gall, (size_t)l->nblk * (s + 1) * sizeof(double)))) goto fail;
     if ((rc = mspi_malloc(l->ctx, (void **)&l->fall, (size_t)l->nblk * s * sizeof(double)))) goto fail;
   } else { /* every block is local: the local partials are the gathered ones */
     l->gall = l->gloc;
@@ -294,6 +303,10 @@ int msp_lsqr_solve(msp_lsqr *l, msp_vec *const *b, msp_vec *x) {
     write_back = e && e[0] == '1';
   }
   const int defer = !seq && !write_back;
+  /* MSPLIT_LSQR_ONEPASS=0: the two passes, PETSc's operation order (same-box A/B; the oracle's onepass = 0);
+   * read per solve, so a test can switch it */
+  const char *ope = getenv("MSPLIT_LSQR_ONEPASS");
+  const int onepass = defer && !(ope && ope[0] == '0');
   const int nsteps = l->o.max_it > 0 ? l->o.max_it : 1; /* the do-while runs at least once */
   for (int i = 0; i < nsteps; ++i) {
     double **U = l->U + (i & 1 ? nloc : 0);
@@ -301,6 +314,18 @@ int msp_lsqr_solve(msp_lsqr *l, msp_vec *const *b, msp_vec *x) {
     /* U of step 0 is the scaled b (written by the first dots); later it is the previous U1, stored unscaled,
      * whose scale 1/beta is still in st->uscale until this step's beta replaces it */
     const double *usc = defer && i > 0 ? &d.st->uscale : NULL;
+    if (onepass) { /* one pass over R: U1, ||U1||^2 and R^T U1 (unscaled) per block, one gather, one lane */
+      for (int k = 0; k < nloc; ++k)
+        if ((rc = mspi_dense_lsqr_onepass(c, l->R[k]->d, l->R[k]->lda, s, l->R[k]->nrows, d.V, &d.st->nalpha, U[k],
+                                          usc, U1[k], l->partial, l->gloc + k * (s + 1), stop)))
+          return rc;
+      if ((rc = gather(l, l->gloc, l->gall, s + 1)) || (rc = mspi_ls_onepass_step(c, d))) return rc;
+      if ((i + 1) % LSQR_CHUNK == 0 || i + 1 == nsteps) {
+        if ((rc = mspi_d2h_sync(c, h, d.st, sizeof(*h)))) return rc;
+        if (h->stop) break;
+      }
+      continue;
+    }
     for (int k = 0; k < nloc; ++k)
       if ((rc = mspi_dense_gemv(c, l->R[k]->d, l->R[k]->lda, s, l->R[k]->nrows, d.V, &d.st->nalpha, U[k], usc,
                                 U1[k], l->partial, l->gloc + k, stop)))

@@ -76,15 +76,18 @@ struct msp_comm {
   double* dsum = nullptr;   // msp_comm_sum_ordered: [own n | gathered nranks*n] on the device, persistent
   double* hsum = nullptr;   //                       pinned host mirror of the same
   int32_t sumcap = 0;       // n it was sized for
-  // host-synchronised hops around the host transport's all-gather (round 4's fix).  MSPLIT_COMM_HOST_SYNC=0 keeps
-  // the persistent buffers but orders the hops by the stream alone: the diagnostic that separates the two changes
-  // that fix made (profiles/r05/comm_cause/)
-  bool host_sync = true;
+  // Round 4's fix of the one-GPU multi-rank wrong answers made two changes at once: persistent buffers in place of
+  // hipMallocAsync / hipFreeAsync staging blocks, and a host synchronisation around every hop of the host
+  // transport.  Round 5 ran the failing cases with the persistent buffers and stream order alone -- the serialised
+  // ones (AMD_SERIALIZE_KERNEL/COPY=3, deterministic failures before the fix) and every multi-rank host-transport
+  // case: all bitwise the oracle (profiles/r05/comm_cause/).  So the stream-ordered allocator's reuse of a freed
+  // block was the cause, and the hops are ordered by the stream alone; MSPLIT_COMM_HOST_SYNC=1 restores the syncs.
+  bool host_sync = false;
 };
 
 static bool comm_host_sync_default() {
   const char* e = getenv("MSPLIT_COMM_HOST_SYNC");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 #define NCCLCHK(call)                                                                            \
@@ -253,7 +256,7 @@ extern "C" int msp_comm_exchange_neighbors(msp_comm* m, const msp_vec* src, int6
     return MSP_SUCCESS;
   }
   // host transport: [lo plane | hi plane] of every rank, gathered.  Persistent device buffers (no stream-ordered
-  // allocation: one-GPU multi-rank runs saw the planes of a freed-and-reused block), every copy host-synchronised
+  // allocation: one-GPU multi-rank runs saw the planes of a freed-and-reused block, see the struct)
   if (count > m->dxcap) {
     HIPCHK(hipStreamSynchronize(c->stream));
     if (m->dx) HIPCHK(hipFree(m->dx));
@@ -297,7 +300,7 @@ static int gather_host(msp_comm* m, const double* in, double* all, int32_t n) {
     m->sumcap = n;
   }
   // up from pinned memory, the all-gather, back to pinned memory, all on the context's stream; the read-back is
-  // waited for.  With host_sync each hop is also host-synchronised (round 4's fix; see the struct)
+  // waited for.  With host_sync (MSPLIT_COMM_HOST_SYNC=1) each hop is also host-synchronised (see the struct)
   memcpy(m->hsum, in, per);
   HIPCHK(hipMemcpyAsync(m->dsum, m->hsum, per, hipMemcpyHostToDevice, c->stream));
   if (m->host_sync) HIPCHK(hipStreamSynchronize(c->stream));

@@ -276,6 +276,115 @@ __global__ __launch_bounds__(kT) void k_scaled_dot(const double* win, double* wo
   if (t < nc) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
 }
 
+// ---------------------------------------------------- one-pass LSQR step (DBR)
+// One LSQR step's two products over R in ONE pass (ksp_lsqr.c, the DBR default): y = U1 = A[:, 0:nc] coef
+// + nal * (U * usc) per row in gemv_body's order (columns in order from 0, then the VecAXPY), stored
+// unscaled, and in the same pass the DBR stage-1 partials of ||U1||^2 (m = 0: gemv's NORM partial) and of
+// column_v . U1 (m = 1 + v: k_scaled_dot's partial of the unscaled U1).  The lane walks its 16 rows as the
+// 8 row pairs j = 0..7 of the DBR element order, loading the pair's nc column values once for both: the
+// row sums need every column of the pair, the dots every pair of the column.  Two pairs' loads are in
+// flight (pa / pb).  NCT >= nc columns' accumulators in registers.  Ragged chunk: guarded scalar loads, and
+// rows past n neither stored nor summed (as gemv_body / k_scaled_dot).
+template <int NCT, bool NTS>
+__device__ __forceinline__ void onepass_load(double2 (&p)[NCT], double2& up, const double* __restrict__ A,
+                                             int64_t lda, int nc, const double* __restrict__ U, bool axpy,
+                                             int64_t e, int64_t n, bool full) {
+#pragma unroll
+  for (int v = 0; v < NCT; ++v) {
+    if (v < nc) {
+      const double* __restrict__ col = A + (int64_t)v * lda + e;
+      if (full) p[v] = ld_col<2>(col);
+      else p[v] = make_double2(e < n ? col[0] : 0.0, e + 1 < n ? col[1] : 0.0);
+    }
+  }
+  if (axpy) {
+    if (full) up = *reinterpret_cast<const double2*>(U + e);
+    else up = make_double2(e < n ? U[e] : 0.0, e + 1 < n ? U[e + 1] : 0.0);
+  }
+}
+
+template <int NCT, bool NTS>
+__device__ __forceinline__ void onepass_pair(const double2 (&p)[NCT], double2 up, const double (&a)[NCT], int nc,
+                                             bool axpy, double nal, double usc, double* __restrict__ y, int64_t e,
+                                             int64_t n, bool full, double& nacc, double (&acc)[NCT]) {
+  double r0 = 0.0, r1 = 0.0;
+#pragma unroll
+  for (int v = 0; v < NCT; ++v) {
+    if (v < nc) {
+      r0 = r0 + a[v] * p[v].x;
+      r1 = r1 + a[v] * p[v].y;
+    }
+  }
+  if (axpy) {  // nal != 0 (uniform): U stored unscaled, its value is U * usc
+    r0 = r0 + nal * (up.x * usc);
+    r1 = r1 + nal * (up.y * usc);
+  }
+  const bool in0 = full || e < n, in1 = full || e + 1 < n;
+  if (full) {
+    st2<NTS>(y + e, r0, r1);
+  } else {
+    if (in0) y[e] = r0;
+    if (in1) y[e + 1] = r1;
+  }
+  if (in0) nacc = nacc + r0 * r0;
+  if (in1) nacc = nacc + r1 * r1;
+#pragma unroll
+  for (int v = 0; v < NCT; ++v) {
+    if (v < nc) {
+      if (in0) acc[v] = acc[v] + r0 * p[v].x;
+      if (in1) acc[v] = acc[v] + r1 * p[v].y;
+    }
+  }
+}
+
+template <int NCT, bool NTS>
+__global__ __launch_bounds__(kT) void k_lsqr_onepass(const double* __restrict__ A, int64_t lda, int nc,
+                                                     const double* __restrict__ coef,
+                                                     const double* __restrict__ naldev, const double* __restrict__ U,
+                                                     const double* __restrict__ uscdev, double* __restrict__ y,
+                                                     int64_t n, double* __restrict__ partial, int64_t nchunks,
+                                                     const int* __restrict__ stop) {
+  if (stopped(stop)) return;
+  __shared__ double red[NCT + 1][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t c = blockIdx.x;
+  const int64_t base = c * kChunk + 2 * t;
+  const bool full = (c + 1) * kChunk <= n;
+  const double nal = *naldev;
+  const bool axpy = U != nullptr && nal != 0.0;  // VecAXPY(y, 0, x) does nothing
+  const double usc = uscdev ? *uscdev : 1.0;
+  double a[NCT];
+#pragma unroll
+  for (int v = 0; v < NCT; ++v) a[v] = v < nc ? coef[v] : 0.0;
+  double acc[NCT];
+#pragma unroll
+  for (int v = 0; v < NCT; ++v) acc[v] = 0.0;
+  double nacc = 0.0;
+  double2 pa[NCT], pb[NCT];
+  double2 ua = make_double2(0.0, 0.0), ub = make_double2(0.0, 0.0);
+  onepass_load<NCT, NTS>(pa, ua, A, lda, nc, U, axpy, base, n, full);
+  onepass_load<NCT, NTS>(pb, ub, A, lda, nc, U, axpy, base + 2 * kT, n, full);
+#pragma unroll 1
+  for (int j = 0; j < kIters; j += 2) {
+    const int64_t e = base + (int64_t)j * (2 * kT);
+    onepass_pair<NCT, NTS>(pa, ua, a, nc, axpy, nal, usc, y, e, n, full, nacc, acc);
+    if (j + 2 < kIters) onepass_load<NCT, NTS>(pa, ua, A, lda, nc, U, axpy, e + 2 * (2 * kT), n, full);
+    onepass_pair<NCT, NTS>(pb, ub, a, nc, axpy, nal, usc, y, e + 2 * kT, n, full, nacc, acc);
+    if (j + 3 < kIters) onepass_load<NCT, NTS>(pb, ub, A, lda, nc, U, axpy, e + 3 * (2 * kT), n, full);
+  }
+  nacc = wave_butterfly(nacc);
+  if (lane == 0) red[0][wv] = nacc;
+#pragma unroll
+  for (int v = 0; v < NCT; ++v) {
+    if (v < nc) {
+      const double r = wave_butterfly(acc[v]);
+      if (lane == 0) red[1 + v][wv] = r;
+    }
+  }
+  __syncthreads();
+  if (t <= nc) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+}
+
 // ------------------------------------------------------------------ SpMM
 // R[:, 0:nc] = A S[:, 0:nc]: one lane per row, the row's CSR entries read once
 // for all nc columns; per column the MatMult_SeqAIJ order (ascending entries,
@@ -530,6 +639,55 @@ extern "C" int mspi_dense_scaled_dots(msp_ctx* c, const double* win, double* wou
     }
     KCHK(msk_dot_stage2(partial, nch, g, out_dev + g0, stop, c->stream));
   }
+  return MSP_SUCCESS;
+}
+
+// One LSQR step's U1 = A coef + nal (U usc), stored unscaled, with out[0] = ||U1||^2 and out[1 + v] =
+// column_v . U1 (DBR; k_lsqr_onepass), in one pass over A when it is 16-byte aligned and nc <= 32; otherwise
+// (the same sums) through the gemv and an unscaled column-dot launch.  partial: nchunks * (nc + 1) doubles.
+extern "C" int mspi_dense_lsqr_onepass(msp_ctx* c, const double* A, int64_t lda, int nc, int64_t n,
+                                       const double* coef_dev, const double* nal_dev, const double* U,
+                                       const double* usc_dev, double* y, double* partial, double* out_dev,
+                                       const int* stop) {
+  ARGCHK(!mspi_reduce_seq(c), MSP_ERR_SUP, "the one-pass LSQR step is the DBR order's");
+  ARGCHK(nc >= 1, MSP_ERR_ARG_OUTOFRANGE, "%d columns", nc);
+  const int64_t nch = nchunks_of(n);
+  if (nch == 0) {
+    HIPCHK(hipMemsetAsync(out_dev, 0, (size_t)(nc + 1) * sizeof(double), c->stream));
+    return MSP_SUCCESS;
+  }
+  const bool vec = aligned16(A) && (lda % 2 == 0) && aligned16(y) && (!U || aligned16(U)) &&
+                   !(msk_get_tuning() & MSK_TUNE_VEC_TEMPORAL);
+  int grp = 4;
+  bool nts = true;
+  if (!dense_tuning(&grp, &nts)) return MSP_ERR_ARG_OUTOFRANGE;
+  if (!vec || nc > kMaxCols) {  // the same sums in two passes
+    int rc = mspi_dense_gemv(c, A, lda, nc, n, coef_dev, nal_dev, U, usc_dev, y, partial, out_dev, stop);
+    if (!rc) rc = mspi_dense_scaled_dots(c, y, nullptr, nullptr, A, lda, nc, n, partial, out_dev + 1, stop);
+    return rc;
+  }
+  {
+    KTimer kt(c, MSP_KERNEL_DGEMV, 8.0 * (double)n * (nc + 2 + (U ? 1 : 0)));
+    const dim3 g((unsigned)nch), b(kT);
+#define OPK(NCT_)                                                                                               \
+  do {                                                                                                          \
+    if (nts) k_lsqr_onepass<NCT_, true><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, usc_dev, y, n,  \
+                                                                 partial, nch, stop);                           \
+    else k_lsqr_onepass<NCT_, false><<<g, b, 0, c->stream>>>(A, lda, nc, coef_dev, nal_dev, U, usc_dev, y, n,     \
+                                                             partial, nch, stop);                               \
+  } while (0)
+    if (nc <= 4) OPK(4);
+    else if (nc <= 8) OPK(8);
+    else if (nc <= 12) OPK(12);
+    else if (nc <= 16) OPK(16);
+    else if (nc <= 20) OPK(20);
+    else if (nc <= 24) OPK(24);
+    else if (nc <= 28) OPK(28);
+    else OPK(32);
+#undef OPK
+    KCHK((int)hipGetLastError());
+  }
+  KCHK(msk_dot_stage2(partial, nch, nc + 1, out_dev, stop, c->stream));
   return MSP_SUCCESS;
 }
 

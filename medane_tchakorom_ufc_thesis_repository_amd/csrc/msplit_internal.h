@@ -79,6 +79,11 @@ int mspi_dense_gemv(msp_ctx *ctx, const double *A, int64_t lda, int nc, int64_t 
  * partial holds nchunks*32 doubles. */
 int mspi_dense_scaled_dots(msp_ctx *ctx, const double *win, double *wout, const double *sc_dev, const double *A,
                            int64_t lda, int nc, int64_t n, double *partial, double *out_dev, const int *stop);
+/* one LSQR step's U1 = A coef + nal (U usc) (unscaled) with out[0] = ||U1||^2, out[1 + v] = A_v . U1 (DBR),
+ * in one pass over A where it can (msplit_dense.hip); partial: nchunks * (nc + 1) doubles */
+int mspi_dense_lsqr_onepass(msp_ctx *ctx, const double *A, int64_t lda, int nc, int64_t n, const double *coef_dev,
+                            const double *nal_dev, const double *U, const double *usc_dev, double *y,
+                            double *partial, double *out_dev, const int *stop);
 /* out_dev[j] = ||column j||^2 (DBR) */
 int mspi_dense_colsumsq(msp_ctx *ctx, const double *A, int64_t lda, int nc, int64_t n, double *partial,
                         double *out_dev);
@@ -197,6 +202,8 @@ int mspi_d2d_sync(msp_ctx *ctx, void *dst, size_t dpitch, const void *src, size_
 /* the asynchronous device slots (amsg.c): a copy enqueued without waiting, and a word of a registered host region
  * stored by the stream once the work before it is done (system-scope release) */
 int mspi_d2d_async(msp_ctx *ctx, void *dst, const void *src, size_t bytes);
+int mspi_d2d_async2d(msp_ctx *ctx, void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
+                     size_t height);
 int mspi_host_device_ptr(void *host, void **dev);
 uint64_t mspi_stream_key(const msp_ctx *ctx);
 int mspi_stream_store_u64(msp_ctx *ctx, uint64_t *dev_word, uint64_t v);
@@ -252,6 +259,7 @@ int mspi_ls_start(msp_ctx *ctx, mspi_lsqr_dev d);
 int mspi_ls_first(msp_ctx *ctx, mspi_lsqr_dev d, const double *gfrob);
 int mspi_ls_beta(msp_ctx *ctx, mspi_lsqr_dev d);
 int mspi_ls_step(msp_ctx *ctx, mspi_lsqr_dev d);
+int mspi_ls_onepass_step(msp_ctx *ctx, mspi_lsqr_dev d);
 
 #ifdef __cplusplus
 }

@@ -88,6 +88,17 @@ extern "C" int mspi_stream_store_u32(msp_ctx* c, uint32_t* dev_word, uint32_t v)
   return MSP_SUCCESS;
 }
 
+// height rows of width bytes, pitched, device to device (either end may be a peer mapping), enqueued only
+extern "C" int mspi_d2d_async2d(msp_ctx* c, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                                size_t height) {
+  if (!width || !height) return MSP_SUCCESS;
+  if (height == 1 || (dpitch == width && spitch == width))
+    HIPCHK(hipMemcpyAsync(dst, src, width * height, hipMemcpyDeviceToDevice, c->stream));
+  else
+    HIPCHK(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToDevice, c->stream));
+  return MSP_SUCCESS;
+}
+
 // height rows of width bytes, pitched, device to device (either end may be a peer mapping)
 extern "C" int mspi_d2d_sync(msp_ctx* c, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
                              size_t height) {

@@ -1520,6 +1520,16 @@ __global__ __launch_bounds__(kT) void k_spmv_box_lines(int32_t nx, int32_t ny, i
   }
 }
 
+// The stencil storage's value of leg k for the lane's row pair j of the chunk at c0 (rows c0 + j*512 + 2t, +1).
+// rvs > 0: structure of arrays, rv[k * rvs + row]; rvs == 0: chunk-blocked, the 7 legs of each 512-row slice
+// of a chunk next to each other (rv[7 * c0 + j * 3584 + k * 512 + (row % 512)]), so a chunk tile's 229 KB of
+// values are one contiguous region instead of seven regions 8n bytes apart.
+__device__ __forceinline__ const double2* rv_pair(const double* __restrict__ rv, int64_t rvs, int64_t c0, int k,
+                                                  int j, int t) {
+  return reinterpret_cast<const double2*>(rvs ? rv + k * rvs + c0 + j * (2 * kT) + 2 * t
+                                              : rv + 7 * c0 + j * (7 * 2 * kT) + k * (2 * kT) + 2 * t);
+}
+
 // The box march over DBR chunk tiles (planes of whole chunks: P % 4096 == 0), for MatMult, MatResidual
 // and the scaled MatMult on their own: the tiling of k_box_spmv_mdot_march without the dots.  A lane owns
 // 16 rows of the tile (rows 2t, 2t+1 + 512j) and loads x, x(z+1), b and the presence bytes as 16- and
@@ -1616,7 +1626,7 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
       double2 rq[7];
       if constexpr (RV) {
 #pragma unroll
-        for (int k = 0; k < 7; ++k) rq[k] = ld_nt(reinterpret_cast<const double2*>(rv + k * rvs + base + j * (2 * kT)));
+        for (int k = 0; k < 7; ++k) rq[k] = ld_nt(rv_pair(rv, rvs, c0, k, j, t));
       }
       double o[2];
 #pragma unroll
@@ -1780,7 +1790,9 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot(int32_t nx, int64_t P, int
 // own rows are written to LDS from xc.  W and every dot are the unmarched kernel's, bit for bit.
 // RV: the stencil storage's per-row values (as k_box_march_chunk<.., RV>); W is then stored (y != null):
 // recomputing it in the MAXPY would re-read the 56 value bytes per row to save W's 16.
-template <int VAR, bool NTY, bool RV>
+// RVP (RV only): the row pairs j < RVP have their values issued with x(z+1), before the LDS turn-around; the
+// others right before their W rows (fewer registers held across the barriers; MSPLIT_RV_PREFETCH, the A/B).
+template <int VAR, bool NTY, bool RV, int RVP = kIters>
 __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
                                                             const uint8_t* __restrict__ mask,
                                                             const double* __restrict__ dval,
@@ -1848,9 +1860,9 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     double2 rqa[RV ? kIters : 1][7];
     if constexpr (RV) {
 #pragma unroll
-      for (int j = 0; j < kIters; ++j)
+      for (int j = 0; j < RVP; ++j)
 #pragma unroll
-        for (int k = 0; k < 7; ++k) rqa[j][k] = ld_nt(reinterpret_cast<const double2*>(rv + k * rvs + base + j * (2 * kT)));
+        for (int k = 0; k < 7; ++k) rqa[j][k] = ld_nt(rv_pair(rv, rvs, c0, k, j, t));
     }
     double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0);
     const bool hasl = t < nh && c0 - nx >= 0, hash = t < nh && c0 + kChunk + nx <= (int64_t)nz * P;
@@ -1875,6 +1887,12 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     double wr[2 * kIters];
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
+      if constexpr (RV) {
+        if (j >= RVP) {
+#pragma unroll
+          for (int k = 0; k < 7; ++k) rqa[j][k] = ld_nt(rv_pair(rv, rvs, c0, k, j, t));
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int e = j * (2 * kT) + 2 * t + q + nx;
@@ -2928,7 +2946,7 @@ extern "C" int msk_box_march_chunk_rv(int32_t nx, int32_t ny, int32_t nz, const 
                                       const double* sdev, double* vout, const int* stop, hipStream_t s) {
   auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad() || !march_chunk_ok(nx, ny, 0) || !rv || (rvs & 1) ||
-      rvs < (int64_t)nx * ny * nz || !a16(rv) || !a16(x) || !a16(y) || (mode == MSK_SPMV_RESID && !a16(b)) ||
+      (rvs != 0 && rvs < (int64_t)nx * ny * nz) || !a16(rv) || !a16(x) || !a16(y) || (mode == MSK_SPMV_RESID && !a16(b)) ||
       (mode == MSK_SPMV_SCALED && vout && !a16(vout)))
     return (int)hipErrorInvalidValue;
   return launch_march_chunk(nx, ny, nz, 0, mask, nullptr, x, b, y, mode, sdev, vout, stop, s, rv, rvs);
@@ -3089,10 +3107,21 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
     const double* last = V->base ? V->base + (int64_t)(nv - 1) * V->stride : V->p[nv - 1];
     const int self = self_env != 0 && last == x;
     if (self_out) *self_out = self;
+    static const int rvp = [] {  // MSPLIT_RV_PREFETCH: row pairs whose values go before the barriers (8, 4 or 2)
+      const char* e = getenv("MSPLIT_RV_PREFETCH");
+      const int v = e ? atoi(e) : kIters;
+      return v == 4 || v == 2 ? v : kIters;
+    }();
+#define MSK_BSMM_P(VAR_, NT_, RV_, P_)                                                                          \
+  k_box_spmv_mdot_march<VAR_, NT_, RV_, P_><<<dim3((unsigned)grid), b, lds, s>>>(nx, P, nz, zt, xcd, mask, dval, rv, \
+                                                                                 rvs, x, sdev, y, *V, nv, self,     \
+                                                                                 partial, nchunks, stop)
 #define MSK_BSMM(VAR_, NT_, RV_)                                                                              \
-  k_box_spmv_mdot_march<VAR_, NT_, RV_><<<dim3((unsigned)grid), b, lds, s>>>(nx, P, nz, zt, xcd, mask, dval, rv, rvs, x, \
-                                                                             sdev, y, *V, nv, self, partial, nchunks,    \
-                                                                             stop)
+  do {                                                                                                        \
+    if (RV_ && rvp == 4) MSK_BSMM_P(VAR_, NT_, RV_, 4);                                                       \
+    else if (RV_ && rvp == 2) MSK_BSMM_P(VAR_, NT_, RV_, 2);                                                  \
+    else MSK_BSMM_P(VAR_, NT_, RV_, kIters);                                                                  \
+  } while (0)
     if (rv) {
       if (vec_var()) { if (nty) MSK_BSMM(1, true, true); else MSK_BSMM(1, false, true); }
       else { if (nty) MSK_BSMM(0, true, true); else MSK_BSMM(0, false, true); }
@@ -3101,6 +3130,7 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
       else { if (nty) MSK_BSMM(0, true, false); else MSK_BSMM(0, false, false); }
     }
 #undef MSK_BSMM
+#undef MSK_BSMM_P
     return (int)hipGetLastError();
   }
 #define MSK_BSM(D, VAR_, NT_) \

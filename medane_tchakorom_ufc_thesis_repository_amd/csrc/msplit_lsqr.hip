@@ -200,7 +200,74 @@ __global__ void k_ls_step(mspi_lsqr_dev d) {
   }
 }
 
+// The one-pass DBR step (ksp_lsqr.c): the gathered block partials are [||U1||^2 | R^T U1] per block (stride
+// s + 1); beta as k_ls_beta, then V1 = (R^T U1) * (1/beta) (unscaled U1's products, scaled after the block sum;
+// beta = 0 leaves them, as VecScale was skipped) and k_ls_step's recurrence.
+__global__ void k_ls_onepass_step(mspi_lsqr_dev d) {
+  mspi_lsqr_state* st = d.st;
+  if (st->stop) return;
+  const int s = st->s, nb = st->nblk;
+  const double beta = sqrt(block_sum(d.g, nb, s + 1, 0));
+  if (bad(beta)) {
+    st->reason = MSP_DIVERGED_NANORINF;
+    st->stop = 1;
+    return;
+  }
+  st->beta = beta;
+  if (beta > 0.0) {
+    st->uscale = 1.0 / beta;
+    if (!st->exact_norm) st->anorm = sqrt(st->anorm * st->anorm + st->alpha * st->alpha + beta * beta);
+  } else {
+    st->uscale = 1.0;
+  }
+  for (int j = 0; j < s; ++j) d.V1[j] = block_sum(d.g, nb, s + 1, 1 + j);
+  if (beta > 0.0) vscale(d.V1, s, st->uscale);
+  vaxpy(d.V1, s, -beta, d.V);
+  const double alpha = snorm(d.V1, s);
+  if (bad(alpha)) {
+    st->reason = MSP_DIVERGED_NANORINF;
+    st->stop = 1;
+    return;
+  }
+  vscale(d.V1, s, 1.0 / alpha);
+  const double rhobar0 = st->rhobar;
+  const double rho = sqrt(rhobar0 * rhobar0 + beta * beta);
+  const double c = rhobar0 / rho;
+  const double sn = beta / rho;
+  const double theta = sn * alpha;
+  st->rhobar = -c * alpha;
+  const double phi = c * st->phibar;
+  st->phibar = sn * st->phibar;
+  const double tau = sn * phi;
+  vaxpy(d.X, s, phi / rho, d.W);
+  vaypx(d.W, s, -theta / rho, d.V1);
+  st->arnorm = alpha * fabs(tau);
+  const double rnorm = st->phibar;
+  st->rnorm = rnorm;
+  st->its++;
+  ls_log(d, rnorm);
+  ls_converged(st, st->i + 1, rnorm);
+  st->alpha = alpha;
+  if (st->reason) {
+    st->stop = 1;
+    return;
+  }
+  for (int j = 0; j < s; ++j) d.V[j] = d.V1[j];  // SWAP(V1, V)
+  st->i++;
+  st->nalpha = -alpha;
+  if (st->i >= st->max_it) {
+    st->reason = MSP_DIVERGED_ITS;
+    st->stop = 1;
+  }
+}
+
 }  // namespace
+
+extern "C" int mspi_ls_onepass_step(msp_ctx* c, mspi_lsqr_dev d) {
+  k_ls_onepass_step<<<1, 1, 0, c->stream>>>(d);
+  KCHK((int)hipGetLastError());
+  return MSP_SUCCESS;
+}
 
 extern "C" int mspi_ls_start(msp_ctx* c, mspi_lsqr_dev d) {
   k_ls_start<<<1, 1, 0, c->stream>>>(d);

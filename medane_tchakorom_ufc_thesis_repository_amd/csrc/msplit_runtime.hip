@@ -466,7 +466,8 @@ struct msp_mat {
   int32_t march_d2 = 0;        // 2D box stencil (five pairs), marched as nx x 1 x ny
   int32_t march_halo = 0;      // bit 0 / 1: the column space adds the plane below / above the box (chunk march only)
   uint8_t* march_mask = nullptr;  // nrows (+16 pad): the rows' presence bytes (msk_march_mask)
-  // STENCIL storage (rv_attach): a 3D box stencil whose rows carry their own values; rv_val[e * rv_stride + r] is
+  // STENCIL storage (rv_attach): a 3D box stencil whose rows carry their own values; rv_stride == 0: chunk-blocked
+  // (msplit_kernels.hip rv_pair; the default), else rv_val[e * rv_stride + r] is
   // row r's entry at neighbour e (column order; 0.0 where the row has none), march_* and march_mask as above
   double* rv_val = nullptr;
   int64_t rv_stride = 0;
@@ -707,10 +708,12 @@ static bool box_dictionary(int32_t nrows, std::vector<int32_t>& dd, std::vector<
 // (rv_val[e * stride + r], 0.0 where absent) with one presence byte per row, and the device checks that no row
 // holds a neighbour across a line or plane edge (k_march_check); a failed check keeps CSR.  The products add
 // the present entries in column order from 0.0, as the CSR kernels: bitwise the same.
+// The storage is optional: under MSPLIT_MAT_STORAGE=csr it is not built, and when HBM cannot hold its 57 B/row
+// next to the resident CSR (which stays: release_csr needs DV storage) the matrix simply stays in CSR.
 static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, const double* val) {
   msp_ctx* c = A->ctx;
   const int32_t n = A->nrows;
-  if (A->compressed || A->matfree || n == 0 || A->ncols != n || A->dv_on) return MSP_SUCCESS;
+  if (A->compressed || A->matfree || n == 0 || A->ncols != n || A->dv_on || !dv_default()) return MSP_SUCCESS;
   std::vector<int32_t> dd;
   for (int32_t r = 0; r < n; ++r)
     for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
@@ -725,21 +728,32 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
   int d2 = 0;
   if (!box_dictionary(n, dd, dummy, &nx, &ny, &nz, &d2) || d2 || !msk_march_chunk_fits(nx, ny, 0)) return MSP_SUCCESS;
   const int64_t stride = ((int64_t)n + 511) / 512 * 512;
+  // the value layout: chunk-blocked (every plane is whole DBR chunks here, so n % 4096 == 0) unless
+  // MSPLIT_RV_LAYOUT=soa (per-leg arrays; the A/B)
+  const char* lay = getenv("MSPLIT_RV_LAYOUT");
+  const bool blocked = !(lay && strcmp(lay, "soa") == 0) && n % MSK_DBR_CHUNK == 0;
+  const size_t need = (size_t)n + 16 + (size_t)7 * stride * sizeof(double);
+  size_t fr = 0, tot = 0;
+  if (mspi_mem_info(c, &fr, &tot) || fr < need + (tot >> 5)) {  // keep 1/32 of HBM free after it
+    (void)hipGetLastError();
+    return MSP_SUCCESS;
+  }
   std::vector<uint8_t> mask((size_t)n + 16, 0);
   std::vector<double> rv((size_t)7 * stride, 0.0);
   for (int32_t r = 0; r < n; ++r)
     for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
       const int e = (int)(std::find(dd.begin(), dd.end(), col[k] - r) - dd.begin());  // dd is in column order now
       mask[r] |= (uint8_t)(1u << e);
-      rv[(size_t)e * stride + r] = val[k];
+      const int64_t o = r % MSK_DBR_CHUNK;
+      rv[blocked ? (size_t)(7 * (r - o) + (o / 512) * 3584 + e * 512 + o % 512) : (size_t)e * stride + r] = val[k];
     }
   if (mspi_big_alloc((void**)&A->march_mask, (size_t)n + 16) != (int)hipSuccess ||
       mspi_big_alloc((void**)&A->rv_val, (size_t)7 * stride * sizeof(double)) != (int)hipSuccess) {
+    (void)hipGetLastError();  // the allocation failure is not the caller's error: the matrix stays in CSR
     rv_free(A);
     if (A->march_mask) (void)hipFree(A->march_mask);
     A->march_mask = nullptr;
-    mspi_set_error(MSP_ERR_MEM, "hipMalloc of the stencil storage failed");
-    return MSP_ERR_MEM;
+    return MSP_SUCCESS;
   }
   HIPCHK(hipMemcpyAsync(A->march_mask, mask.data(), (size_t)n + 16, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(A->rv_val, rv.data(), (size_t)7 * stride * sizeof(double), hipMemcpyHostToDevice, c->stream));
@@ -755,13 +769,13 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
     A->march_mask = nullptr;
     return MSP_SUCCESS;
   }
-  A->rv_stride = stride;
+  A->rv_stride = blocked ? 0 : stride;
   A->march_nx = nx;
   A->march_ny = ny;
   A->march_nz = nz;
   A->march_d2 = 0;
   A->march_halo = 0;
-  A->rv_on = dv_default();
+  A->rv_on = true;
   return MSP_SUCCESS;
 }
 

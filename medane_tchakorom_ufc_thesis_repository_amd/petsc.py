@@ -914,6 +914,12 @@ class AsyncBroadcast:
     def close_peers(self):
         call("msp_abcast_close_peers", self.h)
 
+    def stats(self) -> tuple:
+        """(device publishes enqueued, skipped: previous copy unpublished or the buffer still read)."""
+        a, b = C.c_int64(), C.c_int64()
+        call("msp_abcast_get_stats", self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
     def publish_dense(self, D: "DenseMat") -> bool:
         ok = C.c_int32()
         call("msp_abcast_publish_dense", self.h, D.h, C.byref(ok))

@@ -754,6 +754,7 @@ void orc_lsqr_default_opts(orc_lsqr_opts *o) {
   o->exact_norm = 0;
   o->conv_test = ORC_LSQR_CONV_LSQR; /* KSPCreate_LSQR installs KSPLSQRConvergedDefault */
   o->reduce_mode = ORC_REDUCE_SEQ;
+  o->onepass = 1;
 }
 
 typedef struct {
@@ -972,6 +973,9 @@ int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R
     for (int b = 0; b < nblk; ++b) orc_dense_mult(nrows[b], s, R[b], lda[b], V, U1[b]);
     for (int b = 0; b < nblk; ++b) ls_axpy(nrows[b], U1[b], -alpha, U[b]);
     beta = sqrt(ls_gdot(&L, (const double *const *)U1, (const double *const *)U1));
+    /* DBR one-pass (the device's default): R^T U1 from the unscaled U1, in the pass that formed it */
+    const int onepass = L.mode == ORC_REDUCE_DBR && o->onepass;
+    if (onepass) ls_mult_transpose(&L, R, lda, (const double *const *)U1, V1);
     if (is_bad(beta)) {
       k.reason = ORC_DIVERGED_NANORINF;
       break;
@@ -981,7 +985,11 @@ int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R
       if (!o->exact_norm) k.anorm = sqrt(k.anorm * k.anorm + alpha * alpha + beta * beta);
     }
     /* V1 = R^T U1 - beta V */
-    ls_mult_transpose(&L, R, lda, (const double *const *)U1, V1);
+    if (onepass) {
+      if (beta > 0.0) ls_scale(s, V1, 1.0 / beta); /* (R^T U1) * (1/beta) */
+    } else {
+      ls_mult_transpose(&L, R, lda, (const double *const *)U1, V1);
+    }
     ls_axpy(s, V1, -beta, V);
     alpha = ls_snorm(s, V1);
     if (is_bad(alpha)) {

@@ -181,6 +181,11 @@ typedef struct {
   int exact_norm;     /* -ksp_lsqr_exact_mat_norm */
   int conv_test;      /* -ksp_convergence_test: default | lsqr (KSPCreate_LSQR's choice) | skip */
   int reduce_mode;    /* ORC_REDUCE_* */
+  int onepass;        /* DBR only (default 1, the device's default): each step's R^T U1 is taken in the same pass
+                       * over R as U1 = R V - alpha U, from the unscaled U1, and multiplied by 1/beta afterwards:
+                       * V1_j = (sum_b dbr(R_j, U1)) * (1/beta) where PETSc's order scales U1 first,
+                       * V1_j = sum_b dbr(R_j, U1 * (1/beta)).  0: PETSc's operation order (the device's
+                       * MSPLIT_LSQR_ONEPASS=0).  SEQ always keeps PETSc's order. */
 } orc_lsqr_opts;
 
 typedef struct {

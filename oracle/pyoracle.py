@@ -59,7 +59,7 @@ class SMResult(C.Structure):
 
 class LsqrOpts(C.Structure):
     _fields_ = [("max_it", C.c_int), ("rtol", C.c_double), ("abstol", C.c_double), ("divtol", C.c_double),
-                ("exact_norm", C.c_int), ("conv_test", C.c_int), ("reduce_mode", C.c_int)]
+                ("exact_norm", C.c_int), ("conv_test", C.c_int), ("reduce_mode", C.c_int), ("onepass", C.c_int)]
 
 
 class LsqrResult(C.Structure):

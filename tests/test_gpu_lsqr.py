@@ -95,10 +95,15 @@ CASES = [
 DENSE_G1, DENSE_G2, DENSE_TEMPORAL_ST = 8388608, 16777216, 33554432
 
 
-@pytest.mark.parametrize("flags", [0, DENSE_G1, DENSE_G2, DENSE_TEMPORAL_ST, DENSE_G1 | DENSE_TEMPORAL_ST])
+VEC_TEMPORAL = 16   # default-policy column loads: the one-pass step takes its two-launch form
+
+
+@pytest.mark.parametrize("flags", [0, DENSE_G1, DENSE_G2, DENSE_TEMPORAL_ST, DENSE_G1 | DENSE_TEMPORAL_ST,
+                                   VEC_TEMPORAL])
 @pytest.mark.parametrize("case", CASES)
 def test_lsqr_bitwise_vs_oracle(ctx, oracle, case, flags):
-    """Every load grouping / store policy of k_dense_gemv and k_scaled_dot gives the oracle's bits."""
+    """Every load grouping / store policy of k_lsqr_onepass (and, for s > 32 or default-policy loads, its
+    two-launch form k_dense_gemv + k_scaled_dot) gives the oracle's bits (the DBR one-pass step)."""
     from test_gpu_kernels import tuning
     case = dict(case)
     cuts, s = case.pop("cuts"), case.pop("s")
@@ -116,6 +121,32 @@ def test_lsqr_bitwise_vs_oracle(ctx, oracle, case, flags):
     assert l.get_norms() == (ro["arnorm"], ro["anorm"])
     assert np.array_equal(l.get_residual_history(), ro["hist"])
     assert np.array_equal(x, xo)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_lsqr_two_pass_is_petsc_op_order(ctx, oracle, case, monkeypatch):
+    """MSPLIT_LSQR_ONEPASS=0: the two passes per step, R^T (U1 / beta) as PETSc orders it (VecScale, then
+    MatMultTranspose), bitwise the oracle with onepass = 0; the default one-pass step, (R^T U1) * (1/beta), is
+    the oracle with onepass = 1, and the two differ (one rounding per step: ksp_lsqr.c)."""
+    case = dict(case)
+    cuts, s = case.pop("cuts"), case.pop("s")
+    n = sum(cuts)
+    R = RNG.standard_normal((n, s)) @ np.diag(np.geomspace(1, 1e-3, s))
+    b = RNG.standard_normal(n)
+    edges = np.cumsum([0] + cuts)
+    Rs = [R[a:c] for a, c in zip(edges[:-1], edges[1:])]
+    bs = [b[a:c] for a, c in zip(edges[:-1], edges[1:])]
+    monkeypatch.setenv("MSPLIT_LSQR_ONEPASS", "0")
+    x2, l2 = _lsqr_gpu(ctx, Rs, bs, **case)
+    xo2, ro2 = oracle.lsqr(Rs, bs, reduce_mode=oracle.REDUCE_DBR, onepass=0, **case)
+    assert np.array_equal(l2.get_residual_history(), ro2["hist"]) and np.array_equal(x2, xo2)
+    monkeypatch.setenv("MSPLIT_LSQR_ONEPASS", "1")
+    x1, l1 = _lsqr_gpu(ctx, Rs, bs, **case)
+    xo1, ro1 = oracle.lsqr(Rs, bs, reduce_mode=oracle.REDUCE_DBR, onepass=1, **case)
+    assert np.array_equal(l1.get_residual_history(), ro1["hist"]) and np.array_equal(x1, xo1)
+    if ro1["its"] > 1:
+        assert not np.array_equal(xo1, xo2)
+    assert np.allclose(xo1, xo2, rtol=1e-6, atol=1e-9 * np.abs(xo2).max())
 
 
 def test_dense_tuning_without_kernel_fails_loudly(ctx):
