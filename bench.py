@@ -53,8 +53,9 @@ KERNEL_NAMES = {"mdot": "k_dot_stage1+2 (VecMDot, DBR)",
                          "fused ||w||^2) and k_maxpy_chunk (BuildSoln)",
                 "norm": "k_dot_stage1<1,self>+stage2 (VecNorm)",
                 "scale": "k_blas1<SCALE> (VecScale)", "other": "copy/set/axpy",
-                "spmm": "k_spmm (MatMatMult R = A S)", "dgemv": "k_dense_gemv (LSQR R v - alpha u + norm; S alpha)",
-                "dgemvt": "k_scaled_dot (LSQR scale + R^T u)",
+                "spmm": "k_spmm (MatMatMult R = A S)", "dgemv": "k_lsqr_onepass (LSQR step: R v - alpha u, its norm and R^T u in one pass over R; "
+                                 "DBR default) / k_dense_gemv (S alpha; the two-pass step)",
+                "dgemvt": "k_scaled_dot (LSQR's first R^T u; the two-pass step's scale + R^T u)",
                 "spmvdot": "k_box_spmv_mdot_march (GMRES MatMult of the box stencil fused with VecMDot stage 1: "
                            "W not stored)"}
 SPMV_NAMES = {"dv": "k_spmv_ell (MatMult/MatResidual, DV storage: one byte per entry)",

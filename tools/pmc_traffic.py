@@ -79,7 +79,7 @@ def tmpl_args(name: str):
     return [a.strip() for a in m.group(1).split(",")] if m else []
 
 
-def smsm_alg(name: str, i: int, rows: float, s: int, k: int, lsqr: int = 70):
+def smsm_alg(name: str, i: int, rows: float, s: int, k: int, lsqr: int = 70, onepass: bool = False):
     """Algorithmic bytes of the i-th launch (dispatch order) of this kernel in the SMSM-global per-GPU outer
     iteration (bench.py --variant smsm, SMSM-global.c:288-363): s inner GMRES solves of exactly k Arnoldi steps
     (rtol 1e-20) in the W-free step, then R = A S, the LSQR over R (n x s) of `lsqr` steps and x = S alpha, on
@@ -95,8 +95,11 @@ def smsm_alg(name: str, i: int, rows: float, s: int, k: int, lsqr: int = 70):
     if b == "k_dense_gemv":
         ax = tmpl_args(name)[:1] == ["true"]
         return 8.0 * N * (s + 2) if ax else 8.0 * N * (s + 1)   # U1 = R V - a U, ||U1||^2 / x = S alpha
+    if b == "k_lsqr_onepass":  # the DBR LSQR step: R read once, U read, U1 written (its norm and R^T U1 from registers)
+        return 8.0 * N * (s + 2)
     if b == "k_scaled_dot":   # R^T (U1 / beta), U1 not written back; the solve's first: U = b / beta written
-        return 8.0 * N * (s + 2) if i % (lsqr + 1) == 0 else 8.0 * N * (s + 1)
+        # (the one-pass step launches it only as each solve's first)
+        return 8.0 * N * (s + 2) if onepass or i % (lsqr + 1) == 0 else 8.0 * N * (s + 1)
     return None
 
 
@@ -115,7 +118,7 @@ def smsm_table(fetch, write, rows, s, k, lsqr=70):
             continue
         rd = sum(2.0 * v for _, v in F[:m]) / m
         wr = sum(v for _, v in W[:m]) / m
-        als = [smsm_alg(nm, i, rows, s, k, lsqr) for i, (nm, _) in enumerate(F[:m])]
+        als = [smsm_alg(nm, i, rows, s, k, lsqr, "k_lsqr_onepass" in per_f) for i, (nm, _) in enumerate(F[:m])]
         alg = sum(als) / m if all(a is not None for a in als) else None
         out[b] = {"launches": m, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                   "hbm_bytes_per_launch": rd + wr, "alg_bytes_per_launch": alg,
