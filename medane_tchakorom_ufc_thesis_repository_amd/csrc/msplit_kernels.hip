@@ -1530,6 +1530,72 @@ __device__ __forceinline__ const double2* rv_pair(const double* __restrict__ rv,
                                               : rv + 7 * c0 + j * (7 * 2 * kT) + k * (2 * kT) + 2 * t);
 }
 
+// The symmetric stencil storage (rvs < 0; rv_attach checks A[r, r + d] == A[r + d, r] bit for bit): per row only
+// the diagonal and the three upper legs, k = 0 d, 1 x+1, 2 y+1, 3 z+1, chunk-blocked (rv[4 * c0 + j * 2048 +
+// k * 512 + row % 512]); a row's lower legs are its lower neighbours' upper ones: A[r, r-1] = ux[r-1],
+// A[r, r-nx] = uy[r-nx], A[r, r-P] = uz[r-P] -- 32 value bytes per row instead of 56.
+__device__ __forceinline__ const double* rvs_at(const double* __restrict__ rv, int64_t row, int k) {
+  const int64_t o = row % kChunk;
+  return rv + 4 * (row - o) + (o / (2 * kT)) * (4 * 2 * kT) + k * (2 * kT) + o % (2 * kT);
+}
+__device__ __forceinline__ const double2* rvs_pair(const double* __restrict__ rv, int64_t c0, int k, int j, int t) {
+  return reinterpret_cast<const double2*>(rv + 4 * c0 + j * (4 * 2 * kT) + k * (2 * kT) + 2 * t);
+}
+
+// Symmetric storage, one plane of a chunk tile: the lane's own four legs (prefetched with x(z+1)), then the x+1 /
+// y+1 legs of the window [c0 - nx, c0 + 4096) to LDS (sux, suy; the window's first nx rows are the line below the
+// tile), so that a row's x-1 / y-1 values are read where its neighbour's upper legs lie.
+struct SymTile {
+  double2 own[kIters][4];
+  double2 hx, hy;  // lane t < nx/2: the halo line's x+1 / y+1 legs at c0 - nx + 2t
+};
+
+__device__ __forceinline__ void sym_load(SymTile& st, const double* __restrict__ rv, int64_t c0, int nx, int t) {
+#pragma unroll
+  for (int j = 0; j < kIters; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st.own[j][k] = ld_nt(rvs_pair(rv, c0, k, j, t));
+  st.hx = st.hy = make_double2(0.0, 0.0);
+  if (t < nx / 2 && c0 - nx >= 0) {
+    st.hx = *reinterpret_cast<const double2*>(rvs_at(rv, c0 - nx + 2 * t, 1));
+    st.hy = *reinterpret_cast<const double2*>(rvs_at(rv, c0 - nx + 2 * t, 2));
+  }
+}
+
+// after the barrier that ends the previous plane's LDS reads
+__device__ __forceinline__ void sym_store(const SymTile& st, double* sux, double* suy, const double* __restrict__ rv,
+                                          int64_t c0, int nx, int t) {
+#pragma unroll
+  for (int j = 0; j < kIters; ++j) {
+    *reinterpret_cast<double2*>(sux + nx + j * (2 * kT) + 2 * t) = st.own[j][1];
+    *reinterpret_cast<double2*>(suy + nx + j * (2 * kT) + 2 * t) = st.own[j][2];
+  }
+  if (t < nx / 2) {
+    *reinterpret_cast<double2*>(sux + 2 * t) = st.hx;
+    *reinterpret_cast<double2*>(suy + 2 * t) = st.hy;
+  }
+  for (int i = t + kT; i < nx / 2; i += kT) {  // nx > 512: the rest of the halo line
+    const bool in = c0 - nx >= 0;
+    *reinterpret_cast<double2*>(sux + 2 * i) =
+        in ? *reinterpret_cast<const double2*>(rvs_at(rv, c0 - nx + 2 * i, 1)) : make_double2(0.0, 0.0);
+    *reinterpret_cast<double2*>(suy + 2 * i) =
+        in ? *reinterpret_cast<const double2*>(rvs_at(rv, c0 - nx + 2 * i, 2)) : make_double2(0.0, 0.0);
+  }
+}
+
+// the seven values of row (j, q) in column order: z-1 (carried uz of the plane below), y-1, x-1 (LDS), d, x+1,
+// y+1, z+1 (own); e = the row's window index (nx + j * 512 + 2t + q)
+__device__ __forceinline__ void sym_values(const SymTile& st, const double* sux, const double* suy, double uzm, int j,
+                                           int q, int e, int nx, double (&vv)[7]) {
+  vv[0] = uzm;
+  vv[1] = suy[e - nx];
+  vv[2] = sux[e - 1];
+  vv[3] = q ? st.own[j][0].y : st.own[j][0].x;
+  vv[4] = q ? st.own[j][1].y : st.own[j][1].x;
+  vv[5] = q ? st.own[j][2].y : st.own[j][2].x;
+  vv[6] = q ? st.own[j][3].y : st.own[j][3].x;
+}
+
 // The box march over DBR chunk tiles (planes of whole chunks: P % 4096 == 0), for MatMult, MatResidual
 // and the scaled MatMult on their own: the tiling of k_box_spmv_mdot_march without the dots.  A lane owns
 // 16 rows of the tile (rows 2t, 2t+1 + 512j) and loads x, x(z+1), b and the presence bytes as 16- and
@@ -1540,7 +1606,8 @@ __device__ __forceinline__ const double2* rv_pair(const double* __restrict__ rv,
 // rv[e * rvs + row] (0 where the row has no such neighbour, never added) instead of the dictionary: a box
 // stencil with variable coefficients, 56 value bytes per row read as 16-byte non-temporal vectors, against
 // 88 bytes of CSR (col + val + rowptr).  Same terms, same order: bitwise the CSR kernels' sums.
-template <int MODE, bool NTY, bool RV>
+// RV: 0 dictionary, 1 the seven per-row legs, 2 the symmetric storage (SymTile; lanes carry uz of the plane below).
+template <int MODE, bool NTY, int RV>
 __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
                                                         int halo, const uint8_t* __restrict__ mask,
                                                         const double* __restrict__ dval,
@@ -1569,6 +1636,18 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
   if constexpr (!RV) march_values<false>(dval, v);
   const int nh = nx / 2;  // double2 per halo line
   double xm[2 * kIters], xc[2 * kIters], xp[2 * kIters];
+  double* sux = sx + kChunk + 2 * nx;  // RV == 2: x+1 / y+1 legs of the window [c0 - nx, c0 + 4096)
+  double* suy = sux + kChunk + nx;
+  double uzm[RV == 2 ? 2 * kIters : 1];  // RV == 2: uz of the lane's rows one plane below
+  if constexpr (RV == 2) {
+    const int64_t cb = ((int64_t)z0 - 1) * P + tile * kChunk;
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double2 u = z0 > 0 ? ld_nt(rvs_pair(rv, cb, 3, j, t)) : make_double2(0.0, 0.0);
+      uzm[2 * j] = u.x;
+      uzm[2 * j + 1] = u.y;
+    }
+  }
   {
     const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * t;
 #pragma unroll
@@ -1601,6 +1680,8 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
       m[j] = *reinterpret_cast<const uint16_t*>(mask + base + j * (2 * kT));
       if constexpr (MODE == MSK_SPMV_RESID) bb[j] = ld_nt(reinterpret_cast<const double2*>(b + base + j * (2 * kT)));
     }
+    SymTile st;
+    if constexpr (RV == 2) sym_load(st, rv, c0, nx, t);
     double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0);
     const bool hasl = t < nh && c0 - nx >= 0, hash = t < nh && c0 + kChunk + nx <= (int64_t)nz * P;
     if (hasl) hl = *reinterpret_cast<const double2*>(x + c0 - nx + 2 * t);
@@ -1620,11 +1701,12 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
           c0 + kChunk + nx <= (int64_t)nz * P ? *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * i)
                                               : make_double2(0.0, 0.0);
     }
+    if constexpr (RV == 2) sym_store(st, sux, suy, rv, c0, nx, t);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
       double2 rq[7];
-      if constexpr (RV) {
+      if constexpr (RV == 1) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) rq[k] = ld_nt(rv_pair(rv, rvs, c0, k, j, t));
       }
@@ -1635,10 +1717,12 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
         const uint32_t mr = (m[j] >> (8 * q)) & 255u;
         const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], xc[2 * j + q], sx[e + 1], sx[e + nx],
                               xp[2 * j + q]};
+        double vv[7];
+        if constexpr (RV == 2) sym_values(st, sux, suy, uzm[2 * j + q], j, q, e, nx, vv);
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
-          const double vk = RV ? (q ? rq[k].y : rq[k].x) : v[k];
+          const double vk = RV == 2 ? vv[k] : RV ? (q ? rq[k].y : rq[k].x) : v[k];
           if (mr & (1u << k)) s = s + vk * (MODE == MSK_SPMV_SCALED ? xq[k] * sc : xq[k]);
         }
         if constexpr (MODE == MSK_SPMV_RESID) s = (q ? bb[j].y : bb[j].x) - s;
@@ -1668,6 +1752,13 @@ __global__ __launch_bounds__(kT) void k_box_march_chunk(int32_t nx, int64_t P, i
     for (int i = 0; i < 2 * kIters; ++i) {
       xm[i] = xc[i];
       xc[i] = xp[i];
+    }
+    if constexpr (RV == 2) {
+#pragma unroll
+      for (int j = 0; j < kIters; ++j) {
+        uzm[2 * j] = st.own[j][3].x;
+        uzm[2 * j + 1] = st.own[j][3].y;
+      }
     }
   }
 }
@@ -1792,7 +1883,7 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot(int32_t nx, int64_t P, int
 // recomputing it in the MAXPY would re-read the 56 value bytes per row to save W's 16.
 // RVP (RV only): the row pairs j < RVP have their values issued with x(z+1), before the LDS turn-around; the
 // others right before their W rows (fewer registers held across the barriers; MSPLIT_RV_PREFETCH, the A/B).
-template <int VAR, bool NTY, bool RV, int RVP = kIters>
+template <int VAR, bool NTY, int RV, int RVP = kIters>
 __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
                                                             const uint8_t* __restrict__ mask,
                                                             const double* __restrict__ dval,
@@ -1824,6 +1915,18 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
   if constexpr (!RV) march_values<false>(dval, v);
   const int nh = nx / 2;  // double2 per halo line
   double xm[2 * kIters], xc[2 * kIters], xp[2 * kIters];
+  double* sux = sx + kChunk + 2 * nx;  // RV == 2 (symmetric storage): x+1 / y+1 legs of the window
+  double* suy = sux + kChunk + nx;
+  double uzm[RV == 2 ? 2 * kIters : 1];  // RV == 2: uz of the lane's rows one plane below
+  if constexpr (RV == 2) {
+    const int64_t cb = ((int64_t)z0 - 1) * P + tile * kChunk;
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double2 u = z0 > 0 ? ld_nt(rvs_pair(rv, cb, 3, j, t)) : make_double2(0.0, 0.0);
+      uzm[2 * j] = u.x;
+      uzm[2 * j + 1] = u.y;
+    }
+  }
   {
     const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * t;
 #pragma unroll
@@ -1857,8 +1960,10 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     // RV: the plane's seven value legs for all the lane's rows, issued with x(z+1) before the LDS turn-around (the
     // kernel runs one workgroup per CU, so the unified register file holds them; loaded after the barrier they
     // were a second, exposed round trip per plane)
-    double2 rqa[RV ? kIters : 1][7];
-    if constexpr (RV) {
+    double2 rqa[RV == 1 ? kIters : 1][7];
+    SymTile st;
+    if constexpr (RV == 2) sym_load(st, rv, c0, nx, t);
+    if constexpr (RV == 1) {
 #pragma unroll
       for (int j = 0; j < RVP; ++j)
 #pragma unroll
@@ -1883,11 +1988,12 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
           c0 + kChunk + nx <= (int64_t)nz * P ? *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * i)
                                               : make_double2(0.0, 0.0);
     }
+    if constexpr (RV == 2) sym_store(st, sux, suy, rv, c0, nx, t);
     __syncthreads();
     double wr[2 * kIters];
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
-      if constexpr (RV) {
+      if constexpr (RV == 1) {
         if (j >= RVP) {
 #pragma unroll
           for (int k = 0; k < 7; ++k) rqa[j][k] = ld_nt(rv_pair(rv, rvs, c0, k, j, t));
@@ -1899,10 +2005,12 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
         const uint32_t mr = (m[j] >> (8 * q)) & 255u;
         const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], xc[2 * j + q], sx[e + 1], sx[e + nx],
                               xp[2 * j + q]};
+        double vv[7];
+        if constexpr (RV == 2) sym_values(st, sux, suy, uzm[2 * j + q], j, q, e, nx, vv);
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
-          const double vk = RV ? (q ? rqa[RV ? j : 0][k].y : rqa[RV ? j : 0][k].x) : v[k];
+          const double vk = RV == 2 ? vv[k] : RV ? (q ? rqa[RV == 1 ? j : 0][k].y : rqa[RV == 1 ? j : 0][k].x) : v[k];
           if (mr & (1u << k)) s = s + vk * (xq[k] * sc);
         }
         wr[2 * j + q] = s;
@@ -1946,6 +2054,13 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     for (int i = 0; i < 2 * kIters; ++i) {
       xm[i] = xc[i];
       xc[i] = xp[i];
+    }
+    if constexpr (RV == 2) {
+#pragma unroll
+      for (int j = 0; j < kIters; ++j) {
+        uzm[2 * j] = st.own[j][3].x;
+        uzm[2 * j + 1] = st.own[j][3].y;
+      }
     }
   }
 }
@@ -2849,14 +2964,15 @@ static int launch_march_chunk(int32_t nx, int32_t ny, int32_t nz, int halo, cons
   if (grid > INT32_MAX || (int64_t)nx * ny * nz > INT32_MAX) return (int)hipErrorInvalidValue;
   const int xcd = cpp % 8 == 0 && cpp >= 32 && !(msk_tuning_flags & MSK_TUNE_ELL_MARCH_NOXCD);
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
-  const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
+  const size_t lds = (size_t)(kChunk + 2 * nx + (rv && rvs < 0 ? 2 * (kChunk + nx) : 0)) * sizeof(double);
 #define MSK_BMC(M, NT_, RV_)                                                                                    \
   k_box_march_chunk<M, NT_, RV_><<<dim3((unsigned)grid), dim3(kT), lds, s>>>(nx, P, nz, zt, xcd, halo, mask, dval, rv, \
                                                                              rvs, x, b, y, sdev, vout, stop)
 #define MSK_BMC2(M)                                                           \
   do {                                                                        \
-    if (rv) { if (nty) MSK_BMC(M, true, true); else MSK_BMC(M, false, true); } \
-    else { if (nty) MSK_BMC(M, true, false); else MSK_BMC(M, false, false); }  \
+    if (rv && rvs < 0) { if (nty) MSK_BMC(M, true, 2); else MSK_BMC(M, false, 2); } \
+    else if (rv) { if (nty) MSK_BMC(M, true, 1); else MSK_BMC(M, false, 1); }          \
+    else { if (nty) MSK_BMC(M, true, 0); else MSK_BMC(M, false, 0); }                  \
   } while (0)
   if (mode == MSK_SPMV_RESID) MSK_BMC2(MSK_SPMV_RESID);
   else if (mode == MSK_SPMV_SCALED) MSK_BMC2(MSK_SPMV_SCALED);
@@ -2945,8 +3061,9 @@ extern "C" int msk_box_march_chunk_rv(int32_t nx, int32_t ny, int32_t nz, const 
                                       int64_t rvs, const double* x, const double* b, double* y, int mode,
                                       const double* sdev, double* vout, const int* stop, hipStream_t s) {
   auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad() || !march_chunk_ok(nx, ny, 0) || !rv || (rvs & 1) ||
-      (rvs != 0 && rvs < (int64_t)nx * ny * nz) || !a16(rv) || !a16(x) || !a16(y) || (mode == MSK_SPMV_RESID && !a16(b)) ||
+  if (nx <= 0 || ny <= 0 || nz <= 0 || dv_flags_bad() || !march_chunk_ok(nx, ny, 0) || !rv || (rvs > 0 && (rvs & 1)) ||
+      (rvs > 0 && rvs < (int64_t)nx * ny * nz) || (rvs < 0 && nx > 1024) || !a16(rv) || !a16(x) || !a16(y) ||
+      (mode == MSK_SPMV_RESID && !a16(b)) ||
       (mode == MSK_SPMV_SCALED && vout && !a16(vout)))
     return (int)hipErrorInvalidValue;
   return launch_march_chunk(nx, ny, nz, 0, mask, nullptr, x, b, y, mode, sdev, vout, stop, s, rv, rvs);
@@ -3078,8 +3195,9 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
   if (self_out) *self_out = 0;
   if (n <= 0 || nchunks <= 0) return 0;
   if (nx < 2 || nx > 2048 || P < nx || nv < 1 || nv > MSK_MAX_GROUP || dv_flags_bad()) return (int)hipErrorInvalidValue;
-  if (rv && (!y || d2 || P % kChunk || n % P || (nx & 1))) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)(kChunk + 2 * nx) * sizeof(double);
+  if (rv && (!y || d2 || P % kChunk || n % P || (nx & 1) || (rvs < 0 && nx > 1024))) return (int)hipErrorInvalidValue;
+  // the symmetric storage adds the x+1 / y+1 legs' windows (2 x (4096 + nx) doubles; nx <= 1024: <= 128 KiB in all)
+  const size_t lds = (size_t)(kChunk + 2 * nx + (rv && rvs < 0 ? 2 * (kChunk + nx) : 0)) * sizeof(double);
   const dim3 g((unsigned)nchunks), b(kT);
   const bool nty = !(msk_tuning_flags & MSK_TUNE_ELL_TEMPORAL_Y);
   if (!d2 && P % kChunk == 0 && n % P == 0 && (nx & 1) == 0 && (rv || !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_FLAT))) {
@@ -3118,16 +3236,19 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
                                                                                  partial, nchunks, stop)
 #define MSK_BSMM(VAR_, NT_, RV_)                                                                              \
   do {                                                                                                        \
-    if (RV_ && rvp == 4) MSK_BSMM_P(VAR_, NT_, RV_, 4);                                                       \
-    else if (RV_ && rvp == 2) MSK_BSMM_P(VAR_, NT_, RV_, 2);                                                  \
+    if (RV_ == 1 && rvp == 4) MSK_BSMM_P(VAR_, NT_, RV_, 4);                                                  \
+    else if (RV_ == 1 && rvp == 2) MSK_BSMM_P(VAR_, NT_, RV_, 2);                                             \
     else MSK_BSMM_P(VAR_, NT_, RV_, kIters);                                                                  \
   } while (0)
-    if (rv) {
-      if (vec_var()) { if (nty) MSK_BSMM(1, true, true); else MSK_BSMM(1, false, true); }
-      else { if (nty) MSK_BSMM(0, true, true); else MSK_BSMM(0, false, true); }
+    if (rv && rvs < 0) {  // the symmetric storage
+      if (vec_var()) { if (nty) MSK_BSMM(1, true, 2); else MSK_BSMM(1, false, 2); }
+      else { if (nty) MSK_BSMM(0, true, 2); else MSK_BSMM(0, false, 2); }
+    } else if (rv) {
+      if (vec_var()) { if (nty) MSK_BSMM(1, true, 1); else MSK_BSMM(1, false, 1); }
+      else { if (nty) MSK_BSMM(0, true, 1); else MSK_BSMM(0, false, 1); }
     } else {
-      if (vec_var()) { if (nty) MSK_BSMM(1, true, false); else MSK_BSMM(1, false, false); }
-      else { if (nty) MSK_BSMM(0, true, false); else MSK_BSMM(0, false, false); }
+      if (vec_var()) { if (nty) MSK_BSMM(1, true, 0); else MSK_BSMM(1, false, 0); }
+      else { if (nty) MSK_BSMM(0, true, 0); else MSK_BSMM(0, false, 0); }
     }
 #undef MSK_BSMM
 #undef MSK_BSMM_P

@@ -466,8 +466,8 @@ struct msp_mat {
   int32_t march_d2 = 0;        // 2D box stencil (five pairs), marched as nx x 1 x ny
   int32_t march_halo = 0;      // bit 0 / 1: the column space adds the plane below / above the box (chunk march only)
   uint8_t* march_mask = nullptr;  // nrows (+16 pad): the rows' presence bytes (msk_march_mask)
-  // STENCIL storage (rv_attach): a 3D box stencil whose rows carry their own values; rv_stride == 0: chunk-blocked
-  // (msplit_kernels.hip rv_pair; the default), else rv_val[e * rv_stride + r] is
+  // STENCIL storage (rv_attach): a 3D box stencil whose rows carry their own values; rv_stride == -1: symmetric,
+  // the diagonal and upper legs only (rvs_pair), 0: chunk-blocked seven legs (rv_pair), else rv_val[e * rv_stride + r] is
   // row r's entry at neighbour e (column order; 0.0 where the row has none), march_* and march_mask as above
   double* rv_val = nullptr;
   int64_t rv_stride = 0;
@@ -739,16 +739,50 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
     return MSP_SUCCESS;
   }
   std::vector<uint8_t> mask((size_t)n + 16, 0);
-  std::vector<double> rv((size_t)7 * stride, 0.0);
+  std::vector<double> rv((size_t)7 * stride, 0.0);  // per-leg arrays first
   for (int32_t r = 0; r < n; ++r)
     for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
       const int e = (int)(std::find(dd.begin(), dd.end(), col[k] - r) - dd.begin());  // dd is in column order now
       mask[r] |= (uint8_t)(1u << e);
-      const int64_t o = r % MSK_DBR_CHUNK;
-      rv[blocked ? (size_t)(7 * (r - o) + (o / 512) * 3584 + e * 512 + o % 512) : (size_t)e * stride + r] = val[k];
+      rv[(size_t)e * stride + r] = val[k];
     }
+  // The symmetric storage (like PETSc's SBAIJ, which keeps one triangle): when every upper entry A[r, r + d] has
+  // its mirror A[r + d, r] with the same bits (and every lower entry its upper one), only the diagonal and the
+  // three upper legs are kept (32 B/row instead of 56) and a row's lower values are read at its lower neighbours.
+  // Chunk-blocked only, planes up to 1024 wide (the kernels' LDS windows); MSPLIT_RV_SYM=0 keeps the seven legs.
+  const char* syme = getenv("MSPLIT_RV_SYM");
+  bool sym = blocked && nx <= 1024 && !(syme && syme[0] == '0');
+  {
+    const int64_t P = (int64_t)nx * ny;
+    const int64_t dlt[3] = {1, nx, P};  // upper leg 4 + i mirrors lower leg 2 - i
+    for (int32_t r = 0; r < n && sym; ++r)
+      for (int i = 0; i < 3 && sym; ++i) {
+        const int up = 4 + i, lo = 2 - i;
+        if (mask[r] & (1u << up)) {
+          const int64_t c = r + dlt[i];
+          uint64_t a, b;
+          std::memcpy(&a, &rv[(size_t)up * stride + r], 8);
+          if (c >= n || !(mask[c] & (1u << lo))) { sym = false; break; }
+          std::memcpy(&b, &rv[(size_t)lo * stride + c], 8);
+          sym = a == b;
+        }
+        if (sym && (mask[r] & (1u << lo)) && (r - dlt[i] < 0 || !(mask[r - dlt[i]] & (1u << up)))) sym = false;
+      }
+  }
+  const int nleg = sym ? 4 : 7;
+  if (blocked) {  // chunk-blocked: the legs of each 512-row slice of a DBR chunk next to each other
+    std::vector<double> bl((size_t)nleg * stride, 0.0);
+    const int legs[7] = {0, 1, 2, 3, 4, 5, 6}, sym_legs[4] = {3, 4, 5, 6};  // d, x+1, y+1, z+1
+    for (int32_t r = 0; r < n; ++r) {
+      const int64_t o = r % MSK_DBR_CHUNK;
+      for (int k = 0; k < nleg; ++k)
+        bl[(size_t)(nleg * (r - o) + (o / 512) * (nleg * 512) + k * 512 + o % 512)] =
+            rv[(size_t)(sym ? sym_legs[k] : legs[k]) * stride + r];
+    }
+    rv.swap(bl);
+  }
   if (mspi_big_alloc((void**)&A->march_mask, (size_t)n + 16) != (int)hipSuccess ||
-      mspi_big_alloc((void**)&A->rv_val, (size_t)7 * stride * sizeof(double)) != (int)hipSuccess) {
+      mspi_big_alloc((void**)&A->rv_val, (size_t)nleg * stride * sizeof(double)) != (int)hipSuccess) {
     (void)hipGetLastError();  // the allocation failure is not the caller's error: the matrix stays in CSR
     rv_free(A);
     if (A->march_mask) (void)hipFree(A->march_mask);
@@ -756,7 +790,8 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
     return MSP_SUCCESS;
   }
   HIPCHK(hipMemcpyAsync(A->march_mask, mask.data(), (size_t)n + 16, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(A->rv_val, rv.data(), (size_t)7 * stride * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(A->rv_val, rv.data(), (size_t)nleg * stride * sizeof(double), hipMemcpyHostToDevice,
+                        c->stream));
   int* fail = reinterpret_cast<int*>(mspi_dev_scratch(c));
   HIPCHK(hipMemsetAsync(fail, 0, sizeof(int), c->stream));
   KCHK(msk_march_check(n, nx, ny, 0, A->march_mask, fail, c->stream));
@@ -769,7 +804,7 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
     A->march_mask = nullptr;
     return MSP_SUCCESS;
   }
-  A->rv_stride = blocked ? 0 : stride;
+  A->rv_stride = sym ? -1 : blocked ? 0 : stride;  // -1: the symmetric storage (msplit_kernels.hip rvs_pair)
   A->march_nx = nx;
   A->march_ny = ny;
   A->march_nz = nz;
@@ -1120,8 +1155,8 @@ static double march_bytes(const msp_mat* A, bool resid, bool vout) {
 }
 
 // STENCIL storage: the presence byte and the seven values of every row, x once, y written (b read, vout written)
-static double rv_bytes(const msp_mat* A, bool resid, bool vout) {
-  return 56.0 * (double)A->nrows + march_bytes(A, resid, vout);
+static double rv_bytes(const msp_mat* A, bool resid, bool vout) {  // 7 legs, or the symmetric storage's 4
+  return (A->rv_stride < 0 ? 32.0 : 56.0) * (double)A->nrows + march_bytes(A, resid, vout);
 }
 
 extern "C" int msp_mat_set_storage(msp_mat* A, int storage) {
@@ -1319,7 +1354,7 @@ extern "C" int msp_mat_get_spmv_kernel(const msp_mat* A, const char** name) {
   ARGCHK(A && name, MSP_ERR_ARG_NULL, "NULL argument");
   if (A->matfree) *name = "k_stencil_spmv";
   else if (A->compressed) *name = "k_spmv_rows";
-  else if (A->rv_on) *name = "k_box_march_chunk_rv";
+  else if (A->rv_on) *name = A->rv_stride < 0 ? "k_box_march_chunk_rv_sym" : "k_box_march_chunk_rv";
   else if (A->dv_on && (box_march(A) || box_march_halo(A))) *name = "k_spmv_box_march";
   else if (A->dv_on) *name = A->dv_w ? "k_spmv_ell" : "k_spmv_dv";
   else *name = A->lds_cap > 0 ? "k_spmv_lds8" : "k_spmv_csr";

@@ -716,9 +716,19 @@ def test_non_stencil_aij_keeps_csr_and_equals_oracle(ctx, oracle, n, flags):
         _gmres_vs_oracle(ctx, oracle, A, O, O.mult(np.ones(N)), max_it=75)
 
 
-@pytest.mark.parametrize("layout", ["blocked", "soa"])
+def _unsymmetric(rp, col, val, seed=SEED):
+    """The same operator with a few upper entries scaled: no longer symmetric, so it keeps the seven legs."""
+    val = val.copy()
+    rows = np.repeat(np.arange(rp.size - 1), np.diff(rp))
+    upper = np.flatnonzero(col > rows)
+    pick = np.random.default_rng(seed).choice(upper, size=max(1, upper.size // 1000), replace=False)
+    val[pick] *= 1.5
+    return val
+
+
+@pytest.mark.parametrize("layout", ["sym", "blocked", "soa", "blocked-unsym"])
 @pytest.mark.parametrize("flags", [0, BOX_SEPARATE])
-@pytest.mark.parametrize("shape", [(64, 64, 16), (128, 32, 9), (64, 64, 2), (2048, 2, 3)])
+@pytest.mark.parametrize("shape", [(64, 64, 16), (128, 32, 9), (64, 64, 2), (2048, 2, 3), (1024, 4, 5)])
 def test_variable_coefficient_box_takes_the_stencil_storage(ctx, oracle, shape, flags, layout, monkeypatch):
     """A box stencil with variable coefficients (utils.heterogeneous_poisson3d) whose planes hold whole 4096-row
     chunks: no dictionary fits, so msp_mat_create_csr gives it the STENCIL storage (a presence byte and the row's
@@ -731,10 +741,17 @@ def test_variable_coefficient_box_takes_the_stencil_storage(ctx, oracle, shape, 
     nx, ny, nz = shape
     rp, col, val = heterogeneous_poisson3d(nx, ny, nz)
     N = nx * ny * nz
-    # the value layout chosen at assembly: chunk-blocked (the default) or per-leg arrays (MSPLIT_RV_LAYOUT=soa)
-    monkeypatch.setenv("MSPLIT_RV_LAYOUT", layout)
+    # the value layout chosen at assembly: symmetric (the diagonal and upper legs; the default for a symmetric
+    # operator with planes up to 1024 wide), chunk-blocked seven legs (MSPLIT_RV_SYM=0, or an unsymmetric operator),
+    # or per-leg arrays (MSPLIT_RV_LAYOUT=soa)
+    monkeypatch.setenv("MSPLIT_RV_LAYOUT", "soa" if layout == "soa" else "blocked")
+    monkeypatch.setenv("MSPLIT_RV_SYM", "1" if layout == "sym" else "0" if layout == "blocked" else "1")
+    if layout == "blocked-unsym":
+        val = _unsymmetric(rp, col, val)
     A = Mat.from_csr(ctx, N, N, rp, col, val)
-    assert A.get_storage() == "stencil" and A.spmv_kernel() == "k_box_march_chunk_rv"
+    sym = layout == "sym" and nx <= 1024
+    assert A.get_storage() == "stencil"
+    assert A.spmv_kernel() == ("k_box_march_chunk_rv_sym" if sym else "k_box_march_chunk_rv")
     O = oracle.Mat.from_arrays(N, N, rp, col, val)
     y, res = _products(ctx, A, O, np.random.default_rng(SEED))
     with tuning(flags):
