@@ -332,6 +332,48 @@ __device__ __forceinline__ bool tr_apply_v(const Tr& t, double s, double& out) {
   return z || (!(t.fl & F_BAD) && inb && rng);
 }
 
+// A map prepared for the one-record applies of the walk (round 5): in its binade e (u = 2^(e-52)) the map is valid at
+// s iff |s| = M u lies in [L_p, H_p) -- L_p = max(2^52, 2^52 - lo_p) u, H_p = min(2^53, 2^53 - hi_p) u, every product
+// exact (an integer below 2^61 times a power of two) -- and s has the map's sign; then |s| + d_p u is exact (its M + d
+// lies in [2^52, 2^53)), so the result is one f64 add: a dozen mostly independent instructions where tr_apply_v
+// decodes s's bits and rebuilds the result's.  BAD maps take L = +inf (never valid); zero maps the identity rule.
+struct Prep {
+  double L0, L1, H0, H1, D0, D1;
+  uint32_t fl;
+};
+
+__device__ __forceinline__ Prep prep_of(const Tr& t) {
+  Prep p;
+  const int sh = t.e - 52;
+  p.L0 = ldexp(fmax(kM0, kM0 - t.lo0), sh);
+  p.L1 = ldexp(fmax(kM0, kM0 - t.lo1), sh);
+  p.H0 = ldexp(fmin(kM1, kM1 - t.hi0), sh);
+  p.H1 = ldexp(fmin(kM1, kM1 - t.hi1), sh);
+  p.D0 = ldexp(t.d0, sh);
+  p.D1 = ldexp(t.d1, sh);
+  const bool bad = (t.fl & F_BAD) != 0;
+  p.L0 = bad ? INFINITY : p.L0;
+  p.L1 = bad ? INFINITY : p.L1;
+  p.fl = t.fl;
+  return p;
+}
+
+// tr_apply_v's verdict and result wherever that returns true (every lane its own prepared map at the same s)
+__device__ __forceinline__ bool prep_apply(const Prep& p, double s, double& out) {
+  const uint64_t b = (uint64_t)__double_as_longlong(s);
+  const bool od = (b & 1) != 0;
+  const bool neg = (b >> 63) != 0;
+  const double a = fabs(s);
+  const double L = pickd(od, p.L1, p.L0), H = pickd(od, p.H1, p.H0), D = pickd(od, p.D1, p.D0);
+  const bool ok = a >= L && a < H && neg == ((p.fl & F_NEG) != 0);
+  const double m = a + D;
+  const double ot = neg ? -m : m;
+  const double oz = s == 0.0 ? ((signbit(s) && (p.fl & F_NZERO)) ? -0.0 : 0.0) : s;
+  const bool z = (p.fl & F_ZERO) != 0;
+  out = z ? oz : ot;
+  return z || ok;
+}
+
 __device__ __forceinline__ Tr shfl_xor_tr(const Tr& t, int m) {
   Tr r;
   r.d0 = __shfl_xor(t.d0, m);
@@ -625,7 +667,8 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
                                                       const Tr* __restrict__ segT, const Tr* __restrict__ subT,
                                                       int64_t K, const double* __restrict__ acc_in,
                                                       double* __restrict__ partial, int64_t nchunks,
-                                                      const int* __restrict__ stop, int64_t* __restrict__ stats) {
+                                                      const int* __restrict__ stop, int64_t* __restrict__ stats,
+                                                      int prep) {
   if (stopped(stop)) return;
   __shared__ double sp[kSeg];
   const int v = blockIdx.x, t = threadIdx.x, lane = t & 63;
@@ -644,6 +687,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
     const bool in = kb + lane < K;
     const Tr tw = tr_load(segT + (int64_t)v * K + (in ? kb + lane : 0));
     const Tr tv = tr_sel(in, tw, tr_bad());
+    const Prep pv = prep_of(tv);
     int f0 = 0;
     bool scan = true;
     while (f0 < 64 && kb + f0 < K) {
@@ -653,7 +697,8 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
         ++n_scan;
       } else {  // the segment after a descended one, on its own
         double sn = 0.0;
-        const bool ok = tr_apply_v(tv, s, sn);  // every lane its own segment's map at s; lane f0's is the one
+        const bool ok = prep ? prep_apply(pv, s, sn) : tr_apply_v(tv, s, sn);  // every lane its own segment's map at
+                                                                                  // s; lane f0's is the one
         const bool mine = ((__ballot(ok) >> f0) & 1) != 0;
         ++n_single;
         if (mine) {
@@ -671,6 +716,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
       const int64_t k = kb + f;
       ++n_segdesc;
       const Tr u = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
+      const Prep pu = prep_of(u);
       __syncthreads();  // the previous segment's LDS reads are done
       fill_segment(sp, w, y, sy, n, k);
       int j;
@@ -695,7 +741,8 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
         const int64_t t1 = stats ? wall_clock64() : 0;
         for (++j; j < kSubs; ++j) {
           double sn = 0.0;
-          const bool ok = tr_apply_v(u, s, sn);  // every lane its own sub's map at s; lane j's is the one
+          const bool ok = prep ? prep_apply(pu, s, sn) : tr_apply_v(u, s, sn);  // every lane its own sub's map at s;
+                                                                                  // lane j's is the one
           ++n_single;
           if (!((__ballot(ok) >> j) & 1)) break;
           s = rld(sn, j);
@@ -778,8 +825,13 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
   int64_t* dstats = nullptr;
   if (st && st[0] == '1' && hipMalloc((void**)&dstats, 16 * MSK_MAX_GROUP * sizeof(int64_t)) != hipSuccess)
     dstats = nullptr;
+  // MSPLIT_SEQ_PREP=0: the one-record applies decode s's bits (tr_apply_v, round 4) instead of the prepared maps
+  static const int prep = [] {
+    const char* e = getenv("MSPLIT_SEQ_PREP");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
   k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
-                                                        stop, dstats);
+                                                        stop, dstats, prep);
   if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];
     if (hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&

@@ -303,3 +303,63 @@ def test_f64_decomposition_equals_the_integer_one():
                     # unit higher, which is exact in the only case it decides (s = 2^e: RN(2^e - tiny) = 2^e).
                     assert r_int == (-1, 2) and r_f == (0, 0) and math.ldexp(abs(p), 52 - e) == 0.0, \
                         (p, e, sneg, r_int, r_f)
+
+
+def _ldexp(x, sh):
+    try:
+        return math.ldexp(float(x), sh)
+    except OverflowError:
+        return math.inf if x > 0 else -math.inf
+
+
+def prep(t):
+    """k_seqx_walk's prepared map (Prep, round 5): in the map's binade the valid states are |s| in [L_p, H_p) of the
+    map's sign, and the result is |s| + d_p u, one f64 add."""
+    if t["zero"]:
+        return dict(zero=True, nzero=t["nzero"])
+    sh = t["e"] - 52
+    L = [_ldexp(max(M0, M0 - t["lo"][p]), sh) for p in (0, 1)]
+    H = [_ldexp(min(M1, M1 - t["hi"][p]), sh) for p in (0, 1)]
+    D = [_ldexp(t["d"][p], sh) for p in (0, 1)]
+    if t["bad"]:
+        L = [math.inf, math.inf]
+    return dict(zero=False, L=L, H=H, D=D, neg=t["neg"])
+
+
+def prep_apply(q, s):
+    if q["zero"]:
+        if s == 0.0:
+            return -0.0 if (math.copysign(1.0, s) < 0 and q["nzero"]) else 0.0
+        return s
+    b = bits(s)
+    od, neg, a = b & 1, b >> 63, abs(s)
+    if not (a >= q["L"][od] and a < q["H"][od] and neg == q["neg"]):
+        return None
+    m = a + q["D"][od]
+    return -m if neg else m
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_prepared_map_apply_is_tr_apply(name):
+    """The walk's one-record applies on prepared maps decide and compute exactly as tr_apply: for every sub-segment
+    map of the case (built in the binade of the true and of a jittered guess) and every state the sequential sum
+    passes through near it (and +-0, subnormals, +-inf), the same verdict and the same bits."""
+    ps = [float(v) for v in CASES[name]]
+    pre = [0.0]
+    for p in ps:
+        pre.append(pre[-1] + p)
+    rng = np.random.default_rng(11)
+    extra = [0.0, -0.0, 5e-324, -5e-324, math.inf, -math.inf, 1.0, -1.0]
+    checked = 0
+    for i in range(0, len(ps), 16):
+        for G in (pre[i], pre[i] * (1.0 + 1e-9 * rng.uniform(-1, 1))):
+            gok, e, sn = guess(G)
+            t = run(ps[i:i + 16], e, sn, gok)
+            q = prep(t)
+            for s in [pre[i], pre[min(i + 1, len(ps))], pre[min(i + 16, len(ps))]] + extra:
+                r1, r2 = apply(t, s), prep_apply(q, s)
+                assert (r1 is None) == (r2 is None), (name, i, s, r1, r2)
+                if r1 is not None:
+                    assert bits(r1) == bits(r2), (name, i, s, r1, r2)
+                    checked += 1
+    assert checked > 0 or name in ("inf", "overflow", "neg_zero", "cancel", "subnormal")
