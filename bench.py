@@ -130,6 +130,9 @@ def parse():
     p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--no-seq-mode", action="store_true",
                    help="N=1: skip the seq_mode measurement (one configs[1] step in PETSc's reduction order)")
+    p.add_argument("--seq-smsm", action="store_true",
+                   help="N=1: also time one SMSM-global block outer iteration in PETSc's reduction order, verified "
+                        "first on tests/golden/smsm_seq.json's small block")
     p.add_argument("--no-non-stencil", action="store_true",
                    help="N=1: skip the non_stencil_aij measurement (GMRES on a per-cell-coefficient AIJ in CSR "
                         "storage, default and fused MatMult+MDot steps)")
@@ -572,6 +575,56 @@ def seq_mode_step(ctx, ksp, b, x, ref):
                     "(47.97 s per step with the serial engine, round 3)"}
 
 
+SMSM_SEQ_GOLDEN = os.path.join(ROOT, "tests", "golden", "smsm_seq.json")
+
+
+def smsm_seq_mode(ctx, args):
+    """The N > 1 per-GPU workload (one SMSM-global outer iteration on one z-slab block: s inner GMRES solves, R = A S,
+    the LSQR, x = S alpha) with every reduction in PETSc's sequential order (-msplit_reduction seq).  First the same
+    step on the small block of tests/golden/smsm_seq.json (written by the PETSc-order oracle), compared bit for bit;
+    then one outer iteration of the full-size block, timed."""
+    import hashlib
+    import numpy as np
+    import torch
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import smsm_solve
+    g = json.load(open(SMSM_SEQ_GOLDEN)) if os.path.exists(SMSM_SEQ_GOLDEN) else None
+    out = {"reduction": "seq (PETSc's order)", "workload": None, "verified": None, "mismatch": []}
+    ctx.set_reduction("seq")
+    try:
+        if g is not None:
+            P = g["problem"]
+            a2 = argparse.Namespace(**vars(args))
+            a2.smsm_mesh, a2.smsm_planes, a2.s = P["nx"], P["nz"], P["s"]
+            a2.inner_max_it, a2.outer_max_it = g["inner"]["max_it"], g["outer"]["max_it"]
+            a2.restart, a2.peclet, a2.operator = g["inner"]["restart"], None, "csr"
+            _, _, _, _, (blk, mini, _) = build_smsm(ctx, a2, LocalComm(), 1, 0)
+            res = smsm_solve([blk], LocalComm(), P["s"], mini, rtol=P["rtol"], max_outer=P["outer_its"])
+            got = {"outer_its": res.outer_its, "norm0_hex": float(res.norm0).hex(),
+                   "hist_hex": [float(h).hex() for h in res.hist], "lsqr_its": [int(v) for v in res.lsqr_its],
+                   "inner_its": np.array(res.inner_its).tolist(),
+                   "x_sha256": hashlib.sha256(np.ascontiguousarray(blk.x.get_array(), np.float64).tobytes())
+                   .hexdigest()}
+            mini.close()
+            del blk, mini
+            out["mismatch"] = [k for k in got if got[k] != g[k]]
+            out["verified"] = not out["mismatch"]
+            out["reference"] = "tests/golden/smsm_seq.json (oracle/oracle.c orc_smsm_solve, ORC_REDUCE_SEQ)"
+        step, workload, _, rows, (blk, mini, lsqr_its) = build_smsm(ctx, args, LocalComm(), 1, 0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        its = step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        mini.close()
+    finally:
+        ctx.set_reduction("dbr")
+    out.update({"workload": workload, "value": rows * its / dt, "unit": "DOF-updates/s", "seconds_per_step": dt,
+                "gmres_iterations": its, "lsqr_iterations": lsqr_its[-1],
+                "note": "the parity mode on the SMSM block (configs[2]'s per-GPU workload): one outer iteration"})
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -768,6 +821,8 @@ def main():
             extras["spmv_512_csr"] = spmv512(ctx, args)
         if not args.no_smsm_n1:
             extras["smsm_per_gpu"] = smsm_n1(ctx, args)
+        if args.seq_smsm:
+            extras["smsm_seq_mode"] = smsm_seq_mode(ctx, args)
 
     if rank == 0:
         value = updates / elapsed_max

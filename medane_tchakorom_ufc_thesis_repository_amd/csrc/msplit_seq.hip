@@ -60,6 +60,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 
 #include "msplit_ctx.hpp"
@@ -622,20 +623,37 @@ __device__ __forceinline__ int tr_walk(Tr t, double& s, int lane) {
 constexpr int kWalkT = 256;  // four waves walk one sum redundantly; all four fill a descended segment's terms
 
 // Segment k's terms into LDS (every thread of the workgroup, coalesced), products formed as the serial engine's.
-__device__ __forceinline__ void fill_segment(double* sp, const double* __restrict__ w, const double* __restrict__ y,
-                                             double sy, int64_t n, int64_t k) {
+// Every load is issued before the first product is formed (indices clamped into [0, n), the products past n are
+// +0.0), so a thread waits for memory once, not once per term (the loop of rounds 3-4 waited 16 times, 12 us a
+// segment).  fill_load issues the loads into registers, fill_store forms the products into LDS: work placed between
+// the two overlaps the loads.
+constexpr int kFillR = kSeg / kWalkT;
+struct Fill {
+  double a[kFillR], b[kFillR];
+};
+__device__ __forceinline__ void fill_load(Fill& f, const double* __restrict__ w, const double* __restrict__ y,
+                                          int64_t n, int64_t k) {
   const int t = threadIdx.x;
 #pragma unroll
-  for (int r = 0; r < kSeg / kWalkT; ++r) {
-    const int l = t + r * kWalkT;
-    const int64_t g = k * kSeg + l;
-    double p = 0.0;
-    if (g < n) {
-      const double xi = w[g];
-      p = y ? xi * (y[g] * sy) : xi * xi;
-    }
-    sp[l] = p;
+  for (int r = 0; r < kFillR; ++r) f.a[r] = w[min<int64_t>(k * kSeg + t + r * kWalkT, n - 1)];
+  if (y) {
+#pragma unroll
+    for (int r = 0; r < kFillR; ++r) f.b[r] = y[min<int64_t>(k * kSeg + t + r * kWalkT, n - 1)];
   }
+}
+__device__ __forceinline__ void fill_store(const Fill& f, double* sp, bool self, double sy, int64_t n, int64_t k) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < kFillR; ++r) {
+    const bool in = k * kSeg + t + r * kWalkT < n;
+    sp[t + r * kWalkT] = in ? (self ? f.a[r] * f.a[r] : f.a[r] * (f.b[r] * sy)) : 0.0;
+  }
+}
+__device__ __forceinline__ void fill_segment(double* sp, const double* __restrict__ w, const double* __restrict__ y,
+                                             double sy, int64_t n, int64_t k) {
+  Fill f;
+  fill_load(f, w, y, n, k);
+  fill_store(f, sp, y == nullptr, sy, n, k);
 }
 
 // Wave-uniform: s after the terms [i0, i1) of the LDS segment, added in order by the f64 add (lane 0; broadcast).
@@ -676,6 +694,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
   const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
   int64_t n_scan = 0, n_segdesc = 0, n_subser = 0, n_single = 0, n_fbad = 0, n_fstate = 0, n_fguess = 0, n_frange = 0;
   int64_t c_scan = 0, c_single = 0, c_serial = 0, c_wait = 0, c_all = stats ? wall_clock64() : 0;  // 100 MHz ticks
+  int64_t c_win = 0, c_subld = 0, c_fill = 0;  // stats only: memory waits made explicit (s_waitcnt 0) to time them
 #define TICK(acc, stmt)                     \
   do {                                      \
     const int64_t t0_ = stats ? wall_clock64() : 0; \
@@ -685,9 +704,14 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
   double s = acc_in ? acc_in[v] : 0.0;
   for (int64_t kb = 0; kb < K; kb += 64) {
     const bool in = kb + lane < K;
+    const int64_t tw0 = stats ? wall_clock64() : 0;
     const Tr tw = tr_load(segT + (int64_t)v * K + (in ? kb + lane : 0));
     const Tr tv = tr_sel(in, tw, tr_bad());
     const Prep pv = prep_of(tv);
+    if (stats) {
+      __builtin_amdgcn_s_waitcnt(0);
+      c_win += wall_clock64() - tw0;
+    }
     int f0 = 0;
     bool scan = true;
     while (f0 < 64 && kb + f0 < K) {
@@ -715,10 +739,20 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
       // tried on its own (lane j applies its map to s) and the failing ones are added term by term.
       const int64_t k = kb + f;
       ++n_segdesc;
+      const int64_t tl0 = stats ? wall_clock64() : 0;
       const Tr u = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
       const Prep pu = prep_of(u);
+      if (stats) {
+        __builtin_amdgcn_s_waitcnt(0);
+        c_subld += wall_clock64() - tl0;
+      }
+      const int64_t tf0 = stats ? wall_clock64() : 0;
       __syncthreads();  // the previous segment's LDS reads are done
       fill_segment(sp, w, y, sy, n, k);
+      if (stats) {
+        __builtin_amdgcn_s_waitcnt(0);
+        c_fill += wall_clock64() - tf0;
+      }
       int j;
       TICK(c_scan, j = tr_walk(u, s, lane));
       ++n_scan;
@@ -770,6 +804,164 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_walk(const double* __restrict__
     stats[8 * MSK_MAX_GROUP + v * 8 + 2] = c_serial;
     stats[8 * MSK_MAX_GROUP + v * 8 + 3] = c_wait;
     stats[8 * MSK_MAX_GROUP + v * 8 + 4] = wall_clock64() - c_all;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 5] = c_win;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 6] = c_subld;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 7] = c_fill;
+  }
+}
+
+// ------------------------------------------------------------ the ripple walk (round 5)
+// A prepared map in its one-add form: where it applies, s -> s + SD_p with SD_p = +-D_p carrying the map's sign (s
+// has that sign, and |s| + D_p is exact, so s + SD_p is the same double); a zero map adds -0.0 when all its terms are
+// -0.0 and +0.0 otherwise, which is its identity rule on every s, +-0.0 included.  Its validity is prep_valid.
+struct Rip {
+  double sd0, sd1;
+};
+__device__ __forceinline__ Rip rip_of(const Prep& p) {
+  const bool z = (p.fl & F_ZERO) != 0, ng = (p.fl & F_NEG) != 0;
+  const double zr = (p.fl & F_NZERO) ? -0.0 : 0.0;
+  Rip r;
+  r.sd0 = z ? zr : (ng ? -p.D0 : p.D0);
+  r.sd1 = z ? zr : (ng ? -p.D1 : p.D1);
+  return r;
+}
+// prep_apply's verdict
+__device__ __forceinline__ bool prep_valid(const Prep& p, double s) {
+  const uint64_t b = (uint64_t)__double_as_longlong(s);
+  const bool od = (b & 1) != 0, neg = (b >> 63) != 0;
+  const double a = fabs(s);
+  const double L = pickd(od, p.L1, p.L0), H = pickd(od, p.H1, p.H0);
+  return (p.fl & F_ZERO) != 0 || (a >= L && a < H && neg == ((p.fl & F_NEG) != 0));
+}
+
+// lane l gets lane l - 1's x; lane 0 gets s (DPP wave_shr:1 over the 64 lanes, lane 0's "old" operand)
+__device__ __forceinline__ double shr1_from(double x, double s) {
+  const int64_t b = __double_as_longlong(x), o = __double_as_longlong(s);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x138, 0xf, 0xf, false);
+  return __longlong_as_double((int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+// The lanes' maps j0, j0 + 1, .. applied in order from s, R steps of a ripple through the wave: each step every lane
+// adds its SD to its left neighbour's previous result (lanes below j0 are the identity, lane 0 reads s), so after
+// step i lanes j0 .. j0 + i hold the sequential results wherever every map before theirs applied -- one f64 add, a
+// parity select and two DPP moves a step.  Then one verdict per lane at its final input: returns the first lane in
+// [j0, j0 + r) whose map does not apply at its true input (j0 + r if all do), s advanced to that lane's input.
+template <int R>
+__device__ __forceinline__ int ripple(const Prep& p, const Rip& q, double& s, int j0, int r, int lane) {
+  const bool idn = lane < j0;
+  const double sd0 = idn ? -0.0 : q.sd0, sd1 = idn ? -0.0 : q.sd1;
+  double in = s, out = s;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    if (i) in = shr1_from(out, s);
+    out = in + pickd(((uint32_t)__double_as_longlong(in) & 1u) != 0, sd1, sd0);
+  }
+  const bool ok = idn || prep_valid(p, in);
+  const uint64_t bad = __ballot(!ok) & (~uint64_t(0) << j0);
+  const int f = min(bad ? __builtin_ctzll(bad) : 64, j0 + r);
+  if (f > j0) s = rld(out, f - 1);
+  return f;
+}
+
+// The maps from lane j on, ripple after ripple, up to the first that does not apply or lim; returns its lane.
+template <int R>
+__device__ __forceinline__ int ripple_run(const Prep& p, const Rip& q, double& s, int j, int lim, int lane,
+                                          int64_t& calls) {
+  while (j < lim) {
+    const int r = min(R, lim - j);
+    const int f = ripple<R>(p, q, s, j, r, lane);
+    ++calls;
+    if (f < j + r) return f;
+    j = f;
+  }
+  return lim;
+}
+__device__ __forceinline__ int ripple_runw(int w, const Prep& p, const Rip& q, double& s, int j, int lim, int lane,
+                                           int64_t& calls) {
+  switch (w) {
+    case 4: return ripple_run<4>(p, q, s, j, lim, lane, calls);
+    case 8: return ripple_run<8>(p, q, s, j, lim, lane, calls);
+    case 32: return ripple_run<32>(p, q, s, j, lim, lane, calls);
+    default: return ripple_run<16>(p, q, s, j, lim, lane, calls);
+  }
+}
+
+// Workgroup v: sum v, from +0.0, every map applied by ripples: the window of 64 segment maps up to the first that
+// does not apply; that segment's sub maps likewise (its terms' loads in flight meanwhile); a sub that does not
+// apply is added term by term from LDS, and the ripple resumes after it.  rw: the ripple width over segments and a
+// descended segment's first subs; rs: after a serially added sub.  All four waves compute the same s.
+__global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restrict__ w, Vecs V, int64_t n, int self,
+                                                         const Tr* __restrict__ segT, const Tr* __restrict__ subT,
+                                                         int64_t K, const double* __restrict__ acc_in,
+                                                         double* __restrict__ partial, int64_t nchunks,
+                                                         const int* __restrict__ stop, int64_t* __restrict__ stats,
+                                                         int rw, int rs) {
+  if (stopped(stop)) return;
+  __shared__ double sp[kSeg];
+  const int v = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const double* y = self ? nullptr : vec_row(V, v);
+  const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
+  int64_t n_win = 0, n_segdesc = 0, n_rip = 0, n_subser = 0;
+  int64_t c_win = 0, c_rip = 0, c_serial = 0, c_fill = 0, c_all = stats ? wall_clock64() : 0;  // 100 MHz ticks
+#define TICK(acc, stmt)                             \
+  do {                                              \
+    const int64_t t0_ = stats ? wall_clock64() : 0; \
+    stmt;                                           \
+    if (stats) acc += wall_clock64() - t0_;         \
+  } while (0)
+  double s = acc_in ? acc_in[v] : 0.0;
+  for (int64_t kb = 0; kb < K; kb += 64) {
+    const int lim = (int)min<int64_t>(64, K - kb);
+    const bool in = lane < lim;
+    const Tr tw = tr_load(segT + (int64_t)v * K + (in ? kb + lane : 0));
+    const Prep pv = prep_of(tr_sel(in, tw, tr_bad()));
+    const Rip qv = rip_of(pv);
+    for (int f = 0;;) {
+      TICK(c_win, f = ripple_runw(rw, pv, qv, s, f, lim, lane, n_win));
+      if (f >= lim) break;
+      const int64_t k = kb + f;  // segment k does not apply at s: its sub maps
+      ++n_segdesc;
+      const int64_t tf0 = stats ? wall_clock64() : 0;
+      Fill fl;
+      fill_load(fl, w, y, n, k);
+      const Prep pu = prep_of(tr_load(subT + ((int64_t)v * K + k) * kSubs + lane));
+      const Rip qu = rip_of(pu);
+      int j;
+      TICK(c_rip, j = ripple_runw(rw, pu, qu, s, 0, kSubs, lane, n_rip));
+      if (j < kSubs) {
+        __syncthreads();  // the previous segment's LDS reads are done
+        fill_store(fl, sp, self != 0, sy, n, k);
+        __syncthreads();
+      }
+      if (stats) c_fill += wall_clock64() - tf0;
+      while (j < kSubs) {
+        const int64_t c0 = k * kSeg + (int64_t)j * kSub;
+        const int i1 = (int)max<int64_t>(0, min<int64_t>(kSub, n - c0));
+        TICK(c_serial, s = serial_terms(sp, j * kSub, j * kSub + i1, s, lane));
+        ++n_subser;
+        TICK(c_rip, j = ripple_runw(rs, pu, qu, s, j + 1, kSubs, lane, n_rip));
+      }
+      ++f;
+    }
+  }
+#undef TICK
+  if (t < 64)
+    for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
+  if (stats && t == 0) {
+    stats[v * 8 + 0] = n_win;
+    stats[v * 8 + 1] = n_segdesc;
+    stats[v * 8 + 2] = n_rip;
+    stats[v * 8 + 3] = n_subser;
+    stats[v * 8 + 4] = stats[v * 8 + 5] = stats[v * 8 + 6] = stats[v * 8 + 7] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 0] = c_win;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 1] = c_rip;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 2] = c_serial;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 3] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 4] = wall_clock64() - c_all;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 5] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 6] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 7] = c_fill;
   }
 }
 
@@ -830,8 +1022,19 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
     const char* e = getenv("MSPLIT_SEQ_PREP");
     return e && e[0] == '0' ? 0 : 1;
   }();
-  k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
-                                                        stop, dstats, prep);
+  // MSPLIT_SEQ_WALK=scan: the walk of rounds 4-5 (wave scans of composed transducers and one-record applies) instead
+  // of the ripple walk; MSPLIT_SEQ_RIPPLE_W / MSPLIT_SEQ_RIPPLE: the ripple widths (4, 8, 16, 32) over segments and
+  // after a serially added sub.  Read per call (tests vary them); a getenv is nothing next to a walk.
+  const char* wk = getenv("MSPLIT_SEQ_WALK");
+  const char* rwe = getenv("MSPLIT_SEQ_RIPPLE_W");
+  const char* rse = getenv("MSPLIT_SEQ_RIPPLE");
+  const int rw = rwe ? atoi(rwe) : 16, rs = rse ? atoi(rse) : 8;
+  if (wk && wk[0] == 's')
+    k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
+                                                          stop, dstats, prep);
+  else
+    k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial,
+                                                             nchunks, stop, dstats, rw, rs);
   if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];
     if (hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
@@ -839,12 +1042,14 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
       for (int v = 0; v < nv; ++v)
         fprintf(stderr,
                 "seqx n=%lld nv=%d v=%d scans=%lld seg_desc=%lld single=%lld sub_serial=%lld f_bad=%lld f_state=%lld "
-                "f_guess=%lld f_range=%lld us_scan=%lld us_single=%lld us_serial=%lld us_wait=%lld us_all=%lld\n",
+                "f_guess=%lld f_range=%lld us_scan=%lld us_single=%lld us_serial=%lld us_wait=%lld us_all=%lld "
+                "us_win=%lld us_subld=%lld us_fill=%lld\n",
                 (long long)n, nv, v, (long long)h[8 * v], (long long)h[8 * v + 1], (long long)h[8 * v + 2],
                 (long long)h[8 * v + 3], (long long)h[8 * v + 4], (long long)h[8 * v + 5], (long long)h[8 * v + 6],
                 (long long)h[8 * v + 7], (long long)h[256 + 8 * v] / 100, (long long)h[256 + 8 * v + 1] / 100,
                 (long long)h[256 + 8 * v + 2] / 100, (long long)h[256 + 8 * v + 3] / 100,
-                (long long)h[256 + 8 * v + 4] / 100);
+                (long long)h[256 + 8 * v + 4] / 100, (long long)h[256 + 8 * v + 5] / 100,
+                (long long)h[256 + 8 * v + 6] / 100, (long long)h[256 + 8 * v + 7] / 100);
     (void)hipFree(dstats);
   }
   return (int)hipGetLastError();

@@ -264,3 +264,27 @@ def test_configs1_full_size_petsc_order_bitwise(sctx):
     assert (ksp.get_iteration_number(), ksp.get_converged_reason()) == (g["its"], g["reason"])
     assert [float(h).hex() for h in hist] == g["hist_hex"]
     assert hashlib.sha256(np.ascontiguousarray(x.get_array(), np.float64).tobytes()).hexdigest() == g["x_sha256"]
+
+
+# ------------------------------------------------- the SMSM per-GPU block in PETSc's order
+def test_smsm_block_petsc_order_golden(sctx):
+    """The N > 1 lines' per-GPU workload (one z-slab block, configs[2]'s options: s 20, inner GMRES(30) max_it 20,
+    LSQR max_it 70 exact norm) for one outer iteration in PETSc's reduction order, on the 48x48x32 block of
+    tests/golden/smsm_seq.json (tests/golden/make_smsm_seq.py): bit for bit the PETSc-order oracle record -- the
+    same check bench.py --seq-smsm makes before it times the full-size block in this mode."""
+    import hashlib
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "smsm_seq.json")))
+    P = g["problem"]
+    comm = LocalComm()
+    blocks, mini = make_smsm(sctx, P["dim"], P["nx"], P["ny"], P["nz"], P["nb"], range(P["nb"]), P["s"],
+                             _smsm_opts(P["nb"], g["inner"]["max_it"], g["inner"]["rtol"], P["s"]), comm)
+    res = smsm_solve(blocks, comm, P["s"], mini, rtol=P["rtol"], max_outer=P["outer_its"])
+    x = np.concatenate([blk.x.get_array() for blk in blocks])
+    mini.close()
+    assert res.outer_its == g["outer_its"] and float(res.norm0).hex() == g["norm0_hex"]
+    assert [float(h).hex() for h in res.hist] == g["hist_hex"]
+    assert [int(v) for v in res.lsqr_its] == g["lsqr_its"]
+    assert np.array(res.inner_its).tolist() == g["inner_its"]
+    assert hashlib.sha256(np.ascontiguousarray(x, np.float64).tobytes()).hexdigest() == g["x_sha256"]
