@@ -130,9 +130,9 @@ def parse():
     p.add_argument("--spmv-reps", type=int, default=20)
     p.add_argument("--no-seq-mode", action="store_true",
                    help="N=1: skip the seq_mode measurement (one configs[1] step in PETSc's reduction order)")
-    p.add_argument("--seq-smsm", action="store_true",
-                   help="N=1: also time one SMSM-global block outer iteration in PETSc's reduction order, verified "
-                        "first on tests/golden/smsm_seq.json's small block")
+    p.add_argument("--no-seq-smsm", action="store_true",
+                   help="N=1: skip the SMSM-global block outer iteration in PETSc's reduction order (verified first "
+                        "on tests/golden/smsm_seq.json's small block)")
     p.add_argument("--no-non-stencil", action="store_true",
                    help="N=1: skip the non_stencil_aij measurement (GMRES on a per-cell-coefficient AIJ in CSR "
                         "storage, default and fused MatMult+MDot steps)")
@@ -566,13 +566,14 @@ def seq_mode_step(ctx, ksp, b, x, ref):
         ctx.set_reduction("dbr")
     return {"reduction": "seq (PETSc's order: one running sum per dot/norm/MDot entry)",
             "engine": ("serial (one lane adds in order)" if os.environ.get("MSPLIT_SEQ_ENGINE", "")[:1] in ("s", "S")
-                       else "exact parallel (msplit_seq.hip: binade transducers in wave scans, f64 adds where the sum "
-                            "leaves its binade; sums below 2^19 terms take the serial engine)"),
+                       else "exact parallel (msplit_seq.hip: binade transducers of 64-term subs and 4096-term "
+                            "segments, applied in order as ripples through a wave, the f64 add where the sum leaves "
+                            "its binade; sums below 2^19 terms take the serial engine)"),
             "value": float(x.n) * its / dt, "unit": "DOF-updates/s", "seconds_per_step": dt,
             "gmres_iterations": its, "verified": ok, "mismatch": bad,
             "reference": "tests/golden/configs1_seq.json['seq'] (oracle/oracle.c ORC_REDUCE_SEQ)",
             "note": "the parity mode: identical iteration counts and bitwise PETSc-order histories, at this cost "
-                    "(47.97 s per step with the serial engine, round 3)"}
+                    "(47.97 s per step with the serial engine, round 3; 5.40 s with round 5's scan walk)"}
 
 
 SMSM_SEQ_GOLDEN = os.path.join(ROOT, "tests", "golden", "smsm_seq.json")
@@ -821,7 +822,7 @@ def main():
             extras["spmv_512_csr"] = spmv512(ctx, args)
         if not args.no_smsm_n1:
             extras["smsm_per_gpu"] = smsm_n1(ctx, args)
-        if args.seq_smsm:
+        if not args.no_seq_smsm:
             extras["smsm_seq_mode"] = smsm_seq_mode(ctx, args)
 
     if rank == 0:

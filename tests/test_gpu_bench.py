@@ -75,7 +75,7 @@ def test_single_gpu_line_is_verified():
     """N = 1: the timed GMRES step (configs[1]) equals the committed DBR oracle record -- iterations, reason, every
     history entry, SHA-256 of x -- and the line says verified: true; the CSR-storage rerun is verified too."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
-                        "--no-smsm-n1", "--no-spmv512", "--no-cpu-baseline", "--no-seq-mode"],
+                        "--no-smsm-n1", "--no-spmv512", "--no-cpu-baseline", "--no-seq-mode", "--no-seq-smsm"],
                        capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     out = _json(r.stdout)

@@ -271,7 +271,7 @@ def test_smsm_block_petsc_order_golden(sctx):
     """The N > 1 lines' per-GPU workload (one z-slab block, configs[2]'s options: s 20, inner GMRES(30) max_it 20,
     LSQR max_it 70 exact norm) for one outer iteration in PETSc's reduction order, on the 48x48x32 block of
     tests/golden/smsm_seq.json (tests/golden/make_smsm_seq.py): bit for bit the PETSc-order oracle record -- the
-    same check bench.py --seq-smsm makes before it times the full-size block in this mode."""
+    same check bench.py's smsm_seq_mode line makes before it times the full-size block in this mode."""
     import hashlib
     import json
     import os

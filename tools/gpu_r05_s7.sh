@@ -17,5 +17,5 @@ for r in 0 8 4 16 8; do
   step seq_r$r 200 env MSPLIT_SEQ_RIPPLE=$r python bench.py $SQ
 done
 step seq_stats 200 env MSPLIT_SEQ_STATS=1 python bench.py $SQ
-step seq_smsm 400 python bench.py $SQ --no-seq-mode --seq-smsm
+step seq_smsm 400 python bench.py $SQ --no-seq-mode
 echo done >> $OUT/status

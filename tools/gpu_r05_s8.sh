@@ -19,5 +19,5 @@ for c in "16 8" "8 8" "32 8" "16 4" "16 16"; do
   step seq_w$1_s$2 200 env MSPLIT_SEQ_RIPPLE_W=$1 MSPLIT_SEQ_RIPPLE=$2 python bench.py $SQ
 done
 step seq_stats 200 env MSPLIT_SEQ_STATS=1 python bench.py $SQ
-step seq_smsm 400 python bench.py $SQ --no-seq-mode --seq-smsm
+step seq_smsm 400 python bench.py $SQ --no-seq-mode
 echo done >> $OUT/status
