@@ -46,17 +46,20 @@
 //   2. k_seqx_trans: per 64-term sub-segment the transducer in the binade its
 //      guessed start lies in (integer arithmetic on the terms' bits, exact),
 //      and per segment their composition (BAD where the subs disagree);
-//   3. k_seqx_walk, one wave per sum: from s = +0.0, apply up to 64 segment
-//      transducers at once (an ordered wave scan, checked against the actual
-//      M: LO/HI bound the whole run); where a segment does not apply, its sub
-//      transducers; where a sub does not apply, its terms, 64 at a time
-//      (integer prefix of inc, the same checks), and the one term that leaves
-//      the binade, ties, zeros, subnormals and non-finite values by the f64
-//      add itself.
+//   3. k_seqx_ripwalk, one workgroup per sum (round 5): from s = +0.0, the
+//      maps of a window of 64 segments applied in order as a ripple through
+//      the wave (lane j adds its map's offset to lane j-1's previous result,
+//      DPP wave_shr:1, one verdict per lane at the end), up to the first that
+//      does not apply at the actual s; that segment's 64 sub maps likewise;
+//      a sub that does not apply is added term by term by the f64 add (the
+//      one term that leaves the binade, ties, zeros, subnormals and
+//      non-finite values included), and the ripple resumes after it.
+//      k_seqx_walk (MSPLIT_SEQ_WALK=scan, rounds 4-5) composes the window's
+//      maps in a wave scan and applies subs one record at a time instead.
 // Every step either is the f64 add or provably equals it, so the result is the
 // sequential sum bit for bit whatever the guesses were; the guesses only
-// decide how often the walk descends.  GMRES's dots at 256^3 leave their
-// binade in at most a few hundred of 4096 segments.
+// decide how often the walk descends.  GMRES's dots at 256^3 descend into at
+// most a few hundred of 4096 segments, and add ~1400 of 262144 subs serially.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
