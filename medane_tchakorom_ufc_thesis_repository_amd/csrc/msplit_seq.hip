@@ -899,7 +899,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
                                                          int64_t K, const double* __restrict__ acc_in,
                                                          double* __restrict__ partial, int64_t nchunks,
                                                          const int* __restrict__ stop, int64_t* __restrict__ stats,
-                                                         int rw, int rs) {
+                                                         int rw, int rs, int pf) {
   if (stopped(stop)) return;
   __shared__ double sp[kSeg];
   const int v = blockIdx.x, t = threadIdx.x, lane = t & 63;
@@ -913,29 +913,59 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
     stmt;                                           \
     if (stats) acc += wall_clock64() - t0_;         \
   } while (0)
+  // pf: the next segment the walk will descend into is predicted -- a BAD segment map never applies, so the walk
+  // stops at every one -- and its terms and sub record are loaded while the walk works on the segments before it
+  // (fp / tp hold segment kp; a descent into any other segment loads its own into them).  The next window's segment
+  // records are likewise loaded one window ahead.
+  Fill fp;
+  Tr tp = tr_bad();
+  int64_t kp = -1;
+  int64_t n_hit = 0, n_miss = 0;
   double s = acc_in ? acc_in[v] : 0.0;
+  Tr twn = tr_load(segT + (int64_t)v * K + min<int64_t>(lane, K - 1));
   for (int64_t kb = 0; kb < K; kb += 64) {
     const int lim = (int)min<int64_t>(64, K - kb);
     const bool in = lane < lim;
-    const Tr tw = tr_load(segT + (int64_t)v * K + (in ? kb + lane : 0));
+    const Tr tw = twn;
+    if (kb + 64 < K) twn = tr_load(segT + (int64_t)v * K + min<int64_t>(kb + 64 + lane, K - 1));
     const Prep pv = prep_of(tr_sel(in, tw, tr_bad()));
     const Rip qv = rip_of(pv);
+    const uint64_t badm = __ballot(in && (pv.fl & F_BAD) != 0);  // the window's segments the walk must descend into
+    if (pf && kp < kb && badm) {
+      kp = kb + __builtin_ctzll(badm);
+      fill_load(fp, w, y, n, kp);
+      tp = tr_load(subT + ((int64_t)v * K + kp) * kSubs + lane);
+    }
     for (int f = 0;;) {
       TICK(c_win, f = ripple_runw(rw, pv, qv, s, f, lim, lane, n_win));
       if (f >= lim) break;
       const int64_t k = kb + f;  // segment k does not apply at s: its sub maps
       ++n_segdesc;
       const int64_t tf0 = stats ? wall_clock64() : 0;
-      Fill fl;
-      fill_load(fl, w, y, n, k);
-      const Prep pu = prep_of(tr_load(subT + ((int64_t)v * K + k) * kSubs + lane));
+      if (k != kp) {  // not the predicted one (a map that only fails at the actual s): load it now
+        fill_load(fp, w, y, n, k);
+        tp = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
+        kp = k;
+        ++n_miss;
+      } else {
+        ++n_hit;
+      }
+      const Prep pu = prep_of(tp);
       const Rip qu = rip_of(pu);
       int j;
       TICK(c_rip, j = ripple_runw(rw, pu, qu, s, 0, kSubs, lane, n_rip));
       if (j < kSubs) {
         __syncthreads();  // the previous segment's LDS reads are done
-        fill_store(fl, sp, self != 0, sy, n, k);
+        fill_store(fp, sp, self != 0, sy, n, k);
         __syncthreads();
+      }
+      if (pf) {  // the next BAD segment of this window, while this one's subs are walked
+        const uint64_t m = f < 63 ? badm & (~uint64_t(0) << (f + 1)) : 0;
+        if (m) {
+          kp = kb + __builtin_ctzll(m);
+          fill_load(fp, w, y, n, kp);
+          tp = tr_load(subT + ((int64_t)v * K + kp) * kSubs + lane);
+        }
       }
       if (stats) c_fill += wall_clock64() - tf0;
       while (j < kSubs) {
@@ -956,7 +986,9 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
     stats[v * 8 + 1] = n_segdesc;
     stats[v * 8 + 2] = n_rip;
     stats[v * 8 + 3] = n_subser;
-    stats[v * 8 + 4] = stats[v * 8 + 5] = stats[v * 8 + 6] = stats[v * 8 + 7] = 0;
+    stats[v * 8 + 4] = n_hit;
+    stats[v * 8 + 5] = n_miss;
+    stats[v * 8 + 6] = stats[v * 8 + 7] = 0;
     stats[8 * MSK_MAX_GROUP + v * 8 + 0] = c_win;
     stats[8 * MSK_MAX_GROUP + v * 8 + 1] = c_rip;
     stats[8 * MSK_MAX_GROUP + v * 8 + 2] = c_serial;
@@ -1031,20 +1063,25 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
   const char* wk = getenv("MSPLIT_SEQ_WALK");
   const char* rwe = getenv("MSPLIT_SEQ_RIPPLE_W");
   const char* rse = getenv("MSPLIT_SEQ_RIPPLE");
-  const int rw = rwe ? atoi(rwe) : 16, rs = rse ? atoi(rse) : 8;
-  if (wk && wk[0] == 's')
+  const char* pfe = getenv("MSPLIT_SEQ_PREFETCH");  // 0: a descended segment's loads start at the descent
+  const int rw = rwe ? atoi(rwe) : 16, rs = rse ? atoi(rse) : 8, pf = pfe && pfe[0] == '0' ? 0 : 1;
+  const bool ripwalk = !(wk && wk[0] == 's');
+  if (!ripwalk)
     k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
                                                           stop, dstats, prep);
   else
     k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial,
-                                                             nchunks, stop, dstats, rw, rs);
+                                                             nchunks, stop, dstats, rw, rs, pf);
   if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];
     if (hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
         hipStreamSynchronize(c->stream) == hipSuccess)
       for (int v = 0; v < nv; ++v)
         fprintf(stderr,
-                "seqx n=%lld nv=%d v=%d scans=%lld seg_desc=%lld single=%lld sub_serial=%lld f_bad=%lld f_state=%lld "
+                ripwalk ? "seqx n=%lld nv=%d v=%d win_rip=%lld seg_desc=%lld sub_rip=%lld sub_serial=%lld pf_hit=%lld "
+                          "pf_miss=%lld f_guess=%lld f_range=%lld us_scan=%lld us_single=%lld us_serial=%lld us_wait=%lld "
+                          "us_all=%lld us_win=%lld us_subld=%lld us_fill=%lld\n"
+                        : "seqx n=%lld nv=%d v=%d scans=%lld seg_desc=%lld single=%lld sub_serial=%lld f_bad=%lld f_state=%lld "
                 "f_guess=%lld f_range=%lld us_scan=%lld us_single=%lld us_serial=%lld us_wait=%lld us_all=%lld "
                 "us_win=%lld us_subld=%lld us_fill=%lld\n",
                 (long long)n, nv, v, (long long)h[8 * v], (long long)h[8 * v + 1], (long long)h[8 * v + 2],

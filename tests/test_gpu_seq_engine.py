@@ -199,19 +199,20 @@ RIPPLE_CASES = ["ties_even_start", "ties_odd_start", "random_walk_1M", "cancel_t
                 "dyadic_up_down", "sparse_zeros", "huge_range", "large_in_and_out", "all_neg_zero", "nan_last"]
 
 
-WALKS = [("scan", "16", "8"), ("ripple", "4", "4"), ("ripple", "8", "8"), ("ripple", "16", "8"),
-         ("ripple", "32", "32"), ("ripple", "16", "4")]
+WALKS = [("scan", "16", "8", "1"), ("ripple", "4", "4", "1"), ("ripple", "8", "8", "1"), ("ripple", "16", "8", "1"),
+         ("ripple", "32", "32", "1"), ("ripple", "16", "4", "1"), ("ripple", "16", "8", "0")]
 
 
-@pytest.mark.parametrize("walk,rw,rs", WALKS)
+@pytest.mark.parametrize("walk,rw,rs,pf", WALKS)
 @pytest.mark.parametrize("name", RIPPLE_CASES)
-def test_seq_engine_walks(sctx, oracle, monkeypatch, name, walk, rw, rs):
+def test_seq_engine_walks(sctx, oracle, monkeypatch, name, walk, rw, rs, pf):
     """Both walks give the sequential sum bit for bit: the scan walk of rounds 4-5 (MSPLIT_SEQ_WALK=scan) and the
     ripple walk at every width over segments (MSPLIT_SEQ_RIPPLE_W) and after a serially added sub
-    (MSPLIT_SEQ_RIPPLE)."""
+    (MSPLIT_SEQ_RIPPLE), with and without the predicted segments' early loads (MSPLIT_SEQ_PREFETCH)."""
     monkeypatch.setenv("MSPLIT_SEQ_WALK", walk)
     monkeypatch.setenv("MSPLIT_SEQ_RIPPLE_W", rw)
     monkeypatch.setenv("MSPLIT_SEQ_RIPPLE", rs)
+    monkeypatch.setenv("MSPLIT_SEQ_PREFETCH", pf)
     x, y = CASES[name]
     _check_dot(sctx, oracle, x, y)
     _check_norm(sctx, oracle, x)
