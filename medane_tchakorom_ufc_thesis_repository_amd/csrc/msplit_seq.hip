@@ -837,30 +837,34 @@ __device__ __forceinline__ bool prep_valid(const Prep& p, double s) {
   return (p.fl & F_ZERO) != 0 || (a >= L && a < H && neg == ((p.fl & F_NEG) != 0));
 }
 
-// lane l gets lane l - 1's x; lane 0 gets s (DPP wave_shr:1 over the 64 lanes, lane 0's "old" operand)
-__device__ __forceinline__ double shr1_from(double x, double s) {
-  const int64_t b = __double_as_longlong(x), o = __double_as_longlong(s);
-  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x138, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x138, 0xf, 0xf, false);
+// lane l gets lane l - 1's x; lane 0 keeps its own (the same DPP move with x as the "old" operand: no copy of s)
+__device__ __forceinline__ double shr1_own(double x) {
+  const int64_t b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), 0x138, 0xf, 0xf, false);
   return __longlong_as_double((int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
 }
 
 // The lanes' maps j0, j0 + 1, .. applied in order from s, R steps of a ripple through the wave: each step every lane
-// adds its SD to its left neighbour's previous result (lanes below j0 are the identity, lane 0 reads s), so after
-// step i lanes j0 .. j0 + i hold the sequential results wherever every map before theirs applied -- one f64 add, a
-// parity select and two DPP moves a step.  Then one verdict per lane at its final input: returns the first lane in
-// [j0, j0 + r) whose map does not apply at its true input (j0 + r if all do), s advanced to that lane's input.
-template <int R>
+// adds its SD to its left neighbour's previous result (lanes below j0 are the identity), so after step i lanes j0 ..
+// j0 + i hold the sequential results wherever every map before theirs applied -- one f64 add and two DPP moves a
+// step (wave_shr:1, lane 0 keeping its own value), plus a parity select where a map holds a tie (TIES).  Lane 0 has
+// no left neighbour: below j0 it is an identity lane holding s; as map j0 = 0 (J0) it reads s at step 0 and then
+// turns into the identity, holding its result.  Then one verdict per lane at its true input: returns the first lane
+// in [j0, j0 + r) whose map does not apply (j0 + r if all do), s advanced to that lane's input.
+template <int R, bool TIES, bool J0>
 __device__ __forceinline__ int ripple(const Prep& p, const Rip& q, double& s, int j0, int r, int lane) {
-  const bool idn = lane < j0;
-  const double sd0 = idn ? -0.0 : q.sd0, sd1 = idn ? -0.0 : q.sd1;
-  double in = s, out = s;
+  const bool idn = lane < j0, frz = J0 && lane == 0;
+  const double a0 = idn ? -0.0 : q.sd0, a1 = idn ? -0.0 : q.sd1;  // step 0
+  const double b0 = frz ? -0.0 : a0, b1 = frz ? -0.0 : a1;        // steps 1 ..
+  double in = s;
+  double out = in + (TIES ? pickd(((uint32_t)__double_as_longlong(in) & 1u) != 0, a1, a0) : a0);
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    if (i) in = shr1_from(out, s);
-    out = in + pickd(((uint32_t)__double_as_longlong(in) & 1u) != 0, sd1, sd0);
+  for (int i = 1; i < R; ++i) {
+    in = shr1_own(out);
+    out = in + (TIES ? pickd(((uint32_t)__double_as_longlong(in) & 1u) != 0, b1, b0) : b0);
   }
-  const bool ok = idn || prep_valid(p, in);
+  const bool ok = idn || prep_valid(p, frz ? s : in);
   const uint64_t bad = __ballot(!ok) & (~uint64_t(0) << j0);
   const int f = min(bad ? __builtin_ctzll(bad) : 64, j0 + r);
   if (f > j0) s = rld(out, f - 1);
@@ -868,26 +872,37 @@ __device__ __forceinline__ int ripple(const Prep& p, const Rip& q, double& s, in
 }
 
 // The maps from lane j on, ripple after ripple, up to the first that does not apply or lim; returns its lane.
-template <int R>
-__device__ __forceinline__ int ripple_run(const Prep& p, const Rip& q, double& s, int j, int lim, int lane,
-                                          int64_t& calls) {
+// ties: some lane's map depends on the state's parity (sd0 != sd1), wave-uniform.
+template <int R, bool TIES>
+__device__ __forceinline__ int ripple_run_t(const Prep& p, const Rip& q, double& s, int j, int lim, int lane,
+                                            int64_t& calls) {
   while (j < lim) {
     const int r = min(R, lim - j);
-    const int f = ripple<R>(p, q, s, j, r, lane);
+    const int f = j == 0 ? ripple<R, TIES, true>(p, q, s, j, r, lane) : ripple<R, TIES, false>(p, q, s, j, r, lane);
     ++calls;
     if (f < j + r) return f;
     j = f;
   }
   return lim;
 }
-__device__ __forceinline__ int ripple_runw(int w, const Prep& p, const Rip& q, double& s, int j, int lim, int lane,
-                                           int64_t& calls) {
+template <int R>
+__device__ __forceinline__ int ripple_run(const Prep& p, const Rip& q, bool ties, double& s, int j, int lim, int lane,
+                                          int64_t& calls) {
+  return ties ? ripple_run_t<R, true>(p, q, s, j, lim, lane, calls)
+              : ripple_run_t<R, false>(p, q, s, j, lim, lane, calls);
+}
+__device__ __forceinline__ int ripple_runw(int w, const Prep& p, const Rip& q, bool ties, double& s, int j, int lim,
+                                           int lane, int64_t& calls) {
   switch (w) {
-    case 4: return ripple_run<4>(p, q, s, j, lim, lane, calls);
-    case 8: return ripple_run<8>(p, q, s, j, lim, lane, calls);
-    case 32: return ripple_run<32>(p, q, s, j, lim, lane, calls);
-    default: return ripple_run<16>(p, q, s, j, lim, lane, calls);
+    case 4: return ripple_run<4>(p, q, ties, s, j, lim, lane, calls);
+    case 8: return ripple_run<8>(p, q, ties, s, j, lim, lane, calls);
+    case 32: return ripple_run<32>(p, q, ties, s, j, lim, lane, calls);
+    default: return ripple_run<16>(p, q, ties, s, j, lim, lane, calls);
   }
+}
+// some lane's map of this set depends on the parity of the state (a tie in its run)
+__device__ __forceinline__ bool any_ties(const Rip& q) {
+  return __ballot(__double_as_longlong(q.sd0) != __double_as_longlong(q.sd1)) != 0;
 }
 
 // Workgroup v: sum v, from +0.0, every map applied by ripples: the window of 64 segment maps up to the first that
@@ -930,6 +945,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
     if (kb + 64 < K) twn = tr_load(segT + (int64_t)v * K + min<int64_t>(kb + 64 + lane, K - 1));
     const Prep pv = prep_of(tr_sel(in, tw, tr_bad()));
     const Rip qv = rip_of(pv);
+    const bool tv = any_ties(qv);
     const uint64_t badm = __ballot(in && (pv.fl & F_BAD) != 0);  // the window's segments the walk must descend into
     if (pf && kp < kb && badm) {
       kp = kb + __builtin_ctzll(badm);
@@ -937,7 +953,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
       tp = tr_load(subT + ((int64_t)v * K + kp) * kSubs + lane);
     }
     for (int f = 0;;) {
-      TICK(c_win, f = ripple_runw(rw, pv, qv, s, f, lim, lane, n_win));
+      TICK(c_win, f = ripple_runw(rw, pv, qv, tv, s, f, lim, lane, n_win));
       if (f >= lim) break;
       const int64_t k = kb + f;  // segment k does not apply at s: its sub maps
       ++n_segdesc;
@@ -952,8 +968,9 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
       }
       const Prep pu = prep_of(tp);
       const Rip qu = rip_of(pu);
+      const bool tu = any_ties(qu);
       int j;
-      TICK(c_rip, j = ripple_runw(rw, pu, qu, s, 0, kSubs, lane, n_rip));
+      TICK(c_rip, j = ripple_runw(rw, pu, qu, tu, s, 0, kSubs, lane, n_rip));
       if (j < kSubs) {
         __syncthreads();  // the previous segment's LDS reads are done
         fill_store(fp, sp, self != 0, sy, n, k);
@@ -973,7 +990,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
         const int i1 = (int)max<int64_t>(0, min<int64_t>(kSub, n - c0));
         TICK(c_serial, s = serial_terms(sp, j * kSub, j * kSub + i1, s, lane));
         ++n_subser;
-        TICK(c_rip, j = ripple_runw(rs, pu, qu, s, j + 1, kSubs, lane, n_rip));
+        TICK(c_rip, j = ripple_runw(rs, pu, qu, tu, s, j + 1, kSubs, lane, n_rip));
       }
       ++f;
     }
