@@ -25,7 +25,8 @@ INNER = dict(restart=30, max_it=20, rtol=1e-20, abstol=1e-100)
 OUTER = dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0)
 
 
-def main():
+def record():
+    """The record, computed now (tests/test_oracle.py checks the committed file against it)."""
     po.build()
     P = PROBLEM
     t0 = time.time()
@@ -39,6 +40,11 @@ def main():
            "hist_hex": [float(h).hex() for h in r["hist"]], "lsqr_its": [int(v) for v in r["lsqr_its"]],
            "inner_its": r["inner_its"].tolist(), "x_sha256": hashlib.sha256(x.tobytes()).hexdigest(),
            "seconds": round(time.time() - t0, 1)}
+    return out
+
+
+def main():
+    out = record()
     json.dump(out, open(os.path.join(HERE, "smsm_seq.json"), "w"), indent=1)
     print(out["outer_its"], out["lsqr_its"], [float.fromhex(h) for h in out["hist_hex"]], out["seconds"])
 

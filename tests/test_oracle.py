@@ -263,3 +263,19 @@ def test_configs2_record_matches_oracle(oracle):
     want.pop("seconds")
     assert got == want
     assert rec["cubes"]["256"]["outer_its"] == 4 and all(r == -3 for r in rec["cubes"]["256"]["lsqr_reason"])
+
+
+def test_smsm_seq_record_matches_oracle(oracle):
+    """tests/golden/smsm_seq.json (bench.py's smsm_seq_mode check and tests/test_gpu_seq.py's PETSc-order SMSM block)
+    is what the PETSc-order oracle computes now."""
+    import importlib.util
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_smsm_seq", os.path.join(here, "golden", "make_smsm_seq.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    rec = json.load(open(os.path.join(here, "golden", "smsm_seq.json")))
+    got = gen.record()
+    got.pop("seconds")
+    rec.pop("seconds")
+    assert got == rec
+    assert rec["lsqr_its"] == [70] and len(rec["inner_its"][0]) == rec["problem"]["s"]
