@@ -479,17 +479,27 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
     const int64_t g = c0 + t + i * kT;
     xr[i] = g < n ? w[g] : 0.0;
   }
+  // sum v's y values, loaded one sum ahead (their round trip overlaps sum v - 1's transducers)
+  double yr[kPer], yn[kPer];
+  auto load_y = [&](double (&dst)[kPer], int v) {
+    const double* y = vec_row(V, v);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) dst[i] = y[min<int64_t>(c0 + t + i * kT, n - 1)];
+  };
+  if (!self) load_y(yr, 0);
   for (int v = 0; v < nv; ++v) {
-    const double* y = self ? nullptr : vec_row(V, v);
+    if (!self && v + 1 < nv) load_y(yn, v + 1);
     const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int64_t g = c0 + t + i * kT;
       const int l = t + i * kT;
       double p = 0.0;
-      if (g < n) p = y ? xr[i] * (y[g] * sy) : xr[i] * xr[i];
+      if (g < n) p = self ? xr[i] * xr[i] : xr[i] * (yr[i] * sy);
       sp[l + l / kPer] = p;
     }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) yr[i] = yn[i];
     __syncthreads();
     double pr[kPer];
     double ps = 0.0;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 GPU session 12: the STENCIL storage's fused step with its MDot in software-pipelined vector groups
 # (MSPLIT_RV_DOTPIPE = 2 / 4): the STENCIL parity tests, then an interleaved A/B of bench.py's non_stencil_aij line,
-# and a kernel-trace profile of each variant.
+# and a kernel-trace profile of each variant; then the SEQ parity suites and two seq_mode steps (trans prefetch).
 OUT=gpurun_out/${1:-r05_s12}
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -24,4 +24,9 @@ for d in 0 2 4; do
   step trace_dp$d 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace_dp$d -o run -f csv -- python3 bench.py $NS
 done
 unset MSPLIT_RV_DOTPIPE
+# the SEQ transducer build with the next sum's y loaded one sum ahead
+step seq_tests 600 python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_seq_engine.py tests/test_gpu_seq.py
+SQ="--steps 1 --warmup 0 --no-cpu-baseline --no-csr-compare --no-smsm-n1 --no-spmv512 --no-assembled --no-non-stencil --no-seq-smsm"
+step seq1 200 python bench.py $SQ
+step seq2 200 python bench.py $SQ
 echo done >> $OUT/status
