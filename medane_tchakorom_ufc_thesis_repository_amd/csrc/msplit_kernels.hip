@@ -175,68 +175,6 @@ __device__ __forceinline__ void dot_group_full(const double (&wr)[2 * kIters], c
   }
 }
 
-// dot_group_full in two halves: the loads, and the products and butterflies
-template <int G, int VAR>
-__device__ __forceinline__ void dot_group_load(double2 (&q)[G][kIters], const Vecs& V, int64_t base, int g) {
-#pragma unroll
-  for (int u = 0; u < G; ++u) {
-    const double* __restrict__ y = vec_at(V, g + u);
-#pragma unroll
-    for (int j = 0; j < kIters; ++j) {
-      const double2* pq = reinterpret_cast<const double2*>(y + base + j * (2 * kT));
-      q[u][j] = (VAR & 1) ? ld_nt(pq) : *pq;
-    }
-  }
-}
-template <int G>
-__device__ __forceinline__ void dot_group_sum(const double2 (&q)[G][kIters], const double (&wr)[2 * kIters],
-                                              const Vecs& V, int g, double (*red)[4], int lane, int wv) {
-  double acc[G];
-#pragma unroll
-  for (int u = 0; u < G; ++u) {
-    const double sv = vec_scale(V, g + u);
-    acc[u] = 0.0;
-#pragma unroll
-    for (int j = 0; j < kIters; ++j) {
-      acc[u] = acc[u] + wr[2 * j] * (q[u][j].x * sv);
-      acc[u] = acc[u] + wr[2 * j + 1] * (q[u][j].y * sv);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < G; ++u) {
-    acc[u] = wave_butterfly(acc[u]);
-    if (lane == 0) red[g + u][wv] = acc[u];
-  }
-}
-// Vectors 0 .. nvm - 1 in groups of G, software-pipelined: the next group's loads are issued before this group's
-// products and butterflies (for the kernels that run one workgroup per CU, whose single wave per SIMD would
-// otherwise wait out every group's round trip); the remainder as dot_group_full.  Same sums as dot_group_full.
-template <int G, int VAR>
-__device__ __forceinline__ void dot_groups_pipe(const double (&wr)[2 * kIters], const Vecs& V, int64_t base, int nvm,
-                                                int nv, double (*red)[4], int lane, int wv) {
-  const int ng = nvm / G;
-  double2 qa[G][kIters], qb[G][kIters];
-  if (ng > 0) dot_group_load<G, VAR>(qa, V, base, 0);
-#pragma unroll 1
-  for (int k = 0; k < ng; k += 2) {
-    if (k + 1 < ng) dot_group_load<G, VAR>(qb, V, base, (k + 1) * G);
-    dot_group_sum<G>(qa, wr, V, k * G, red, lane, wv);
-    if (k + 2 < ng) dot_group_load<G, VAR>(qa, V, base, (k + 2) * G);
-    if (k + 1 < ng) dot_group_sum<G>(qb, wr, V, (k + 1) * G, red, lane, wv);
-  }
-  const int g = ng * G;
-  if constexpr (G == 4) {
-    switch (nvm - g) {
-      case 3: dot_group_full<3, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
-      case 2: dot_group_full<2, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
-      case 1: dot_group_full<1, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
-      default: break;
-    }
-  } else {
-    if (nvm - g == 1) dot_group_full<1, VAR>(wr, V, base, 0, nv, g, red, lane, wv);
-  }
-}
-
 // Stage 1: workgroup c reduces chunk c of every vector: lane t accumulates its
 // elements base + j*512 + 2t, +1 (j = 0..7) in order, wave butterfly, then
 // (w0 + w1) + (w2 + w3).  partial[v * nchunks + c].  w stays in registers and
@@ -1945,7 +1883,7 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot(int32_t nx, int64_t P, int
 // recomputing it in the MAXPY would re-read the 56 value bytes per row to save W's 16.
 // RVP (RV only): the row pairs j < RVP have their values issued with x(z+1), before the LDS turn-around; the
 // others right before their W rows (fewer registers held across the barriers; MSPLIT_RV_PREFETCH, the A/B).
-template <int VAR, bool NTY, int RV, int RVP = kIters, int DP = 0>
+template <int VAR, bool NTY, int RV, int RVP = kIters>
 __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t P, int32_t nz, int32_t zt, int xcd,
                                                             const uint8_t* __restrict__ mask,
                                                             const double* __restrict__ dval,
@@ -2090,18 +2028,14 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
     // self: the last basis vector is x itself, whose rows of this plane the lane holds in xc at exactly
     // its DBR positions: that dot is taken from the registers (8n bytes fewer), the same sum term for term
     const int nvm = nv - self;
-    if constexpr (DP > 0) {
-      dot_groups_pipe<DP, VAR>(wr, V, base, nvm, nv, red, lane, wv);
-    } else {
-      int g = 0;
+    int g = 0;
 #pragma unroll 1
-      for (; g + 4 <= nvm; g += 4) dot_group_full<4, VAR>(wr, V, base, 0, nv, g, red, lane, wv);
-      switch (nvm - g) {
-        case 3: dot_group_full<3, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
-        case 2: dot_group_full<2, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
-        case 1: dot_group_full<1, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
-        default: break;
-      }
+    for (; g + 4 <= nvm; g += 4) dot_group_full<4, VAR>(wr, V, base, 0, nv, g, red, lane, wv);
+    switch (nvm - g) {
+      case 3: dot_group_full<3, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 2: dot_group_full<2, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      case 1: dot_group_full<1, VAR>(wr, V, base, 0, nv, g, red, lane, wv); break;
+      default: break;
     }
     if (self) {
       const double sv = vec_scale(V, nv - 1);
@@ -3296,19 +3230,10 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
       const int v = e ? atoi(e) : kIters;
       return v == 4 || v == 2 ? v : kIters;
     }();
-    // MSPLIT_RV_DOTPIPE = 2 / 4: the STENCIL storage's kernels (one workgroup a CU) take the MDot in software-
-    // pipelined groups of 2 / 4 vectors (read per call: an A/B and the tests)
-    const char* dpe = getenv("MSPLIT_RV_DOTPIPE");
-    const int dpv = dpe ? atoi(dpe) : 0, dp = rv ? (dpv == 2 || dpv == 4 ? dpv : 0) : 0;
-#define MSK_BSMM_PD(VAR_, NT_, RV_, P_, D_)                                                                       \
-  k_box_spmv_mdot_march<VAR_, NT_, RV_, P_, D_><<<dim3((unsigned)grid), b, lds, s>>>(                            \
-      nx, P, nz, zt, xcd, mask, dval, rv, rvs, x, sdev, y, *V, nv, self, partial, nchunks, stop)
-#define MSK_BSMM_P(VAR_, NT_, RV_, P_)                                         \
-  do {                                                                         \
-    if (RV_ && dp == 2) MSK_BSMM_PD(VAR_, NT_, RV_, P_, (RV_ && P_ == kIters ? 2 : 0));        \
-    else if (RV_ && dp == 4) MSK_BSMM_PD(VAR_, NT_, RV_, P_, (RV_ && P_ == kIters ? 4 : 0));   \
-    else MSK_BSMM_PD(VAR_, NT_, RV_, P_, 0);                                   \
-  } while (0)
+#define MSK_BSMM_P(VAR_, NT_, RV_, P_)                                                                          \
+  k_box_spmv_mdot_march<VAR_, NT_, RV_, P_><<<dim3((unsigned)grid), b, lds, s>>>(nx, P, nz, zt, xcd, mask, dval, rv, \
+                                                                                 rvs, x, sdev, y, *V, nv, self,     \
+                                                                                 partial, nchunks, stop)
 #define MSK_BSMM(VAR_, NT_, RV_)                                                                              \
   do {                                                                                                        \
     if (RV_ == 1 && rvp == 4) MSK_BSMM_P(VAR_, NT_, RV_, 4);                                                  \
@@ -3327,7 +3252,6 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
     }
 #undef MSK_BSMM
 #undef MSK_BSMM_P
-#undef MSK_BSMM_PD
     return (int)hipGetLastError();
   }
 #define MSK_BSM(D, VAR_, NT_) \
