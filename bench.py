@@ -568,7 +568,7 @@ def seq_mode_step(ctx, ksp, b, x, ref):
             "engine": ("serial (one lane adds in order)" if os.environ.get("MSPLIT_SEQ_ENGINE", "")[:1] in ("s", "S")
                        else "exact parallel (msplit_seq.hip: binade transducers of 64-term subs and 4096-term "
                             "segments, applied in order as ripples through a wave, the f64 add where the sum leaves "
-                            "its binade; sums below 2^19 terms take the serial engine)"),
+                            "its binade; short sums take the serial engine: norms below 2^13 terms, dots 2^17, MDots 2^19)"),
             "value": float(x.n) * its / dt, "unit": "DOF-updates/s", "seconds_per_step": dt,
             "gmres_iterations": its, "verified": ok, "mismatch": bad,
             "reference": "tests/golden/configs1_seq.json['seq'] (oracle/oracle.c ORC_REDUCE_SEQ)",

@@ -1040,15 +1040,21 @@ extern "C" int mspi_reduce_seq(const msp_ctx* c) { return c->reduce == MSP_REDUC
 
 // Which engine takes a PETSc-order sum of n terms: MSPLIT_SEQ_ENGINE=serial / parallel forces one, else the parallel
 // engine from min_n terms on.  Below that its four launches and the per-segment transducers cost more than the
-// serial adds save (profiles/r04/seq/crossover.jsonl: a dot is 59 us parallel against 22 us serial at n = 1024, and
-// the engines meet between 65 K and 1 M terms, depending on how often the sum changes binade).
+// serial adds save (a dot is 53 us parallel against 23 us serial at n = 1024), and where the engines meet depends on
+// how often the sum changes binade (below).
 static bool parallel_engine(int64_t n, int64_t min_n) {
   const char* eng = getenv("MSPLIT_SEQ_ENGINE");
   if (eng && (eng[0] == 's' || eng[0] == 'S')) return false;
   if (eng && (eng[0] == 'p' || eng[0] == 'P')) return n > 0;
   return n >= min_n;
 }
-constexpr int64_t kParMinSum = int64_t(1) << 19;    // one dot / norm / MDot
+// profiles/r05/seq_crossover/ (tools/seq_crossover.py, random data: the hardest sums): a norm's running sum only grows,
+// so it leaves its binade log2(n) times and the parallel engine wins from 8 K terms (65 K: 73 against 315 us); a
+// random dot hovers near zero and wins from ~100 K; an MDot of 30 random sums costs its slowest walk, about the
+// serial time up to 1 M.
+constexpr int64_t kParMinNorm = int64_t(1) << 13;   // a norm (sum of squares)
+constexpr int64_t kParMinDot = int64_t(1) << 17;    // one dot
+constexpr int64_t kParMinSum = int64_t(1) << 19;    // an MDot
 constexpr int64_t kParMinChain = int64_t(1) << 17;  // an LSQR chain: its total length per sum
 
 // The parallel engine: nv sums of n terms w[i] * (V_v[i] * sy_v) (self: w[i] * w[i]), each from acc_in[v] (device;
@@ -1125,7 +1131,8 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
 // MSP_REDUCE_SEQ's stage 1: the exact parallel engine, or the serial one (parallel_engine decides).
 int mspi_seq_stage1(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial,
                     int64_t nchunks, const int* stop) {
-  if (!parallel_engine(n, kParMinSum)) return msk_seq_stage1(w, V, nv, n, self, partial, nchunks, stop, c->stream);
+  if (!parallel_engine(n, self ? kParMinNorm : nv == 1 ? kParMinDot : kParMinSum))
+    return msk_seq_stage1(w, V, nv, n, self, partial, nchunks, stop, c->stream);
   return seqx_core(c, w, V, nv, n, self, nullptr, partial, nchunks, stop);
 }
 
