@@ -461,6 +461,129 @@ __global__ __launch_bounds__(kT) void k_seqx_prefix(double* __restrict__ a, int6
   }
 }
 
+// One segment's transducers for one sum, from its products the caller has staged in sp (thread t's term i at l + l/16,
+// l = t + 256 i) and g0, the guessed sum at the segment's start: thread t's run of 16 terms, four threads to a
+// sub-segment (sub_out[0..63]), the waves' trees and thread 0's composition to the segment (*seg_out).  Begins and
+// ends with a barrier.  cnt: thread t's terms inside n.
+__device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str, double g0, int cnt,
+                                              Tr* __restrict__ sub_out, Tr* __restrict__ seg_out) {
+  const int t = threadIdx.x, lane = t & 63, j = t >> 2;
+  __syncthreads();
+  double pr[kPer];
+  double ps = 0.0;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    pr[i] = sp[t * (kPer + 1) + i];
+    ps += pr[i];
+  }
+  ps += __shfl_xor(ps, 1);
+  ps += __shfl_xor(ps, 2);
+  if ((t & 3) == 0) ssum[j] = ps;
+  __syncthreads();
+  if (t < kSubs) {  // exclusive prefix of the sub sums (wave 0)
+    const double a = ssum[t];
+    double incl = a;
+#pragma unroll
+    for (int o = 1; o < kSubs; o <<= 1) {
+      const double u = __shfl_up(incl, o);
+      if (t >= o) incl += u;
+    }
+    ssum[t] = incl - a;
+  }
+  __syncthreads();
+  const double G = g0 + ssum[j];
+  const uint64_t gb = (uint64_t)__double_as_longlong(G);
+  const int GE = (int)((gb >> 52) & 0x7ff);
+  const bool gok = GE != 0 && GE != 0x7ff;
+  const int e = GE - 1023;
+  const uint32_t sneg = (uint32_t)(gb >> 63);
+  // the lane's run, in f64 arithmetic on integer values (exact below 2^53; a run that leaves that range cannot
+  // be valid and is marked BAD): every term decomposed once (decomp_f), then input parity 0's track; parity 1's
+  // differs only through ties, so it is the same track unless the run holds one (then it is run again)
+  Tr a = tr_ident();
+  double qv[kPer];
+  uint32_t cls = 0;  // 2 bits per term: 0 / 1 (tie) / 2 as decomp's class, 3: a +-0 term (no effect)
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    qv[i] = 0.0;
+    uint32_t ci = 3;
+    if (i < cnt) {
+      const uint64_t b = (uint64_t)__double_as_longlong(pr[i]);
+      if ((b << 1) == 0) {
+        if (!(b >> 63)) a.fl &= ~F_NZERO;
+      } else {
+        if (a.fl & F_ZERO) {
+          a.fl = sneg ? F_NEG : 0u;
+          a.e = e;
+        }
+        int c = 0;
+        if (!gok || !decomp_f(pr[i], e, sneg, qv[i], c)) bad = true;
+        ci = (uint32_t)c;
+      }
+    }
+    cls |= ci << (2 * i);
+  }
+  if (!(a.fl & F_ZERO)) {
+    const double big = kBig;
+    double d0 = 0.0, lo0 = big, hi0 = -big, d1 = 0.0, lo1 = big, hi1 = -big;
+    bool tie = false;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t ci = (cls >> (2 * i)) & 3u;
+      if (ci == 3) continue;
+      const double x = d0 + qv[i];
+      lo0 = fmin(lo0, x);
+      d0 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? x - 2.0 * floor(0.5 * x) : 0.0);  // a tie rounds to even
+      hi0 = fmax(hi0, d0);
+      tie |= ci == 1;
+    }
+    if (tie) {
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const uint32_t ci = (cls >> (2 * i)) & 3u;
+        if (ci == 3) continue;
+        const double x = d1 + qv[i];
+        lo1 = fmin(lo1, x);
+        d1 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? (x + 1.0) - 2.0 * floor(0.5 * (x + 1.0)) : 0.0);
+        hi1 = fmax(hi1, d1);
+      }
+    } else {
+      d1 = d0;
+      lo1 = lo0;
+      hi1 = hi0;
+    }
+    const double lim = 4503599627370496.0;  // 2^52: every offset of a valid run is below this
+    if (bad || fabs(d0) > lim || fabs(d1) > lim || (lo0 < big && fabs(lo0) > lim) ||
+        (lo1 < big && fabs(lo1) > lim) || (hi0 > -big && fabs(hi0) > lim) || (hi1 > -big && fabs(hi1) > lim)) {
+      a.fl |= F_BAD;
+    } else {
+      a.d0 = d0;
+      a.d1 = d1;
+      a.lo0 = lo0;
+      a.lo1 = lo1;
+      a.hi0 = hi0;
+      a.hi1 = hi1;
+    }
+  }
+  Tr o = shfl_xor_tr(a, 1);
+  if ((t & 1) == 0) a = tr_comb(a, o);
+  o = shfl_xor_tr(a, 2);
+  if ((t & 3) == 0) {
+    a = tr_comb(a, o);
+    sub_out[j] = a;
+  }
+#pragma unroll
+  for (int s = 4; s < 64; s <<= 1) {  // each wave: the ordered tree over its 16 subs (leaders 0, 4, .., 60)
+    const Tr u = shfl_down_tr(a, s);
+    if ((lane & (2 * s - 1)) == 0) a = tr_comb(a, u);
+  }
+  if (lane == 0) str[t >> 6] = a;
+  __syncthreads();
+  if (t == 0) *seg_out = tr_comb(tr_comb(str[0], str[1]), tr_comb(str[2], str[3]));
+  __syncthreads();
+}
+
 // Workgroup k: segment k of every sum.  Thread t holds terms 16t..16t+15 of the segment (the products staged
 // through LDS from coalesced loads); four threads make a sub-segment's transducer, wave 0 composes the 64 subs.
 __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w, Vecs V, int nv, int64_t n,
@@ -470,7 +593,7 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
   __shared__ double sp[kSeg + kSeg / kPer];  // products, one pad slot per 16: thread t's run at 17t
   __shared__ double ssum[kSubs];
   __shared__ Tr str[kT / 64];
-  const int t = threadIdx.x, lane = t & 63, j = t >> 2;
+  const int t = threadIdx.x;
   const int64_t k = blockIdx.x, c0 = k * kSeg;
   const int cnt = (int)max<int64_t>(0, min<int64_t>(kPer, n - (c0 + (int64_t)kPer * t)));
   double xr[kPer];
@@ -500,120 +623,8 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) yr[i] = yn[i];
-    __syncthreads();
-    double pr[kPer];
-    double ps = 0.0;
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      pr[i] = sp[t * (kPer + 1) + i];
-      ps += pr[i];
-    }
-    ps += __shfl_xor(ps, 1);
-    ps += __shfl_xor(ps, 2);
-    if ((t & 3) == 0) ssum[j] = ps;
-    __syncthreads();
-    if (t < kSubs) {  // exclusive prefix of the sub sums (wave 0)
-      const double a = ssum[t];
-      double incl = a;
-#pragma unroll
-      for (int o = 1; o < kSubs; o <<= 1) {
-        const double u = __shfl_up(incl, o);
-        if (t >= o) incl += u;
-      }
-      ssum[t] = incl - a;
-    }
-    __syncthreads();
-    const double G = pre[(int64_t)v * K + k] + ssum[j];
-    const uint64_t gb = (uint64_t)__double_as_longlong(G);
-    const int GE = (int)((gb >> 52) & 0x7ff);
-    const bool gok = GE != 0 && GE != 0x7ff;
-    const int e = GE - 1023;
-    const uint32_t sneg = (uint32_t)(gb >> 63);
-    // the lane's run, in f64 arithmetic on integer values (exact below 2^53; a run that leaves that range cannot
-    // be valid and is marked BAD): every term decomposed once (decomp_f), then input parity 0's track; parity 1's
-    // differs only through ties, so it is the same track unless the run holds one (then it is run again)
-    Tr a = tr_ident();
-    double qv[kPer];
-    uint32_t cls = 0;  // 2 bits per term: 0 / 1 (tie) / 2 as decomp's class, 3: a +-0 term (no effect)
-    bool bad = false;
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      qv[i] = 0.0;
-      uint32_t ci = 3;
-      if (i < cnt) {
-        const uint64_t b = (uint64_t)__double_as_longlong(pr[i]);
-        if ((b << 1) == 0) {
-          if (!(b >> 63)) a.fl &= ~F_NZERO;
-        } else {
-          if (a.fl & F_ZERO) {
-            a.fl = sneg ? F_NEG : 0u;
-            a.e = e;
-          }
-          int c = 0;
-          if (!gok || !decomp_f(pr[i], e, sneg, qv[i], c)) bad = true;
-          ci = (uint32_t)c;
-        }
-      }
-      cls |= ci << (2 * i);
-    }
-    if (!(a.fl & F_ZERO)) {
-      const double big = kBig;
-      double d0 = 0.0, lo0 = big, hi0 = -big, d1 = 0.0, lo1 = big, hi1 = -big;
-      bool tie = false;
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const uint32_t ci = (cls >> (2 * i)) & 3u;
-        if (ci == 3) continue;
-        const double x = d0 + qv[i];
-        lo0 = fmin(lo0, x);
-        d0 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? x - 2.0 * floor(0.5 * x) : 0.0);  // a tie rounds to even
-        hi0 = fmax(hi0, d0);
-        tie |= ci == 1;
-      }
-      if (tie) {
-#pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-          const uint32_t ci = (cls >> (2 * i)) & 3u;
-          if (ci == 3) continue;
-          const double x = d1 + qv[i];
-          lo1 = fmin(lo1, x);
-          d1 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? (x + 1.0) - 2.0 * floor(0.5 * (x + 1.0)) : 0.0);
-          hi1 = fmax(hi1, d1);
-        }
-      } else {
-        d1 = d0;
-        lo1 = lo0;
-        hi1 = hi0;
-      }
-      const double lim = 4503599627370496.0;  // 2^52: every offset of a valid run is below this
-      if (bad || fabs(d0) > lim || fabs(d1) > lim || (lo0 < big && fabs(lo0) > lim) ||
-          (lo1 < big && fabs(lo1) > lim) || (hi0 > -big && fabs(hi0) > lim) || (hi1 > -big && fabs(hi1) > lim)) {
-        a.fl |= F_BAD;
-      } else {
-        a.d0 = d0;
-        a.d1 = d1;
-        a.lo0 = lo0;
-        a.lo1 = lo1;
-        a.hi0 = hi0;
-        a.hi1 = hi1;
-      }
-    }
-    Tr o = shfl_xor_tr(a, 1);
-    if ((t & 1) == 0) a = tr_comb(a, o);
-    o = shfl_xor_tr(a, 2);
-    if ((t & 3) == 0) {
-      a = tr_comb(a, o);
-      subT[((int64_t)v * K + k) * kSubs + j] = a;
-    }
-#pragma unroll
-    for (int s = 4; s < 64; s <<= 1) {  // each wave: the ordered tree over its 16 subs (leaders 0, 4, .., 60)
-      const Tr u = shfl_down_tr(a, s);
-      if ((lane & (2 * s - 1)) == 0) a = tr_comb(a, u);
-    }
-    if (lane == 0) str[t >> 6] = a;
-    __syncthreads();
-    if (t == 0) segT[(int64_t)v * K + k] = tr_comb(tr_comb(str[0], str[1]), tr_comb(str[2], str[3]));
-    __syncthreads();
+    trans_segment(sp, ssum, str, pre[(int64_t)v * K + k], cnt, subT + ((int64_t)v * K + k) * kSubs,
+                  segT + (int64_t)v * K + k);
   }
 }
 
@@ -919,15 +930,12 @@ __device__ __forceinline__ bool any_ties(const Rip& q) {
 // does not apply; that segment's sub maps likewise (its terms' loads in flight meanwhile); a sub that does not
 // apply is added term by term from LDS, and the ripple resumes after it.  rw: the ripple width over segments and a
 // descended segment's first subs; rs: after a serially added sub.  All four waves compute the same s.
-__global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restrict__ w, Vecs V, int64_t n, int self,
-                                                         const Tr* __restrict__ segT, const Tr* __restrict__ subT,
-                                                         int64_t K, const double* __restrict__ acc_in,
-                                                         double* __restrict__ partial, int64_t nchunks,
-                                                         const int* __restrict__ stop, int64_t* __restrict__ stats,
-                                                         int rw, int rs, int pf) {
-  if (stopped(stop)) return;
-  __shared__ double sp[kSeg];
-  const int v = blockIdx.x, t = threadIdx.x, lane = t & 63;
+__device__ __forceinline__ void ripwalk_sum(int v, const double* __restrict__ w, const Vecs& V, int64_t n, int self,
+                                            const Tr* __restrict__ segT, const Tr* __restrict__ subT, int64_t K,
+                                            const double* __restrict__ acc_in, double* __restrict__ partial,
+                                            int64_t nchunks, int64_t* __restrict__ stats, int rw, int rs, int pf,
+                                            double* sp) {
+  const int t = threadIdx.x, lane = t & 63;
   const double* y = self ? nullptr : vec_row(V, v);
   const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
   int64_t n_win = 0, n_segdesc = 0, n_rip = 0, n_subser = 0;
@@ -1027,6 +1035,17 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
   }
 }
 
+__global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restrict__ w, Vecs V, int64_t n, int self,
+                                                         const Tr* __restrict__ segT, const Tr* __restrict__ subT,
+                                                         int64_t K, const double* __restrict__ acc_in,
+                                                         double* __restrict__ partial, int64_t nchunks,
+                                                         const int* __restrict__ stop, int64_t* __restrict__ stats,
+                                                         int rw, int rs, int pf) {
+  if (stopped(stop)) return;
+  __shared__ double sp[kSeg];
+  ripwalk_sum(blockIdx.x, w, V, n, self, segT, subT, K, acc_in, partial, nchunks, stats, rw, rs, pf, sp);
+}
+
 }  // namespace
 
 extern "C" int msk_seq_stage1(const double* w, const Vecs* V, int nv, int64_t n, int self, double* partial,
@@ -1076,7 +1095,7 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
   Tr* subT = static_cast<Tr*>(c->seqbuf);
   Tr* segT = subT + (int64_t)nv * K * kSubs;
   double* pre = reinterpret_cast<double*>(segT + (int64_t)nv * K);
-  int rc = msk_dot_stage1(w, V, nv, n, pre, K, self, stop, c->stream);
+  const int rc = msk_dot_stage1(w, V, nv, n, pre, K, self, stop, c->stream);
   if (rc) return rc;
   k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, acc_in, stop);
   k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop);

@@ -216,3 +216,4 @@ def test_seq_engine_walks(sctx, oracle, monkeypatch, name, walk, rw, rs, pf):
     x, y = CASES[name]
     _check_dot(sctx, oracle, x, y)
     _check_norm(sctx, oracle, x)
+
