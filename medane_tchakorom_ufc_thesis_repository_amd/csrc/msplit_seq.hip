@@ -621,8 +621,10 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
       if (g < n) p = self ? xr[i] * xr[i] : xr[i] * (yr[i] * sy);
       sp[l + l / kPer] = p;
     }
+    if (!self && v + 1 < nv) {
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) yr[i] = yn[i];
+      for (int i = 0; i < kPer; ++i) yr[i] = yn[i];
+    }
     trans_segment(sp, ssum, str, pre[(int64_t)v * K + k], cnt, subT + ((int64_t)v * K + k) * kSubs,
                   segT + (int64_t)v * K + k);
   }
