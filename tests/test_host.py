@@ -164,6 +164,27 @@ def test_bench_reads_the_measured_streaming_ceiling():
     assert 5.0 < c["copy_TBps"] < bench.HBM_PEAK_GBS / 1e3
 
 
+def test_bench_smsm_seq_line_reads_its_record():
+    """bench.py's smsm_seq_mode line (in every N = 1 run; --no-seq-smsm skips it) checks the fields of
+    tests/golden/smsm_seq.json that smsm_solve reports, at the block and options the record names."""
+    import importlib
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    g = json.load(open(bench.SMSM_SEQ_GOLDEN))
+    assert {"outer_its", "norm0_hex", "hist_hex", "lsqr_its", "inner_its", "x_sha256"} <= set(g)
+    assert g["problem"]["nb"] == 1 and g["inner"]["restart"] == 30 and g["outer"]["max_it"] == 70
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py", "--no-seq-smsm"]
+        assert bench.parse().no_seq_smsm
+        sys.argv = ["bench.py"]
+        assert not bench.parse().no_seq_smsm
+    finally:
+        sys.argv = old
+
+
 def _isolve(args, **env):
     e = dict(os.environ, ISOLVE_DRYRUN="1", **env)
     p = subprocess.run([os.path.join(ROOT, "host", "isolve")] + args, capture_output=True, text=True, env=e,
