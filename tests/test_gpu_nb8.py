@@ -91,6 +91,33 @@ def test_smsm_eight_blocks_one_process_bitwise_oracle(ctx, oracle, dim, nx, ny, 
     mini.close()
 
 
+@pytest.mark.parametrize("variant", ["sm", "smsm"])
+def test_eight_blocks_petsc_order_bitwise_oracle(oracle, variant):
+    """The PETSc-order mode at nb = 8 (-msplit_reduction seq): SM and SMSM-global with 8 blocks in one process equal
+    the oracle's ORC_REDUCE_SEQ bit for bit (every history entry, the inner and LSQR counts, x); the LSQR sums run
+    chained across the 8 row blocks as the reference's one-rank LSQR does."""
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context
+    sctx = Context(0)
+    sctx.set_reduction("seq")
+    comm = LocalComm()
+    dim, nx, ny, nz, s, rtol = 3, 8, 8, 16, 4, 1e-6
+    if variant == "sm":
+        blocks = make_blocks(sctx, dim, nx, ny, nz, NB, range(NB), _opts(NB, outer=False), comm)
+        res = sm_solve(blocks, comm, rtol=rtol, max_outer=400)
+        ro = oracle.sm_solve(dim, nx, ny, nz, NB, rtol, dict(INNER, reduce_mode=oracle.REDUCE_SEQ), max_outer=400)
+    else:
+        blocks, mini = make_smsm(sctx, dim, nx, ny, nz, NB, range(NB), s, _opts(NB), comm)
+        res = smsm_solve(blocks, comm, s, mini, rtol=rtol, max_outer=100)
+        ro = oracle.smsm_solve(dim, nx, ny, nz, NB, s, rtol, dict(INNER, reduce_mode=oracle.REDUCE_SEQ),
+                               dict(OUTER, reduce_mode=oracle.REDUCE_SEQ), max_outer=100)
+        assert np.array_equal(np.array(res.lsqr_its), ro["lsqr_its"])
+        mini.close()
+    assert res.outer_its == ro["outer_its"] and res.norm0 == ro["norm0"]
+    assert np.array_equal(np.array(res.hist), ro["hist"])
+    assert np.array_equal(np.array(res.inner_its), ro["inner_its"])
+    assert np.array_equal(np.concatenate([blk.x.get_array() for blk in blocks]), ro["x"])
+
+
 def _ranks_problem():
     P = RANKS["problem"]
     return P, P["nx"], P["ny"], P["planes_per_block"] * NB
