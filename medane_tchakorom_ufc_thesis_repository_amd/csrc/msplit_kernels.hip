@@ -2065,6 +2065,179 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
   }
 }
 
+// The symmetric STENCIL fused step with two threads per DBR lane (round 5): 512 threads a tile, thread t < 256 takes
+// the lane's row pairs j = 0..3, thread t + 256 its pairs j = 4..7 -- half the registers of the one-thread form
+// (legs, x(z-1..z+1), uz), so a CU holds eight waves of it where it held four.  The rows' W values are exchanged
+// through LDS (the x+1 leg window's space, free once the rows are done), then each half takes every other pair of
+// basis vectors over all 16 rows of its lane: lane t's sum, the butterflies and the (w0 + w1) + (w2 + w3) of
+// every vector are k_box_spmv_mdot_march<.., 2>'s, term for term, and so are W and the values (bitwise).  The
+// x(z) dot comes from the LDS window.  nx <= 512 (LDS: the windows of x and of the x+1 / y+1 legs).
+template <int VAR, bool NTY>
+__global__ __launch_bounds__(2 * kT) void k_box_spmv_mdot_march_sym2(int32_t nx, int64_t P, int32_t nz, int32_t zt,
+                                                                    int xcd, const uint8_t* __restrict__ mask,
+                                                                    const double* __restrict__ rv,
+                                                                    const double* __restrict__ x,
+                                                                    const double* __restrict__ sdev,
+                                                                    double* __restrict__ y, Vecs V, int nv, int self,
+                                                                    double* __restrict__ partial, int64_t nchunks,
+                                                                    const int* __restrict__ stop) {
+  constexpr int H = kIters / 2;  // row pairs per thread
+  if (stopped(stop)) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sx = reinterpret_cast<double*>(smem);  // window of plane z: kChunk + 2 nx doubles
+  double* sux = sx + kChunk + 2 * nx;           // x+1 / y+1 legs of the window [c0 - nx, c0 + 4096)
+  double* suy = sux + kChunk + nx;
+  __shared__ double red[MSK_MAX_GROUP][4];
+  const int t = threadIdx.x, h = t >> 8, tl = t & (kT - 1), lane = t & 63, wv = (t >> 6) & 3;
+  const int j0 = h * H;  // this thread's first row pair
+  const int64_t cpp = P / kChunk;
+  int64_t tile, zg;
+  if (xcd & 1) {
+    const int64_t per = cpp / 8, slot = blockIdx.x / 8;
+    tile = (blockIdx.x % 8) * per + slot % per;
+    zg = slot / per;
+  } else {
+    tile = blockIdx.x % cpp;
+    zg = blockIdx.x / cpp;
+  }
+  if (xcd & 2) zg = (nz + zt - 1) / zt - 1 - zg;
+  const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
+  const double sc = *sdev;
+  const int nh = nx / 2;
+  double xm[2 * H], xc[2 * H], xp[2 * H], uzm[2 * H];
+  {
+    const int64_t cb = ((int64_t)z0 - 1) * P + tile * kChunk;
+    const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * tl;
+#pragma unroll
+    for (int jj = 0; jj < H; ++jj) {
+      const int j = j0 + jj;
+      const double2 u = z0 > 0 ? ld_nt(rvs_pair(rv, cb, 3, j, tl)) : make_double2(0.0, 0.0);
+      uzm[2 * jj] = u.x;
+      uzm[2 * jj + 1] = u.y;
+      const double2 a = *reinterpret_cast<const double2*>(x + b0 + j * (2 * kT));
+      xc[2 * jj] = a.x;
+      xc[2 * jj + 1] = a.y;
+      const double2 m2 = z0 > 0 ? *reinterpret_cast<const double2*>(x + b0 - P + j * (2 * kT)) : make_double2(0.0, 0.0);
+      xm[2 * jj] = m2.x;
+      xm[2 * jj + 1] = m2.y;
+    }
+  }
+  for (int32_t z = z0; z < z1; ++z) {
+    const int64_t c = (int64_t)z * cpp + tile, c0 = c * kChunk, base = c0 + 2 * tl;
+    uint32_t m[H];
+    double2 own[H][4];
+#pragma unroll
+    for (int jj = 0; jj < H; ++jj) {
+      const int j = j0 + jj;
+      if (z + 1 < nz) {
+        const double2 p2 = *reinterpret_cast<const double2*>(x + base + P + j * (2 * kT));
+        xp[2 * jj] = p2.x;
+        xp[2 * jj + 1] = p2.y;
+      } else {
+        xp[2 * jj] = xp[2 * jj + 1] = 0.0;
+      }
+      m[jj] = *reinterpret_cast<const uint16_t*>(mask + base + j * (2 * kT));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) own[jj][k] = ld_nt(rvs_pair(rv, c0, k, j, tl));
+    }
+    double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0), hx = hl, hy = hl;
+    const bool hal = h == 0 && tl < nh;
+    if (hal && c0 - nx >= 0) {
+      hl = *reinterpret_cast<const double2*>(x + c0 - nx + 2 * tl);
+      hx = *reinterpret_cast<const double2*>(rvs_at(rv, c0 - nx + 2 * tl, 1));
+      hy = *reinterpret_cast<const double2*>(rvs_at(rv, c0 - nx + 2 * tl, 2));
+    }
+    if (hal && c0 + kChunk + nx <= (int64_t)nz * P) hh = *reinterpret_cast<const double2*>(x + c0 + kChunk + 2 * tl);
+    __syncthreads();  // the previous plane's window and exchange reads (and its partial writes) are done
+#pragma unroll
+    for (int jj = 0; jj < H; ++jj) {
+      const int o = nx + (j0 + jj) * (2 * kT) + 2 * tl;
+      *reinterpret_cast<double2*>(sx + o) = make_double2(xc[2 * jj], xc[2 * jj + 1]);
+      *reinterpret_cast<double2*>(sux + o) = own[jj][1];
+      *reinterpret_cast<double2*>(suy + o) = own[jj][2];
+    }
+    if (hal) {
+      *reinterpret_cast<double2*>(sx + 2 * tl) = hl;
+      *reinterpret_cast<double2*>(sx + nx + kChunk + 2 * tl) = hh;
+      *reinterpret_cast<double2*>(sux + 2 * tl) = hx;
+      *reinterpret_cast<double2*>(suy + 2 * tl) = hy;
+    }
+    __syncthreads();
+    double wr[2 * H];
+#pragma unroll
+    for (int jj = 0; jj < H; ++jj) {
+      const int j = j0 + jj;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int e = j * (2 * kT) + 2 * tl + q + nx;
+        const uint32_t mr = (m[jj] >> (8 * q)) & 255u;
+        const double xq[7] = {xm[2 * jj + q], sx[e - nx], sx[e - 1], xc[2 * jj + q], sx[e + 1], sx[e + nx],
+                              xp[2 * jj + q]};
+        const double vv[7] = {uzm[2 * jj + q], suy[e - nx], sux[e - 1], q ? own[jj][0].y : own[jj][0].x,
+                              q ? own[jj][1].y : own[jj][1].x, q ? own[jj][2].y : own[jj][2].x,
+                              q ? own[jj][3].y : own[jj][3].x};
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+          if (mr & (1u << k)) s = s + vv[k] * (xq[k] * sc);
+        wr[2 * jj + q] = s;
+      }
+      if constexpr (NTY) {
+        dx2 o;
+        o.x = wr[2 * jj];
+        o.y = wr[2 * jj + 1];
+        __builtin_nontemporal_store(o, reinterpret_cast<dx2*>(y + base + j * (2 * kT)));
+      } else {
+        *reinterpret_cast<double2*>(y + base + j * (2 * kT)) = make_double2(wr[2 * jj], wr[2 * jj + 1]);
+      }
+      uzm[2 * jj] = own[jj][3].x;  // the next plane's z-1 values
+      uzm[2 * jj + 1] = own[jj][3].y;
+    }
+    __syncthreads();  // every row is done with the leg windows: the x+1 window's space takes the W exchange
+    double* wx = sux;
+#pragma unroll
+    for (int jj = 0; jj < H; ++jj)
+      *reinterpret_cast<double2*>(wx + (j0 + jj) * (2 * kT) + 2 * tl) = make_double2(wr[2 * jj], wr[2 * jj + 1]);
+    __syncthreads();
+    double wf[2 * kIters];  // all 16 W values of lane tl, in its DBR order
+#pragma unroll
+    for (int j = 0; j < kIters; ++j) {
+      const double2 a = *reinterpret_cast<const double2*>(wx + j * (2 * kT) + 2 * tl);
+      wf[2 * j] = a.x;
+      wf[2 * j + 1] = a.y;
+    }
+    // pairs of vectors alternate between the halves (two vectors' 16 rows in flight per thread: the registers of the
+    // one-thread form's groups of four, spread over twice the threads); the odd vector and x(z)'s dot go to the
+    // half with fewer pairs
+    const int nvm = nv - self, ng = nvm / 2;
+#pragma unroll 1
+    for (int gi = h; gi < ng; gi += 2) dot_group_full<2, VAR>(wf, V, base, 0, nv, 2 * gi, red, lane, wv);
+    const int hr = ng & 1;  // the half that took one pair fewer (or as many)
+    if (h == hr) {
+      if (nvm & 1) dot_group_full<1, VAR>(wf, V, base, 0, nv, 2 * ng, red, lane, wv);
+      if (self) {
+        const double sv = vec_scale(V, nv - 1);
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < kIters; ++j) {
+          const double2 xr = *reinterpret_cast<const double2*>(sx + nx + j * (2 * kT) + 2 * tl);
+          acc = acc + wf[2 * j] * (xr.x * sv);
+          acc = acc + wf[2 * j + 1] * (xr.y * sv);
+        }
+        acc = wave_butterfly(acc);
+        if (lane == 0) red[nv - 1][wv] = acc;
+      }
+    }
+    __syncthreads();
+    if (t < nv) partial[t * nchunks + c] = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
+#pragma unroll
+    for (int i = 0; i < 2 * H; ++i) {
+      xm[i] = xc[i];
+      xc[i] = xp[i];
+    }
+  }
+}
+
 // One vector group of the CGS MAXPY over a full chunk, u += sum_q a_q (V_{g+q} * s_q) in chunk_group's
 // arithmetic (group_sum left to right; G == 1: s + u), a_q = -adev[g + q].  SELF: the group's last vector is
 // x itself, whose 16 values of this chunk the caller holds in xs (the march registers): not read again.
@@ -3240,7 +3413,16 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
     else if (RV_ == 1 && rvp == 2) MSK_BSMM_P(VAR_, NT_, RV_, 2);                                             \
     else MSK_BSMM_P(VAR_, NT_, RV_, kIters);                                                                  \
   } while (0)
-    if (rv && rvs < 0) {  // the symmetric storage
+    // the symmetric storage: two threads per DBR lane where the windows fit (nx <= 512; MSPLIT_RV_SYM2=0: one, A/B)
+    const char* s2e = getenv("MSPLIT_RV_SYM2");  // read per call: the tests hold the two forms to each other
+    const bool sym2 = !(s2e && s2e[0] == '0') && nx <= 512;
+#define MSK_SYM2(VAR_, NT_)                                                                               \
+  k_box_spmv_mdot_march_sym2<VAR_, NT_><<<dim3((unsigned)grid), dim3(2 * kT), lds, s>>>(                   \
+      nx, P, nz, zt, xcd, mask, rv, x, sdev, y, *V, nv, self, partial, nchunks, stop)
+    if (rv && rvs < 0 && sym2) {
+      if (vec_var()) { if (nty) MSK_SYM2(1, true); else MSK_SYM2(1, false); }
+      else { if (nty) MSK_SYM2(0, true); else MSK_SYM2(0, false); }
+    } else if (rv && rvs < 0) {  // the symmetric storage
       if (vec_var()) { if (nty) MSK_BSMM(1, true, 2); else MSK_BSMM(1, false, 2); }
       else { if (nty) MSK_BSMM(0, true, 2); else MSK_BSMM(0, false, 2); }
     } else if (rv) {
@@ -3250,6 +3432,7 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
       if (vec_var()) { if (nty) MSK_BSMM(1, true, 0); else MSK_BSMM(1, false, 0); }
       else { if (nty) MSK_BSMM(0, true, 0); else MSK_BSMM(0, false, 0); }
     }
+#undef MSK_SYM2
 #undef MSK_BSMM
 #undef MSK_BSMM_P
     return (int)hipGetLastError();

@@ -726,7 +726,7 @@ def _unsymmetric(rp, col, val, seed=SEED):
     return val
 
 
-@pytest.mark.parametrize("layout", ["sym", "blocked", "soa", "blocked-unsym"])
+@pytest.mark.parametrize("layout", ["sym", "sym-one", "blocked", "soa", "blocked-unsym"])
 @pytest.mark.parametrize("flags", [0, BOX_SEPARATE])
 @pytest.mark.parametrize("shape", [(64, 64, 16), (128, 32, 9), (64, 64, 2), (2048, 2, 3), (1024, 4, 5)])
 def test_variable_coefficient_box_takes_the_stencil_storage(ctx, oracle, shape, flags, layout, monkeypatch):
@@ -744,12 +744,15 @@ def test_variable_coefficient_box_takes_the_stencil_storage(ctx, oracle, shape, 
     # the value layout chosen at assembly: symmetric (the diagonal and upper legs; the default for a symmetric
     # operator with planes up to 1024 wide), chunk-blocked seven legs (MSPLIT_RV_SYM=0, or an unsymmetric operator),
     # or per-leg arrays (MSPLIT_RV_LAYOUT=soa)
+    # sym: the fused step with two threads per DBR lane where nx <= 512 (k_box_spmv_mdot_march_sym2); sym-one: the
+    # one-thread form (MSPLIT_RV_SYM2=0)
     monkeypatch.setenv("MSPLIT_RV_LAYOUT", "soa" if layout == "soa" else "blocked")
-    monkeypatch.setenv("MSPLIT_RV_SYM", "1" if layout == "sym" else "0" if layout == "blocked" else "1")
+    monkeypatch.setenv("MSPLIT_RV_SYM", "0" if layout == "blocked" else "1")
+    monkeypatch.setenv("MSPLIT_RV_SYM2", "0" if layout == "sym-one" else "1")
     if layout == "blocked-unsym":
         val = _unsymmetric(rp, col, val)
     A = Mat.from_csr(ctx, N, N, rp, col, val)
-    sym = layout == "sym" and nx <= 1024
+    sym = layout.startswith("sym") and nx <= 1024
     assert A.get_storage() == "stencil"
     assert A.spmv_kernel() == ("k_box_march_chunk_rv_sym" if sym else "k_box_march_chunk_rv")
     O = oracle.Mat.from_arrays(N, N, rp, col, val)
