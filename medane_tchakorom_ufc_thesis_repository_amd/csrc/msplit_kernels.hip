@@ -3380,10 +3380,10 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
       return e ? atoi(e) : 0;
     }();
     const int32_t nz = (int32_t)(n / P);
-    // two planes per workgroup for the constant-coefficient step (one: -1.0 %, profiles/r03/wfree/fused_depth/);
-    // four for the STENCIL storage, whose first plane also re-reads the plane below's z+1 leg (+1.9 % against two,
-    // profiles/r05/stencil_sym2/zt/)
-    const int32_t zt = zenv > 0 ? zenv : (rv ? 4 : 2);
+    // four planes per workgroup: the first plane of each re-reads the plane below (x, and for the STENCIL storage its
+    // z+1 leg): STENCIL step +1.9 %, SMSM block +0.3 %, 256^3 GMRES +0.1 % against two (profiles/r05/stencil_sym2/zt/,
+    // profiles/r05/zt_dv/); one plane was -1.0 % (profiles/r03/wfree/fused_depth/)
+    const int32_t zt = zenv > 0 ? zenv : 4;
     const int64_t grid = (P / kChunk) * ((nz + zt - 1) / zt);
     if (grid > INT32_MAX) return (int)hipErrorInvalidValue;
     // XCD-contiguous eighths from 32 tiles per plane (SMSM's 512^2 planes: +1.9 % over plane order, same box);
