@@ -3380,9 +3380,9 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
       return e ? atoi(e) : 0;
     }();
     const int32_t nz = (int32_t)(n / P);
-    // four planes per workgroup: the first plane of each re-reads the plane below (x, and for the STENCIL storage its
-    // z+1 leg): STENCIL step +1.9 %, SMSM block +0.3 %, 256^3 GMRES +0.1 % against two (profiles/r05/stencil_sym2/zt/,
-    // profiles/r05/zt_dv/); one plane was -1.0 % (profiles/r03/wfree/fused_depth/)
+    // four planes per workgroup: half the workgroup prologues (the dependent loads of the plane below the first: x,
+    // and for the STENCIL storage its z+1 leg) -- STENCIL step +1.9 %, SMSM block +0.3 %, 256^3 GMRES +0.1 % against
+    // two (profiles/r05/stencil_sym2/zt/, profiles/r05/zt_dv/); one plane was -1.0 % (profiles/r03/wfree/fused_depth/)
     const int32_t zt = zenv > 0 ? zenv : 4;
     const int64_t grid = (P / kChunk) * ((nz + zt - 1) / zt);
     if (grid > INT32_MAX) return (int)hipErrorInvalidValue;
