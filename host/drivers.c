@@ -683,8 +683,15 @@ int msd_am_solve(msp_ctx *ctx, const msd_problem *p, const msd_options *o, const
   CK(sum_over_blocks(&R, block_residual_sq, &res->final_norm));
   CK(sum_over_blocks(&R, error_sq, &res->error));
   res->nlocal = R.nlocal;
-  for (int i = 0; i < R.nlocal; ++i) res->iterations[i] = R.blk[i]->it;
+  for (int i = 0; i < R.nlocal; ++i) {
+    res->iterations[i] = R.blk[i]->it;
+    res->states[i] = R.blk[i]->state;
+    res->tags[i] = R.blk[i]->tag;
+  }
   res->last_norm = limited ? -1.0 : 0.0;
+  barrier(&R);
+  for (int i = 0; i < R.nlocal; ++i) /* drain and cancel, AM_prime.c's end of run (every rank is past its loop) */
+    CK(msp_amsg_discard_pending(R.blk[i]->am, &res->discarded[i], &res->in_flight[i]));
   barrier(&R);
   for (int i = 0; i < R.nlocal; ++i) msp_amsg_close_peers(R.blk[i]->am);
   barrier(&R);
@@ -889,8 +896,20 @@ int msd_amam_global_solve(msp_ctx *ctx, const msd_problem *p, const msd_options 
   CK(sum_over_blocks(&R, block_residual_sq, &res->final_norm));
   CK(sum_over_blocks(&R, error_sq, &res->error));
   res->nlocal = R.nlocal;
-  for (int i = 0; i < R.nlocal; ++i) res->iterations[i] = R.blk[i]->it;
+  for (int i = 0; i < R.nlocal; ++i) {
+    res->iterations[i] = R.blk[i]->it;
+    res->states[i] = R.blk[i]->state;
+    res->tags[i] = R.blk[i]->tag;
+  }
   res->last_norm = limited ? -1.0 : 0.0;
+  barrier(&R);
+  for (int i = 0; i < R.nlocal; ++i) { /* drain and cancel (AMAM-global_prime.c:522-572) */
+    int64_t d, f;
+    CK(msp_amsg_discard_pending(R.blk[i]->am, &res->discarded[i], &res->in_flight[i]));
+    CK(msp_abcast_discard_pending(R.blk[i]->bc, &d, &f));
+    res->discarded[i] += d;
+    res->in_flight[i] += f;
+  }
   barrier(&R);
   for (int i = 0; i < R.nlocal; ++i) {
     msp_amsg_close_peers(R.blk[i]->am);

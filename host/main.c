@@ -148,6 +148,36 @@ int main(int argc, char **argv) {
                        : msd_amam_global_solve(ctx, &p, o, &t, &r);
   const int async = kind >= 2;
   if (rc == MSP_ERR_ARG_OUTOFRANGE && async) rc = 0; /* stopped at -max_outer: still report */
+  /* asynchronous runs: every block's own end state -- detection state, phase tag, iterations, messages discarded
+   * and sends still in flight at shutdown, and the final residual as that block's rank computed it -- gathered on
+   * rank 0 (one block per rank under MPI, every block locally otherwise) */
+  enum { REP = 8 };
+  double rep[64 * REP];
+  int nrep = 0;
+  if (async && !rc) {
+    double mine[64 * REP];
+    for (int i = 0; i < r.nlocal; ++i) {
+      double *q = mine + i * REP;
+      q[0] = world > 1 ? rank : i;
+      q[1] = r.iterations[i];
+      q[2] = r.states[i];
+      q[3] = r.tags[i];
+      q[4] = (double)r.discarded[i];
+      q[5] = (double)r.in_flight[i];
+      q[6] = r.final_norm;
+      q[7] = r.error;
+    }
+#ifdef MSD_MPI
+    if (world > 1) {
+      MPI_Gather(mine, REP, MPI_DOUBLE, rep, REP, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+      nrep = world;
+    } else
+#endif
+    {
+      memcpy(rep, mine, sizeof(double) * REP * (size_t)r.nlocal);
+      nrep = r.nlocal;
+    }
+  }
   if (!rc && rank == 0) {
     if (msd_opt_has(o, NULL, "json")) {
       printf("{\"program\": \"%s\", \"host\": \"c\", \"ranks\": %d, \"blocks\": %d, \"transport\": \"%s\", ", prog,
@@ -155,6 +185,13 @@ int main(int argc, char **argv) {
       if (async) {
         printf("\"iterations\": [");
         for (int i = 0; i < r.nlocal; ++i) printf("%s%d", i ? ", " : "", r.iterations[i]);
+        printf("], \"blocks_report\": [");
+        for (int i = 0; i < nrep; ++i) {
+          const double *q = rep + i * REP;
+          printf("%s{\"block\": %d, \"iterations\": %d, \"state\": %d, \"tag\": %d, \"discarded\": %lld, "
+                 "\"in_flight\": %lld, \"final_norm\": %.17g, \"error\": %.17g}",
+                 i ? ", " : "", (int)q[0], (int)q[1], (int)q[2], (int)q[3], (long long)q[4], (long long)q[5], q[6], q[7]);
+        }
         printf("], ");
       } else {
         printf("\"outer_its\": %d, \"hist_hex\": [", r.outer_its);

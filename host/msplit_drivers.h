@@ -64,6 +64,9 @@ typedef struct {
   double hist[MSD_HIST_CAP]; /* SM / SMSM: the stop test's norm of each outer iteration (first MSD_HIST_CAP) */
   int lsqr_its[MSD_HIST_CAP]; /* SMSM: the outer LSQR's iteration count of each outer iteration */
   int iterations[64];      /* AM: per local block */
+  int states[64], tags[64]; /* AM: the detection's state and phase tag of each local block at the end */
+  int64_t discarded[64];   /* AM: messages / R blocks discarded unread at shutdown (comm_discard_pending_messages) */
+  int64_t in_flight[64];   /* AM: own sends still in flight at shutdown (the reference's MPI_Cancel), completed */
   int nlocal;
   double norm0, final_norm, error, elapsed;
   double last_norm;        /* the stop test's last value */

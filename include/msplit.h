@@ -463,6 +463,14 @@ int msp_amsg_recv_vec(msp_amsg *am, int32_t src, int32_t *ints, int32_t nints, m
 int msp_amsg_enable_device(msp_amsg *am, msp_ctx *ctx);
 int msp_amsg_close_peers(msp_amsg *am);
 int msp_amsg_get_stats(const msp_amsg *am, int64_t *sent, int64_t *skipped);
+/* End of run, after the detection finished and before close_peers (every rank):
+ * comm_discard_pending_messages (comm.c:426-453) and the MPI_Cancel of the sends
+ * still pending (asynchronous-multisplitting-asynchronous-minimization-global_prime.c:
+ * 522-572).  Every message newer than the last one taken -- any source, any
+ * kind -- is marked taken unread (discarded); this rank's device sends whose
+ * copy is enqueued but not yet published (in_flight) cannot be withdrawn, a
+ * DMA, so they are counted and completed by draining the stream. */
+int msp_amsg_discard_pending(msp_amsg *am, int64_t *discarded, int64_t *in_flight);
 
 /* ------------------------------------------- async minimization broadcast */
 /* Newest-value broadcast of each block's rows of R (AMAM-global), in POSIX
@@ -502,6 +510,10 @@ int msp_abcast_enable_device(msp_abcast *bc, msp_ctx *ctx, int32_t nbuf);
 int msp_abcast_get_nbuf(const msp_abcast *bc, int32_t *nbuf);
 int msp_abcast_get_stats(const msp_abcast *bc, int64_t *sent, int64_t *skipped);
 int msp_abcast_close_peers(msp_abcast *bc);
+/* the same for the R rows (send_minimization_data_request, comm.c:288-351): every
+ * source's block newer than the last one fetched is marked taken unread; this
+ * rank's unpublished device publish is counted and completed */
+int msp_abcast_discard_pending(msp_abcast *bc, int64_t *discarded, int64_t *in_flight);
 
 /* ------------------------------------------------- convergence detection */
 /* Algorithm 5.15 of Bahi/Contassot-Vivier/Couturier as the reference implements

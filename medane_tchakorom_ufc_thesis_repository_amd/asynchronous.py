@@ -57,6 +57,9 @@ class AMResult:
     timers: dict = field(default_factory=dict)         # host seconds per phase, summed over local blocks
     converged: bool = True                             # False: stopped at max_iterations (stop_at_limit)
     transport: str = "host"                            # "device" (HBM slots, xGMI) or "host" (shared memory)
+    states: list = field(default_factory=list)         # detection state of each local block at the end (FINISHED)
+    discarded: list = field(default_factory=list)      # messages / R blocks discarded unread at shutdown, per block
+    in_flight: list = field(default_factory=list)      # own sends still in flight at shutdown (completed), per block
 
 
 class AsyncBlock:
@@ -151,6 +154,15 @@ class AsyncBlock:
             nbuf = int(os.environ.get("MSPLIT_ABCAST_NBUF", "0"))
             self.bcast_nbuf = self.bcast.enable_device(self.blk.ctx, nbuf if nbuf in (1, 2) else 0)
 
+    def discard_pending(self):
+        """comm_discard_pending_messages and the MPI_Cancel of the pending sends
+        (AMAM-global_prime.c:522-572): (discarded unread, own sends in flight)."""
+        d, f = self.am.discard_pending()
+        if self.bcast is not None:
+            d2, f2 = self.bcast.discard_pending()
+            d, f = d + d2, f + f2
+        return d, f
+
     def close_peers(self):
         self.am.close_peers()
         if self.bcast is not None:
@@ -240,10 +252,16 @@ def am_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_iterations: in
         res.iterations.append(ab.it)
         res.inner_its.append(ab.inner)
         res.phase_tags.append(ab.tag)
+        res.states.append(ab.state)
         for k, v in ab.timers.items():
             res.timers[k] = res.timers.get(k, 0.0) + v
     res.trace = trace or []
     res.transport = transport
+    comm.barrier()
+    for blk in blocks:                               # drain and cancel (every rank is past its loop)
+        d, f = asyncs[blk.layout.b].discard_pending()
+        res.discarded.append(d)
+        res.in_flight.append(f)
     comm.barrier()
     for ab in asyncs.values():                       # unmap the peers' slots before anyone frees its own
         ab.close_peers()

@@ -285,6 +285,42 @@ int msp_abcast_close_peers(msp_abcast *b) {
   return MSP_SUCCESS;
 }
 
+/* comm_discard_pending_messages (comm.c:426-453) for the R rows and the MPI_Cancel of
+ * send_minimization_data_request (AMAM-global_prime.c:522-572): every source's block newer than the last one taken
+ * is marked taken without being copied; this rank's own publish whose copy is enqueued but not yet published is
+ * counted and completed by draining the stream (a DMA cannot be withdrawn). */
+int msp_abcast_discard_pending(msp_abcast *b, int64_t *discarded, int64_t *in_flight) {
+  if (!b) return berr(MSP_ERR_ARG_NULL, "abcast is NULL");
+  int64_t nd = 0, nf = 0;
+  for (int src = 0; src < b->nranks; ++src) {
+    if (src == b->rank) continue;
+    if (b->dctx) {
+      const uint64_t P = atomic_load_explicit(&b->dl[src].pub, memory_order_seq_cst);
+      if (P && P != b->dseen[src]) {
+        b->dseen[src] = P;
+        ++nd;
+      }
+      continue;
+    }
+    src_line *L = &b->lines[src];
+    const int32_t k = atomic_load_explicit(&L->newest, memory_order_acquire);
+    if (k >= 0 && L->version[k] != b->seen[src]) {
+      b->seen[src] = L->version[k];
+      ++nd;
+    }
+  }
+  if (b->dctx) {
+    abc_dline *d = &b->dl[b->rank];
+    if (atomic_load_explicit(&d->claim, memory_order_seq_cst) != atomic_load_explicit(&d->pub, memory_order_seq_cst))
+      ++nf;
+    int rc = msp_ctx_synchronize(b->dctx);
+    if (rc) return rc;
+  }
+  if (discarded) *discarded = nd;
+  if (in_flight) *in_flight = nf;
+  return MSP_SUCCESS;
+}
+
 static int peer_bufs(msp_abcast *b, int src, double **out) {
   *out = b->peer[src];
   if (*out) return MSP_SUCCESS;
@@ -454,14 +490,29 @@ static int fetch_device(msp_abcast *b, int32_t src, const abc_view *v, int32_t *
 }
 
 /* ------------------------------------------------------------ publish / fetch */
+/* A dense block of another context (another stream) than the one the device buffers' copies run on: its producer's
+ * work is finished before the copy is enqueued, and the copy before the caller's stream can touch the block again
+ * (same context: stream order does both). */
+static int fence_in(const msp_abcast *b, const abc_view *v) {
+  return v->ctx != b->dctx ? msp_ctx_synchronize(v->ctx) : MSP_SUCCESS;
+}
+
+static int fence_out(const msp_abcast *b, const abc_view *v, int rc) {
+  return !rc && v->ctx != b->dctx ? msp_ctx_synchronize(b->dctx) : rc;
+}
+
 static int publish(msp_abcast *b, const abc_view *v, int32_t *published) {
   *published = 0;
   if (b->dctx && !v->ctx) return berr(MSP_ERR_ARG_WRONG, "device buffers enabled: publish a dense block in HBM");
   if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
     return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
   if (v->nrows * (int64_t)v->ncols > b->cap) return berr(MSP_ERR_ARG_SIZ, "payload larger than the broadcast slot");
-  if (b->dctx) return publish_device(b, v, published);
-  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
+  int rc;
+  if (b->dctx) {
+    rc = fence_in(b, v);
+    return rc ? rc : fence_out(b, v, publish_device(b, v, published));
+  }
+  rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
   if (rc) return rc;
   src_line *L = &b->lines[b->rank];
   const int32_t newest = atomic_load_explicit(&L->newest, memory_order_acquire);
@@ -490,8 +541,12 @@ static int fetch(msp_abcast *b, int32_t src, const abc_view *v, int32_t *got) {
   if (src < 0 || src >= b->nranks || src == b->rank) return berr(MSP_ERR_ARG_OUTOFRANGE, "source rank out of range");
   if (v->nrows < 0 || v->ncols < 0 || v->ld < v->nrows || (v->nrows > 0 && v->ncols > 0 && !v->p))
     return berr(MSP_ERR_ARG_WRONG, "bad payload shape");
-  if (b->dctx) return fetch_device(b, src, v, got);
-  int rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
+  int rc;
+  if (b->dctx) {
+    rc = fence_in(b, v);
+    return rc ? rc : fence_out(b, v, fetch_device(b, src, v, got));
+  }
+  rc = v->ctx ? ensure_registered(b) : MSP_SUCCESS;
   if (rc) return rc;
   src_line *L = &b->lines[src];
   for (int attempt = 0; attempt < 64; ++attempt) {

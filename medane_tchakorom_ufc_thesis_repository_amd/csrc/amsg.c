@@ -138,6 +138,11 @@ static ctrl_slot *data_at(msp_amsg *m, int src, int dst) {
   return (ctrl_slot *)(m->data + ((size_t)src * 2 + dir) * m->data_bytes);
 }
 
+static ctrl_slot *slot_for(msp_amsg *m, int src, int dst, int kind) {
+  if (kind == MSP_AMSG_DATA) return data_at(m, src, dst);
+  return ctrl_at(m, src, dst, kind);
+}
+
 int msp_amsg_create(const char *name, int32_t nranks, int32_t rank, int64_t data_cap, int32_t owner,
                     msp_amsg **out) {
   if (!name || !out) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
@@ -275,6 +280,51 @@ int msp_amsg_close_peers(msp_amsg *m) {
   return MSP_SUCCESS;
 }
 
+static dslot_state *dstate(msp_amsg *m, int src, int dir);
+
+/* comm_discard_pending_messages (comm.c:426-453) and the MPI_Cancel of the sends still pending at the end of a run
+ * (AMAM-global_prime.c:522-572).  Every message newer than the last one this rank took -- any source, any kind --
+ * is marked taken without being read; this rank's device sends whose copy is enqueued but not yet published cannot
+ * be withdrawn (a DMA), so they are counted and completed by draining the stream. */
+int msp_amsg_discard_pending(msp_amsg *m, int64_t *discarded, int64_t *in_flight) {
+  if (!m) return aerr(MSP_ERR_ARG_NULL, "amsg is NULL");
+  int64_t nd = 0, nf = 0;
+  for (int src = 0; src < m->nranks; ++src) {
+    if (src == m->rank) continue;
+    for (int kind = 0; kind < MSP_AMSG_NKINDS; ++kind) {
+      uint64_t *seen = m->seen + (size_t)src * MSP_AMSG_NKINDS + kind;
+      if (kind == MSP_AMSG_DATA && !data_at(m, src, m->rank)) continue;
+      if (kind == MSP_AMSG_DATA && m->dctx) {
+        dslot_state *d = dstate(m, src, m->rank == src - 1 ? 0 : 1);
+        const uint64_t P = atomic_load_explicit(&d->pub, memory_order_seq_cst);
+        if (P && P != *seen) {
+          *seen = P;
+          ++nd;
+        }
+        continue;
+      }
+      ctrl_slot *s = slot_for(m, src, m->rank, kind);
+      const uint64_t q = atomic_load_explicit(&s->seq, memory_order_acquire);
+      if (!(q & 1) && q != *seen) {
+        *seen = q;
+        ++nd;
+      }
+    }
+  }
+  if (m->dctx) {
+    for (int dir = 0; dir < 2; ++dir) {
+      dslot_state *d = dstate(m, m->rank, dir);
+      if (atomic_load_explicit(&d->claim, memory_order_seq_cst) != atomic_load_explicit(&d->pub, memory_order_seq_cst))
+        ++nf;
+    }
+    int rc = msp_ctx_synchronize(m->dctx);
+    if (rc) return rc;
+  }
+  if (discarded) *discarded = nd;
+  if (in_flight) *in_flight = nf;
+  return MSP_SUCCESS;
+}
+
 /* the device slots of src, opened on first use; NULL while src has not enabled them */
 static int peer_slots(msp_amsg *m, int src, double **out) {
   *out = m->peer[src];
@@ -317,11 +367,6 @@ int msp_amsg_destroy(msp_amsg **pm) {
 
 /* the slot direction of this rank's messages to dst (0: dst = rank - 1, 1: dst = rank + 1) */
 static int dst_rank_dir(const msp_amsg *m, int dst) { return dst == m->rank - 1 ? 0 : 1; }
-
-static ctrl_slot *slot_for(msp_amsg *m, int src, int dst, int kind) {
-  if (kind == MSP_AMSG_DATA) return data_at(m, src, dst);
-  return ctrl_at(m, src, dst, kind);
-}
 
 /* seqlock writer: seq odd, payload, seq even */
 static void write_begin(ctrl_slot *s) {
@@ -507,7 +552,11 @@ int msp_amsg_send_vec(msp_amsg *m, int32_t dst, const int32_t *ints, int32_t nin
   if (off < 0 || n < 0 || off + n > v->n || n > m->data_cap) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
   ctrl_slot *s = data_at(m, m->rank, dst);
   if (!s) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
-  if (m->dctx) return send_vec_device(m, dst, ints, nints, v, off, n);
+  if (m->dctx) { /* a plane of another context: its producer done before the copy, the copy before its next use */
+    if (v->ctx != m->dctx && (rc = msp_ctx_synchronize(v->ctx))) return rc;
+    rc = send_vec_device(m, dst, ints, nints, v, off, n);
+    return !rc && v->ctx != m->dctx ? msp_ctx_synchronize(m->dctx) : rc;
+  }
   if ((rc = ensure_registered(m))) return rc;
   write_begin(s);
   memset(s->ints, 0, sizeof(s->ints));
@@ -530,7 +579,11 @@ int msp_amsg_recv_vec(msp_amsg *m, int32_t src, int32_t *ints, int32_t nints, ms
   if (nints < 0 || nints > AMSG_INTS || (nints && !ints)) return aerr(MSP_ERR_ARG_SIZ, "at most 6 ints per message");
   if (off < 0 || cap < 0 || off + cap > v->n) return aerr(MSP_ERR_ARG_OUTOFRANGE, "range");
   if (!data_at(m, src, m->rank)) return aerr(MSP_ERR_ARG_WRONG, "iterate data only travels between chain neighbours");
-  if (m->dctx) return recv_vec_device(m, src, ints, nints, v, off, cap, n, got);
+  if (m->dctx) {
+    if (v->ctx != m->dctx && (rc = msp_ctx_synchronize(v->ctx))) return rc;
+    rc = recv_vec_device(m, src, ints, nints, v, off, cap, n, got);
+    return !rc && v->ctx != m->dctx ? msp_ctx_synchronize(m->dctx) : rc;
+  }
   if ((rc = ensure_registered(m))) return rc;
   return read_slot(m, src, MSP_AMSG_DATA, ints, nints, NULL, cap, n, got, v, off);
 }

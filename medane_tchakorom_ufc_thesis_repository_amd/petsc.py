@@ -853,6 +853,13 @@ class AsyncMessages:
         call("msp_amsg_get_stats", self.h, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def discard_pending(self) -> tuple:
+        """comm_discard_pending_messages + the MPI_Cancel of pending sends at the end of a run
+        (AMAM-global_prime.c:522-572): (messages discarded unread, own sends still in flight, completed)."""
+        a, b = C.c_int64(), C.c_int64()
+        call("msp_amsg_discard_pending", self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
     def recv_vec(self, src: int, nints: int, v: Vec, off: int, cap: int):
         iv = np.zeros(max(nints, 1), np.int32)
         n = C.c_int64()
@@ -918,6 +925,12 @@ class AsyncBroadcast:
         """(device publishes enqueued, skipped: previous copy unpublished or the buffer still read)."""
         a, b = C.c_int64(), C.c_int64()
         call("msp_abcast_get_stats", self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def discard_pending(self) -> tuple:
+        """(newer R blocks discarded unread, own publish still in flight, completed) at the end of a run."""
+        a, b = C.c_int64(), C.c_int64()
+        call("msp_abcast_discard_pending", self.h, C.byref(a), C.byref(b))
         return a.value, b.value
 
     def publish_dense(self, D: "DenseMat") -> bool:

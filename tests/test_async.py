@@ -422,12 +422,14 @@ def _am_worker(rank, world, port, problem, q):
         dim, nx, ny, nz, rtol = problem
         blk = _Block(block_layout(dim, nx, ny, nz, world, rank), po, dict(restart=30, max_it=5, rtol=1e-20))
         res = am_solve([blk], TorchComm(), rtol=rtol, max_iterations=20000)
-        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.error))
+        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.error, res.states[0],
+               res.discarded[0], res.in_flight[0]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,problem", [(2, (3, 8, 8, 8, 1e-6)), (3, (2, 24, 20, 1, 1e-5))])
+@pytest.mark.parametrize("world,problem", [(2, (3, 8, 8, 8, 1e-6)), (3, (2, 24, 20, 1, 1e-5)),
+                                           (8, (3, 6, 6, 24, 1e-6))])
 def test_am_multiprocess_gloo_terminates(world, problem):
     from test_distributed_gloo import _free_port
     ctx = mp.get_context("spawn")
@@ -450,6 +452,8 @@ def test_am_multiprocess_gloo_terminates(world, problem):
     # protocol has the same property.  The bitwise check of the protocol is the round-robin twin test above.
     assert out[0][4] <= max(10 * rtol, 1e-3) * norm0
     assert len({o[2] for o in out}) == 1                             # same phase tag at the verdict
+    assert all(o[6] == 3 for o in out)                               # every block FINISHED
+    assert all(o[7] >= 0 and o[8] == 0 for o in out)                 # host slots: nothing left in flight
 
 
 @pytest.mark.parametrize("minimization", ["lsqr", "rtr"])
@@ -498,22 +502,24 @@ def _global_worker(rank, world, port, problem, q):
         blk = _Block(block_layout(dim, nx, ny, nz, world, rank), po, dict(restart=30, max_it=max_it, rtol=1e-20))
         blk.setup_global_async_minimization(s, OUTER, minimization)
         res = am_solve([blk], TorchComm(), rtol=rtol, max_iterations=20000, variant="amam_global", s=s)
-        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.error))
+        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.error, res.states[0]))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("minimization", ["lsqr", "rtr"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_amam_global_multiprocess_gloo_terminates(world, minimization):
     """One process per block, truly asynchronous (R -- or the Gram part -- broadcast through shared
     memory while the others compute): the detection terminates every block
-    in the same phase, with one global final residual."""
-    out = _run(world, (3, 6, 6, 12, 3, 1e-6, 5, minimization), _global_worker)
+    in the same phase, with one global final residual.  At 8 processes (configs[3]/[4]'s world size)
+    the detection runs over a chain of diameter 7."""
+    out = _run(world, (3, 6, 6, 3 * world if world > 3 else 12, 3, 1e-6, 5, minimization), _global_worker)
     assert all(o[3] == out[0][3] for o in out)
     assert all(o[4] == out[0][4] for o in out)
     assert out[0][4] <= 1e-2 * out[0][3]
     assert len({o[2] for o in out}) == 1
+    assert all(o[6] == 3 for o in out)
 
 
 def test_semi_local_twins_converge(oracle):

@@ -127,6 +127,7 @@ def _am_worker(rank, world, port, problem, q):
     try:
         variant, dim, nx, ny, nz, s, max_it, rtol = problem[:8]
         minimization = problem[8] if len(problem) > 8 else "lsqr"
+        peclet = problem[9] if len(problem) > 9 else None
         b = rank
         opts = Options(f"-inner{b + 1}_ksp_max_it {max_it} -inner{b + 1}_ksp_rtol 1e-20 -inner{b + 1}_pc_type none "
                        f"-outer{b + 1}_ksp_type lsqr -outer{b + 1}_ksp_convergence_test default "
@@ -134,11 +135,12 @@ def _am_worker(rank, world, port, problem, q):
                        f"-outer{b + 1}_ksp_max_it 70 -outer{b + 1}_ksp_rtol 1e-15")
         ctx = Context(0)
         comm = TorchComm()
-        (blk,) = make_blocks(ctx, dim, nx, ny, nz, world, [rank], opts, comm)
+        (blk,) = make_blocks(ctx, dim, nx, ny, nz, world, [rank], opts, comm, peclet=peclet)
         if variant == "amam_global":
             blk.setup_global_async_minimization(s, minimization=minimization)
         res = am_solve([blk], comm, rtol=rtol, max_iterations=20000, variant=variant, s=s)
-        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.transport))
+        q.put((rank, res.iterations[0], res.phase_tags[0], res.norm0, res.final_norm, res.transport, res.states[0],
+               res.discarded[0], res.in_flight[0]))
     finally:
         dist.destroy_process_group()
 
@@ -168,6 +170,53 @@ def test_am_processes_device_transport(world, problem, nbuf, monkeypatch):
     assert all(o[3] == out[0][3] and o[4] == out[0][4] for o in out)
     assert out[0][4] <= 1e-4 * out[0][3]
     assert all(o[2] == out[0][2] for o in out)
+    assert all(o[6] == 3 for o in out)                    # every block FINISHED (constants.h State)
+
+
+PE = (0.5, 0.25, -0.3)
+
+
+@pytest.mark.parametrize("problem,nbuf", [
+    (("am", 3, 8, 8, 32, 0, 5, 1e-6), "2"),
+    (("am", 3, 8, 8, 32, 0, 5, 1e-6, "lsqr", PE), "2"),
+    (("amam_global", 3, 8, 8, 32, 4, 5, 1e-6), "2"),
+    (("amam_global", 3, 8, 8, 32, 4, 5, 1e-6), "1"),
+    (("amam_global", 3, 8, 8, 32, 4, 5, 1e-6, "lsqr", PE), "1"),
+    (("amam_global", 3, 8, 8, 32, 4, 5, 1e-6, "rtr"), "2"),
+    (("amam_global", 3, 8, 8, 32, 4, 5, 1e-6, "rtr", PE), "1"),
+], ids=["am", "am-convdiff", "amam-lsqr-nbuf2", "amam-lsqr-nbuf1", "amam-lsqr-convdiff-nbuf1", "amam-rtr-nbuf2",
+        "amam-rtr-convdiff-nbuf1"])
+def test_am_eight_processes_device_transport(problem, nbuf, monkeypatch):
+    """configs[3]/[4]'s world size: 8 processes, one block each, truly asynchronous on the one GPU -- the planes
+    and (AMAM-global) the R rows or Gram parts through HBM slots opened by IPC, the detection over a chain of
+    diameter 7 (conv_detection_prime.c:11-210; AMAM-global_prime.c:371-481).  Every process ends FINISHED in one
+    phase tag, all report the same global final residual below the threshold, each drains the messages still
+    pending and completes its sends still in flight (comm_discard_pending_messages and the MPI_Cancel calls,
+    AMAM-global_prime.c:522-572), and every process exits 0."""
+    world = 8
+    monkeypatch.setenv("MSPLIT_ABCAST_NBUF", nbuf)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_am_worker, args=(r, world, port, problem, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted([q.get(timeout=300) for _ in range(world)])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert [p.exitcode for p in procs] == [0] * world
+    assert [o[0] for o in out] == list(range(world))
+    assert all(o[5] == "device" for o in out)
+    assert all(o[6] == 3 for o in out), [o[6] for o in out]          # FINISHED
+    assert len({o[2] for o in out}) == 1, [o[2] for o in out]        # one phase tag
+    assert all(o[3] == out[0][3] and o[4] == out[0][4] for o in out)
+    assert out[0][4] <= 1e-4 * out[0][3]
+    assert all(o[7] >= 0 and o[8] >= 0 for o in out)
+    print("iterations", [o[1] for o in out], "discarded", [o[7] for o in out], "in_flight", [o[8] for o in out])
 
 
 def _comm_worker(rank, world, port, q):

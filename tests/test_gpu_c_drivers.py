@@ -340,3 +340,38 @@ def test_c_host_mpi_stop_disagreement_exits_instead_of_hanging(built, prog):
     assert p.returncode != 0
     assert "disagree" in p.stderr, p.stderr[-2000:]
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+AM = "asynchronous-multisplitting"
+PE3 = ["-peclet", "0.5,0.25,-0.3"]
+
+
+@pytest.mark.parametrize("prog,extra,nbuf", [
+    (AM, [], "2"),
+    (AM, PE3, "2"),
+    (AMAM, ["-msplit_minimization", "lsqr"], "2"),
+    (AMAM, ["-msplit_minimization", "lsqr"], "1"),
+    (AMAM, ["-msplit_minimization", "lsqr"] + PE3, "1"),
+    (AMAM, ["-msplit_minimization", "rtr"], "2"),
+    (AMAM, ["-msplit_minimization", "rtr"] + PE3, "1"),
+], ids=["am", "am-convdiff", "amam-lsqr-nbuf2", "amam-lsqr-nbuf1", "amam-lsqr-convdiff-nbuf1", "amam-rtr-nbuf2",
+        "amam-rtr-convdiff-nbuf1"])
+def test_c_host_eight_mpi_ranks_async_terminates(ctx, built, prog, extra, nbuf):
+    """configs[3]/[4]'s world size on the C host: 8 MPI ranks, one block each, truly asynchronous on the one GPU
+    (planes, and the R rows or Gram parts, through HBM slots opened by IPC; the detection over a chain of
+    diameter 7: conv_detection_prime.c:11-210, AMAM-global_prime.c:371-481).  Every rank's own report (gathered on
+    rank 0): FINISHED, one phase tag, the same global final residual below the threshold, the drain of the pending
+    messages and the completion of the sends still in flight done (comm.c:426-453, AMAM-global_prime.c:522-572),
+    and the run exits 0."""
+    args = [prog, "-dim", "3", "-m", "8", "-n", "8", "-p", "32", "-rtol", "1e-6", "-msplit_transport", "host"]
+    args += _inner(8, 5) + (["-s", "4"] + _outer(8) if prog == AMAM else []) + extra
+    r = _run(args, mpi=8, timeout=300, env={"MSPLIT_ABCAST_NBUF": nbuf})
+    rep = r["blocks_report"]
+    assert r["ranks"] == 8 and [q["block"] for q in rep] == list(range(8))
+    assert all(q["state"] == 3 for q in rep), rep                       # MSP_CVD_FINISHED
+    assert len({q["tag"] for q in rep}) == 1, rep
+    assert all(q["final_norm"] == r["final_norm"] and q["error"] == r["error"] for q in rep)
+    assert r["final_norm"] <= 1e-4 * r["norm0"]
+    assert all(q["discarded"] >= 0 and q["in_flight"] >= 0 for q in rep)
+    print("iterations", [q["iterations"] for q in rep], "discarded", [q["discarded"] for q in rep],
+          "in_flight", [q["in_flight"] for q in rep])
