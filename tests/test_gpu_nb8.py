@@ -234,10 +234,15 @@ C4_MAX_ITS = 60
 
 
 def _c4_run(ctx, blocks, comm):
-    for blk in blocks:
+    for blk in blocks:                  # x = 0 and the replicated R (or Gram parts) zeroed: MatZeroEntries(R)
         blk.x.set(0.0)
-        for D in blk.Gc_rep:
-            D.zero_entries()
+        if blk.minimization == "rtr":
+            for D in blk.Gc_rep:
+                D.zero_entries()
+        else:
+            for j, D in enumerate(blk.R_rep):
+                if j != blk.layout.b:
+                    D.zero_entries()
     def progress(b, it, ln, st, tag):   # a line per block iteration: a long run is visibly alive (pytest -s)
         print(f"configs[4] block {b} iteration {it} local residual {ln:.3e} state {st}", flush=True)
     res = am_solve(blocks, comm, rtol=C4_RTOL, record=True, variant="amam_global", s=20, max_iterations=C4_MAX_ITS,
@@ -251,7 +256,9 @@ def test_configs4_whole_eight_blocks_roundrobin_rtr(ctx):
     """BASELINE configs[4] as configured: 3D upwind convection-diffusion on 512^3 in 8 z-slab blocks of
     512 x 512 x 64, AMAM-global (AMAM-global_prime.c:371-481) with s 20, inner GMRES(30) max_it 20 rtol 1e-20,
     outer LSQR max_it 70 rtol 1e-15 (running_bulk_test_g5k:296-317), -rtol 1e-4 -- all 8 blocks round-robin on
-    this GPU with the reference's outer_solver minimization (-msplit_minimization rtr; Gram parts broadcast).
+    this GPU with the normal-equations minimization (-msplit_minimization rtr: the reference's outer_solver,
+    utils.c:972-996, on R^T R with Gram parts broadcast -- a mode of this library; AMAM-global itself calls
+    outer_solver_norm_equation, the LSQR over the replicated R: the test below).
     The run terminates by the detection protocol (every block FINISHED in one phase, no iteration cap hit), its
     blocks passed the per-block threshold rtol/sqrt(8)*||b|| in the detection's verification, and a rerun is bitwise the first run (trace, x,
     final residual).  Asynchronous runs have no reference history."""
@@ -270,6 +277,38 @@ def test_configs4_whole_eight_blocks_roundrobin_rtr(ctx):
         assert np.isfinite(res.final_norm) and res.final_norm < res.norm0
         print(f"configs[4] whole: iterations {res.iterations}, final residual {res.final_norm:.6e} "
               f"(||b|| {res.norm0:.6e}, ratio {res.final_norm / res.norm0:.3e}), {res.elapsed:.1f} s")
+        res2, fp2 = _c4_run(ctx, blocks, comm)
+        assert fp2 == fp
+    finally:
+        del blocks
+        gc.collect()
+
+
+@pytest.mark.timeout(1100)
+def test_configs4_whole_eight_blocks_roundrobin_lsqr(ctx):
+    """BASELINE configs[4] with the minimization AMAM-global actually calls: outer_solver_norm_equation
+    (AMAM-global_prime.c:425-434, utils.c:1061-1078), the LSQR over the replicated R -- every block holds all 8
+    row blocks of R as last received (8 x 2.68 GB) and the global b, and publishes its own rows newest-value.
+    3D upwind convection-diffusion 512^3 in 8 z-slab blocks of 512 x 512 x 64, all round-robin on this GPU (peak
+    282 GB of the 309 GB HBM, tools/amam_configs.py whole: profiles/r06/configs4_lsqr/), s 20, inner GMRES(30)
+    max_it 20 rtol 1e-20, outer LSQR max_it 70 rtol 1e-15, -rtol 1e-4.  The run terminates by the detection
+    (every block FINISHED in one phase, no cap hit), and a rerun is bitwise the first (trace, x, residual)."""
+    comm = LocalComm()
+    blocks = make_blocks(ctx, 3, 512, 512, 512, NB, range(NB), _opts(NB, extra="-msplit_minimization lsqr"), comm,
+                         PE)
+    try:
+        for blk in blocks:
+            blk.setup_global_async_minimization(20)
+            assert blk.minimization == "lsqr" and len(blk.R_rep) == NB
+        res, fp = _c4_run(ctx, blocks, comm)
+        assert res.converged and max(res.iterations) < C4_MAX_ITS, res.iterations
+        last = {b: st for b, _, _, st, _ in res.trace}
+        assert last == {b: ConvDetection.FINISHED for b in range(NB)}
+        assert len(set(res.phase_tags)) == 1
+        assert np.isfinite(res.final_norm) and res.final_norm < res.norm0
+        print(f"configs[4] whole (lsqr): iterations {res.iterations}, final residual {res.final_norm:.6e} "
+              f"(||b|| {res.norm0:.6e}, ratio {res.final_norm / res.norm0:.3e}), {res.elapsed:.1f} s, "
+              f"timers {res.timers}")
         res2, fp2 = _c4_run(ctx, blocks, comm)
         assert fp2 == fp
     finally:

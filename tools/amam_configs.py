@@ -12,7 +12,13 @@
              For "rtr" the same rank with 8 Gram parts instead.  Peak HBM (device-wide, sampled) and the
              minimization time.
 
+  whole      all 8 blocks of configs[4] (--n 512 --peclet ...; or configs[3] geometry at --n) round-robin on this
+             GPU, each with its replicated R, global b and broadcast buffers: HBM marks after the blocks, after the
+             minimization setup, and the peak over --its outer iterations per block (stop_at_limit), or the
+             allocation that failed.
+
   python tools/amam_configs.py pair [--peclet 0.5,0.25,-0.3] [--its 2] [--minimization lsqr,rtr]
+  python tools/amam_configs.py whole --n 512 --peclet 0.5,0.25,-0.3 --its 1 [--minimization lsqr]
   python tools/amam_configs.py footprint [--minimization lsqr|rtr]
 Prints one JSON object per measurement.
 """
@@ -163,9 +169,47 @@ def footprint(args, minimization):
             "replicated_R_GB": (8 * L.nrows * args.s * 8 / 1e9) if minimization == "lsqr" else 8 * args.s * (args.s + 1) * 8 / 1e9}
 
 
+def whole(args, minimization):
+    import torch
+    from medane_tchakorom_ufc_thesis_repository_amd.asynchronous import am_solve
+    from medane_tchakorom_ufc_thesis_repository_amd.comm import LocalComm
+    from medane_tchakorom_ufc_thesis_repository_amd.multisplitting import make_blocks
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import Context, Options
+    nb, n = 8, args.n
+    ctx = Context(0)
+    hbm = HbmSampler()
+    marks, t0 = {}, time.perf_counter()
+    out = {"mode": "whole", "minimization": minimization, "geometry": f"{n}^3 in {nb} blocks of {n}x{n}x{n // nb}",
+           "peclet": args.peclet, "s": args.s, "inner_max_it": args.inner_max_it,
+           "nbuf_env": os.environ.get("MSPLIT_ABCAST_NBUF", "0")}
+    stage = "blocks"
+    try:
+        comm = LocalComm()
+        blocks = make_blocks(ctx, 3, n, n, n, nb, range(nb), Options(options(nb, args.s, args.inner_max_it,
+                                                                            minimization)), comm, args.peclet)
+        ctx.synchronize()
+        marks["after_blocks_GB"] = hbm.used() / 1e9
+        stage = "minimization setup"
+        for blk in blocks:
+            blk.setup_global_async_minimization(args.s)
+        ctx.synchronize()
+        marks["after_minimization_setup_GB"] = hbm.used() / 1e9
+        stage = "run"
+        res = am_solve(blocks, comm, rtol=args.rtol, variant="amam_global", s=args.s, max_iterations=args.its,
+                       stop_at_limit=True)
+        torch.cuda.synchronize()
+        out.update({"iterations": res.iterations, "inner_its": res.inner_its, "elapsed_s": res.elapsed,
+                    "timers_s": res.timers, "final_norm": res.final_norm, "norm0": res.norm0, "ok": True})
+    except Exception as e:                            # an allocation that does not fit: say which stage
+        out.update({"ok": False, "failed_stage": stage, "error": str(e)[:300]})
+    out.update({"hbm": hbm.stop(), "hbm_marks": marks, "wall_s": time.perf_counter() - t0})
+    return out
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("mode", choices=["pair", "footprint"])
+    p.add_argument("mode", choices=["pair", "footprint", "whole"])
+    p.add_argument("--n", type=int, default=512)
     p.add_argument("--minimization", default="lsqr,rtr")
     p.add_argument("--peclet", default=None)
     p.add_argument("--its", type=int, default=2)
@@ -177,7 +221,7 @@ def main():
     import torch
     torch.cuda.set_device(0)
     for m in a.minimization.split(","):
-        out = pair(a, m) if a.mode == "pair" else footprint(a, m)
+        out = pair(a, m) if a.mode == "pair" else footprint(a, m) if a.mode == "footprint" else whole(a, m)
         print(json.dumps(out), flush=True)
 
 
