@@ -290,17 +290,22 @@ def build_smsm(ctx, args, comm, world, rank):
     mini = GpuMinimizer(ctx, [blk], comm, o, prefix="outer1_")
     blk.reset_halo()
     lsqr_its = []
+    lsqr_rnorm = []                         # KSPGetResidualNorm of each step's LSQR: the outer history
+    inner_its = []
 
     def step():
         its = 0
         for k in range(args.s):
             blk.update_rhs()                # updateLocalRHS
-            its += blk.solve()              # inner_solver
+            k_its = blk.solve()             # inner_solver
+            its += k_its
+            inner_its.append(k_its)
             comm.exchange([blk])            # comm_sync_send_and_receive
             blk.store_column(k)             # S(:, k) = x
         blk.form_R()                        # R = A S
-        _, lits, _ = mini.solve([blk])      # LSQR, x = S alpha
+        rn, lits, _ = mini.solve([blk])     # LSQR, x = S alpha
         lsqr_its.append(lits)
+        lsqr_rnorm.append(rn)
         return its
     transport = {"local": "single block", "nccl": "one library RCCL communicator",
                  "gloo": "gloo (rehearsal: the library's host transport)"}[getattr(comm, "backend", "local")]
@@ -310,7 +315,50 @@ def build_smsm(ctx, args, comm, world, rank):
                 f"(one per MI355X), s = {args.s} inner GMRES({args.restart}) solves of max_it {args.inner_max_it} "
                 f"per outer iteration, LSQR max_it {args.outer_max_it}; {transport} for the exchange, residual sums "
                 f"and LSQR partials (configs[2] at N = 2)")
+    step.lsqr_rnorm, step.inner_its, step.lsqr_its = lsqr_rnorm, inner_its, lsqr_its
     return step, workload, kspopts, n * n * args.smsm_planes, (blk, mini, lsqr_its)
+
+
+SMSM_BLOCK_GOLDEN = os.path.join(ROOT, "tests", "golden", "smsm_block.json")
+
+
+def smsm_block_record(args, order):
+    """The committed oracle record of exactly the N = 1 SMSM block (tests/golden/smsm_block.json, written by
+    tests/golden/make_smsm_block.py: one 512 x 512 x 256 z-slab block, configs[2]'s options, outer iterations from
+    x = 0 in the DBR order -- the smsm_per_gpu warm-up and timed steps -- and one in PETSc's order -- the
+    smsm_seq_mode step), or None when the bench runs another block."""
+    if not os.path.exists(SMSM_BLOCK_GOLDEN):
+        return None
+    g = json.load(open(SMSM_BLOCK_GOLDEN))
+    P, inn, out = g["problem"], g["inner"], g["outer"]
+    if (args.smsm_mesh, args.smsm_planes, args.s, args.inner_max_it, args.outer_max_it, args.restart) != (
+            P["nx"], P["nz"], P["s"], inn["max_it"], out["max_it"], inn["restart"]) or args.peclet is not None:
+        return None
+    return g.get(order)
+
+
+def check_smsm_block(step, blk, ref, nsteps):
+    """(verified, mismatches): the first nsteps outer iterations of an SMSM block run against its oracle record --
+    every LSQR residual (hex), LSQR count and inner count, and the SHA-256 of x after the last one."""
+    import hashlib
+    import numpy as np
+    if ref is None:
+        return None, ["no record for this block"]
+    if nsteps > len(ref["hist_hex"]):
+        return None, [f"record holds {len(ref['hist_hex'])} outer iterations, the run did {nsteps}"]
+    bad = []
+    if [float(h).hex() for h in step.lsqr_rnorm[:nsteps]] != ref["hist_hex"][:nsteps]:
+        bad.append("hist_hex")
+    if list(step.lsqr_its[:nsteps]) != ref["lsqr_its"][:nsteps]:
+        bad.append("lsqr_its")
+    want_inner = [v for outer in ref["inner_its"][:nsteps] for v in outer]
+    if step.inner_its[:len(want_inner)] != want_inner:
+        bad.append("inner_its")
+    if nsteps == len(ref["hist_hex"]):
+        xs = hashlib.sha256(np.ascontiguousarray(blk.x.get_array(), np.float64).tobytes()).hexdigest()
+        if xs != ref["x_sha256"]:
+            bad.append("x_sha256")
+    return not bad, bad
 
 
 def smsm_n1(ctx, args):
@@ -325,10 +373,16 @@ def smsm_n1(ctx, args):
     its = sum(step() for _ in range(args.smsm_n1_steps))
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # after timing: the warm-up and every timed outer iteration against the DBR oracle record of this block
+    ok, bad = check_smsm_block(step, blk, smsm_block_record(args, "dbr"), 1 + args.smsm_n1_steps)
     mini.close()
     return {"workload": workload, "value": rows * its / dt, "unit": "DOF-updates/s", "steps": args.smsm_n1_steps,
             "warmup": 1, "ms_per_step": 1e3 * dt / args.smsm_n1_steps,
             "gmres_iterations_per_step": its / args.smsm_n1_steps, "lsqr_iterations_per_step": lsqr_its[1:],
+            "verified": ok, "mismatch": bad,
+            "reference": "tests/golden/smsm_block.json['dbr'] (oracle/oracle.c orc_smsm_solve, DBR order, lean): "
+                         "every outer LSQR residual (hex), LSQR and inner count of the warm-up and timed steps, and "
+                         "the SHA-256 of x after them",
             "note": "same per-GPU block and step as the N > 1 lines: N-GPU scaling of SMSM = "
                     "value(N) / (N x this value)"}
 
@@ -617,11 +671,20 @@ def smsm_seq_mode(ctx, args):
         its = step()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        # after timing: the timed full-size outer iteration against the PETSc-order oracle record of this block
+        ok_full, bad_full = check_smsm_block(step, blk, smsm_block_record(args, "seq"), 1)
         mini.close()
     finally:
         ctx.set_reduction("dbr")
+    out["small_block"] = {"verified": out["verified"], "mismatch": out["mismatch"]}
+    out["verified"] = (ok_full if out["verified"] is None else (out["verified"] and ok_full)
+                       if ok_full is not None else None)
+    out["mismatch"] = out["mismatch"] + [f"full block: {m}" for m in bad_full]
     out.update({"workload": workload, "value": rows * its / dt, "unit": "DOF-updates/s", "seconds_per_step": dt,
                 "gmres_iterations": its, "lsqr_iterations": lsqr_its[-1],
+                "full_block_reference": "tests/golden/smsm_block.json['seq'] (oracle/oracle.c orc_smsm_solve, "
+                                        "ORC_REDUCE_SEQ, lean): the LSQR residual (hex), LSQR and inner counts and "
+                                        "the SHA-256 of x of the timed outer iteration",
                 "note": "the parity mode on the SMSM block (configs[2]'s per-GPU workload): one outer iteration"})
     return out
 
@@ -891,6 +954,8 @@ def main():
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     failed = (verified is False or (extras.get("seq_mode") or {}).get("verified") is False
+              or (extras.get("smsm_per_gpu") or {}).get("verified") is False
+              or (extras.get("smsm_seq_mode") or {}).get("verified") is False
               or (extras.get("assembled_csr_operator") or {}).get("verified") is False
               or (extras.get("non_stencil_aij") or {}).get("verified") is False)
     if variant == "smsm":

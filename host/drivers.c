@@ -336,6 +336,7 @@ typedef struct {
   const msd_transport *t;
   msd_block *blk[MSD_MAX_BLOCKS];
   int nlocal;
+  int fault_stop_rank; /* MSPLIT_FAULT_STOP_RANK, read once at setup (-1: none) */
 } msd_run;
 
 static int ordered_sum(msd_run *R, const double *v, double *out) { /* block order, from 0.0 */
@@ -377,10 +378,12 @@ static int sum_over_blocks(msd_run *R, int (*f)(msd_block *, double *), double *
 /* Every rank takes the same stop decision at the same outer iteration (synchronous-multisplitting.c:187-206 assumes
  * it; a rank that stops alone leaves the others waiting in their next collective forever): one msp_comm_agree of
  * (outer_its, stop) per outer iteration, an error on every rank on a mismatch.  MSPLIT_FAULT_STOP_RANK=r flips rank
- * r's decision at the first outer iteration (the tests' fault injection; multisplitting.py agree_on_stop). */
+ * r's decision at the first outer iteration (the tests' fault injection; multisplitting.py agree_on_stop).  The
+ * guard cannot ride on the residual sum's all-gather: the stop decision is taken from that sum's result, and a rank
+ * that stopped alone would be missing from the next one.  Its price is one 8-byte all-gather per outer iteration
+ * (an outer iteration is s inner GMRES solves: SMSM-global's per-GPU block, about 1 s). */
 static int agree_on_stop(msd_run *R, int outer_its, int *stop) {
-  const char *f = getenv("MSPLIT_FAULT_STOP_RANK");
-  if (f && atoi(f) == R->t->rank && outer_its == 1) *stop = !*stop;
+  if (R->fault_stop_rank == R->t->rank && outer_its == 1) *stop = !*stop;
   if (R->t->world == 1) return MSP_SUCCESS;
   int32_t ok = 0;
   const int rc = msp_comm_agree(R->t->comm, (int64_t)outer_its * 2 + (*stop ? 1 : 0), &ok);
@@ -414,6 +417,8 @@ static int setup_run(msp_ctx *ctx, const msd_problem *p, const msd_options *o, c
                      msd_block *store) {
   memset(R, 0, sizeof(*R));
   R->t = t;
+  const char *fault = getenv("MSPLIT_FAULT_STOP_RANK");
+  R->fault_stop_rank = fault && *fault ? atoi(fault) : -1;
   if (t->world > 1) {
     if (p->nb != t->world) {
       fprintf(stderr, "one block per rank: %d blocks on %d ranks\n", p->nb, t->world);

@@ -713,7 +713,9 @@ static bool box_dictionary(int32_t nrows, std::vector<int32_t>& dd, std::vector<
 static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, const double* val) {
   msp_ctx* c = A->ctx;
   const int32_t n = A->nrows;
-  if (A->compressed || A->matfree || n == 0 || A->ncols != n || A->dv_on || !dv_default()) return MSP_SUCCESS;
+  // built whatever MSPLIT_MAT_STORAGE says (as the DV storage is): under "csr" the products stay in CSR until
+  // msp_mat_set_storage(MSP_STORAGE_STENCIL) switches
+  if (A->compressed || A->matfree || n == 0 || A->ncols != n || A->dv_on) return MSP_SUCCESS;
   std::vector<int32_t> dd;
   for (int32_t r = 0; r < n; ++r)
     for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
@@ -732,12 +734,6 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
   // MSPLIT_RV_LAYOUT=soa (per-leg arrays; the A/B)
   const char* lay = getenv("MSPLIT_RV_LAYOUT");
   const bool blocked = !(lay && strcmp(lay, "soa") == 0) && n % MSK_DBR_CHUNK == 0;
-  const size_t need = (size_t)n + 16 + (size_t)7 * stride * sizeof(double);
-  size_t fr = 0, tot = 0;
-  if (mspi_mem_info(c, &fr, &tot) || fr < need + (tot >> 5)) {  // keep 1/32 of HBM free after it
-    (void)hipGetLastError();
-    return MSP_SUCCESS;
-  }
   std::vector<uint8_t> mask((size_t)n + 16, 0);
   std::vector<double> rv((size_t)7 * stride, 0.0);  // per-leg arrays first
   for (int32_t r = 0; r < n; ++r)
@@ -770,6 +766,13 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
       }
   }
   const int nleg = sym ? 4 : 7;
+  // the HBM it takes, sized once the leg count is known (the symmetric storage needs four legs, not seven)
+  const size_t need = (size_t)n + 16 + (size_t)nleg * stride * sizeof(double);
+  size_t fr = 0, tot = 0;
+  if (mspi_mem_info(c, &fr, &tot) || fr < need + (tot >> 5)) {  // keep 1/32 of HBM free after it
+    (void)hipGetLastError();
+    return MSP_SUCCESS;
+  }
   if (blocked) {  // chunk-blocked: the legs of each 512-row slice of a DBR chunk next to each other
     std::vector<double> bl((size_t)nleg * stride, 0.0);
     const int legs[7] = {0, 1, 2, 3, 4, 5, 6}, sym_legs[4] = {3, 4, 5, 6};  // d, x+1, y+1, z+1
@@ -810,7 +813,7 @@ static int rv_attach(msp_mat* A, const int32_t* rowptr, const int32_t* col, cons
   A->march_nz = nz;
   A->march_d2 = 0;
   A->march_halo = 0;
-  A->rv_on = true;
+  A->rv_on = dv_default();
   return MSP_SUCCESS;
 }
 

@@ -376,14 +376,19 @@ class SMResult:
     elapsed: float = 0.0
 
 
-def agree_on_stop(comm, outer_its: int, stop: bool) -> bool:
+def fault_stop_rank() -> int:
+    """MSPLIT_FAULT_STOP_RANK (the tests' fault injection), read once when a solve sets up; -1: none."""
+    v = os.environ.get("MSPLIT_FAULT_STOP_RANK")
+    return int(v) if v else -1
+
+
+def agree_on_stop(comm, outer_its: int, stop: bool, fault: int = -1) -> bool:
     """Every rank must take the same stop decision at the same outer iteration, or the next collective of the
     rank that goes on waits forever for the one that stopped (synchronous-multisplitting.c:187-206 assumes
     agreement).  One all-gather of (outer_its, stop) per outer iteration (comm.agree, msp_comm_agree) turns a
     disagreement -- e.g. from a transport fault -- into an error on every rank.  MSPLIT_FAULT_STOP_RANK=r flips
     rank r's decision at the first outer iteration: the fault injection the tests use."""
-    fault = os.environ.get("MSPLIT_FAULT_STOP_RANK")
-    if fault is not None and int(fault) == comm.rank and outer_its == 1:
+    if fault == comm.rank and outer_its == 1:
         stop = not stop
     if comm.world > 1:
         comm.agree(outer_its * 2 + int(stop))
@@ -394,6 +399,7 @@ def sm_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_outer: int = 1
              monitor=None) -> SMResult:
     """The synchronous multisplitting outer loop (synchronous-multisplitting.c:155-206)."""
     res = SMResult()
+    fault = fault_stop_rank()
     # global_norm_0 (:162): sqrt of the block-ordered sum of squared local norms
     res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
     for blk in blocks:                                      # updateLocalRHS before the loop (:164)
@@ -415,7 +421,8 @@ def sm_solve(blocks, comm, rtol: float, atol: float = 1e-100, max_outer: int = 1
         if monitor:
             monitor(res.outer_its, norm, its)
         # (:198) and the outer cap, agreed by every rank
-        if agree_on_stop(comm, res.outer_its, norm <= max(atol, rtol * res.norm0) or res.outer_its >= max_outer):
+        if agree_on_stop(comm, res.outer_its, norm <= max(atol, rtol * res.norm0) or res.outer_its >= max_outer,
+                         fault):
             break
     comm.barrier()
     res.elapsed = time.perf_counter() - t0
@@ -478,6 +485,7 @@ def smsm_solve(blocks, comm, s: int, minimizer, rtol: float, atol: float = 1e-10
     s times {rhs_i = b_i - A_ij x_j; inner GMRES; exchange; S(:,k) = x},
     R = A S, alpha = LSQR(R, b), x = S alpha; stop on the LSQR residual norm."""
     res = SMSMResult()
+    fault = fault_stop_rank()
     # global_norm_0 = computeFinalResidualNorm at x = 0 (:280)
     res.norm0 = math.sqrt(comm.ordered_sum(blocks, [blk.norm0_sq() for blk in blocks]))
     for blk in blocks:
@@ -504,7 +512,8 @@ def smsm_solve(blocks, comm, s: int, minimizer, rtol: float, atol: float = 1e-10
         if monitor:
             monitor(res.outer_its, norm, its_outer, lits)
         # (:342) and the outer cap, agreed by every rank
-        if agree_on_stop(comm, res.outer_its, norm <= max(atol, rtol * res.norm0) or res.outer_its >= max_outer):
+        if agree_on_stop(comm, res.outer_its, norm <= max(atol, rtol * res.norm0) or res.outer_its >= max_outer,
+                         fault):
             break
     comm.barrier()
     res.elapsed = time.perf_counter() - t0

@@ -17,6 +17,7 @@
 #endif
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -240,6 +241,93 @@ void orc_residual(const orc_csr *A, const double *b, const double *x, double *r)
   }
 }
 
+/* ---- Operators for the memory-lean records (orc_smsm_solve with lean = 1; test infrastructure) ----
+ * An operator is either assembled rows (orc_csr) or the rows [r0, r1) of the dim-3 nx x ny x nz operator of
+ * orc_convdiff_rows applied without storage (at P = 0 its values, -1 and 6, and its column order are exactly
+ * orc_poisson3d_rows').  A stencil row sums the CSR row's terms in the CSR's column order from 0.0, so
+ * op_spmv / op_residual are bit for bit orc_spmv / orc_residual of the assembled rows -- of the whole block rows
+ * (OP_BLOCK, global columns), of orc_split's A_ii (OP_DIAG, columns in [r0, r1) shifted by -r0) or of its
+ * coupling rows (OP_OFF, the other columns, global).  tests/test_oracle.py holds lean = 1 to lean = 0. */
+enum { OP_BLOCK = 0, OP_DIAG = 1, OP_OFF = 2 };
+
+typedef struct {
+  const orc_csr *A; /* assembled, or NULL: the stencil */
+  int part;
+  int64_t nx, ny, nz, r0, r1;
+  double lo[3], up[3], diag; /* lower / upper neighbour values in x, y, z; diagonal */
+} orc_op;
+
+static orc_op op_csr(const orc_csr *A) {
+  orc_op o;
+  memset(&o, 0, sizeof(o));
+  o.A = A;
+  return o;
+}
+
+static orc_op op_stencil(int nx, int ny, int nz, int64_t r0, int64_t r1, const double *P, int part) {
+  orc_op o;
+  memset(&o, 0, sizeof(o));
+  o.part = part;
+  o.nx = nx, o.ny = ny, o.nz = nz, o.r0 = r0, o.r1 = r1;
+  for (int d = 0; d < 3; ++d) {
+    o.lo[d] = cd_lower(P[d]);
+    o.up[d] = cd_upper(P[d]);
+  }
+  o.diag = ((6.0 + 2.0 * fabs(P[0])) + 2.0 * fabs(P[1])) + 2.0 * fabs(P[2]);
+  return o;
+}
+
+static int64_t op_rows(const orc_op *o) { return o->A ? o->A->nrows : o->r1 - o->r0; }
+
+/* one term of a stencil row: column c (global) with value v, if this operator's part holds it */
+#define OP_TERM(o, c, v, x, s)                                            \
+  do {                                                                    \
+    const int64_t c_ = (c);                                               \
+    const int in_ = c_ >= (o)->r0 && c_ < (o)->r1;                        \
+    if ((o)->part == OP_BLOCK) (s) += (v) * (x)[c_];                      \
+    else if ((o)->part == OP_DIAG) { if (in_) (s) += (v) * (x)[c_ - (o)->r0]; } \
+    else if (!in_) (s) += (v) * (x)[c_];                                  \
+  } while (0)
+
+/* row lr of the operator applied to x (x indexed as the part's columns) */
+static inline double op_row(const orc_op *o, int64_t lr, const double *x) {
+  double s = 0.0;
+  if (o->A) {
+    for (int32_t k = o->A->rowptr[lr]; k < o->A->rowptr[lr + 1]; ++k) s += o->A->val[k] * x[o->A->col[k]];
+    return s;
+  }
+  const int64_t g = o->r0 + lr, nx = o->nx, pl = o->nx * o->ny;
+  const int64_t i = g % nx, j = (g / nx) % o->ny, k = g / pl;
+  if (k > 0) OP_TERM(o, g - pl, o->lo[2], x, s);
+  if (j > 0) OP_TERM(o, g - nx, o->lo[1], x, s);
+  if (i > 0) OP_TERM(o, g - 1, o->lo[0], x, s);
+  OP_TERM(o, g, o->diag, x, s);
+  if (i < nx - 1) OP_TERM(o, g + 1, o->up[0], x, s);
+  if (j < o->ny - 1) OP_TERM(o, g + nx, o->up[1], x, s);
+  if (k < o->nz - 1) OP_TERM(o, g + pl, o->up[2], x, s);
+  return s;
+}
+
+static void op_spmv(const orc_op *o, const double *x, double *y) {
+  if (o->A) {
+    orc_spmv(o->A, x, y);
+    return;
+  }
+  const int64_t n = op_rows(o);
+  ORC_PAR
+  for (int64_t r = 0; r < n; ++r) y[r] = op_row(o, r, x);
+}
+
+static void op_residual(const orc_op *o, const double *b, const double *x, double *r) {
+  if (o->A) {
+    orc_residual(o->A, b, x, r);
+    return;
+  }
+  const int64_t n = op_rows(o);
+  ORC_PAR
+  for (int64_t row = 0; row < n; ++row) r[row] = b[row] - op_row(o, row, x);
+}
+
 /* Butterfly over one wave of 64 lane values: v[l] <- v[l] + v[l ^ off],
  * off = 32,16,...,1.  Lane 0 holds the result (all lanes agree). */
 static double dbr_wave(const double *lanes) {
@@ -259,34 +347,47 @@ static double dbr_group(const double *lanes) {
   return (w0 + w1) + (w2 + w3);
 }
 
-/* Deterministic blocked reduction of sum_i x[i]*y[i] (the device order). */
-static double dbr_dot(int64_t n, const double *x, const double *y) {
-  const int64_t nchunks = (n + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
-  double *part = (double *)malloc((size_t)(nchunks > 0 ? nchunks : 1) * sizeof(double));
+/* One DBR chunk of sum_i x[i]*y[i] over its len <= ORC_DBR_CHUNK elements (x, y at the chunk's first element):
+ * lane t accumulates its elements j*(threads*vw) + vw*t + v in order, then the workgroup combine. */
+static double dbr_chunk(int64_t len, const double *x, const double *y) {
   double lanes[ORC_DBR_THREADS];
-  /* chunks are independent: threads split them, each chunk's arithmetic unchanged */
-  ORC_PAR
-  for (int64_t c = 0; c < nchunks; ++c) {
-    const int64_t base = c * ORC_DBR_CHUNK;
-    double lanes[ORC_DBR_THREADS];
-    for (int t = 0; t < ORC_DBR_THREADS; ++t) {
-      double acc = 0.0;
-      for (int j = 0; j < ORC_DBR_ITERS; ++j) {
-        const int64_t e = base + (int64_t)j * (ORC_DBR_THREADS * ORC_DBR_VW) + ORC_DBR_VW * t;
-        for (int v = 0; v < ORC_DBR_VW; ++v)
-          if (e + v < n) acc += x[e + v] * y[e + v];
-      }
-      lanes[t] = acc;
+  for (int t = 0; t < ORC_DBR_THREADS; ++t) {
+    double acc = 0.0;
+    for (int j = 0; j < ORC_DBR_ITERS; ++j) {
+      const int64_t e = (int64_t)j * (ORC_DBR_THREADS * ORC_DBR_VW) + ORC_DBR_VW * t;
+      for (int v = 0; v < ORC_DBR_VW; ++v)
+        if (e + v < len) acc += x[e + v] * y[e + v];
     }
-    part[c] = dbr_group(lanes);
+    lanes[t] = acc;
   }
+  return dbr_group(lanes);
+}
+
+/* The second DBR stage: the chunk partials, lane t taking chunks t, t + threads, ... in order. */
+static double dbr_finish(int64_t nchunks, const double *part) {
+  double lanes[ORC_DBR_THREADS];
   for (int t = 0; t < ORC_DBR_THREADS; ++t) {
     double acc = 0.0;
     for (int64_t i = t; i < nchunks; i += ORC_DBR_THREADS) acc += part[i];
     lanes[t] = acc;
   }
-  free(part);
   return dbr_group(lanes);
+}
+
+/* Deterministic blocked reduction of sum_i x[i]*y[i] (the device order). */
+static double dbr_dot(int64_t n, const double *x, const double *y) {
+  const int64_t nchunks = (n + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
+  double *part = (double *)malloc((size_t)(nchunks > 0 ? nchunks : 1) * sizeof(double));
+  /* chunks are independent: threads split them, each chunk's arithmetic unchanged */
+  ORC_PAR
+  for (int64_t c = 0; c < nchunks; ++c) {
+    const int64_t base = c * ORC_DBR_CHUNK;
+    const int64_t len = n - base < ORC_DBR_CHUNK ? n - base : ORC_DBR_CHUNK;
+    part[c] = dbr_chunk(len, x + base, y + base);
+  }
+  const double r = dbr_finish(nchunks, part);
+  free(part);
+  return r;
 }
 
 /* VecDot / BLAS ddot order: sequential (reference ddot's unroll-by-5 is
@@ -366,7 +467,7 @@ void orc_gmres_default_opts(orc_gmres_opts *o) {
 }
 
 typedef struct {
-  const orc_csr *A;
+  const orc_op *A;
   const double *b;
   double *x;
   const orc_gmres_opts *o;
@@ -523,7 +624,7 @@ static void gm_cycle(gm_t *g, int *itcount) {
   while (!g->reason && it < g->m && g->its < g->o->max_it) {
     if (it) gm_log(g, res);
     /* KSP_PCApplyBAorAB, PCNONE: VV(it+1) = A * VV(it) */
-    orc_spmv(g->A, g->VV[it], g->VV[it + 1]);
+    op_spmv(g->A, g->VV[it], g->VV[it + 1]);
     gm_cgs(g, it);
     if (g->reason) break;
     const double tt = gm_normalize(g, g->VV[it + 1]);
@@ -554,16 +655,15 @@ static void gm_cycle(gm_t *g, int *itcount) {
 }
 
 /* KSPSolve -> KSPSolve_GMRES [PETSc-ext] */
-int orc_gmres_solve(const orc_csr *A, const double *b, double *x, const orc_gmres_opts *o,
-                    orc_gmres_result *res, double *hist, int hist_cap) {
-  if (!A || !o || o->restart < 1 || A->nrows != A->ncols) return ORC_ERR_ARG;
+static int gmres_solve_op(const orc_op *A, const double *b, double *x, const orc_gmres_opts *o,
+                          orc_gmres_result *res, double *hist, int hist_cap) {
   gm_t g;
   memset(&g, 0, sizeof(g));
   g.A = A;
   g.b = b;
   g.x = x;
   g.o = o;
-  g.n = A->nrows;
+  g.n = op_rows(A);
   g.m = o->restart;
   g.hist = hist;
   g.hist_cap = hist_cap;
@@ -592,7 +692,7 @@ int orc_gmres_solve(const orc_csr *A, const double *b, double *x, const orc_gmre
   while (!g.reason) {
     /* KSPInitialResidual: r = b - A x (VecCopy + VecAXPY(-1)), or r = b for a zero guess */
     if (!g.guess_zero) {
-      orc_spmv(A, x, g.tmp);
+      op_spmv(A, x, g.tmp);
       for (int64_t i = 0; i < n; ++i) g.VV[0][i] = b[i] + (-1.0) * g.tmp[i];
     } else {
       memcpy(g.VV[0], b, (size_t)n * sizeof(double));
@@ -616,6 +716,13 @@ int orc_gmres_solve(const orc_csr *A, const double *b, double *x, const orc_gmre
   return ORC_OK;
 }
 
+int orc_gmres_solve(const orc_csr *A, const double *b, double *x, const orc_gmres_opts *o,
+                    orc_gmres_result *res, double *hist, int hist_cap) {
+  if (!A || !o || o->restart < 1 || A->nrows != A->ncols) return ORC_ERR_ARG;
+  const orc_op op = op_csr(A);
+  return gmres_solve_op(&op, b, x, o, res, hist, hist_cap);
+}
+
 /* ------------------------------------------------------------------------ */
 /* Reference glue                                                            */
 /* ------------------------------------------------------------------------ */
@@ -630,6 +737,19 @@ double orc_final_residual_norm(int mode, int nb, const orc_csr *const *Ab, const
     double *r = (double *)malloc((size_t)(Ab[b]->nrows > 0 ? Ab[b]->nrows : 1) * sizeof(double));
     orc_residual(Ab[b], bb[b], x, r);
     const double ln = orc_norm2(mode, Ab[b]->nrows, r);
+    total += ln * ln;
+    free(r);
+  }
+  return sqrt(total);
+}
+
+static double final_residual_norm_op(int mode, int nb, const orc_op *Ab, const double *x, const double *const *bb) {
+  double total = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    const int64_t n = op_rows(&Ab[b]);
+    double *r = (double *)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    op_residual(&Ab[b], bb[b], x, r);
+    const double ln = orc_norm2(mode, n, r);
     total += ln * ln;
     free(r);
   }
@@ -879,6 +999,219 @@ static void ls_aypx(int64_t n, double *y, double a, const double *x) {
   }
 }
 
+/* The LSQR operator R as nblk row blocks: stored (R[b] + j*lda[b]), or -- the memory-lean records -- formed on
+ * the fly as R_b = A_b S (A_b the block's rows over global columns, S column j at S + j*lds): every element is
+ * the stored R's element (op_row is orc_spmv's row), so every sum below is bit for bit the stored one. */
+#define ORC_RS_MAXS 256 /* columns of an on-the-fly R (s) */
+
+typedef struct {
+  const double *const *R;
+  const int64_t *lda;
+  const orc_op *A;
+  const double *S;
+  int64_t lds;
+} ls_rsrc;
+
+/* rows [i0, i1) of block b, columns [j0, j1), into buf (column-major, leading dimension i1 - i0).  A stencil row's
+ * legs are found once per row (a presence mask) and then applied column by column, each column's rows in order:
+ * every element still sums its row's terms in the row's order from 0.0. */
+static void rs_fill(const ls_rsrc *src, int b, int64_t i0, int64_t i1, int j0, int j1, double *buf) {
+  const int64_t m = i1 - i0;
+  const orc_op *o = &src->A[b];
+  if (o->A || o->part != OP_BLOCK) {
+    for (int j = j0; j < j1; ++j) {
+      const double *Sj = src->S + (int64_t)j * src->lds;
+      double *d = buf + (int64_t)(j - j0) * m;
+      for (int64_t i = i0; i < i1; ++i) d[i - i0] = op_row(o, i, Sj);
+    }
+    return;
+  }
+  const int64_t nx = o->nx, pl = o->nx * o->ny;
+  const int64_t off[7] = {-pl, -nx, -1, 0, 1, nx, pl};
+  const double val[7] = {o->lo[2], o->lo[1], o->lo[0], o->diag, o->up[0], o->up[1], o->up[2]};
+  uint8_t *mask = (uint8_t *)malloc((size_t)(m > 0 ? m : 1));
+  for (int64_t r = i0; r < i1; ++r) {
+    const int64_t g = o->r0 + r, i = g % nx, jy = (g / nx) % o->ny, k = g / pl;
+    mask[r - i0] = (uint8_t)((k > 0) | (jy > 0) << 1 | (i > 0) << 2 | 1 << 3 | (i < nx - 1) << 4 |
+                             (jy < o->ny - 1) << 5 | (k < o->nz - 1) << 6);
+  }
+  for (int j = j0; j < j1; ++j) {
+    const double *Sj = src->S + (int64_t)j * src->lds + o->r0;
+    double *d = buf + (int64_t)(j - j0) * m;
+    for (int64_t r = i0; r < i1; ++r) {
+      const uint8_t mk = mask[r - i0];
+      const double *c = Sj + r;
+      double acc = 0.0;
+      if (mk == 0x7f) {
+        acc += val[0] * c[off[0]];
+        acc += val[1] * c[off[1]];
+        acc += val[2] * c[off[2]];
+        acc += val[3] * c[0];
+        acc += val[4] * c[off[4]];
+        acc += val[5] * c[off[5]];
+        acc += val[6] * c[off[6]];
+      } else {
+        for (int t = 0; t < 7; ++t)
+          if (mk >> t & 1) acc += val[t] * c[off[t]];
+      }
+      d[r - i0] = acc;
+    }
+  }
+  free(mask);
+}
+
+/* U1_b = R_b V (orc_dense_mult's row order) */
+static void rs_mult(const ls_layout *L, const ls_rsrc *src, const double *V, double *const *U1) {
+  for (int b = 0; b < L->nblk; ++b) {
+    if (src->R) {
+      orc_dense_mult(L->n[b], L->s, src->R[b], src->lda[b], V, U1[b]);
+      continue;
+    }
+    const int64_t n = L->n[b], nt = (n + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
+    ORC_PAR
+    for (int64_t t = 0; t < nt; ++t) {
+      const int64_t i0 = t * ORC_DBR_CHUNK, i1 = i0 + ORC_DBR_CHUNK < n ? i0 + ORC_DBR_CHUNK : n, m = i1 - i0;
+      double *tile = (double *)malloc((size_t)(m * L->s) * sizeof(double));
+      rs_fill(src, b, i0, i1, 0, L->s, tile);
+      orc_dense_mult(m, L->s, tile, m, V, U1[b] + i0);
+      free(tile);
+    }
+  }
+}
+
+/* DBR dots of every column of R_b with y_b (y_b = NULL: with itself), out[j] */
+static void rs_dbr_block_dots(const ls_layout *L, const ls_rsrc *src, int b, const double *y, double *out) {
+  const int64_t n = L->n[b], nc = (n + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
+  const int s = L->s;
+  double *part = (double *)malloc((size_t)((nc > 0 ? nc : 1) * s) * sizeof(double));
+  ORC_PAR
+  for (int64_t c = 0; c < nc; ++c) {
+    const int64_t i0 = c * ORC_DBR_CHUNK, m = n - i0 < ORC_DBR_CHUNK ? n - i0 : ORC_DBR_CHUNK;
+    double *tile = (double *)malloc((size_t)(m * s) * sizeof(double));
+    rs_fill(src, b, i0, i0 + m, 0, s, tile);
+    for (int j = 0; j < s; ++j) {
+      const double *col = tile + (int64_t)j * m;
+      part[(int64_t)j * nc + c] = dbr_chunk(m, col, y ? y + i0 : col);
+    }
+    free(tile);
+  }
+  for (int j = 0; j < s; ++j) out[j] = dbr_finish(nc, part + (int64_t)j * nc);
+  free(part);
+}
+
+/* rows [i0, i0 + m) of block b, every column, filled by tiles in parallel (the sequential consumers stream them) */
+static void rs_fill_rows(const ls_rsrc *src, int b, int s, int64_t i0, int64_t m, double *buf) {
+  const int64_t nt = (m + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
+  ORC_PAR
+  for (int64_t t = 0; t < nt; ++t) {
+    const int64_t a = t * ORC_DBR_CHUNK, e = a + ORC_DBR_CHUNK < m ? a + ORC_DBR_CHUNK : m;
+    double *tile = (double *)malloc((size_t)((e - a) * s) * sizeof(double));
+    rs_fill(src, b, i0 + a, i0 + e, 0, s, tile);
+    for (int j = 0; j < s; ++j) memcpy(buf + (int64_t)j * m + a, tile + (int64_t)j * (e - a), (size_t)(e - a) * sizeof(double));
+    free(tile);
+  }
+}
+
+#define RS_BATCH ((int64_t)1 << 18) /* rows per batch of the sequential (SEQ-order) streams */
+
+/* MatMultTranspose(R, u, out) */
+static void rs_mult_transpose(const ls_layout *L, const ls_rsrc *src, const double *const *u, double *out) {
+  if (src->R) {
+    ls_mult_transpose(L, src->R, src->lda, u, out);
+    return;
+  }
+  const int s = L->s;
+  if (L->mode == ORC_REDUCE_SEQ) { /* one running sum per column over all rows, block 0's rows first */
+    for (int j = 0; j < s; ++j) out[j] = 0.0;
+    double *buf = (double *)malloc((size_t)(RS_BATCH * s) * sizeof(double));
+    for (int b = 0; b < L->nblk; ++b)
+      for (int64_t i0 = 0; i0 < L->n[b]; i0 += RS_BATCH) {
+        const int64_t m = L->n[b] - i0 < RS_BATCH ? L->n[b] - i0 : RS_BATCH;
+        rs_fill_rows(src, b, s, i0, m, buf);
+        for (int j = 0; j < s; ++j) {
+          double acc = out[j];
+          const double *c = buf + (int64_t)j * m, *ub = u[b] + i0;
+          for (int64_t i = 0; i < m; ++i) acc += c[i] * ub[i];
+          out[j] = acc;
+        }
+      }
+    free(buf);
+    return;
+  }
+  double *d = (double *)malloc((size_t)s * sizeof(double));
+  for (int j = 0; j < s; ++j) out[j] = 0.0;
+  for (int b = 0; b < L->nblk; ++b) { /* ls_gdot: block sums added in block order from 0.0 */
+    rs_dbr_block_dots(L, src, b, u[b], d);
+    for (int j = 0; j < s; ++j) out[j] += d[j];
+  }
+  free(d);
+}
+
+/* The DBR one-pass step on an on-the-fly R (one formation of R per step instead of two): per DBR chunk of each
+ * block, U1 = R V (orc_dense_mult's rows), U1 += -alpha U (ls_axpy), the chunk's U1.U1 partial and the chunk's
+ * R_j.U1 partials; then per block the second stage of each, added over blocks in block order from 0.0 -- every
+ * operation as rs_mult, ls_axpy, ls_gdot and rs_mult_transpose perform it, one chunk at a time. */
+static void rs_onepass_step(const ls_layout *L, const ls_rsrc *src, const double *V, double alpha,
+                            double *const *U, double *const *U1, double *beta_sq, double *RtU1) {
+  const int s = L->s;
+  double *d = (double *)malloc((size_t)(s + 1) * sizeof(double));
+  double bsq = 0.0;
+  for (int j = 0; j < s; ++j) RtU1[j] = 0.0;
+  for (int b = 0; b < L->nblk; ++b) {
+    const int64_t n = L->n[b], nc = (n + ORC_DBR_CHUNK - 1) / ORC_DBR_CHUNK;
+    double *part = (double *)malloc((size_t)((nc > 0 ? nc : 1) * (s + 1)) * sizeof(double));
+    ORC_PAR
+    for (int64_t c = 0; c < nc; ++c) {
+      const int64_t i0 = c * ORC_DBR_CHUNK, m = n - i0 < ORC_DBR_CHUNK ? n - i0 : ORC_DBR_CHUNK;
+      double *tile = (double *)malloc((size_t)(m * s) * sizeof(double));
+      rs_fill(src, b, i0, i0 + m, 0, s, tile);
+      double *u1 = U1[b] + i0;
+      orc_dense_mult(m, s, tile, m, V, u1);
+      if (alpha != 0.0)
+        for (int64_t i = 0; i < m; ++i) u1[i] = u1[i] + (-alpha) * U[b][i0 + i];
+      part[(int64_t)s * nc + c] = dbr_chunk(m, u1, u1);
+      for (int j = 0; j < s; ++j) part[(int64_t)j * nc + c] = dbr_chunk(m, tile + (int64_t)j * m, u1);
+      free(tile);
+    }
+    for (int j = 0; j <= s; ++j) d[j] = dbr_finish(nc, part + (int64_t)j * nc);
+    free(part);
+    bsq += d[s];
+    for (int j = 0; j < s; ++j) RtU1[j] += d[j];
+  }
+  *beta_sq = bsq;
+  free(d);
+}
+
+/* MatNorm(R, NORM_FROBENIUS) in ls_frobenius' orders */
+static double rs_frobenius(const ls_layout *L, const ls_rsrc *src) {
+  if (src->R) return ls_frobenius(L, src->R, src->lda);
+  const int s = L->s;
+  double t = 0.0;
+  if (L->mode == ORC_REDUCE_SEQ) { /* column-major: every row of column 0 (all blocks), then column 1, ... */
+    double *buf = (double *)malloc((size_t)RS_BATCH * sizeof(double));
+    for (int j = 0; j < s; ++j)
+      for (int b = 0; b < L->nblk; ++b)
+        for (int64_t i0 = 0; i0 < L->n[b]; i0 += RS_BATCH) {
+          const int64_t m = L->n[b] - i0 < RS_BATCH ? L->n[b] - i0 : RS_BATCH;
+          ls_rsrc one = *src;
+          one.S = src->S + (int64_t)j * src->lds;
+          rs_fill_rows(&one, b, 1, i0, m, buf);
+          for (int64_t i = 0; i < m; ++i) t += buf[i] * buf[i];
+        }
+    free(buf);
+    return sqrt(t);
+  }
+  double *d = (double *)malloc((size_t)s * sizeof(double));
+  for (int b = 0; b < L->nblk; ++b) {
+    rs_dbr_block_dots(L, src, b, NULL, d);
+    double tb = 0.0;
+    for (int j = 0; j < s; ++j) tb += d[j];
+    t += tb;
+  }
+  free(d);
+  return sqrt(t);
+}
+
 typedef struct {
   const orc_lsqr_opts *o;
   int reason, its, nhist, hist_cap;
@@ -917,9 +1250,8 @@ static void ls_log(ls_state *k, double r) {
 
 /* KSPSolve(outer_ksp, b, x) -> KSPSolve_LSQR [PETSc-ext] with PCNONE and a zero guess
  * (outer_solver_norm_equation, utils.c:1061-1078). */
-int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R, const int64_t *lda,
-                   const double *const *rhs, double *x, const orc_lsqr_opts *o, orc_lsqr_result *res,
-                   double *hist, int hist_cap) {
+static int lsqr_solve_src(int nblk, const int64_t *nrows, int s, const ls_rsrc *src, const double *const *rhs,
+                          double *x, const orc_lsqr_opts *o, orc_lsqr_result *res, double *hist, int hist_cap) {
   if (nblk < 1 || s < 1 || !o) return ORC_ERR_ARG;
   ls_layout L = {nblk, s, o->reduce_mode, nrows};
   ls_state k;
@@ -960,22 +1292,28 @@ int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R
 
   beta = rnorm;
   for (int b = 0; b < nblk; ++b) ls_scale(nrows[b], U[b], 1.0 / beta);
-  ls_mult_transpose(&L, R, lda, (const double *const *)U, V);
+  rs_mult_transpose(&L, src, (const double *const *)U, V);
   alpha = ls_snorm(s, V);
   ls_scale(s, V, 1.0 / alpha);
   memcpy(W, V, (size_t)s * sizeof(double));
-  k.anorm = o->exact_norm ? ls_frobenius(&L, R, lda) : 0.0;
+  k.anorm = o->exact_norm ? rs_frobenius(&L, src) : 0.0;
   k.arnorm = alpha * beta;
   double phibar = beta, rhobar = alpha;
   int i = 0;
   do {
-    /* U1 = R V - alpha U */
-    for (int b = 0; b < nblk; ++b) orc_dense_mult(nrows[b], s, R[b], lda[b], V, U1[b]);
-    for (int b = 0; b < nblk; ++b) ls_axpy(nrows[b], U1[b], -alpha, U[b]);
-    beta = sqrt(ls_gdot(&L, (const double *const *)U1, (const double *const *)U1));
     /* DBR one-pass (the device's default): R^T U1 from the unscaled U1, in the pass that formed it */
     const int onepass = L.mode == ORC_REDUCE_DBR && o->onepass;
-    if (onepass) ls_mult_transpose(&L, R, lda, (const double *const *)U1, V1);
+    if (onepass && !src->R) { /* an on-the-fly R: formed once for the whole step */
+      double bsq;
+      rs_onepass_step(&L, src, V, alpha, U, U1, &bsq, V1);
+      beta = sqrt(bsq);
+    } else {
+      /* U1 = R V - alpha U */
+      rs_mult(&L, src, V, U1);
+      for (int b = 0; b < nblk; ++b) ls_axpy(nrows[b], U1[b], -alpha, U[b]);
+      beta = sqrt(ls_gdot(&L, (const double *const *)U1, (const double *const *)U1));
+      if (onepass) rs_mult_transpose(&L, src, (const double *const *)U1, V1);
+    }
     if (is_bad(beta)) {
       k.reason = ORC_DIVERGED_NANORINF;
       break;
@@ -988,7 +1326,7 @@ int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R
     if (onepass) {
       if (beta > 0.0) ls_scale(s, V1, 1.0 / beta); /* (R^T U1) * (1/beta) */
     } else {
-      ls_mult_transpose(&L, R, lda, (const double *const *)U1, V1);
+      rs_mult_transpose(&L, src, (const double *const *)U1, V1);
     }
     ls_axpy(s, V1, -beta, V);
     alpha = ls_snorm(s, V1);
@@ -1033,6 +1371,13 @@ out:
   return ORC_OK;
 }
 
+int orc_lsqr_solve(int nblk, const int64_t *nrows, int s, const double *const *R, const int64_t *lda,
+                   const double *const *rhs, double *x, const orc_lsqr_opts *o, orc_lsqr_result *res,
+                   double *hist, int hist_cap) {
+  const ls_rsrc src = {R, lda, NULL, NULL, 0};
+  return lsqr_solve_src(nblk, nrows, s, &src, rhs, x, o, res, hist, hist_cap);
+}
+
 /* Synchronous multisplitting with synchronous global minimization (SMSM-global),
  * src/synchronous-multisplitting-synchronous-minimization-global/
  * synchronous-multisplitting-synchronous-minimization-global.c, setup :134-284,
@@ -1047,17 +1392,21 @@ out:
 int orc_smsm_solve(const orc_smsm_problem *p, const orc_gmres_opts *inner, const orc_lsqr_opts *outer,
                    orc_smsm_result *res, double *outer_hist, int outer_cap, int *lsqr_its,
                    int *lsqr_reason, int *inner_its, double *x_out) {
-  const int nb = p->nb, s = p->s;
-  if (nb < 1 || s < 1 || (p->dim != 2 && p->dim != 3)) return ORC_ERR_ARG;
+  const int nb = p->nb, s = p->s, lean = p->lean != 0;
+  if (nb < 1 || s < 1 || (p->dim != 2 && p->dim != 3) || (lean && (p->dim != 3 || s > ORC_RS_MAXS))) return ORC_ERR_ARG;
   if (p->dim == 3 && p->nz % nb) return ORC_ERR_ARG;
   if (p->dim == 2 && ((int64_t)p->nx * p->ny) % nb) return ORC_ERR_ARG;
   orc_sm_problem sp = {p->dim, p->nx, p->ny, p->nz, nb, p->rtol, p->atol, p->max_outer,
                        {p->peclet[0], p->peclet[1], p->peclet[2]}};
   const int64_t N = (int64_t)p->nx * p->ny * (p->dim == 3 ? p->nz : 1);
   const int mode = inner->reduce_mode;
+  const int progress = getenv("ORC_PROGRESS") != NULL; /* one stderr line per outer iteration (long records) */
   orc_csr *Ab = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
   orc_csr *Aii = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
   orc_csr *Aoff = (orc_csr *)calloc((size_t)nb, sizeof(orc_csr));
+  orc_op *Abo = (orc_op *)calloc((size_t)nb, sizeof(orc_op));
+  orc_op *Aiio = (orc_op *)calloc((size_t)nb, sizeof(orc_op));
+  orc_op *Aoffo = (orc_op *)calloc((size_t)nb, sizeof(orc_op));
   int64_t *r0 = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
   int64_t *r1 = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
   int64_t *nrow = (int64_t *)calloc((size_t)nb, sizeof(int64_t));
@@ -1068,55 +1417,72 @@ int orc_smsm_solve(const orc_smsm_problem *p, const orc_gmres_opts *inner, const
   double *rhs = (double *)calloc((size_t)N, sizeof(double));
   double *y = (double *)calloc((size_t)N, sizeof(double));
   double *S = (double *)calloc((size_t)(N * s), sizeof(double));
-  double *Rm = (double *)calloc((size_t)(N * s), sizeof(double));
+  double *Rm = lean ? NULL : (double *)calloc((size_t)(N * s), sizeof(double));
   double *alpha = (double *)calloc((size_t)s, sizeof(double));
-  const orc_csr **Abp = (const orc_csr **)calloc((size_t)nb, sizeof(orc_csr *));
   const double **bbp = (const double **)calloc((size_t)nb, sizeof(double *));
   const double **Rp = (const double **)calloc((size_t)nb, sizeof(double *));
   int rc = ORC_OK;
-  if (!Ab || !Aii || !Aoff || !r0 || !r1 || !nrow || !ldab || !x || !u || !bvec || !rhs || !y || !S || !Rm ||
-      !alpha || !Abp || !bbp || !Rp) {
+  if (!Ab || !Aii || !Aoff || !Abo || !Aiio || !Aoffo || !r0 || !r1 || !nrow || !ldab || !x || !u || !bvec ||
+      !rhs || !y || !S || (!lean && !Rm) || !alpha || !bbp || !Rp) {
     rc = ORC_ERR_MEM;
     goto done;
   }
   for (int64_t i = 0; i < N; ++i) u[i] = 1.0;
   for (int b = 0; b < nb; ++b) {
-    if ((rc = build_block(&sp, b, &Ab[b], &r0[b], &r1[b]))) goto done;
-    if ((rc = orc_split(&Ab[b], r0[b], r1[b], &Aii[b], &Aoff[b]))) goto done;
-    orc_spmv(&Ab[b], u, bvec + r0[b]); /* computeTheRightHandSideWithInitialGuess */
-    Abp[b] = &Ab[b];
+    if (lean) {
+      const int64_t ppb = p->nz / nb, nxny = (int64_t)p->nx * p->ny;
+      r0[b] = b * ppb * nxny;
+      r1[b] = (b + 1) * ppb * nxny;
+      Abo[b] = op_stencil(p->nx, p->ny, p->nz, r0[b], r1[b], p->peclet, OP_BLOCK);
+      Aiio[b] = op_stencil(p->nx, p->ny, p->nz, r0[b], r1[b], p->peclet, OP_DIAG);
+      Aoffo[b] = op_stencil(p->nx, p->ny, p->nz, r0[b], r1[b], p->peclet, OP_OFF);
+    } else {
+      if ((rc = build_block(&sp, b, &Ab[b], &r0[b], &r1[b]))) goto done;
+      if ((rc = orc_split(&Ab[b], r0[b], r1[b], &Aii[b], &Aoff[b]))) goto done;
+      Abo[b] = op_csr(&Ab[b]);
+      Aiio[b] = op_csr(&Aii[b]);
+      Aoffo[b] = op_csr(&Aoff[b]);
+    }
+    op_spmv(&Abo[b], u, bvec + r0[b]); /* computeTheRightHandSideWithInitialGuess */
     bbp[b] = bvec + r0[b];
-    Rp[b] = Rm + r0[b];
+    Rp[b] = lean ? NULL : Rm + r0[b];
     nrow[b] = r1[b] - r0[b];
     ldab[b] = N;
   }
-  const double norm0 = orc_final_residual_norm(mode, nb, Abp, x, bbp); /* :280 */
+  const double norm0 = final_residual_norm_op(mode, nb, Abo, x, bbp); /* :280 */
   orc_gmres_opts io = *inner;
   io.guess_nonzero = 1;
   io.uirnorm = 1;
   int outer_it = 0;
   int64_t total_inner = 0;
+  const ls_rsrc src = {lean ? NULL : Rp, lean ? NULL : ldab, Abo, S, N};
   for (;;) {
     for (int k = 0; k < s; ++k) {
-      for (int b = 0; b < nb; ++b) orc_residual(&Aoff[b], bvec + r0[b], x, rhs + r0[b]);
+      for (int b = 0; b < nb; ++b) op_residual(&Aoffo[b], bvec + r0[b], x, rhs + r0[b]);
       for (int b = 0; b < nb; ++b) {
         orc_gmres_result gr;
-        if ((rc = orc_gmres_solve(&Aii[b], rhs + r0[b], x + r0[b], &io, &gr, NULL, 0))) goto done;
+        if ((rc = gmres_solve_op(&Aiio[b], rhs + r0[b], x + r0[b], &io, &gr, NULL, 0))) goto done;
         if (inner_its && outer_it < outer_cap) inner_its[((int64_t)outer_it * s + k) * nb + b] = gr.its;
         total_inner += gr.its;
       }
       memcpy(S + (int64_t)k * N, x, (size_t)N * sizeof(double)); /* MatSetValuesLocal(S, .., k, x) */
     }
-    for (int b = 0; b < nb; ++b)
-      for (int k = 0; k < s; ++k) orc_spmv(&Ab[b], S + (int64_t)k * N, Rm + (int64_t)k * N + r0[b]);
+    if (!lean)
+      for (int b = 0; b < nb; ++b)
+        for (int k = 0; k < s; ++k) orc_spmv(&Ab[b], S + (int64_t)k * N, Rm + (int64_t)k * N + r0[b]);
     orc_lsqr_result lr;
-    if ((rc = orc_lsqr_solve(nb, nrow, s, Rp, ldab, bbp, alpha, outer, &lr, NULL, 0))) goto done;
+    if ((rc = lsqr_solve_src(nb, nrow, s, &src, bbp, alpha, outer, &lr, NULL, 0))) goto done;
     orc_dense_mult(N, s, S, N, alpha, x); /* x_minimized = S alpha */
     const double norm = lr.rnorm;         /* KSPGetResidualNorm(outer_ksp) */
     if (outer_it < outer_cap) {
       if (outer_hist) outer_hist[outer_it] = norm;
       if (lsqr_its) lsqr_its[outer_it] = lr.its;
       if (lsqr_reason) lsqr_reason[outer_it] = lr.reason;
+    }
+    if (progress) {
+      fprintf(stderr, "orc_smsm_solve: outer %d lsqr_rnorm %a (%.17g) lsqr_its %d reason %d inner_total %lld\n",
+              outer_it, norm, norm, lr.its, lr.reason, (long long)total_inner);
+      fflush(stderr);
     }
     outer_it++;
     if (norm <= PMAX(p->atol, p->rtol * norm0)) break;
@@ -1125,16 +1491,16 @@ int orc_smsm_solve(const orc_smsm_problem *p, const orc_gmres_opts *inner, const
   if (res) {
     res->outer_its = outer_it;
     res->norm0 = norm0;
-    res->final_norm = orc_final_residual_norm(mode, nb, Abp, x, bbp);
+    res->final_norm = final_residual_norm_op(mode, nb, Abo, x, bbp);
     for (int64_t i = 0; i < N; ++i) y[i] = -1.0 * u[i] + x[i];
     res->error = orc_norm2(mode, N, y);
     res->total_inner_its = total_inner;
   }
   if (x_out) memcpy(x_out, x, (size_t)N * sizeof(double));
 done:
-  if (Ab)
+  if (Ab && !lean)
     for (int b = 0; b < nb; ++b) { orc_csr_free(&Ab[b]); orc_csr_free(&Aii[b]); orc_csr_free(&Aoff[b]); }
-  free(Ab); free(Aii); free(Aoff); free(r0); free(r1); free(nrow); free(ldab); free(x); free(u); free(bvec);
-  free(rhs); free(y); free(S); free(Rm); free(alpha); free(Abp); free(bbp); free(Rp);
+  free(Ab); free(Aii); free(Aoff); free(Abo); free(Aiio); free(Aoffo); free(r0); free(r1); free(nrow); free(ldab);
+  free(x); free(u); free(bvec); free(rhs); free(y); free(S); free(Rm); free(alpha); free(bbp); free(Rp);
   return rc;
 }

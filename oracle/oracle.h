@@ -220,6 +220,9 @@ typedef struct {
   double atol;        /* 1e-100 (SMSM-global.c:33) */
   int max_outer;      /* safety cap */
   double peclet[3];   /* as orc_sm_problem */
+  int lean;           /* dim 3 only: the operators applied without storage and R = A S formed on the fly inside
+                       * the LSQR (S is the only N x s array): bit for bit lean = 0, in a third of the memory --
+                       * the records at 512^3 (tests/golden/make_configs2.py, make_smsm_block.py) */
 } orc_smsm_problem;
 
 typedef struct {

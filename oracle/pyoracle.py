@@ -70,7 +70,7 @@ class LsqrResult(C.Structure):
 class SMSMProblem(C.Structure):
     _fields_ = [("dim", C.c_int), ("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("nb", C.c_int),
                 ("s", C.c_int), ("rtol", C.c_double), ("atol", C.c_double), ("max_outer", C.c_int),
-                ("peclet", C.c_double * 3)]
+                ("peclet", C.c_double * 3), ("lean", C.c_int)]
 
 
 CONV_DEFAULT, CONV_LSQR, CONV_SKIP = 0, 1, 2
@@ -361,9 +361,11 @@ def dense_mult(S, alpha) -> np.ndarray:
 
 
 def smsm_solve(dim, nx, ny, nz, nb, s, rtol, inner: dict, outer: dict, atol=1e-100, max_outer=1000,
-               peclet=(0.0, 0.0, 0.0)):
-    """SMSM with global minimization over nb blocks (see oracle.h).  Returns a dict."""
-    p = SMSMProblem(dim, nx, ny, nz if dim == 3 else 1, nb, s, rtol, atol, max_outer, (C.c_double * 3)(*peclet))
+               peclet=(0.0, 0.0, 0.0), lean=False):
+    """SMSM with global minimization over nb blocks (see oracle.h).  Returns a dict.  lean (dim 3): the same
+    record without assembled matrices or a stored R (the 512^3 records)."""
+    p = SMSMProblem(dim, nx, ny, nz if dim == 3 else 1, nb, s, rtol, atol, max_outer, (C.c_double * 3)(*peclet),
+                    1 if lean else 0)
     io = gmres_opts(**inner)
     oo = lsqr_opts(**outer)
     res = SMResult()

@@ -12,7 +12,7 @@ typedef struct {
   msp_vec *b, *x;
   PetscInt restart;
   PetscReal haptol, breakdowntol;
-  PetscInt reduction; /* -msplit_reduction dbr|seq: MSP_REDUCE_DBR (default) or PETSc's own order */
+  PetscInt reduction; /* -msplit_reduction dbr|seq on this KSP's prefix; -1: the shared context's order */
 } KSP_MSplit;
 
 /* -msplit_reduction: the device reduction order (include/msplit.h msp_ctx_set_reduction).  "seq" is
@@ -21,6 +21,37 @@ typedef struct {
 static const char *const MSplitReductions[] = {"dbr", "seq", "MSplitReduction", "MSPLIT_REDUCTION_", NULL};
 
 #define MSPCall(e) do { int _rc = (e); PetscCheck(!_rc, PETSC_COMM_SELF, _rc, "%s", msp_get_last_error()); } while (0)
+
+/* -msplit_reduction under a KSP's prefix: that order for this KSP's solves only.  The process's one context also
+ * serves every VECMSPLIT / aijmsplit operation (the drivers' outer VecNorm / VecDot / MatResidual), whose order is
+ * the global -msplit_reduction: a solve sets its KSP's order and restores the context's on every exit, so one KSP's
+ * choice never leaks into the outer residual norms or into another KSP. */
+static PetscErrorCode MSplitSetFromOptionsReduction(PetscOptionItems *PetscOptionsObject, PetscInt *reduction)
+{
+  PetscEnum red = (PetscEnum)(*reduction >= 0 ? *reduction : 0);
+  PetscBool set = PETSC_FALSE;
+  PetscFunctionBegin;
+  PetscCall(PetscOptionsEnum("-msplit_reduction", "device reduction order (seq: PETSc's, bitwise)", NULL,
+                             MSplitReductions, red, &red, &set));
+  if (set) *reduction = (PetscInt)red;
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
+static PetscErrorCode MSplitSolveInOrder(KSP ksp, msp_ctx *ctx, PetscInt reduction, PetscErrorCode (*body)(KSP))
+{
+  int saved = 0;
+  PetscFunctionBegin;
+  if (reduction < 0) {
+    PetscCall(body(ksp));
+    PetscFunctionReturn(PETSC_SUCCESS);
+  }
+  MSPCall(msp_ctx_get_reduction(ctx, &saved));
+  MSPCall(msp_ctx_set_reduction(ctx, (int)reduction));
+  PetscErrorCode ierr = body(ksp);
+  MSPCall(msp_ctx_set_reduction(ctx, saved));
+  PetscCall(ierr);
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
 
 #if defined(PETSC_USE_64BIT_INDICES)
 #error "the MI355X path takes PetscInt = int32 (msp_mat_create_csr); configure PETSc without --with-64-bit-indices"
@@ -160,7 +191,7 @@ static PetscErrorCode KSPSetUp_MSplitGMRES(KSP ksp)
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
-static PetscErrorCode KSPSolve_MSplitGMRES(KSP ksp)
+static PetscErrorCode KSPSolve_MSplitGMRES_Body(KSP ksp)
 {
   KSP_MSplit        *ms = (KSP_MSplit *)ksp->data;
   msp_ksp_opts       o;
@@ -184,7 +215,6 @@ static PetscErrorCode KSPSolve_MSplitGMRES(KSP ksp)
       MSPCall(msp_ksp_set_operators(ms->ksp, ms->A));
     }
   }
-  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction)); /* the shared context: this KSP's order */
   MSPCall(msp_ksp_get_default_opts(&o));
   o.restart       = (int32_t)ms->restart;
   o.max_it        = (int32_t)ksp->max_it;
@@ -214,6 +244,14 @@ static PetscErrorCode KSPSolve_MSplitGMRES(KSP ksp)
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
+static PetscErrorCode KSPSolve_MSplitGMRES(KSP ksp)
+{
+  KSP_MSplit *ms = (KSP_MSplit *)ksp->data;
+  PetscFunctionBegin;
+  PetscCall(MSplitSolveInOrder(ksp, ms->ctx, ms->reduction, KSPSolve_MSplitGMRES_Body));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
 static PetscErrorCode KSPSetFromOptions_MSplitGMRES(KSP ksp, PetscOptionItems *PetscOptionsObject)
 {
   KSP_MSplit *ms = (KSP_MSplit *)ksp->data;
@@ -221,8 +259,7 @@ static PetscErrorCode KSPSetFromOptions_MSplitGMRES(KSP ksp, PetscOptionItems *P
   PetscOptionsHeadBegin(PetscOptionsObject, "KSP MSplit GMRES Options");
   PetscCall(PetscOptionsInt("-ksp_gmres_restart", "Krylov directions", NULL, ms->restart, &ms->restart, NULL));
   PetscCall(PetscOptionsReal("-ksp_gmres_haptol", "happy breakdown tolerance", NULL, ms->haptol, &ms->haptol, NULL));
-  PetscCall(PetscOptionsEnum("-msplit_reduction", "device reduction order (seq: PETSc's, bitwise)", NULL,
-                             MSplitReductions, (PetscEnum)ms->reduction, (PetscEnum *)&ms->reduction, NULL));
+  PetscCall(MSplitSetFromOptionsReduction(PetscOptionsObject, &ms->reduction));
   PetscCall(PetscOptionsReal("-ksp_gmres_breakdown_tolerance", "restart breakdown tolerance", NULL, ms->breakdowntol,
                              &ms->breakdowntol, NULL));
   PetscOptionsHeadEnd();
@@ -247,7 +284,7 @@ PetscErrorCode KSPCreate_MSplitGMRES(KSP ksp)
   KSP_MSplit *ms;
   PetscFunctionBegin;
   PetscCall(PetscNew(&ms));
-  ms->restart = 30; ms->haptol = 1.0e-30; ms->breakdowntol = 0.1;
+  ms->restart = 30; ms->haptol = 1.0e-30; ms->breakdowntol = 0.1; ms->reduction = -1;
   ksp->data = (void *)ms;
   PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_PRECONDITIONED, PC_LEFT, 3));
   PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_UNPRECONDITIONED, PC_RIGHT, 2));
@@ -270,7 +307,7 @@ typedef struct {
   msp_lsqr *lsqr;
   msp_vec *b, *x;
   PetscBool exact_norm;
-  PetscInt reduction; /* -msplit_reduction, as for msplitgmres */
+  PetscInt reduction; /* -msplit_reduction, as for msplitgmres (-1: the shared context's order) */
 } KSP_MSplitLSQR;
 
 static PetscErrorCode KSPSetUp_MSplitLSQR(KSP ksp)
@@ -303,7 +340,7 @@ static PetscErrorCode KSPSetUp_MSplitLSQR(KSP ksp)
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
-static PetscErrorCode KSPSolve_MSplitLSQR(KSP ksp)
+static PetscErrorCode KSPSolve_MSplitLSQR_Body(KSP ksp)
 {
   KSP_MSplitLSQR    *ms = (KSP_MSplitLSQR *)ksp->data;
   msp_lsqr_opts      o;
@@ -314,7 +351,6 @@ static PetscErrorCode KSPSolve_MSplitLSQR(KSP ksp)
   double             rnorm;
 
   PetscFunctionBegin;
-  MSPCall(msp_ctx_set_reduction(ms->ctx, (int)ms->reduction));
   MSPCall(msp_lsqr_get_default_opts(&o));
   o.max_it     = (int32_t)ksp->max_it;
   o.rtol       = ksp->rtol;
@@ -343,13 +379,20 @@ static PetscErrorCode KSPSolve_MSplitLSQR(KSP ksp)
   PetscFunctionReturn(PETSC_SUCCESS);
 }
 
+static PetscErrorCode KSPSolve_MSplitLSQR(KSP ksp)
+{
+  KSP_MSplitLSQR *ms = (KSP_MSplitLSQR *)ksp->data;
+  PetscFunctionBegin;
+  PetscCall(MSplitSolveInOrder(ksp, ms->ctx, ms->reduction, KSPSolve_MSplitLSQR_Body));
+  PetscFunctionReturn(PETSC_SUCCESS);
+}
+
 static PetscErrorCode KSPSetFromOptions_MSplitLSQR(KSP ksp, PetscOptionItems *PetscOptionsObject)
 {
   KSP_MSplitLSQR *ms = (KSP_MSplitLSQR *)ksp->data;
   PetscFunctionBegin;
   PetscOptionsHeadBegin(PetscOptionsObject, "KSP MSplit LSQR Options");
-  PetscCall(PetscOptionsEnum("-msplit_reduction", "device reduction order (seq: PETSc's, bitwise)", NULL,
-                             MSplitReductions, (PetscEnum)ms->reduction, (PetscEnum *)&ms->reduction, NULL));
+  PetscCall(MSplitSetFromOptionsReduction(PetscOptionsObject, &ms->reduction));
   PetscCall(PetscOptionsBool("-ksp_lsqr_exact_mat_norm", "exact Frobenius norm of the operator", NULL,
                              ms->exact_norm, &ms->exact_norm, NULL));
   PetscOptionsHeadEnd();
@@ -374,6 +417,7 @@ PetscErrorCode KSPCreate_MSplitLSQR(KSP ksp)
   KSP_MSplitLSQR *ms;
   PetscFunctionBegin;
   PetscCall(PetscNew(&ms));
+  ms->reduction = -1;
   ksp->data = (void *)ms;
   PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_UNPRECONDITIONED, PC_LEFT, 3));
   PetscCall(KSPSetSupportedNorm(ksp, KSP_NORM_NONE, PC_LEFT, 1));

@@ -1,8 +1,11 @@
 """Writes tests/golden/configs2_smsm.json: the CPU oracle's SMSM-global (SMSM-global.c:288-363) with
 BASELINE configs[2]'s exact options -- 2 z-slab blocks, s 20, inner GMRES(30) max_it 20 rtol 1e-20,
 outer LSQR max_it 70 rtol 1e-15 with the exact matrix norm and the default convergence test, -rtol 1e-4
-(running_bulk_test_g5k:230, :247-248) -- in the DBR order the device runs by default, on the largest cube
-the container's memory holds in a test-generation time (256^3; configs[2] itself is 512^3).
+(running_bulk_test_g5k:230, :247-248) -- in the DBR order the device runs by default, up to configs[2] itself,
+512^3.  From 512^3 on the oracle runs lean (orc_smsm_problem.lean: the operators applied without storage and
+R = A S formed inside the LSQR, bit for bit the assembled run -- tests/test_oracle.py): S (21.5 GB) is its only
+large array, so the record fits the container's memory; it takes the 8-thread oracle about 20 minutes per outer
+iteration (ORC_PROGRESS=1 prints each one).
 
 Per cube the record holds the outer count, norm0, every outer-history entry (hex), the LSQR counts and
 reasons, the inner iteration counts, the final residual and the SHA-256 of x.  tests/test_gpu_configs.py
@@ -31,14 +34,15 @@ OUT = os.path.join(HERE, "configs2_smsm.json")
 def record(n):
     t0 = time.time()
     r = po.smsm_solve(3, n, n, n, NB, S, RTOL, dict(INNER, reduce_mode=po.REDUCE_DBR),
-                      dict(OUTER, reduce_mode=po.REDUCE_DBR), max_outer=40)
+                      dict(OUTER, reduce_mode=po.REDUCE_DBR), max_outer=40, lean=n >= 512)
     x = np.ascontiguousarray(r["x"], np.float64)
     return {"outer_its": int(r["outer_its"]), "norm0_hex": float(r["norm0"]).hex(),
             "hist_hex": [float(h).hex() for h in r["hist"]], "lsqr_its": [int(v) for v in r["lsqr_its"]],
             "lsqr_reason": [int(v) for v in r["lsqr_reason"]],
             "inner_its": r["inner_its"].tolist(), "total_inner_its": int(r["total_inner_its"]),
             "final_norm_hex": float(r["final_norm"]).hex(), "error": int(r["error"]),
-            "x_sha256": hashlib.sha256(x.tobytes()).hexdigest(), "seconds": round(time.time() - t0, 1)}
+            "x_sha256": hashlib.sha256(x.tobytes()).hexdigest(), "seconds": round(time.time() - t0, 1),
+            **({"lean": True} if n >= 512 else {})}
 
 
 def main():

@@ -298,3 +298,20 @@ def test_plugin_device_choice_is_not_collective_per_object():
     assert "MPI_Comm_split_type" not in body and "MPI_" not in body
     reg = src[src.index("PetscErrorCode MSplitRegisterAll(void)"):]
     assert "MSplitCacheLocalRank()" in reg[:reg.index("\n}\n")]
+
+
+def test_plugin_ksp_reduction_does_not_leak_into_the_shared_context():
+    """msplitgmres / msplitlsqr share the process's one context with VECMSPLIT and aijmsplit, whose
+    order is the global -msplit_reduction.  A KSP's own (prefixed) -msplit_reduction is applied only around its
+    solve: both KSPSolve entries go through MSplitSolveInOrder, which restores the context's order on every exit,
+    and no other plugin code sets the order except the global option (petsc_msplit_vecmat.c).  PETSc is absent,
+    so the plugin is checked as source."""
+    import re
+    src = open(os.path.join(ROOT, "plugin", "petsc", "petsc_msplit_ksp.c")).read()
+    for kind in ("GMRES", "LSQR"):
+        body = re.search(r"static PetscErrorCode KSPSolve_MSplit%s\(KSP ksp\)\n\{(.*?)\n\}" % kind, src, re.S)
+        assert body and "MSplitSolveInOrder" in body.group(1), kind
+    order = re.search(r"static PetscErrorCode MSplitSolveInOrder\(.*?\n\}", src, re.S).group(0)
+    assert order.index("msp_ctx_get_reduction") < order.index("ierr = body(ksp)") < order.rindex("msp_ctx_set_reduction")
+    assert src.count("MSPCall(msp_ctx_set_reduction") == order.count("MSPCall(msp_ctx_set_reduction") == 2
+    assert src.count("reduction = -1") == 2          # unset: the KSP follows the context's (global) order

@@ -252,7 +252,7 @@ def test_configs2_record_matches_oracle(oracle):
     gen = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(gen)
     rec = json.load(open(os.path.join(here, "golden", "configs2_smsm.json")))
-    assert sorted(rec["cubes"], key=int) == ["32", "64", "128", "256"]
+    assert sorted(rec["cubes"], key=int)[:4] == ["32", "64", "128", "256"]
     oracle.set_threads(min(8, os.cpu_count() or 1))
     try:
         got = gen.record(64)
@@ -279,3 +279,41 @@ def test_smsm_seq_record_matches_oracle(oracle):
     rec.pop("seconds")
     assert got == rec
     assert rec["lsqr_its"] == [70] and len(rec["inner_its"][0]) == rec["problem"]["s"]
+
+
+@pytest.mark.parametrize("nx,ny,nz,nb,s,peclet,order", [
+    (8, 8, 8, 2, 4, (0.0, 0.0, 0.0), "dbr"), (12, 10, 12, 3, 5, (0.5, 0.25, -0.3), "seq"),
+    (16, 16, 16, 2, 6, (0.0, 0.0, 0.0), "dbr"), (24, 20, 16, 1, 20, (0.0, 0.0, 0.0), "seq"),
+    (20, 16, 24, 4, 8, (0.5, 0.25, -0.3), "dbr")])
+def test_oracle_lean_smsm_equals_assembled(oracle, nx, ny, nz, nb, s, peclet, order):
+    """orc_smsm_problem.lean -- the operators applied without storage and R = A S formed inside the LSQR (the DBR
+    one-pass step fused over each chunk), the mode the 512^3 records run in -- is bit for bit the assembled run:
+    every outer LSQR residual, LSQR and inner count, norm0, the final residual, the error and x."""
+    mode = oracle.REDUCE_DBR if order == "dbr" else oracle.REDUCE_SEQ
+    inner = dict(restart=30, max_it=20, rtol=1e-20, abstol=1e-100, reduce_mode=mode)
+    outer = dict(max_it=70, rtol=1e-15, abstol=1e-100, exact_norm=1, conv_test=0, reduce_mode=mode)
+    oracle.set_threads(4)
+    try:
+        a, b = (oracle.smsm_solve(3, nx, ny, nz, nb, s, 1e-30, inner, outer, max_outer=2, peclet=peclet, lean=lean)
+                for lean in (False, True))
+    finally:
+        oracle.set_threads(1)
+    assert a["hist"].tobytes() == b["hist"].tobytes()
+    assert np.array_equal(a["lsqr_its"], b["lsqr_its"]) and np.array_equal(a["inner_its"], b["inner_its"])
+    assert (a["norm0"], a["final_norm"], a["error"]) == (b["norm0"], b["final_norm"], b["error"])
+    assert a["x"].tobytes() == b["x"].tobytes()
+
+
+def test_smsm_block_record_covers_the_bench_block():
+    """tests/golden/smsm_block.json holds the bench's N = 1 SMSM block (512 x 512 x 256, configs[2]'s options): the
+    DBR order's warm-up and two timed outer iterations (smsm_per_gpu) and PETSc's order's one (smsm_seq_mode), as
+    bench.py's check_smsm_block reads them."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    rec = json.load(open(os.path.join(here, "golden", "smsm_block.json")))
+    P = rec["problem"]
+    assert (P["nx"], P["ny"], P["nz"], P["nb"], P["s"]) == (512, 512, 256, 1, 20)
+    assert rec["dbr"]["outer_its"] == 3 and rec["seq"]["outer_its"] == 1
+    for o in ("dbr", "seq"):
+        r = rec[o]
+        assert len(r["hist_hex"]) == len(r["lsqr_its"]) == len(r["inner_its"]) == r["outer_its"]
+        assert all(len(row) == P["s"] for row in r["inner_its"]) and len(r["x_sha256"]) == 64
