@@ -412,10 +412,45 @@ def spmv512(ctx, args):
     avg_ms = st["ms"] / st["launches"]
     gbs = alg / (avg_ms * 1e-3) / 1e9
     A.destroy()
+    # after timing: the last product against MatMult_SeqAIJ's row sums restated in numpy (bit for bit)
+    xs, ys = x.get_array(), y.get_array()
+    bad_rows = sum(int(np.count_nonzero(poisson3d_rows_product(xs, n, z).view(np.uint64)
+                                        != ys[z * n * n:(z + 1) * n * n].view(np.uint64))) for z in range(n))
     return {"kernel": SPMV_NAMES["csr"], "rows": N, "nnz": A.nnz, "alg_bytes_per_launch": alg,
+            "verified": bad_rows == 0, "mismatched_rows": bad_rows,
+            "verification": "the last timed product, every row bit for bit against MatMult_SeqAIJ's ordered row sums "
+                            "restated in numpy",
             "bytes_formula": "12 nnz + 20 N + 4 (val 8 + col 4 per entry, rowptr, x read once, y written)",
             "launches": st["launches"], "avg_launch_ms": avg_ms, "achieved_GBps": gbs,
             "peak_GBps": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS, "target_frac": 0.70}
+
+
+def poisson3d_rows_product(xs, n, z):
+    """Plane z of y = A x for the n^3 7-point Poisson matrix (utils.c:30-121) as MatMult_SeqAIJ forms each row: from
+    0.0, the row's entries in column order (z-1, y-1, x-1, d, x+1, y+1, z+1), one product and one add each, no FMA --
+    numpy's element-wise double arithmetic, so bit for bit what the CSR kernel must give."""
+    import numpy as np
+    P = n * n
+    o = z * P
+    idx = np.arange(P)
+    i, j = idx % n, idx // n
+    acc = np.zeros(P)
+
+    def add(mask, src):
+        nonlocal acc
+        t = np.zeros(P)
+        t[mask] = (-1.0) * xs[src[mask]]
+        acc = np.where(mask, acc + t, acc)
+    if z > 0:
+        acc = acc + (-1.0) * xs[o - P:o]
+    add(j > 0, o + idx - n)
+    add(i > 0, o + idx - 1)
+    acc = acc + 6.0 * xs[o:o + P]
+    add(i < n - 1, o + idx + 1)
+    add(j < n - 1, o + idx + n)
+    if z < n - 1:
+        acc = acc + (-1.0) * xs[o + P:o + 2 * P]
+    return acc
 
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "configs1_seq.json")
@@ -955,6 +990,7 @@ def main():
         print(json.dumps(out), flush=True)
     failed = (verified is False or (extras.get("seq_mode") or {}).get("verified") is False
               or (extras.get("smsm_per_gpu") or {}).get("verified") is False
+              or (extras.get("spmv_512_csr") or {}).get("verified") is False
               or (extras.get("smsm_seq_mode") or {}).get("verified") is False
               or (extras.get("assembled_csr_operator") or {}).get("verified") is False
               or (extras.get("non_stencil_aij") or {}).get("verified") is False)

@@ -1910,6 +1910,13 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
   }
   if (xcd & 2) zg = (nz + zt - 1) / zt - 1 - zg;  // top plane groups first
   const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
+  // xcd & 4: odd plane groups march down (round 6).  A group reads one plane of x beyond each end of its range (and,
+  // RV == 2, the z+1 leg of the plane below): marching up, the plane below at its start and the plane above at its
+  // end, which its neighbour groups read at their opposite ends, a whole group's time apart -- from HBM twice.
+  // Groups marching toward each other in pairs meet their neighbours at the shared boundary at the same moment
+  // (both start there, or both end there; same tile, same XCD), so the second read finds the first in the L2.
+  // The march order changes nothing else: every chunk's terms, sums and stores are the same (bitwise).
+  const bool down = RV != 2 && (xcd & 4) && (zg & 1);
   const double sc = *sdev;
   double v[7];
   if constexpr (!RV) march_values<false>(dval, v);
@@ -1927,15 +1934,17 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
       uzm[2 * j + 1] = u.y;
     }
   }
-  {
-    const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * t;
+  {  // xc: the first plane; xm: the plane marched from (z-1 going up, z+1 going down), 0 beyond the box
+    const int32_t zf = down ? z1 - 1 : z0;
+    const bool hasm = down ? z1 < nz : z0 > 0;
+    const int64_t b0 = (int64_t)zf * P + tile * kChunk + 2 * t, bm = b0 + (down ? P : -P);
 #pragma unroll
     for (int j = 0; j < kIters; ++j) {
       const double2 a = *reinterpret_cast<const double2*>(x + b0 + j * (2 * kT));
       xc[2 * j] = a.x;
       xc[2 * j + 1] = a.y;
-      if (z0 > 0) {
-        const double2 m2 = *reinterpret_cast<const double2*>(x + b0 - P + j * (2 * kT));
+      if (hasm) {
+        const double2 m2 = *reinterpret_cast<const double2*>(x + bm + j * (2 * kT));
         xm[2 * j] = m2.x;
         xm[2 * j + 1] = m2.y;
       } else {
@@ -1943,13 +1952,16 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
       }
     }
   }
-  for (int32_t z = z0; z < z1; ++z) {
+  for (int32_t zi = 0; zi < z1 - z0; ++zi) {
+    const int32_t z = down ? z1 - 1 - zi : z0 + zi;
     const int64_t c = (int64_t)z * cpp + tile, c0 = c * kChunk, base = c0 + 2 * t;
+    const bool hasp = down ? z > 0 : z + 1 < nz;  // xp: the plane marched to (z+1 going up, z-1 going down)
+    const int64_t dp = down ? -P : P;
     uint32_t m[kIters];
 #pragma unroll
-    for (int j = 0; j < kIters; ++j) {  // plane z+1, the presence bytes: issued before the LDS turn-around
-      if (z + 1 < nz) {
-        const double2 p2 = *reinterpret_cast<const double2*>(x + base + P + j * (2 * kT));
+    for (int j = 0; j < kIters; ++j) {  // the next plane, the presence bytes: issued before the LDS turn-around
+      if (hasp) {
+        const double2 p2 = *reinterpret_cast<const double2*>(x + base + dp + j * (2 * kT));
         xp[2 * j] = p2.x;
         xp[2 * j + 1] = p2.y;
       } else {
@@ -2003,8 +2015,8 @@ __global__ __launch_bounds__(kT) void k_box_spmv_mdot_march(int32_t nx, int64_t 
       for (int q = 0; q < 2; ++q) {
         const int e = j * (2 * kT) + 2 * t + q + nx;
         const uint32_t mr = (m[j] >> (8 * q)) & 255u;
-        const double xq[7] = {xm[2 * j + q], sx[e - nx], sx[e - 1], xc[2 * j + q], sx[e + 1], sx[e + nx],
-                              xp[2 * j + q]};
+        const double xq[7] = {down ? xp[2 * j + q] : xm[2 * j + q], sx[e - nx], sx[e - 1], xc[2 * j + q],
+                              sx[e + 1], sx[e + nx], down ? xm[2 * j + q] : xp[2 * j + q]};
         double vv[7];
         if constexpr (RV == 2) sym_values(st, sux, suy, uzm[2 * j + q], j, q, e, nx, vv);
         double s = 0.0;
@@ -2102,35 +2114,45 @@ __global__ __launch_bounds__(2 * kT) void k_box_spmv_mdot_march_sym2(int32_t nx,
   }
   if (xcd & 2) zg = (nz + zt - 1) / zt - 1 - zg;
   const int32_t z0 = (int32_t)zg * zt, z1 = min(z0 + zt, nz);
+  // xcd & 4: odd plane groups march down (as k_box_spmv_mdot_march).  Going down, plane z's z-1 values are the z+1
+  // legs of the plane below, the plane marched to: they are loaded with its x (own[.][3] holds them), and its z+1
+  // values are its own z+1 legs, loaded one plane earlier (uzm).  Going up it is the other way round.
+  const bool down = (xcd & 4) && (zg & 1);
   const double sc = *sdev;
   const int nh = nx / 2;
   double xm[2 * H], xc[2 * H], xp[2 * H], uzm[2 * H];
-  {
-    const int64_t cb = ((int64_t)z0 - 1) * P + tile * kChunk;
-    const int64_t b0 = (int64_t)z0 * P + tile * kChunk + 2 * tl;
+  {  // xc: the first plane; xm: the plane marched from; uzm: the z+1 legs of the plane below the first (up) or of
+     // the first plane itself (down)
+    const int32_t zf = down ? z1 - 1 : z0;
+    const bool hasm = down ? z1 < nz : z0 > 0;
+    const int64_t cb = ((int64_t)(down ? zf : z0 - 1)) * P + tile * kChunk;
+    const int64_t b0 = (int64_t)zf * P + tile * kChunk + 2 * tl, bm = b0 + (down ? P : -P);
 #pragma unroll
     for (int jj = 0; jj < H; ++jj) {
       const int j = j0 + jj;
-      const double2 u = z0 > 0 ? ld_nt(rvs_pair(rv, cb, 3, j, tl)) : make_double2(0.0, 0.0);
+      const double2 u = down || z0 > 0 ? ld_nt(rvs_pair(rv, cb, 3, j, tl)) : make_double2(0.0, 0.0);
       uzm[2 * jj] = u.x;
       uzm[2 * jj + 1] = u.y;
       const double2 a = *reinterpret_cast<const double2*>(x + b0 + j * (2 * kT));
       xc[2 * jj] = a.x;
       xc[2 * jj + 1] = a.y;
-      const double2 m2 = z0 > 0 ? *reinterpret_cast<const double2*>(x + b0 - P + j * (2 * kT)) : make_double2(0.0, 0.0);
+      const double2 m2 = hasm ? *reinterpret_cast<const double2*>(x + bm + j * (2 * kT)) : make_double2(0.0, 0.0);
       xm[2 * jj] = m2.x;
       xm[2 * jj + 1] = m2.y;
     }
   }
-  for (int32_t z = z0; z < z1; ++z) {
+  for (int32_t zi = 0; zi < z1 - z0; ++zi) {
+    const int32_t z = down ? z1 - 1 - zi : z0 + zi;
     const int64_t c = (int64_t)z * cpp + tile, c0 = c * kChunk, base = c0 + 2 * tl;
+    const bool hasp = down ? z > 0 : z + 1 < nz;  // xp: the plane marched to
+    const int64_t dp = down ? -P : P;
     uint32_t m[H];
-    double2 own[H][4];
+    double2 own[H][4];  // own[.][3]: the z+1 legs of plane z (up) or of the plane below (down)
 #pragma unroll
     for (int jj = 0; jj < H; ++jj) {
       const int j = j0 + jj;
-      if (z + 1 < nz) {
-        const double2 p2 = *reinterpret_cast<const double2*>(x + base + P + j * (2 * kT));
+      if (hasp) {
+        const double2 p2 = *reinterpret_cast<const double2*>(x + base + dp + j * (2 * kT));
         xp[2 * jj] = p2.x;
         xp[2 * jj + 1] = p2.y;
       } else {
@@ -2138,7 +2160,9 @@ __global__ __launch_bounds__(2 * kT) void k_box_spmv_mdot_march_sym2(int32_t nx,
       }
       m[jj] = *reinterpret_cast<const uint16_t*>(mask + base + j * (2 * kT));
 #pragma unroll
-      for (int k = 0; k < 4; ++k) own[jj][k] = ld_nt(rvs_pair(rv, c0, k, j, tl));
+      for (int k = 0; k < 3; ++k) own[jj][k] = ld_nt(rvs_pair(rv, c0, k, j, tl));
+      own[jj][3] = !down ? ld_nt(rvs_pair(rv, c0, 3, j, tl))
+                         : hasp ? ld_nt(rvs_pair(rv, c0 - P, 3, j, tl)) : make_double2(0.0, 0.0);
     }
     double2 hl = make_double2(0.0, 0.0), hh = make_double2(0.0, 0.0), hx = hl, hy = hl;
     const bool hal = h == 0 && tl < nh;
@@ -2171,11 +2195,12 @@ __global__ __launch_bounds__(2 * kT) void k_box_spmv_mdot_march_sym2(int32_t nx,
       for (int q = 0; q < 2; ++q) {
         const int e = j * (2 * kT) + 2 * tl + q + nx;
         const uint32_t mr = (m[jj] >> (8 * q)) & 255u;
-        const double xq[7] = {xm[2 * jj + q], sx[e - nx], sx[e - 1], xc[2 * jj + q], sx[e + 1], sx[e + nx],
-                              xp[2 * jj + q]};
-        const double vv[7] = {uzm[2 * jj + q], suy[e - nx], sux[e - 1], q ? own[jj][0].y : own[jj][0].x,
+        const double xq[7] = {down ? xp[2 * jj + q] : xm[2 * jj + q], sx[e - nx], sx[e - 1], xc[2 * jj + q],
+                              sx[e + 1], sx[e + nx], down ? xm[2 * jj + q] : xp[2 * jj + q]};
+        const double uf = q ? own[jj][3].y : own[jj][3].x;
+        const double vv[7] = {down ? uf : uzm[2 * jj + q], suy[e - nx], sux[e - 1], q ? own[jj][0].y : own[jj][0].x,
                               q ? own[jj][1].y : own[jj][1].x, q ? own[jj][2].y : own[jj][2].x,
-                              q ? own[jj][3].y : own[jj][3].x};
+                              down ? uzm[2 * jj + q] : uf};
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < 7; ++k)
@@ -2190,7 +2215,7 @@ __global__ __launch_bounds__(2 * kT) void k_box_spmv_mdot_march_sym2(int32_t nx,
       } else {
         *reinterpret_cast<double2*>(y + base + j * (2 * kT)) = make_double2(wr[2 * jj], wr[2 * jj + 1]);
       }
-      uzm[2 * jj] = own[jj][3].x;  // the next plane's z-1 values
+      uzm[2 * jj] = own[jj][3].x;  // the next plane's z-1 values (up) or its z+1 values (down)
       uzm[2 * jj + 1] = own[jj][3].y;
     }
     __syncthreads();  // every row is done with the leg windows: the x+1 window's space takes the W exchange
@@ -3392,7 +3417,16 @@ extern "C" int msk_box_spmv_mdot_rv(int32_t nx, int64_t P, int64_t n, int d2, co
       const char* e = getenv("MSPLIT_BOXMDOT_REV");
       return e && atoi(e) ? 2 : 0;
     }();
-    const int xcd = ((P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD)) | rev;
+    // MSPLIT_BOXMDOT_ALT=1: odd plane groups march down (k_box_spmv_mdot_march, xcd & 4), so the boundary planes
+    // two groups both read are read at the same moment, the second time from the L2.  Measured (round 6,
+    // profiles/r06/march_alt/): PMC 1.048 -> 1.019 of the algorithmic bytes for the symmetric STENCIL step and
+    // 1.035 -> 1.011 for the DV step, but no faster (STENCIL -2.9 %, DV -0.1 %): those re-reads were MALL hits, the
+    // kernels are bound by their streaming rate.  Off by default; read per call (the tests hold both orders to each
+    // other and to the oracle).
+    const char* alte = getenv("MSPLIT_BOXMDOT_ALT");
+    const int alt = alte && alte[0] == '1' ? 4 : 0;
+    const int xcd =
+        ((P / kChunk) % 8 == 0 && P / kChunk >= 32 && !(msk_tuning_flags & MSK_TUNE_BOX_MDOT_NOXCD)) | rev | alt;
     // GMRES's basis ends with x (VV(it)): its dot from the march registers (MSPLIT_BOXMDOT_SELF=0: streamed, A/B)
     static const int self_env = [] {
       const char* e = getenv("MSPLIT_BOXMDOT_SELF");

@@ -166,3 +166,16 @@ def test_wfree_maxpy_class_bytes(ctx):
     spmvdot = sum(8.0 * n * nv + n for nv in range(1, 11))
     assert st["maxpy"]["bytes"] == pytest.approx(maxpy, rel=1e-12)
     assert st["spmvdot"]["bytes"] == pytest.approx(spmvdot, rel=1e-12)
+
+
+@pytest.mark.parametrize("alt", ["1", "0"])
+@pytest.mark.parametrize("shape", [(64, 64, 33), (128, 32, 5), (256, 16, 7), (64, 64, 8)])
+def test_fused_march_direction_bitwise(ctx, oracle, shape, alt, monkeypatch):
+    """Round 6: odd plane groups of the fused MatMult+MDot march down (MSPLIT_BOXMDOT_ALT, default on), so that the
+    boundary planes two groups share are read by both at the same moment (the second time from the L2).  Both
+    orders give the stored-W step's and the oracle's bits: the march order changes no chunk's arithmetic."""
+    monkeypatch.setenv("MSPLIT_BOXMDOT_ALT", alt)  # 1: alternating, 0: up only
+    nx, ny, nz = shape
+    A = Mat.box_stencil(ctx, 3, nx, ny, nz)
+    b = np.random.default_rng(SEED + nz).uniform(-1, 1, A.shape[0])
+    _check(ctx, oracle, A, b, 30, 45)

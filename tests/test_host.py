@@ -2,6 +2,7 @@
 import glob
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -315,3 +316,17 @@ def test_plugin_ksp_reduction_does_not_leak_into_the_shared_context():
     assert order.index("msp_ctx_get_reduction") < order.index("ierr = body(ksp)") < order.rindex("msp_ctx_set_reduction")
     assert src.count("MSPCall(msp_ctx_set_reduction") == order.count("MSPCall(msp_ctx_set_reduction") == 2
     assert src.count("reduction = -1") == 2          # unset: the KSP follows the context's (global) order
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 12])
+def test_bench_spmv_check_restates_matmult_seqaij(oracle, n):
+    """bench.py's spmv_512_csr line checks its last product row by row against poisson3d_rows_product (numpy):
+    that restatement is bit for bit the oracle's MatMult_SeqAIJ on the reference's 3D assembly."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    A = oracle.poisson3d_rows(n, n, n, 0, n)
+    x = np.random.default_rng(n).uniform(-1, 1, n ** 3)
+    x[0] = -0.0
+    yb = np.concatenate([bench.poisson3d_rows_product(x, n, z) for z in range(n)])
+    assert np.array_equal(A.mult(x).view(np.uint64), yb.view(np.uint64))

@@ -150,10 +150,31 @@ def main():
     ap.add_argument("--smsm", default=None, metavar="NX,NY,NZ,S,K[,L]",
                     help="per-kernel table for the SMSM-global per-GPU outer iteration (bench.py --variant smsm): "
                          "an NX x NY x NZ block, S inner solves of K Arnoldi steps, L LSQR steps (70) over S columns")
+    ap.add_argument("--kernel", default=None, metavar="NAME,ROW_BYTES",
+                    help="one kernel of the GMRES(30) step only: every launch whose name contains NAME, in dispatch "
+                         "order, against N x (ROW_BYTES + 8 x (i mod 30)) algorithmic bytes -- launch i of a cycle "
+                         "dots W with i + 1 basis vectors, the last one from the march registers (e.g. "
+                         "k_box_spmv_mdot_march_sym2,49: presence byte, 32 value bytes, x, W written)")
     a = ap.parse_args()
     N = a.n ** 3
     fetch = load(a.fetch_dir, "FETCH_SIZE")
     write = load(a.write_dir, "WRITE_SIZE")
+    if a.kernel:
+        name, row = a.kernel.split(",")
+        F = [v for _, (nm, v) in sorted(fetch.items()) if name in nm]
+        W = [v for _, (nm, v) in sorted(write.items()) if name in nm]
+        m = min(len(F), len(W))
+        hbm = [2.0 * F[i] + W[i] for i in range(m)]
+        alg = [N * (float(row) + 8.0 * (i % 30)) for i in range(m)]
+        out = {"kernel": name, "launches": m, "n": a.n, "row_bytes": float(row),
+               "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950), write = WRITE_SIZE x 1024",
+               "hbm_bytes_per_launch": sum(hbm) / max(m, 1), "alg_bytes_per_launch": sum(alg) / max(m, 1),
+               "hbm_over_alg": sum(hbm) / sum(alg) if m else None,
+               "excess_bytes_per_launch": (sum(hbm) - sum(alg)) / max(m, 1)}
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        json.dump(out, open(a.out, "w"), indent=1)
+        print(json.dumps(out, indent=1))
+        return
     if a.smsm:
         f = [int(v) for v in a.smsm.split(",")]
         nx, ny, nz, s_, k_ = f[:5]
