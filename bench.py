@@ -337,6 +337,32 @@ def smsm_block_record(args, order):
     return g.get(order)
 
 
+C2_GOLDEN = os.path.join(ROOT, "tests", "golden", "configs2_smsm.json")
+
+
+def check_configs2_run(args, step, rank):
+    """(verified, mismatches, outer iterations checked): an N = 2 SMSM run is configs[2] (512^3, two z-slab blocks
+    of 512 x 512 x 256, configs[2]'s options) -- its first outer iterations against the oracle record of that
+    problem: LSQR residual (hex), LSQR count, and this rank's inner counts.  (None, ...) for another problem."""
+    if not os.path.exists(C2_GOLDEN):
+        return None, ["no record"], 0
+    g = json.load(open(C2_GOLDEN))
+    rec = g.get("cubes", {}).get("512")
+    if (rec is None or (args.smsm_mesh, args.smsm_planes, args.s, args.inner_max_it, args.outer_max_it,
+                        args.restart) != (512, 256, g["s"], g["inner"]["max_it"], g["outer"]["max_it"],
+                                          g["inner"]["restart"]) or args.peclet is not None):
+        return None, ["not configs[2]'s problem"], 0
+    k = min(len(step.lsqr_rnorm), len(rec["hist_hex"]))
+    bad = []
+    if [float(h).hex() for h in step.lsqr_rnorm[:k]] != rec["hist_hex"][:k]:
+        bad.append("hist_hex")
+    if list(step.lsqr_its[:k]) != rec["lsqr_its"][:k]:
+        bad.append("lsqr_its")
+    if step.inner_its[:k * args.s] != [rec["inner_its"][o][j][rank] for o in range(k) for j in range(args.s)]:
+        bad.append("inner_its")
+    return not bad, bad, k
+
+
 def check_smsm_block(step, blk, ref, nsteps):
     """(verified, mismatches): the first nsteps outer iterations of an SMSM block run against its oracle record --
     every LSQR residual (hex), LSQR count and inner count, and the SHA-256 of x after the last one."""
@@ -895,6 +921,22 @@ def main():
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed_max, updates = float(tmax[0]), float(t[1])
+        timed_check = None
+        if variant == "smsm" and world == 2:
+            # N = 2 is configs[2] itself (512^3, two blocks): the run's own outer iterations -- warm-up and timed --
+            # against the oracle record of that problem, as far as the record goes (it ends where configs[2]
+            # converges); every rank checks its block's inner counts, the verdict is all ranks'
+            ok_t, bad_t, nchk = check_configs2_run(args, step, rank)
+            if ok_t is not None:
+                flag = torch.tensor([0.0 if ok_t else 1.0], dtype=torch.float64,
+                                    device="cuda" if args.backend == "nccl" else "cpu")
+                dist.all_reduce(flag, op=dist.ReduceOp.SUM)
+                ok_t = float(flag[0]) == 0.0
+            timed_check = {"verified": ok_t, "mismatch": bad_t, "outer_iterations_checked": nchk,
+                           "outer_iterations_run": args.warmup + args.steps,
+                           "reference": "tests/golden/configs2_smsm.json['cubes']['512'] (oracle/oracle.c "
+                                        "orc_smsm_solve, DBR order, lean): every outer LSQR residual (hex), LSQR "
+                                        "count and inner count of the run's first outer iterations"}
         if not args.no_verify_ranks:
             # collective on every rank, after the timed loop and outside it
             verified, vmis, vsec = verify_ranks(ctx, comm, world, rank)
@@ -939,6 +981,11 @@ def main():
                "verified": verified}
         if ref_ranks is not None:
             out["verification"] = ref_ranks
+        if world > 1 and timed_check is not None:
+            out["timed_run_verification"] = timed_check
+            if timed_check["verified"] is False:
+                verified = False
+                out["verified"] = False
         if ref is not None:
             out["verification"] = {"reference": "tests/golden/configs1_seq.json['dbr'] (oracle/oracle.c, DBR order)",
                                    "checked": "iterations, reason, every residual-history entry (hex), SHA-256 of x",

@@ -60,6 +60,12 @@ struct msp_ctx {
   int64_t partial_cap = 0;     // doubles
   void* seqbuf = nullptr;      // MSP_REDUCE_SEQ's transducers and guesses (msplit_seq.hip)
   int64_t seqbuf_cap = 0;      // bytes
+  uint32_t seq_epoch = 0;      // the overlapped transducer builds' flag value (msplit_seq.hip seqx_core)
+  hipStream_t seq_aux = nullptr;   // their stream (CU-masked), the walks' stream (the other CUs), and the events
+  hipStream_t seq_walk = nullptr;  // that order them with the context's
+  hipEvent_t seq_ev[3] = {nullptr, nullptr, nullptr};
+  uint32_t* seqready = nullptr;  // the builds' per-segment ready words (zeroed when allocated; never hold anything else)
+  int64_t seqready_cap = 0;      // words
   double* seqacc = nullptr;    // MSP_REDUCE_SEQ chains: two rows of MSK_MAX_GROUP running sums
   uint64_t epoch = 0;          // bumped when a buffer captured graphs point at is reallocated
   int reduce = MSP_REDUCE_DBR;  // MSP_REDUCE_SEQ: PETSc's sequential order (msplit_seq.hip)

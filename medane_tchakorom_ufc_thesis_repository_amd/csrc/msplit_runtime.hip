@@ -83,6 +83,11 @@ static void ctx_free(msp_ctx* c) {
   for (auto e : c->pool) (void)hipEventDestroy(e);
   if (c->partial) (void)hipFree(c->partial);
   if (c->seqbuf) (void)hipFree(c->seqbuf);
+  if (c->seqready) (void)hipFree(c->seqready);
+  if (c->seq_aux) (void)hipStreamSynchronize(c->seq_aux), (void)hipStreamDestroy(c->seq_aux);
+  if (c->seq_walk) (void)hipStreamSynchronize(c->seq_walk), (void)hipStreamDestroy(c->seq_walk);
+  for (auto e : c->seq_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->seqacc) (void)hipFree(c->seqacc);
   if (c->dscratch) (void)hipFree(c->dscratch);
   if (c->hscratch) (void)hipHostFree(c->hscratch);

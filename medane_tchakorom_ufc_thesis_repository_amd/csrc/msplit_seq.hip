@@ -586,15 +586,11 @@ __device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str,
 
 // Workgroup k: segment k of every sum.  Thread t holds terms 16t..16t+15 of the segment (the products staged
 // through LDS from coalesced loads); four threads make a sub-segment's transducer, wave 0 composes the 64 subs.
-__global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w, Vecs V, int nv, int64_t n,
-                                                   int self, const double* __restrict__ pre, Tr* __restrict__ segT,
-                                                   Tr* __restrict__ subT, int64_t K, const int* __restrict__ stop) {
-  if (stopped(stop)) return;
-  __shared__ double sp[kSeg + kSeg / kPer];  // products, one pad slot per 16: thread t's run at 17t
-  __shared__ double ssum[kSubs];
-  __shared__ Tr str[kT / 64];
+__device__ __forceinline__ void trans_block(int64_t k, const double* __restrict__ w, const Vecs& V, int nv, int64_t n,
+                                            int self, const double* __restrict__ pre, Tr* __restrict__ segT,
+                                            Tr* __restrict__ subT, int64_t K, double* sp, double* ssum, Tr* str) {
   const int t = threadIdx.x;
-  const int64_t k = blockIdx.x, c0 = k * kSeg;
+  const int64_t c0 = k * kSeg;
   const int cnt = (int)max<int64_t>(0, min<int64_t>(kPer, n - (c0 + (int64_t)kPer * t)));
   double xr[kPer];
 #pragma unroll
@@ -628,6 +624,25 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
     trans_segment(sp, ssum, str, pre[(int64_t)v * K + k], cnt, subT + ((int64_t)v * K + k) * kSubs,
                   segT + (int64_t)v * K + k);
   }
+}
+
+constexpr int kSpTrans = kSeg + kSeg / kPer;  // products, one pad slot per 16: thread t's run at 17t
+
+// ready != nullptr (round 6, the overlapped launch): after its records, the workgroup publishes ready[k] = epoch for
+// the walk that runs concurrently on the context's stream (ripwalk_sum's wait_ready).
+__global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w, Vecs V, int nv, int64_t n,
+                                                   int self, const double* __restrict__ pre, Tr* __restrict__ segT,
+                                                   Tr* __restrict__ subT, int64_t K, const int* __restrict__ stop,
+                                                   uint32_t* ready, uint32_t epoch) {
+  if (stopped(stop)) return;
+  __shared__ double sp[kSpTrans];
+  __shared__ double ssum[kSubs];
+  __shared__ Tr str[kT / 64];
+  trans_block(blockIdx.x, w, V, nv, n, self, pre, segT, subT, K, sp, ssum, str);
+  if (!ready) return;
+  __threadfence();  // every thread's records, at agent scope, before the flag
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(ready + blockIdx.x, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Apply the longest prefix of the lanes' runs (lane order) that is valid at s; returns its length.
@@ -928,6 +943,23 @@ __device__ __forceinline__ bool any_ties(const Rip& q) {
   return __ballot(__double_as_longlong(q.sd0) != __double_as_longlong(q.sd1)) != 0;
 }
 
+// The overlapped builds (seqx_core, round 6): segment k's records are read only once its builder has published
+// ready[k] = epoch (an agent-scope release behind the records; the acquire here orders the wave's later loads of
+// them).  Lane l waits for segment k0 + l.  A wait that outlasts 4 s gives up: the sum then comes out NaN, a loud
+// failure instead of a hang.
+__device__ __forceinline__ bool wait_ready(uint32_t* ready, uint32_t epoch, int64_t k0, int64_t K, int lane) {
+  if (!ready || k0 >= K) return true;
+  uint32_t* f = ready + min<int64_t>(k0 + lane, K - 1);
+  bool ok = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+  const int64_t t0 = wall_clock64();
+  while (__ballot(!ok)) {
+    if (wall_clock64() - t0 > 400000000) return false;  // 100 MHz ticks
+    __builtin_amdgcn_s_sleep(2);
+    if (!ok) ok = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+  }
+  return true;
+}
+
 // Workgroup v: sum v, from +0.0, every map applied by ripples: the window of 64 segment maps up to the first that
 // does not apply; that segment's sub maps likewise (its terms' loads in flight meanwhile); a sub that does not
 // apply is added term by term from LDS, and the ripple resumes after it.  rw: the ripple width over segments and a
@@ -936,7 +968,7 @@ __device__ __forceinline__ void ripwalk_sum(int v, const double* __restrict__ w,
                                             const Tr* __restrict__ segT, const Tr* __restrict__ subT, int64_t K,
                                             const double* __restrict__ acc_in, double* __restrict__ partial,
                                             int64_t nchunks, int64_t* __restrict__ stats, int rw, int rs, int pf,
-                                            double* sp) {
+                                            double* sp, uint32_t* ready = nullptr, uint32_t epoch = 0) {
   const int t = threadIdx.x, lane = t & 63;
   const double* y = self ? nullptr : vec_row(V, v);
   const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
@@ -957,12 +989,16 @@ __device__ __forceinline__ void ripwalk_sum(int v, const double* __restrict__ w,
   int64_t kp = -1;
   int64_t n_hit = 0, n_miss = 0;
   double s = acc_in ? acc_in[v] : 0.0;
+  bool live = wait_ready(ready, epoch, 0, K, lane);
   Tr twn = tr_load(segT + (int64_t)v * K + min<int64_t>(lane, K - 1));
-  for (int64_t kb = 0; kb < K; kb += 64) {
+  for (int64_t kb = 0; kb < K && live; kb += 64) {
     const int lim = (int)min<int64_t>(64, K - kb);
     const bool in = lane < lim;
     const Tr tw = twn;
-    if (kb + 64 < K) twn = tr_load(segT + (int64_t)v * K + min<int64_t>(kb + 64 + lane, K - 1));
+    if (kb + 64 < K) {
+      live = wait_ready(ready, epoch, kb + 64, K, lane);  // the overlapped builds: the next window is built
+      twn = tr_load(segT + (int64_t)v * K + min<int64_t>(kb + 64 + lane, K - 1));
+    }
     const Prep pv = prep_of(tr_sel(in, tw, tr_bad()));
     const Rip qv = rip_of(pv);
     const bool tv = any_ties(qv);
@@ -1016,6 +1052,7 @@ __device__ __forceinline__ void ripwalk_sum(int v, const double* __restrict__ w,
     }
   }
 #undef TICK
+  if (!live) s = __builtin_nan("");  // a builder never published: no result
   if (t < 64)
     for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
   if (stats && t == 0) {
@@ -1042,11 +1079,13 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
                                                          int64_t K, const double* __restrict__ acc_in,
                                                          double* __restrict__ partial, int64_t nchunks,
                                                          const int* __restrict__ stop, int64_t* __restrict__ stats,
-                                                         int rw, int rs, int pf) {
+                                                         int rw, int rs, int pf, uint32_t* ready, uint32_t epoch) {
   if (stopped(stop)) return;
   __shared__ double sp[kSeg];
-  ripwalk_sum(blockIdx.x, w, V, n, self, segT, subT, K, acc_in, partial, nchunks, stats, rw, rs, pf, sp);
+  ripwalk_sum(blockIdx.x, w, V, n, self, segT, subT, K, acc_in, partial, nchunks, stats, rw, rs, pf, sp, ready,
+              epoch);
 }
+
 
 }  // namespace
 
@@ -1078,6 +1117,37 @@ constexpr int64_t kParMinDot = int64_t(1) << 17;    // one dot
 constexpr int64_t kParMinSum = int64_t(1) << 19;    // an MDot
 constexpr int64_t kParMinChain = int64_t(1) << 17;  // an LSQR chain: its total length per sum
 
+// The overlapped builds' two streams, made on first use: the walks on the first kSeqWalkCUs compute units, the
+// builds on the others (CU masks), so that no build wave shares a CU with a walk -- a walk is a chain of dependent
+// ripple steps, and co-resident build waves took its issue slots (the SMSM block in PETSc's order: +6 % with both
+// streams on every CU); plus the events that order them with the context's stream.  Nonzero: no such streams.
+constexpr int kSeqWalkCUs = 32;  // >= MSK_MAX_GROUP: one CU per walked sum
+static int seq_aux(msp_ctx* c) {
+  if (c->seq_aux) return 0;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+      ncu < 2 * kSeqWalkCUs || ncu > 1024)
+    return 1;
+  uint32_t mw[32] = {0}, mb[32] = {0};
+  const int words = (ncu + 31) / 32;
+  for (int i = 0; i < ncu; ++i) (i < kSeqWalkCUs ? mw : mb)[i / 32] |= 1u << (i % 32);
+  hipStream_t sw = nullptr, sb = nullptr;
+  if (hipExtStreamCreateWithCUMask(&sw, (uint32_t)words, mw) != hipSuccess) return 1;
+  if (hipExtStreamCreateWithCUMask(&sb, (uint32_t)words, mb) != hipSuccess) {
+    (void)hipStreamDestroy(sw);
+    return 1;
+  }
+  for (auto& e : c->seq_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      (void)hipStreamDestroy(sw);
+      (void)hipStreamDestroy(sb);
+      return 1;
+    }
+  c->seq_walk = sw;
+  c->seq_aux = sb;
+  return 0;
+}
+
 // The parallel engine: nv sums of n terms w[i] * (V_v[i] * sy_v) (self: w[i] * w[i]), each from acc_in[v] (device;
 // nullptr: +0.0), into partial's DBR layout.  n > 0.
 static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t n, int self, const double* acc_in,
@@ -1094,13 +1164,24 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
     if (e != hipSuccess) return (int)e;
     c->seqbuf_cap = need;
   }
+  if (K > c->seqready_cap) {  // the overlapped builds' ready words: a buffer of their own, zeroed, so that no word ever
+                              // held anything but an earlier launch's epoch (every launch takes a new, nonzero one)
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return (int)hipErrorUnknown;
+    if (c->seqready) (void)hipFree(c->seqready);
+    c->seqready = nullptr;
+    c->seqready_cap = 0;
+    hipError_t e = hipMalloc((void**)&c->seqready, (size_t)K * sizeof(uint32_t));
+    if (e != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(c->seqready, 0, (size_t)K * sizeof(uint32_t), c->stream)) != hipSuccess) return (int)e;
+    c->seqready_cap = K;
+  }
   Tr* subT = static_cast<Tr*>(c->seqbuf);
   Tr* segT = subT + (int64_t)nv * K * kSubs;
   double* pre = reinterpret_cast<double*>(segT + (int64_t)nv * K);
+  uint32_t* ready = c->seqready;
   const int rc = msk_dot_stage1(w, V, nv, n, pre, K, self, stop, c->stream);
   if (rc) return rc;
   k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, acc_in, stop);
-  k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop);
   // MSPLIT_SEQ_STATS=1: per-sum walk counters on stderr (a diagnostic; its buffer lives for this call only)
   const char* st = getenv("MSPLIT_SEQ_STATS");
   int64_t* dstats = nullptr;
@@ -1120,12 +1201,42 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
   const char* pfe = getenv("MSPLIT_SEQ_PREFETCH");  // 0: a descended segment's loads start at the descent
   const int rw = rwe ? atoi(rwe) : 16, rs = rse ? atoi(rse) : 8, pf = pfe && pfe[0] == '0' ? 0 : 1;
   const bool ripwalk = !(wk && wk[0] == 's');
-  if (!ripwalk)
-    k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
-                                                          stop, dstats, prep);
-  else
-    k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial,
-                                                             nchunks, stop, dstats, rw, rs, pf);
+  // The transducer builds and the walk run on two streams of their own (seq_aux: disjoint compute units) while the
+  // walk follows the builds (round 6): it waits per window of 64 segments for their builders' ready words
+  // (ripwalk_sum's wait_ready), so the builds -- about a fifth of a PETSc-order GMRES step -- overlap the walks.
+  // The builds are enqueued first, so two streams that share one hardware queue still make progress (the walk then
+  // starts after them).
+  // MSPLIT_SEQ_OVERLAP=0: one stream, the builds before the walk (rounds 4-5).
+  const char* ove = getenv("MSPLIT_SEQ_OVERLAP");
+  // only where walks are long next to their builds: MDots (several sums, each hovering near zero); a norm's walk
+  // (one sum that only grows) or a single dot would just wait for its builds
+  const bool overlap = ripwalk && !(ove && ove[0] == '0') && (ove && ove[0] == '2' ? true : nv >= 2 && !self) &&
+                       seq_aux(c) == 0;
+  if (overlap) {
+    if (++c->seq_epoch == 0) c->seq_epoch = 1;  // 0 is the words' initial value
+    if (hipEventRecord(c->seq_ev[0], c->stream) != hipSuccess ||
+        hipStreamWaitEvent(c->seq_aux, c->seq_ev[0], 0) != hipSuccess ||
+        hipStreamWaitEvent(c->seq_walk, c->seq_ev[0], 0) != hipSuccess)
+      return (int)hipErrorUnknown;
+    k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->seq_aux>>>(w, *V, nv, n, self, pre, segT, subT, K, stop, ready,
+                                                                 c->seq_epoch);
+    k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, c->seq_walk>>>(w, *V, n, self, segT, subT, K, acc_in, partial,
+                                                               nchunks, stop, dstats, rw, rs, pf, ready, c->seq_epoch);
+    if (hipEventRecord(c->seq_ev[1], c->seq_aux) != hipSuccess ||
+        hipEventRecord(c->seq_ev[2], c->seq_walk) != hipSuccess ||
+        hipStreamWaitEvent(c->stream, c->seq_ev[1], 0) != hipSuccess ||  // the next call reuses the records
+        hipStreamWaitEvent(c->stream, c->seq_ev[2], 0) != hipSuccess)    // and reads the sums
+      return (int)hipErrorUnknown;
+  } else {
+    k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop,
+                                                                nullptr, 0);
+    if (!ripwalk)
+      k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
+                                                            stop, dstats, prep);
+    else
+      k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial,
+                                                               nchunks, stop, dstats, rw, rs, pf, nullptr, 0);
+  }
   if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];
     if (hipMemcpyAsync(h, dstats, sizeof(h), hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
