@@ -471,6 +471,9 @@ int msp_amsg_get_stats(const msp_amsg *am, int64_t *sent, int64_t *skipped);
  * copy is enqueued but not yet published (in_flight) cannot be withdrawn, a
  * DMA, so they are counted and completed by draining the stream. */
 int msp_amsg_discard_pending(msp_amsg *am, int64_t *discarded, int64_t *in_flight);
+/* diagnostics: the link src -> this rank as this rank sees it: data pub, data claim, data seen, partial-CV seq,
+ * partial-CV seen, verdict seq, src's device slots opened, ranks attached (up to n of these 8) */
+int msp_amsg_get_link_info(const msp_amsg *am, int32_t src, int64_t *info, int32_t n);
 
 /* ------------------------------------------- async minimization broadcast */
 /* Newest-value broadcast of each block's rows of R (AMAM-global), in POSIX

@@ -164,6 +164,7 @@ _SIGS = {
     "msp_amsg_close_peers": [_vp],
     "msp_amsg_get_stats": [_vp, _P(C.c_int64), _P(C.c_int64)],
     "msp_amsg_discard_pending": [_vp, _P(C.c_int64), _P(C.c_int64)],
+    "msp_amsg_get_link_info": [_vp, C.c_int32, _P(C.c_int64), C.c_int32],
     "msp_abcast_discard_pending": [_vp, _P(C.c_int64), _P(C.c_int64)],
     "msp_abcast_enable_device": [_vp, _vp, C.c_int32],
     "msp_abcast_get_nbuf": [_vp, _i32p],

@@ -325,6 +325,27 @@ int msp_amsg_discard_pending(msp_amsg *m, int64_t *discarded, int64_t *in_flight
   return MSP_SUCCESS;
 }
 
+/* diagnostics (tools, tests): the state of the link src -> this rank as this rank sees it */
+int msp_amsg_get_link_info(const msp_amsg *m, int32_t src, int64_t *info, int32_t n) {
+  if (!m || !info) return aerr(MSP_ERR_ARG_NULL, "NULL argument");
+  if (src < 0 || src >= m->nranks || src == m->rank) return aerr(MSP_ERR_ARG_OUTOFRANGE, "peer rank out of range");
+  int64_t v[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  msp_amsg *mm = (msp_amsg *)m;
+  if (data_at(mm, src, m->rank) && m->dst_) {
+    dslot_state *d = mm->dst_ + (size_t)src * 2 + (m->rank == src - 1 ? 0 : 1);
+    v[0] = (int64_t)atomic_load_explicit(&d->pub, memory_order_seq_cst);
+    v[1] = (int64_t)atomic_load_explicit(&d->claim, memory_order_seq_cst);
+  }
+  v[2] = (int64_t)m->seen[(size_t)src * MSP_AMSG_NKINDS + MSP_AMSG_DATA];
+  v[3] = (int64_t)atomic_load_explicit(&ctrl_at(mm, src, m->rank, MSP_AMSG_PARTIAL_CV)->seq, memory_order_acquire);
+  v[4] = (int64_t)m->seen[(size_t)src * MSP_AMSG_NKINDS + MSP_AMSG_PARTIAL_CV];
+  v[5] = (int64_t)atomic_load_explicit(&ctrl_at(mm, src, m->rank, MSP_AMSG_VERDICT)->seq, memory_order_acquire);
+  v[6] = m->peer ? (int64_t)(m->peer[src] != NULL) : -1;
+  v[7] = (int64_t)atomic_load_explicit(&m->hdr->attached, memory_order_acquire);
+  for (int i = 0; i < n && i < 8; ++i) info[i] = v[i];
+  return MSP_SUCCESS;
+}
+
 /* the device slots of src, opened on first use; NULL while src has not enabled them */
 static int peer_slots(msp_amsg *m, int src, double **out) {
   *out = m->peer[src];

@@ -860,6 +860,13 @@ class AsyncMessages:
         call("msp_amsg_discard_pending", self.h, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def link_info(self, src: int) -> list:
+        """Diagnostics: [data pub, data claim, data seen, partial-CV seq, partial-CV seen, verdict seq, src's slots
+        opened, ranks attached] of the link src -> this rank."""
+        v = np.zeros(8, np.int64)
+        call("msp_amsg_get_link_info", self.h, int(src), v.ctypes.data_as(C.POINTER(C.c_int64)), 8)
+        return v.tolist()
+
     def recv_vec(self, src: int, nints: int, v: Vec, off: int, cap: int):
         iv = np.zeros(max(nints, 1), np.int32)
         n = C.c_int64()

@@ -48,7 +48,7 @@ def record(order, problem=PROBLEM):
 def main():
     orders = sys.argv[1:] or ["dbr", "seq"]
     po.build()
-    po.set_threads(min(8, os.cpu_count() or 1))   # element-wise loops and DBR chunks only; SEQ sums stay serial
+    po.set_threads(int(os.environ.get("ORC_THREADS", min(8, os.cpu_count() or 1))))  # element-wise loops, DBR chunks
     out = json.load(open(OUT)) if os.path.exists(OUT) else {}
     out.update({"problem": PROBLEM, "inner": INNER, "outer": OUTER,
                 "generator": "tests/golden/make_smsm_block.py (oracle/oracle.c orc_smsm_solve, lean)"})
