@@ -229,12 +229,20 @@ def test_am_eight_processes_device_transport(problem, nbuf, monkeypatch):
     AMAM-global_prime.c:522-572), and every process exits 0."""
     world = 8
     monkeypatch.setenv("MSPLIT_ABCAST_NBUF", nbuf)
-    # two hardware queues per process (HIP's default is four): eight ranks plus a parent that has touched the GPU
-    # would otherwise oversubscribe the GPU's queue slots, and the scheduler then time-slices the mapped queues so
-    # unfairly that one rank runs thousands of iterations while the others run tens (seen: one rank at its 20000-
-    # iteration cap while its neighbours, starved, had not answered its verification) -- a property of the
-    # oversubscribed schedule, not of the asynchronous protocol, which terminates under any fair one
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
+    # one hardware queue per rank.  This GPU's KFD node maps 24 compute queues (topology `num_cp_queues`, recorded in
+    # profiles/r06/async8/kfd_props.txt); HIP gives each process up to four.  Eight ranks plus a pytest parent that
+    # has run GPU tests (its own four queues) oversubscribe those slots, and the scheduler then runs the processes
+    # one at a time: one rank ran 600 iterations alone in 5 s while the seven others sat at their second (and, with
+    # no iteration cap, forever: the hang of the first suite run).  With one queue per rank the eight interleave
+    # and the run terminates in ~30 iterations per rank (profiles/r06/async8/).  Not a property of the asynchronous
+    # protocol: configs[3]/[4] run one process per GPU.
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", os.environ.get("MSPLIT_TEST_WORKER_HW_QUEUES", "1"))
+    tdir = os.environ.get("MSPLIT_TEST_TRACE_DIR")
+    if tdir:                                               # diagnostics: what the GPU holds before the ranks start
+        import subprocess
+        with open(os.path.join(tdir, "parent_vram.txt"), "w") as f:
+            f.write(subprocess.run(["rocm-smi", "--showmeminfo", "vram", "--showpids"], capture_output=True,
+                                   text=True, timeout=60).stdout)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
