@@ -1086,6 +1086,245 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
               epoch);
 }
 
+// ------------------------------------------------------------ the ripple walk with filler waves (round 6)
+// ripwalk_sum's four waves all walk, and all four fill a descended segment's terms: the walk stops at each fill and
+// waits out its loads (a third of a PETSc-order step's walk time, profiles/r06/seq_pc/).  Here wave 0 walks alone
+// and waves 1-3 fill: in walk order, each BAD segment's products and its 64 sub records go into a ring of kRing LDS
+// slots, as far ahead of the walk as the ring allows.  A BAD segment never applies, so the walk descends into every
+// one of them, in order, and finds it filled; a segment that fails only at the actual s (rare: 3 % of descents) is
+// read by the walk itself, sub record and failing subs' terms.  The sums are the same bits: the same maps, the
+// same products (formed as fill_store forms them), the same adds.
+//
+// Hand-off through LDS: a filler wave stores its part of a slot, then one add of its lane 0 to the slot's counter
+// (workgroup-scope release, so the wave's LDS stores come first); the wave whose add completes the count publishes
+// the slot's segment (release).  The walk polls for that segment (acquire) and only then reads the slot.  A slot is
+// refilled only once the walk has moved past its segment (walk_pos, published by the walk before it looks for a
+// slot), so the segment it reads is never rewritten under it.  Every wait gives up after 4 s: the sum then comes out
+// NaN and the fillers stop.
+constexpr int kRing = 3;
+constexpr int kFillW = 3;
+constexpr int kFillT = kFillW * 64;
+constexpr int kFillPer = (kSeg + kFillT - 1) / kFillT;
+struct alignas(16) RingSlot {
+  double p[kSeg];
+  Tr sub[kSubs];
+};
+struct RingCtl {
+  int32_t seg[kRing];  // the segment a slot holds (published), -1: none yet
+  int32_t cnt[kRing];  // filler waves done with the slot's current fill
+  int32_t walk_pos;    // the walk is at this segment or past it: slots holding earlier ones are free
+  int32_t done;        // the walk has finished (or given up): the fillers stop
+};
+__device__ __forceinline__ int32_t lds_acq(int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_rel(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+constexpr int64_t kSpinTicks = 400000000;  // 4 s of 100 MHz ticks
+
+// The filler waves' loop: BAD segments in order into the ring.  ft: thread index among the fillers.
+__device__ __forceinline__ void fill_ring(int v, const double* __restrict__ w, const double* __restrict__ y, double sy,
+                                          int64_t n, int self, const Tr* __restrict__ segT,
+                                          const Tr* __restrict__ subT, int64_t K, RingSlot* ring, RingCtl* ctl,
+                                          uint32_t* ready, uint32_t epoch) {
+  const int t = threadIdx.x, lane = t & 63, ft = t - 64;
+  const bool recs = t < 128;  // wave 1 also moves the slot's sub records
+  int32_t pk0 = -1, pk1 = -1, pk2 = -1;  // the segments of the last kRing fills (the oldest first)
+  int u = 0;
+  for (int64_t kb = 0; kb < K; kb += 64) {
+    if (!wait_ready(ready, epoch, kb, K, lane)) return;
+    const int64_t kl = kb + lane;
+    const uint32_t fl = kl < K ? segT[(int64_t)v * K + kl].fl : 0u;
+    uint64_t badm = __ballot((fl & F_BAD) != 0);
+    while (badm) {
+      const int32_t k = (int32_t)(kb + __builtin_ctzll(badm));
+      badm &= badm - 1;
+      const int slot = u % kRing;
+      // the slot's previous segment (pk0) published by every filler wave, and passed by the walk
+      const int64_t t0 = wall_clock64();
+      for (;;) {
+        if (lds_acq(&ctl->done)) return;
+        if (lds_acq(&ctl->seg[slot]) == pk0 && pk0 < lds_acq(&ctl->walk_pos)) break;
+        if (wall_clock64() - t0 > kSpinTicks) return;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      RingSlot* S = ring + slot;
+      double a[kFillPer], b[kFillPer];
+      const int64_t c0 = (int64_t)k * kSeg;
+#pragma unroll
+      for (int r = 0; r < kFillPer; ++r) {
+        const int i = ft + r * kFillT;
+        const int64_t g = min<int64_t>(c0 + min(i, kSeg - 1), n - 1);
+        a[r] = w[g];
+        b[r] = y ? y[g] : 0.0;
+      }
+      Tr tr;
+      if (recs) tr = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
+#pragma unroll
+      for (int r = 0; r < kFillPer; ++r) {
+        const int i = ft + r * kFillT;
+        if (i < kSeg) S->p[i] = c0 + i < n ? (self ? a[r] * a[r] : a[r] * (b[r] * sy)) : 0.0;
+      }
+      if (recs) S->sub[lane] = tr;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) {
+        const int32_t old = __hip_atomic_fetch_add(&ctl->cnt[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old == kFillW - 1) {  // the last of the filler waves: the slot is whole
+          __hip_atomic_store(&ctl->cnt[slot], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          lds_rel(&ctl->seg[slot], k);
+        }
+      }
+      pk0 = pk1;
+      pk1 = pk2;
+      pk2 = k;
+      ++u;
+    }
+  }
+}
+
+// Wave 0: sum v, as ripwalk_sum (the same ripples, the same serial adds), its descended segments from the ring.
+__device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict__ w, const double* __restrict__ y,
+                                                double sy, int64_t n, int self, const Tr* __restrict__ segT,
+                                                const Tr* __restrict__ subT, int64_t K,
+                                                const double* __restrict__ acc_in, double* __restrict__ partial,
+                                                int64_t nchunks, int64_t* __restrict__ stats, int rw, int rs,
+                                                RingSlot* ring, RingCtl* ctl, double* sp1, uint32_t* ready,
+                                                uint32_t epoch) {
+  const int lane = threadIdx.x & 63;
+  int64_t n_win = 0, n_segdesc = 0, n_rip = 0, n_subser = 0, n_hit = 0, n_miss = 0;
+  int64_t c_win = 0, c_rip = 0, c_serial = 0, c_fill = 0, c_all = stats ? wall_clock64() : 0;
+#define TICK(acc, stmt)                             \
+  do {                                              \
+    const int64_t t0_ = stats ? wall_clock64() : 0; \
+    stmt;                                           \
+    if (stats) acc += wall_clock64() - t0_;         \
+  } while (0)
+  double s = acc_in ? acc_in[v] : 0.0;
+  bool live = wait_ready(ready, epoch, 0, K, lane);
+  Tr twn = tr_load(segT + (int64_t)v * K + min<int64_t>(lane, K - 1));
+  for (int64_t kb = 0; kb < K && live; kb += 64) {
+    if (lane == 0) lds_rel(&ctl->walk_pos, (int32_t)kb);
+    const int lim = (int)min<int64_t>(64, K - kb);
+    const bool in = lane < lim;
+    const Tr tw = twn;
+    if (kb + 64 < K) {
+      live = wait_ready(ready, epoch, kb + 64, K, lane);
+      twn = tr_load(segT + (int64_t)v * K + min<int64_t>(kb + 64 + lane, K - 1));
+    }
+    const Prep pv = prep_of(tr_sel(in, tw, tr_bad()));
+    const Rip qv = rip_of(pv);
+    const bool tv = any_ties(qv);
+    const uint64_t badm = __ballot(in && (pv.fl & F_BAD) != 0);
+    for (int f = 0; live;) {
+      TICK(c_win, f = ripple_runw(rw, pv, qv, tv, s, f, lim, lane, n_win));
+      if (f >= lim) break;
+      const int32_t k = (int32_t)(kb + f);
+      ++n_segdesc;
+      if (lane == 0) lds_rel(&ctl->walk_pos, k);
+      const int64_t tf0 = stats ? wall_clock64() : 0;
+      int slot = -1;
+      Tr tp;
+      if ((badm >> f) & 1) {  // the fillers bring it
+        const int64_t t0 = wall_clock64();
+        while (slot < 0) {
+#pragma unroll
+          for (int q = 0; q < kRing; ++q)
+            if (lds_acq(&ctl->seg[q]) == k) slot = q;
+          if (slot >= 0) break;
+          if (wall_clock64() - t0 > kSpinTicks) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (slot < 0) {
+          live = false;
+          break;
+        }
+        tp = ring[slot].sub[lane];
+        ++n_hit;
+      } else {  // a map that only fails at the actual s
+        tp = tr_load(subT + ((int64_t)v * K + k) * kSubs + lane);
+        ++n_miss;
+      }
+      if (stats) c_fill += wall_clock64() - tf0;
+      const Prep pu = prep_of(tp);
+      const Rip qu = rip_of(pu);
+      const bool tu = any_ties(qu);
+      int j;
+      TICK(c_rip, j = ripple_runw(rw, pu, qu, tu, s, 0, kSubs, lane, n_rip));
+      while (j < kSubs) {
+        const int64_t c0 = (int64_t)k * kSeg + (int64_t)j * kSub;
+        const int i1 = (int)max<int64_t>(0, min<int64_t>(kSub, n - c0));
+        if (slot >= 0) {
+          TICK(c_serial, s = serial_terms(ring[slot].p, j * kSub, j * kSub + i1, s, lane));
+        } else {  // this sub's terms, formed as fill_store forms them
+          const int64_t g = min<int64_t>(c0 + lane, n - 1);
+          const double a = w[g], b = y ? y[g] : 0.0;
+          sp1[lane] = c0 + lane < n ? (self ? a * a : a * (b * sy)) : 0.0;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          TICK(c_serial, s = serial_terms(sp1, 0, i1, s, lane));
+          __builtin_amdgcn_wave_barrier();  // lane 0's reads before the next sub's stores
+        }
+        ++n_subser;
+        TICK(c_rip, j = ripple_runw(rs, pu, qu, tu, s, j + 1, kSubs, lane, n_rip));
+      }
+      ++f;
+    }
+  }
+#undef TICK
+  if (lane == 0) lds_rel(&ctl->done, 1);
+  if (!live) s = __builtin_nan("");
+  for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
+  if (stats && lane == 0) {
+    stats[v * 8 + 0] = n_win;
+    stats[v * 8 + 1] = n_segdesc;
+    stats[v * 8 + 2] = n_rip;
+    stats[v * 8 + 3] = n_subser;
+    stats[v * 8 + 4] = n_hit;
+    stats[v * 8 + 5] = n_miss;
+    stats[v * 8 + 6] = stats[v * 8 + 7] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 0] = c_win;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 1] = c_rip;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 2] = c_serial;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 3] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 4] = wall_clock64() - c_all;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 5] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 6] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 7] = c_fill;
+  }
+}
+
+__global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk_pc(const double* __restrict__ w, Vecs V, int64_t n, int self,
+                                                            const Tr* __restrict__ segT, const Tr* __restrict__ subT,
+                                                            int64_t K, const double* __restrict__ acc_in,
+                                                            double* __restrict__ partial, int64_t nchunks,
+                                                            const int* __restrict__ stop, int64_t* __restrict__ stats,
+                                                            int rw, int rs, uint32_t* ready, uint32_t epoch) {
+  static_assert(kWalkT == 64 + kFillT, "one walking wave and the filler waves");
+  if (stopped(stop)) return;
+  __shared__ RingSlot ring[kRing];
+  __shared__ RingCtl ctl;
+  __shared__ double sp1[kSub];
+  const int t = threadIdx.x, v = blockIdx.x;
+  if (t < kRing) {
+    ctl.seg[t] = -1;
+    ctl.cnt[t] = 0;
+  }
+  if (t == 0) {
+    ctl.walk_pos = 0;
+    ctl.done = 0;
+  }
+  __syncthreads();
+  const double* y = self ? nullptr : vec_row(V, v);
+  const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
+  if (t < 64)
+    ripwalk_pc_walk(v, w, y, sy, n, self, segT, subT, K, acc_in, partial, nchunks, stats, rw, rs, ring, &ctl, sp1,
+                    ready, epoch);
+  else
+    fill_ring(v, w, y, sy, n, self, segT, subT, K, ring, &ctl, ready, epoch);
+}
+
 
 }  // namespace
 
@@ -1201,6 +1440,17 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
   const char* pfe = getenv("MSPLIT_SEQ_PREFETCH");  // 0: a descended segment's loads start at the descent
   const int rw = rwe ? atoi(rwe) : 16, rs = rse ? atoi(rse) : 8, pf = pfe && pfe[0] == '0' ? 0 : 1;
   const bool ripwalk = !(wk && wk[0] == 's');
+  // MSPLIT_SEQ_FILLERS=0: every wave of the walk's workgroup walks and fills (round 5) instead of filler waves
+  const char* fle = getenv("MSPLIT_SEQ_FILLERS");
+  const bool fillers = !(fle && fle[0] == '0');
+  auto launch_walk = [&](hipStream_t st, uint32_t* rdy, uint32_t ep) {
+    if (fillers)
+      k_seqx_ripwalk_pc<<<dim3(nv), dim3(kWalkT), 0, st>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
+                                                           stop, dstats, rw, rs, rdy, ep);
+    else
+      k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, st>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks, stop,
+                                                        dstats, rw, rs, pf, rdy, ep);
+  };
   // The transducer builds and the walk run on two streams of their own (seq_aux: disjoint compute units) while the
   // walk follows the builds (round 6): it waits per window of 64 segments for their builders' ready words
   // (ripwalk_sum's wait_ready), so the builds -- about a fifth of a PETSc-order GMRES step -- overlap the walks.
@@ -1220,8 +1470,7 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
       return (int)hipErrorUnknown;
     k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->seq_aux>>>(w, *V, nv, n, self, pre, segT, subT, K, stop, ready,
                                                                  c->seq_epoch);
-    k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, c->seq_walk>>>(w, *V, n, self, segT, subT, K, acc_in, partial,
-                                                               nchunks, stop, dstats, rw, rs, pf, ready, c->seq_epoch);
+    launch_walk(c->seq_walk, ready, c->seq_epoch);
     if (hipEventRecord(c->seq_ev[1], c->seq_aux) != hipSuccess ||
         hipEventRecord(c->seq_ev[2], c->seq_walk) != hipSuccess ||
         hipStreamWaitEvent(c->stream, c->seq_ev[1], 0) != hipSuccess ||  // the next call reuses the records
@@ -1234,8 +1483,7 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
       k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
                                                             stop, dstats, prep);
     else
-      k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial,
-                                                               nchunks, stop, dstats, rw, rs, pf, nullptr, 0);
+      launch_walk(c->stream, nullptr, 0);
   }
   if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];
