@@ -1192,8 +1192,8 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
                                                 RingSlot* ring, RingCtl* ctl, double* sp1, uint32_t* ready,
                                                 uint32_t epoch) {
   const int lane = threadIdx.x & 63;
-  int64_t n_win = 0, n_segdesc = 0, n_rip = 0, n_subser = 0, n_hit = 0, n_miss = 0;
-  int64_t c_win = 0, c_rip = 0, c_serial = 0, c_fill = 0, c_all = stats ? wall_clock64() : 0;
+  int64_t n_win = 0, n_segdesc = 0, n_rip = 0, n_subser = 0, n_hit = 0, n_miss = 0, n_badsub = 0, n_guess = 0;
+  int64_t c_win = 0, c_rip = 0, c_serial = 0, c_fill = 0, c_wait = 0, c_all = stats ? wall_clock64() : 0;
 #define TICK(acc, stmt)                             \
   do {                                              \
     const int64_t t0_ = stats ? wall_clock64() : 0; \
@@ -1201,7 +1201,8 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
     if (stats) acc += wall_clock64() - t0_;         \
   } while (0)
   double s = acc_in ? acc_in[v] : 0.0;
-  bool live = wait_ready(ready, epoch, 0, K, lane);
+  bool live;
+  TICK(c_wait, live = wait_ready(ready, epoch, 0, K, lane));
   Tr twn = tr_load(segT + (int64_t)v * K + min<int64_t>(lane, K - 1));
   for (int64_t kb = 0; kb < K && live; kb += 64) {
     if (lane == 0) lds_rel(&ctl->walk_pos, (int32_t)kb);
@@ -1209,7 +1210,7 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
     const bool in = lane < lim;
     const Tr tw = twn;
     if (kb + 64 < K) {
-      live = wait_ready(ready, epoch, kb + 64, K, lane);
+      TICK(c_wait, live = wait_ready(ready, epoch, kb + 64, K, lane));
       twn = tr_load(segT + (int64_t)v * K + min<int64_t>(kb + 64 + lane, K - 1));
     }
     const Prep pv = prep_of(tr_sel(in, tw, tr_bad()));
@@ -1254,6 +1255,14 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
       while (j < kSubs) {
         const int64_t c0 = (int64_t)k * kSeg + (int64_t)j * kSub;
         const int i1 = (int)max<int64_t>(0, min<int64_t>(kSub, n - c0));
+        if (stats) {  // why sub j failed: a BAD record, s outside the record's binade (the guess), or inside it
+          const uint32_t fj = (uint32_t)__builtin_amdgcn_readlane((int)tp.fl, j);
+          const int ej = __builtin_amdgcn_readlane(tp.e, j);
+          const uint64_t sb = (uint64_t)__double_as_longlong(s);
+          const int es = (int)((sb >> 52) & 0x7ff) - 1023;
+          if (fj & F_BAD) ++n_badsub;
+          else if (!(fj & F_ZERO) && (es != ej || (uint32_t)(sb >> 63) != (fj & F_NEG))) ++n_guess;
+        }
         if (slot >= 0) {
           TICK(c_serial, s = serial_terms(ring[slot].p, j * kSub, j * kSub + i1, s, lane));
         } else {  // this sub's terms, formed as fill_store forms them
@@ -1283,11 +1292,12 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
     stats[v * 8 + 3] = n_subser;
     stats[v * 8 + 4] = n_hit;
     stats[v * 8 + 5] = n_miss;
-    stats[v * 8 + 6] = stats[v * 8 + 7] = 0;
+    stats[v * 8 + 6] = n_badsub;
+    stats[v * 8 + 7] = n_guess;
     stats[8 * MSK_MAX_GROUP + v * 8 + 0] = c_win;
     stats[8 * MSK_MAX_GROUP + v * 8 + 1] = c_rip;
     stats[8 * MSK_MAX_GROUP + v * 8 + 2] = c_serial;
-    stats[8 * MSK_MAX_GROUP + v * 8 + 3] = 0;
+    stats[8 * MSK_MAX_GROUP + v * 8 + 3] = c_wait;
     stats[8 * MSK_MAX_GROUP + v * 8 + 4] = wall_clock64() - c_all;
     stats[8 * MSK_MAX_GROUP + v * 8 + 5] = 0;
     stats[8 * MSK_MAX_GROUP + v * 8 + 6] = 0;
