@@ -469,13 +469,12 @@ __device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str,
                                               Tr* __restrict__ sub_out, Tr* __restrict__ seg_out) {
   const int t = threadIdx.x, lane = t & 63, j = t >> 2;
   __syncthreads();
-  double pr[kPer];
+  // the thread's 16 terms are read from LDS in each pass rather than held (three passes at most: the sum, track 0,
+  // and track 1 where a tie needs it), which keeps the kernel at three waves per SIMD
+  const double* mine = sp + t * (kPer + 1);
   double ps = 0.0;
 #pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    pr[i] = sp[t * (kPer + 1) + i];
-    ps += pr[i];
-  }
+  for (int i = 0; i < kPer; ++i) ps += mine[i];
   ps += __shfl_xor(ps, 1);
   ps += __shfl_xor(ps, 2);
   if ((t & 3) == 0) ssum[j] = ps;
@@ -498,18 +497,17 @@ __device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str,
   const int e = GE - 1023;
   const uint32_t sneg = (uint32_t)(gb >> 63);
   // the lane's run, in f64 arithmetic on integer values (exact below 2^53; a run that leaves that range cannot
-  // be valid and is marked BAD): every term decomposed once (decomp_f), then input parity 0's track; parity 1's
-  // differs only through ties, so it is the same track unless the run holds one (then it is run again)
+  // be valid and is marked BAD): every term decomposed (decomp_f) and input parity 0's track advanced in one pass;
+  // parity 1's differs only through ties, so it is the same track unless the run holds one (then a second pass)
   Tr a = tr_ident();
-  double qv[kPer];
-  uint32_t cls = 0;  // 2 bits per term: 0 / 1 (tie) / 2 as decomp's class, 3: a +-0 term (no effect)
-  bool bad = false;
+  bool bad = false, tie = false;
+  const double big = kBig;
+  double d0 = 0.0, lo0 = big, hi0 = -big;
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
-    qv[i] = 0.0;
-    uint32_t ci = 3;
     if (i < cnt) {
-      const uint64_t b = (uint64_t)__double_as_longlong(pr[i]);
+      const double p = mine[i];
+      const uint64_t b = (uint64_t)__double_as_longlong(p);
       if ((b << 1) == 0) {
         if (!(b >> 63)) a.fl &= ~F_NZERO;
       } else {
@@ -517,41 +515,37 @@ __device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str,
           a.fl = sneg ? F_NEG : 0u;
           a.e = e;
         }
+        double q = 0.0;
         int c = 0;
-        if (!gok || !decomp_f(pr[i], e, sneg, qv[i], c)) bad = true;
-        ci = (uint32_t)c;
+        if (!gok || !decomp_f(p, e, sneg, q, c)) bad = true;
+        const double x = d0 + q;
+        lo0 = fmin(lo0, x);
+        d0 = x + (c == 2 ? 1.0 : 0.0) + (c == 1 ? x - 2.0 * floor(0.5 * x) : 0.0);  // a tie rounds to even
+        hi0 = fmax(hi0, d0);
+        tie |= c == 1;
       }
     }
-    cls |= ci << (2 * i);
   }
   if (!(a.fl & F_ZERO)) {
-    const double big = kBig;
-    double d0 = 0.0, lo0 = big, hi0 = -big, d1 = 0.0, lo1 = big, hi1 = -big;
-    bool tie = false;
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const uint32_t ci = (cls >> (2 * i)) & 3u;
-      if (ci == 3) continue;
-      const double x = d0 + qv[i];
-      lo0 = fmin(lo0, x);
-      d0 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? x - 2.0 * floor(0.5 * x) : 0.0);  // a tie rounds to even
-      hi0 = fmax(hi0, d0);
-      tie |= ci == 1;
-    }
+    double d1 = d0, lo1 = lo0, hi1 = hi0;
     if (tie) {
+      d1 = 0.0;
+      lo1 = big;
+      hi1 = -big;
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
-        const uint32_t ci = (cls >> (2 * i)) & 3u;
-        if (ci == 3) continue;
-        const double x = d1 + qv[i];
-        lo1 = fmin(lo1, x);
-        d1 = x + (ci == 2 ? 1.0 : 0.0) + (ci == 1 ? (x + 1.0) - 2.0 * floor(0.5 * (x + 1.0)) : 0.0);
-        hi1 = fmax(hi1, d1);
+        if (i < cnt) {
+          const double p = mine[i];
+          if (((uint64_t)__double_as_longlong(p) << 1) == 0) continue;
+          double q = 0.0;
+          int c = 0;
+          if (gok) (void)decomp_f(p, e, sneg, q, c);
+          const double x = d1 + q;
+          lo1 = fmin(lo1, x);
+          d1 = x + (c == 2 ? 1.0 : 0.0) + (c == 1 ? (x + 1.0) - 2.0 * floor(0.5 * (x + 1.0)) : 0.0);
+          hi1 = fmax(hi1, d1);
+        }
       }
-    } else {
-      d1 = d0;
-      lo1 = lo0;
-      hi1 = hi0;
     }
     const double lim = 4503599627370496.0;  // 2^52: every offset of a valid run is below this
     if (bad || fabs(d0) > lim || fabs(d1) > lim || (lo0 < big && fabs(lo0) > lim) ||
@@ -586,51 +580,51 @@ __device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str,
 
 // Workgroup k: segment k of every sum.  Thread t holds terms 16t..16t+15 of the segment (the products staged
 // through LDS from coalesced loads); four threads make a sub-segment's transducer, wave 0 composes the 64 subs.
+template <bool PF>
 __device__ __forceinline__ void trans_block(int64_t k, const double* __restrict__ w, const Vecs& V, int nv, int64_t n,
                                             int self, const double* __restrict__ pre, Tr* __restrict__ segT,
                                             Tr* __restrict__ subT, int64_t K, double* sp, double* ssum, Tr* str) {
   const int t = threadIdx.x;
   const int64_t c0 = k * kSeg;
   const int cnt = (int)max<int64_t>(0, min<int64_t>(kPer, n - (c0 + (int64_t)kPer * t)));
-  double xr[kPer];
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const int64_t g = c0 + t + i * kT;
-    xr[i] = g < n ? w[g] : 0.0;
-  }
-  // sum v's y values, loaded one sum ahead (their round trip overlaps sum v - 1's transducers)
-  double yr[kPer], yn[kPer];
-  auto load_y = [&](double (&dst)[kPer], int v) {
-    const double* y = vec_row(V, v);
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) dst[i] = y[min<int64_t>(c0 + t + i * kT, n - 1)];
-  };
-  if (!self) load_y(yr, 0);
+  // sum v's w and y values, loaded one sum ahead (their round trip overlaps sum v - 1's transducers); w is the same
+  // for every sum and re-read from the L2 each time rather than held, which keeps the kernel's registers down
+  double wn[kPer], yn[kPer];
+#define MSK_SEQX_LOAD(v_)                                        \
+  do {                                                           \
+    const double* y_ = self ? nullptr : vec_row(V, (v_));        \
+    _Pragma("unroll") for (int i = 0; i < kPer; ++i) {           \
+      const int64_t g = min<int64_t>(c0 + t + i * kT, n - 1);    \
+      wn[i] = w[g];                                              \
+      yn[i] = y_ ? y_[g] : 0.0;                                  \
+    }                                                            \
+  } while (0)
+  if (PF) MSK_SEQX_LOAD(0);
   for (int v = 0; v < nv; ++v) {
-    if (!self && v + 1 < nv) load_y(yn, v + 1);
+    if (!PF) MSK_SEQX_LOAD(v);  // no loads in flight across the transducers: fewer registers, more waves
     const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int64_t g = c0 + t + i * kT;
       const int l = t + i * kT;
       double p = 0.0;
-      if (g < n) p = self ? xr[i] * xr[i] : xr[i] * (yr[i] * sy);
+      if (g < n) p = self ? wn[i] * wn[i] : wn[i] * (yn[i] * sy);
       sp[l + l / kPer] = p;
     }
-    if (!self && v + 1 < nv) {
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) yr[i] = yn[i];
-    }
+    if (PF && v + 1 < nv) MSK_SEQX_LOAD(v + 1);
     trans_segment(sp, ssum, str, pre[(int64_t)v * K + k], cnt, subT + ((int64_t)v * K + k) * kSubs,
                   segT + (int64_t)v * K + k);
   }
+#undef MSK_SEQX_LOAD
 }
 
 constexpr int kSpTrans = kSeg + kSeg / kPer;  // products, one pad slot per 16: thread t's run at 17t
 
 // ready != nullptr (round 6, the overlapped launch): after its records, the workgroup publishes ready[k] = epoch for
 // the walk that runs concurrently on the context's stream (ripwalk_sum's wait_ready).
-__global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w, Vecs V, int nv, int64_t n,
+// PF: the next sum's loads in flight during this sum's transducers (two waves per SIMD); else three waves per SIMD
+template <bool PF>
+__global__ __launch_bounds__(kT, PF ? 2 : 3) void k_seqx_trans(const double* __restrict__ w, Vecs V, int nv, int64_t n,
                                                    int self, const double* __restrict__ pre, Tr* __restrict__ segT,
                                                    Tr* __restrict__ subT, int64_t K, const int* __restrict__ stop,
                                                    uint32_t* ready, uint32_t epoch) {
@@ -638,7 +632,7 @@ __global__ __launch_bounds__(kT) void k_seqx_trans(const double* __restrict__ w,
   __shared__ double sp[kSpTrans];
   __shared__ double ssum[kSubs];
   __shared__ Tr str[kT / 64];
-  trans_block(blockIdx.x, w, V, nv, n, self, pre, segT, subT, K, sp, ssum, str);
+  trans_block<PF>(blockIdx.x, w, V, nv, n, self, pre, segT, subT, K, sp, ssum, str);
   if (!ready) return;
   __threadfence();  // every thread's records, at agent scope, before the flag
   __syncthreads();
@@ -1451,6 +1445,9 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
   const int rw = rwe ? atoi(rwe) : 16, rs = rse ? atoi(rse) : 8, pf = pfe && pfe[0] == '0' ? 0 : 1;
   const bool ripwalk = !(wk && wk[0] == 's');
   // MSPLIT_SEQ_FILLERS=0: every wave of the walk's workgroup walks and fills (round 5) instead of filler waves
+  // MSPLIT_SEQ_TRANS_PF=1: the transducer build loads the next sum's terms during this sum's maps (round 5)
+  const char* tpe = getenv("MSPLIT_SEQ_TRANS_PF");
+  auto trans_kernel = tpe && tpe[0] == '1' ? k_seqx_trans<true> : k_seqx_trans<false>;
   const char* fle = getenv("MSPLIT_SEQ_FILLERS");
   const bool fillers = !(fle && fle[0] == '0');
   auto launch_walk = [&](hipStream_t st, uint32_t* rdy, uint32_t ep) {
@@ -1478,7 +1475,7 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
         hipStreamWaitEvent(c->seq_aux, c->seq_ev[0], 0) != hipSuccess ||
         hipStreamWaitEvent(c->seq_walk, c->seq_ev[0], 0) != hipSuccess)
       return (int)hipErrorUnknown;
-    k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->seq_aux>>>(w, *V, nv, n, self, pre, segT, subT, K, stop, ready,
+    trans_kernel<<<dim3((unsigned)K), dim3(kT), 0, c->seq_aux>>>(w, *V, nv, n, self, pre, segT, subT, K, stop, ready,
                                                                  c->seq_epoch);
     launch_walk(c->seq_walk, ready, c->seq_epoch);
     if (hipEventRecord(c->seq_ev[1], c->seq_aux) != hipSuccess ||
@@ -1487,7 +1484,7 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
         hipStreamWaitEvent(c->stream, c->seq_ev[2], 0) != hipSuccess)    // and reads the sums
       return (int)hipErrorUnknown;
   } else {
-    k_seqx_trans<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop,
+    trans_kernel<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop,
                                                                 nullptr, 0);
     if (!ripwalk)
       k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,

@@ -330,3 +330,40 @@ def test_bench_spmv_check_restates_matmult_seqaij(oracle, n):
     x[0] = -0.0
     yb = np.concatenate([bench.poisson3d_rows_product(x, n, z) for z in range(n)])
     assert np.array_equal(A.mult(x).view(np.uint64), yb.view(np.uint64))
+
+
+def test_bench_smsm_record_checks():
+    """bench.py's SMSM verifications (check_smsm_block for the N = 1 lines, check_configs2_run for an N = 2 run):
+    a step that matches the committed record is verified, one changed bit in any checked field is not, and another
+    problem has no record."""
+    import copy
+    import json
+    import types
+    sys.path.insert(0, ROOT)
+    import bench
+    blk_rec = json.load(open(bench.SMSM_BLOCK_GOLDEN))["dbr"]
+    step = types.SimpleNamespace(lsqr_rnorm=[float.fromhex(h) for h in blk_rec["hist_hex"][:2]],
+                                 lsqr_its=list(blk_rec["lsqr_its"][:2]),
+                                 inner_its=[v for o in blk_rec["inner_its"][:2] for v in o])
+    assert bench.check_smsm_block(step, None, blk_rec, 2) == (True, [])
+    bad = copy.deepcopy(step)
+    bad.lsqr_rnorm[1] = float.fromhex(blk_rec["hist_hex"][1]) * (1 + 2 ** -52)
+    assert bench.check_smsm_block(bad, None, blk_rec, 2) == (False, ["hist_hex"])
+    bad = copy.deepcopy(step)
+    bad.inner_its[-1] += 1
+    assert bench.check_smsm_block(bad, None, blk_rec, 2) == (False, ["inner_its"])
+    assert bench.check_smsm_block(step, None, blk_rec, 9)[0] is None      # more steps than the record holds
+    assert bench.check_smsm_block(step, None, None, 1)[0] is None
+
+    args = types.SimpleNamespace(smsm_mesh=512, smsm_planes=256, s=20, inner_max_it=20, outer_max_it=70, restart=30,
+                                 peclet=None)
+    rec = json.load(open(bench.C2_GOLDEN))["cubes"]["512"]
+    for rank in (0, 1):
+        st = types.SimpleNamespace(lsqr_rnorm=[float.fromhex(h) for h in rec["hist_hex"][:3]],
+                                   lsqr_its=list(rec["lsqr_its"][:3]),
+                                   inner_its=[rec["inner_its"][o][j][rank] for o in range(3) for j in range(20)])
+        assert bench.check_configs2_run(args, st, rank) == (True, [], 3)
+        st.lsqr_its[0] -= 1
+        assert bench.check_configs2_run(args, st, rank) == (False, ["lsqr_its"], 3)
+    other = types.SimpleNamespace(**{**vars(args), "smsm_mesh": 256})
+    assert bench.check_configs2_run(other, st, 0)[0] is None
