@@ -61,6 +61,7 @@ struct msp_ctx {
   void* seqbuf = nullptr;      // MSP_REDUCE_SEQ's transducers and guesses (msplit_seq.hip)
   int64_t seqbuf_cap = 0;      // bytes
   uint32_t seq_epoch = 0;      // the overlapped transducer builds' flag value (msplit_seq.hip seqx_core)
+  int64_t seq_spin = 400000000; // the device's g_seq_spin_ticks as this context last set it (msplit_seq.hip)
   hipStream_t seq_aux = nullptr;   // their stream (CU-masked), the walks' stream (the other CUs), and the events
   hipStream_t seq_walk = nullptr;  // that order them with the context's
   hipEvent_t seq_ev[3] = {nullptr, nullptr, nullptr};

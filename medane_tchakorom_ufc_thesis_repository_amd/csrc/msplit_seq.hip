@@ -941,13 +941,17 @@ __device__ __forceinline__ bool any_ties(const Rip& q) {
 // ready[k] = epoch (an agent-scope release behind the records; the acquire here orders the wave's later loads of
 // them).  Lane l waits for segment k0 + l.  A wait that outlasts 4 s gives up: the sum then comes out NaN, a loud
 // failure instead of a hang.
+// How long a wait of the overlapped walk spins before it gives up (100 MHz ticks): 4 s; MSPLIT_SEQ_SPIN_TICKS sets it
+// (tests: 0 makes every wait that is not already satisfied give up, which exercises the retry launch)
+__device__ int64_t g_seq_spin_ticks = 400000000;
+
 __device__ __forceinline__ bool wait_ready(uint32_t* ready, uint32_t epoch, int64_t k0, int64_t K, int lane) {
   if (!ready || k0 >= K) return true;
   uint32_t* f = ready + min<int64_t>(k0 + lane, K - 1);
   bool ok = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch;
   const int64_t t0 = wall_clock64();
   while (__ballot(!ok)) {
-    if (wall_clock64() - t0 > 400000000) return false;  // 100 MHz ticks
+    if (wall_clock64() - t0 > g_seq_spin_ticks) return false;
     __builtin_amdgcn_s_sleep(2);
     if (!ok) ok = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch;
   }
@@ -962,7 +966,8 @@ __device__ __forceinline__ void ripwalk_sum(int v, const double* __restrict__ w,
                                             const Tr* __restrict__ segT, const Tr* __restrict__ subT, int64_t K,
                                             const double* __restrict__ acc_in, double* __restrict__ partial,
                                             int64_t nchunks, int64_t* __restrict__ stats, int rw, int rs, int pf,
-                                            double* sp, uint32_t* ready = nullptr, uint32_t epoch = 0) {
+                                            double* sp, uint32_t* ready = nullptr, uint32_t epoch = 0,
+                                            uint32_t* fail = nullptr) {
   const int t = threadIdx.x, lane = t & 63;
   const double* y = self ? nullptr : vec_row(V, v);
   const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
@@ -1046,7 +1051,8 @@ __device__ __forceinline__ void ripwalk_sum(int v, const double* __restrict__ w,
     }
   }
 #undef TICK
-  if (!live) s = __builtin_nan("");  // a builder never published: no result
+  if (!live) s = __builtin_nan("");  // a builder never published: no result (the retry launch redoes it)
+  if (!live && fail && t == 0) fail[0] = epoch;
   if (t < 64)
     for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
   if (stats && t == 0) {
@@ -1073,11 +1079,13 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
                                                          int64_t K, const double* __restrict__ acc_in,
                                                          double* __restrict__ partial, int64_t nchunks,
                                                          const int* __restrict__ stop, int64_t* __restrict__ stats,
-                                                         int rw, int rs, int pf, uint32_t* ready, uint32_t epoch) {
+                                                         int rw, int rs, int pf, uint32_t* ready, uint32_t epoch,
+                                                         uint32_t* fail, uint32_t guard) {
   if (stopped(stop)) return;
+  if (guard && fail[0] != guard) return;  // the retry launch: only when this call's overlapped walk gave up
   __shared__ double sp[kSeg];
   ripwalk_sum(blockIdx.x, w, V, n, self, segT, subT, K, acc_in, partial, nchunks, stats, rw, rs, pf, sp, ready,
-              epoch);
+              epoch, fail);
 }
 
 // ------------------------------------------------------------ the ripple walk with filler waves (round 6)
@@ -1096,6 +1104,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk(const double* __restric
 // slot), so the segment it reads is never rewritten under it.  Every wait gives up after 4 s: the sum then comes out
 // NaN and the fillers stop.
 constexpr int kRing = 3;
+constexpr int64_t kRingSpin = 400000000;  // 4 s of 100 MHz ticks: a ring wait that outlasts it gives up
 constexpr int kFillW = 3;
 constexpr int kFillT = kFillW * 64;
 constexpr int kFillPer = (kSeg + kFillT - 1) / kFillT;
@@ -1115,7 +1124,6 @@ __device__ __forceinline__ int32_t lds_acq(int32_t* p) {
 __device__ __forceinline__ void lds_rel(int32_t* p, int32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-constexpr int64_t kSpinTicks = 400000000;  // 4 s of 100 MHz ticks
 
 // The filler waves' loop: BAD segments in order into the ring.  ft: thread index among the fillers.
 __device__ __forceinline__ void fill_ring(int v, const double* __restrict__ w, const double* __restrict__ y, double sy,
@@ -1140,7 +1148,7 @@ __device__ __forceinline__ void fill_ring(int v, const double* __restrict__ w, c
       for (;;) {
         if (lds_acq(&ctl->done)) return;
         if (lds_acq(&ctl->seg[slot]) == pk0 && pk0 < lds_acq(&ctl->walk_pos)) break;
-        if (wall_clock64() - t0 > kSpinTicks) return;
+        if (wall_clock64() - t0 > kRingSpin) return;
         __builtin_amdgcn_s_sleep(1);
       }
       RingSlot* S = ring + slot;
@@ -1184,7 +1192,7 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
                                                 const double* __restrict__ acc_in, double* __restrict__ partial,
                                                 int64_t nchunks, int64_t* __restrict__ stats, int rw, int rs,
                                                 RingSlot* ring, RingCtl* ctl, double* sp1, uint32_t* ready,
-                                                uint32_t epoch) {
+                                                uint32_t epoch, uint32_t* fail) {
   const int lane = threadIdx.x & 63;
   int64_t n_win = 0, n_segdesc = 0, n_rip = 0, n_subser = 0, n_hit = 0, n_miss = 0, n_badsub = 0, n_guess = 0;
   int64_t c_win = 0, c_rip = 0, c_serial = 0, c_fill = 0, c_wait = 0, c_all = stats ? wall_clock64() : 0;
@@ -1227,7 +1235,7 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
           for (int q = 0; q < kRing; ++q)
             if (lds_acq(&ctl->seg[q]) == k) slot = q;
           if (slot >= 0) break;
-          if (wall_clock64() - t0 > kSpinTicks) break;
+          if (wall_clock64() - t0 > kRingSpin) break;
           __builtin_amdgcn_s_sleep(1);
         }
         if (slot < 0) {
@@ -1277,7 +1285,8 @@ __device__ __forceinline__ void ripwalk_pc_walk(int v, const double* __restrict_
   }
 #undef TICK
   if (lane == 0) lds_rel(&ctl->done, 1);
-  if (!live) s = __builtin_nan("");
+  if (!live) s = __builtin_nan("");  // a builder never published (the retry launch redoes the sum)
+  if (!live && fail && lane == 0) fail[0] = epoch;
   for (int64_t c = lane; c < nchunks; c += 64) partial[(int64_t)v * nchunks + c] = c == 0 ? s : 0.0;
   if (stats && lane == 0) {
     stats[v * 8 + 0] = n_win;
@@ -1304,9 +1313,11 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk_pc(const double* __rest
                                                             int64_t K, const double* __restrict__ acc_in,
                                                             double* __restrict__ partial, int64_t nchunks,
                                                             const int* __restrict__ stop, int64_t* __restrict__ stats,
-                                                            int rw, int rs, uint32_t* ready, uint32_t epoch) {
+                                                            int rw, int rs, uint32_t* ready, uint32_t epoch,
+                                                            uint32_t* fail, uint32_t guard) {
   static_assert(kWalkT == 64 + kFillT, "one walking wave and the filler waves");
   if (stopped(stop)) return;
+  if (guard && fail[0] != guard) return;  // the retry launch: only when this call's overlapped walk gave up
   __shared__ RingSlot ring[kRing];
   __shared__ RingCtl ctl;
   __shared__ double sp1[kSub];
@@ -1324,7 +1335,7 @@ __global__ __launch_bounds__(kWalkT) void k_seqx_ripwalk_pc(const double* __rest
   const double sy = (!self && V.scale) ? V.scale[v] : 1.0;
   if (t < 64)
     ripwalk_pc_walk(v, w, y, sy, n, self, segT, subT, K, acc_in, partial, nchunks, stats, rw, rs, ring, &ctl, sp1,
-                    ready, epoch);
+                    ready, epoch, fail);
   else
     fill_ring(v, w, y, sy, n, self, segT, subT, K, ring, &ctl, ready, epoch);
 }
@@ -1413,15 +1424,16 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
     if (c->seqready) (void)hipFree(c->seqready);
     c->seqready = nullptr;
     c->seqready_cap = 0;
-    hipError_t e = hipMalloc((void**)&c->seqready, (size_t)K * sizeof(uint32_t));
+    hipError_t e = hipMalloc((void**)&c->seqready, (size_t)(K + 1) * sizeof(uint32_t));  // + the retry flag
     if (e != hipSuccess) return (int)e;
-    if ((e = hipMemsetAsync(c->seqready, 0, (size_t)K * sizeof(uint32_t), c->stream)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(c->seqready, 0, (size_t)(K + 1) * sizeof(uint32_t), c->stream)) != hipSuccess) return (int)e;
     c->seqready_cap = K;
   }
   Tr* subT = static_cast<Tr*>(c->seqbuf);
   Tr* segT = subT + (int64_t)nv * K * kSubs;
   double* pre = reinterpret_cast<double*>(segT + (int64_t)nv * K);
   uint32_t* ready = c->seqready;
+  uint32_t* fail = c->seqready + c->seqready_cap;  // an overlapped walk that gave up writes its epoch here
   const int rc = msk_dot_stage1(w, V, nv, n, pre, K, self, stop, c->stream);
   if (rc) return rc;
   k_seqx_prefix<<<dim3(nv), dim3(kT), 0, c->stream>>>(pre, K, acc_in, stop);
@@ -1450,13 +1462,13 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
   auto trans_kernel = tpe && tpe[0] == '1' ? k_seqx_trans<true> : k_seqx_trans<false>;
   const char* fle = getenv("MSPLIT_SEQ_FILLERS");
   const bool fillers = !(fle && fle[0] == '0');
-  auto launch_walk = [&](hipStream_t st, uint32_t* rdy, uint32_t ep) {
+  auto launch_walk = [&](hipStream_t st, uint32_t* rdy, uint32_t ep, uint32_t* fl, uint32_t guard) {
     if (fillers)
       k_seqx_ripwalk_pc<<<dim3(nv), dim3(kWalkT), 0, st>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
-                                                           stop, dstats, rw, rs, rdy, ep);
+                                                           stop, dstats, rw, rs, rdy, ep, fl, guard);
     else
       k_seqx_ripwalk<<<dim3(nv), dim3(kWalkT), 0, st>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks, stop,
-                                                        dstats, rw, rs, pf, rdy, ep);
+                                                        dstats, rw, rs, pf, rdy, ep, fl, guard);
   };
   // The transducer builds and the walk run on two streams of their own (seq_aux: disjoint compute units) while the
   // walk follows the builds (round 6): it waits per window of 64 segments for their builders' ready words
@@ -1471,18 +1483,32 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
                        seq_aux(c) == 0;
   if (overlap) {
     if (++c->seq_epoch == 0) c->seq_epoch = 1;  // 0 is the words' initial value
+    const char* spe = getenv("MSPLIT_SEQ_SPIN_TICKS");
+    const int64_t ticks = spe ? atoll(spe) : 400000000;
+    if (ticks != c->seq_spin) {  // ordered before the walk by the stream and seq_ev[0]
+      c->seq_spin = ticks;
+      if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_seq_spin_ticks), &c->seq_spin, sizeof(int64_t), 0,
+                                 hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+          hipStreamSynchronize(c->stream) != hipSuccess)
+        return (int)hipErrorUnknown;
+    }
     if (hipEventRecord(c->seq_ev[0], c->stream) != hipSuccess ||
         hipStreamWaitEvent(c->seq_aux, c->seq_ev[0], 0) != hipSuccess ||
         hipStreamWaitEvent(c->seq_walk, c->seq_ev[0], 0) != hipSuccess)
       return (int)hipErrorUnknown;
     trans_kernel<<<dim3((unsigned)K), dim3(kT), 0, c->seq_aux>>>(w, *V, nv, n, self, pre, segT, subT, K, stop, ready,
                                                                  c->seq_epoch);
-    launch_walk(c->seq_walk, ready, c->seq_epoch);
+    launch_walk(c->seq_walk, ready, c->seq_epoch, fail, 0);
     if (hipEventRecord(c->seq_ev[1], c->seq_aux) != hipSuccess ||
         hipEventRecord(c->seq_ev[2], c->seq_walk) != hipSuccess ||
         hipStreamWaitEvent(c->stream, c->seq_ev[1], 0) != hipSuccess ||  // the next call reuses the records
         hipStreamWaitEvent(c->stream, c->seq_ev[2], 0) != hipSuccess)    // and reads the sums
       return (int)hipErrorUnknown;
+    // The overlap needs the builds and the walk resident together.  Where they are not (a profiler that serialises
+    // dispatches, another process holding the GPU's queues), the walk's waits give up after 4 s and it leaves its
+    // epoch in *fail; this launch, behind both on the context's stream, then walks the now complete records again.
+    // Otherwise every workgroup of it returns at once.
+    launch_walk(c->stream, nullptr, 0, fail, c->seq_epoch);
   } else {
     trans_kernel<<<dim3((unsigned)K), dim3(kT), 0, c->stream>>>(w, *V, nv, n, self, pre, segT, subT, K, stop,
                                                                 nullptr, 0);
@@ -1490,7 +1516,7 @@ static int seqx_core(msp_ctx* c, const double* w, const Vecs* V, int nv, int64_t
       k_seqx_walk<<<dim3(nv), dim3(kWalkT), 0, c->stream>>>(w, *V, n, self, segT, subT, K, acc_in, partial, nchunks,
                                                             stop, dstats, prep);
     else
-      launch_walk(c->stream, nullptr, 0);
+      launch_walk(c->stream, nullptr, 0, nullptr, 0);
   }
   if (dstats) {
     int64_t h[16 * MSK_MAX_GROUP];

@@ -145,8 +145,18 @@ def test_seq_engine_norms(sctx, oracle, name):
     _check_norm(sctx, oracle, CASES[name][0])
 
 
-def test_seq_engine_mdot_32_mixed(sctx, oracle):
-    """One MDot launch of 32 sums of very different kinds (the walk runs one wave per sum)."""
+@pytest.mark.parametrize("mode", ["default", "fillers_off", "walk_gives_up", "no_overlap"])
+def test_seq_engine_mdot_32_mixed(sctx, oracle, monkeypatch, mode):
+    """One MDot launch of 32 sums of very different kinds (one walking wave per sum, three filler waves), bitwise the
+    PETSc-order oracle -- also with the round-5 walk (every wave walks and fills), with the builds not overlapped,
+    and with the overlapped walk made to give up at its first unsatisfied wait (MSPLIT_SEQ_SPIN_TICKS=0: what a
+    serialising profiler or a starved queue causes), where the retry launch behind the builds redoes the sums."""
+    if mode == "fillers_off":
+        monkeypatch.setenv("MSPLIT_SEQ_FILLERS", "0")
+    elif mode == "walk_gives_up":
+        monkeypatch.setenv("MSPLIT_SEQ_SPIN_TICKS", "0")
+    elif mode == "no_overlap":
+        monkeypatch.setenv("MSPLIT_SEQ_OVERLAP", "0")
     rng = np.random.default_rng(SEED)
     n = 300_001
     w = rng.standard_normal(n)
