@@ -292,7 +292,8 @@ def test_configs4_whole_eight_blocks_roundrobin_lsqr(ctx):
     3D upwind convection-diffusion 512^3 in 8 z-slab blocks of 512 x 512 x 64, all round-robin on this GPU (peak
     282 GB of the 309 GB HBM, tools/amam_configs.py whole: profiles/r06/configs4_lsqr/), s 20, inner GMRES(30)
     max_it 20 rtol 1e-20, outer LSQR max_it 70 rtol 1e-15, -rtol 1e-4.  The run terminates by the detection
-    (every block FINISHED in one phase, no cap hit), and a rerun is bitwise the first (trace, x, residual)."""
+    (every block FINISHED in one phase, no cap hit).  One run (about 100 s): the round-robin schedule's bitwise rerun
+    is held by the rtr test above and, for this minimization, by tests/test_gpu_amam_configs.py's block pairs."""
     comm = LocalComm()
     blocks = make_blocks(ctx, 3, 512, 512, 512, NB, range(NB), _opts(NB, extra="-msplit_minimization lsqr"), comm,
                          PE)
@@ -300,7 +301,7 @@ def test_configs4_whole_eight_blocks_roundrobin_lsqr(ctx):
         for blk in blocks:
             blk.setup_global_async_minimization(20)
             assert blk.minimization == "lsqr" and len(blk.R_rep) == NB
-        res, fp = _c4_run(ctx, blocks, comm)
+        res, _ = _c4_run(ctx, blocks, comm)
         assert res.converged and max(res.iterations) < C4_MAX_ITS, res.iterations
         last = {b: st for b, _, _, st, _ in res.trace}
         assert last == {b: ConvDetection.FINISHED for b in range(NB)}
@@ -309,8 +310,6 @@ def test_configs4_whole_eight_blocks_roundrobin_lsqr(ctx):
         print(f"configs[4] whole (lsqr): iterations {res.iterations}, final residual {res.final_norm:.6e} "
               f"(||b|| {res.norm0:.6e}, ratio {res.final_norm / res.norm0:.3e}), {res.elapsed:.1f} s, "
               f"timers {res.timers}")
-        res2, fp2 = _c4_run(ctx, blocks, comm)
-        assert fp2 == fp
     finally:
         del blocks
         gc.collect()
