@@ -92,6 +92,76 @@ def _transport_worker(rank, name, n_msgs, n, q, nbuf=2):
     q.put((rank, ok, taken, last))
 
 
+def _inflight_worker(rank, name, n, q):
+    sys.path.insert(0, ROOT)
+    import time
+    import torch  # noqa: F401
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncMessages, Context, Vec
+    ctx = Context(0)
+    if rank == 1:
+        t0 = time.time()
+        while True:
+            try:
+                am = AsyncMessages(name, 2, 1, n, owner=False)
+                break
+            except Exception:
+                if time.time() - t0 > 60:
+                    raise
+                time.sleep(0.05)
+    else:
+        am = AsyncMessages(name, 2, 0, n, owner=True)
+    am.enable_device(ctx)
+    while am.attached() < 2:
+        time.sleep(0.01)
+    if rank == 1:                       # the sender: its last send still queued on the stream at shutdown
+        v = Vec(ctx, n)
+        v.set(7.0)
+        busy = Vec(ctx, 1 << 27)        # 1 GiB: milliseconds of stream work ahead of the send's copy and publish
+        busy.set(1.0)
+        for _ in range(12):
+            busy.scale(-1.0)            # (VecScale returns at once for 1.0)
+        am.send_vec(0, [7, 7], v, 0, n)
+        discarded, in_flight = am.discard_pending()    # the MPI_Cancel point: the send cannot be withdrawn (a DMA),
+        sent, skipped = am.stats()                      # so the drain completes it
+        am.send(0, AsyncMessages.VERDICT, [1])
+        while not am.recv(0, AsyncMessages.VERDICT, 1)[0]:
+            time.sleep(0.01)
+        am.close_peers()
+        am.destroy()
+        q.put((rank, in_flight, sent, skipped))
+        return
+    while not am.recv(1, AsyncMessages.VERDICT, 1)[0]:  # the sender has drained
+        time.sleep(0.01)
+    y = Vec(ctx, n)
+    got, ints, m = am.recv_vec(1, 2, y, 0, n)
+    ok = got and ints == [7, 7] and m == n and bool(np.all(y.get_array() == 7.0))
+    am.close_peers()
+    am.send(1, AsyncMessages.VERDICT, [1])
+    time.sleep(0.5)
+    am.destroy()
+    q.put((rank, ok))
+
+
+def test_send_in_flight_at_shutdown_is_completed():
+    """The end of an asynchronous run (AMAM-global_prime.c:522-572: MPI_Cancel of the sends still pending, then
+    comm_discard_pending_messages): a plane send whose copy and publish are still queued behind milliseconds of
+    stream work when the sender drains is counted in flight, completed by the drain (a DMA cannot be withdrawn), and
+    its plane reaches the receiver whole."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/msplit_inflight_{os.getpid()}"
+    n = 1 << 22
+    procs = [ctx.Process(target=_inflight_worker, args=(r, name, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0][1]                                    # the receiver got the whole plane
+    assert out[1][1] == 1 and out[1][2] == 1 and out[1][3] == 0, out[1]   # one send, posted, in flight at the drain
+
+
 @pytest.mark.parametrize("nbuf", [2, 1])
 def test_device_slots_cross_process_whole_and_newest(nbuf):
     """Every plane and block a receiver takes from the sender's HBM is whole and
