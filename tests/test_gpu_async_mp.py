@@ -96,13 +96,14 @@ def _inflight_worker(rank, name, n, q):
     sys.path.insert(0, ROOT)
     import time
     import torch  # noqa: F401
-    from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncMessages, Context, Vec
+    from medane_tchakorom_ufc_thesis_repository_amd.petsc import AsyncBroadcast, AsyncMessages, Context, DenseMat, Vec
     ctx = Context(0)
     if rank == 1:
         t0 = time.time()
         while True:
             try:
                 am = AsyncMessages(name, 2, 1, n, owner=False)
+                bc = AsyncBroadcast(name + "_R", 2, 1, n * 2, owner=False)
                 break
             except Exception:
                 if time.time() - t0 > 60:
@@ -110,7 +111,9 @@ def _inflight_worker(rank, name, n, q):
                 time.sleep(0.05)
     else:
         am = AsyncMessages(name, 2, 0, n, owner=True)
+        bc = AsyncBroadcast(name + "_R", 2, 0, n * 2, owner=True)
     am.enable_device(ctx)
+    bc.enable_device(ctx, 2)
     while am.attached() < 2:
         time.sleep(0.01)
     if rank == 1:                       # the sender: its last send still queued on the stream at shutdown
@@ -122,23 +125,37 @@ def _inflight_worker(rank, name, n, q):
             busy.scale(-1.0)            # (VecScale returns at once for 1.0)
         am.send_vec(0, [7, 7], v, 0, n)
         discarded, in_flight = am.discard_pending()    # the MPI_Cancel point: the send cannot be withdrawn (a DMA),
-        sent, skipped = am.stats()                      # so the drain completes it
+        sent, skipped = am.stats()                      # so the drain completes it (and syncs the stream)
+        D = DenseMat(ctx, n, 2)                         # an R block, queued the same way behind stream work
+        v.set(9.0)
+        D.set_column(0, 0, v)
+        D.set_column(1, 0, v)
+        for _ in range(12):
+            busy.scale(-1.0)
+        published = bc.publish_dense(D)
+        bdisc, bflight = bc.discard_pending()
         am.send(0, AsyncMessages.VERDICT, [1])
         while not am.recv(0, AsyncMessages.VERDICT, 1)[0]:
             time.sleep(0.01)
         am.close_peers()
+        bc.close_peers()
         am.destroy()
-        q.put((rank, in_flight, sent, skipped))
+        bc.destroy()
+        q.put((rank, in_flight, sent, skipped, published, bflight))
         return
     while not am.recv(1, AsyncMessages.VERDICT, 1)[0]:  # the sender has drained
         time.sleep(0.01)
     y = Vec(ctx, n)
     got, ints, m = am.recv_vec(1, 2, y, 0, n)
     ok = got and ints == [7, 7] and m == n and bool(np.all(y.get_array() == 7.0))
+    R = DenseMat(ctx, n, 2)
+    ok = ok and bc.fetch_dense(1, R) and bool(np.all(R.get_values() == 9.0))
     am.close_peers()
+    bc.close_peers()
     am.send(1, AsyncMessages.VERDICT, [1])
     time.sleep(0.5)
     am.destroy()
+    bc.destroy()
     q.put((rank, ok))
 
 
@@ -146,7 +163,7 @@ def test_send_in_flight_at_shutdown_is_completed():
     """The end of an asynchronous run (AMAM-global_prime.c:522-572: MPI_Cancel of the sends still pending, then
     comm_discard_pending_messages): a plane send whose copy and publish are still queued behind milliseconds of
     stream work when the sender drains is counted in flight, completed by the drain (a DMA cannot be withdrawn), and
-    its plane reaches the receiver whole."""
+    its plane reaches the receiver whole; the same for an R block published through the broadcast."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     name = f"/msplit_inflight_{os.getpid()}"
@@ -160,6 +177,7 @@ def test_send_in_flight_at_shutdown_is_completed():
         assert p.exitcode == 0
     assert out[0][1]                                    # the receiver got the whole plane
     assert out[1][1] == 1 and out[1][2] == 1 and out[1][3] == 0, out[1]   # one send, posted, in flight at the drain
+    assert out[1][4] and out[1][5] == 1, out[1]                           # the R block likewise
 
 
 @pytest.mark.parametrize("nbuf", [2, 1])
