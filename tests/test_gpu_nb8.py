@@ -32,6 +32,11 @@ from medane_tchakorom_ufc_thesis_repository_amd.petsc import ConvDetection, Opti
 
 from test_gpu_c_drivers import SM, SMSM, _run, _run_rccl, built  # noqa: F401  (built: the C host fixture)
 
+# eight ranks on the one GPU, one hardware queue each: with HIP's four, eight ranks and this GPU-using pytest parent
+# oversubscribe the GPU's 24 compute-queue slots and the scheduler runs them a process at a time
+# (tests/test_gpu_async_mp.py, profiles/r06/async8/)
+ONE_QUEUE = {"GPU_MAX_HW_QUEUES": "1"}
+
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -169,7 +174,8 @@ def test_c_host_eight_mpi_ranks_host_transport_equals_record(ctx, built):
     committed 8-block oracle record's, bit for bit."""
     with tempfile.TemporaryDirectory() as d:
         dump = os.path.join(d, "x")
-        got = _run(_ranks_args(SMSM) + ["-msplit_transport", "host", "-msplit_dump_x", dump], mpi=NB, timeout=240)
+        got = _run(_ranks_args(SMSM) + ["-msplit_transport", "host", "-msplit_dump_x", dump], mpi=NB, timeout=240,
+                   env=ONE_QUEUE)
         assert got["transport"] == "host"
         _check_record(got, dump)
 
@@ -192,7 +198,7 @@ def test_c_host_eight_mpi_ranks_sm_bitwise_oracle(ctx, oracle, built):
     ro = oracle.sm_solve(3, 8, 8, 16, NB, 1e-6, dict(INNER, reduce_mode=oracle.REDUCE_DBR), max_outer=400)
     with tempfile.TemporaryDirectory() as d:
         dump = os.path.join(d, "x")
-        got = _run(args + ["-msplit_transport", "host", "-msplit_dump_x", dump], mpi=NB, timeout=240)
+        got = _run(args + ["-msplit_transport", "host", "-msplit_dump_x", dump], mpi=NB, timeout=240, env=ONE_QUEUE)
         x = np.concatenate([np.fromfile(f"{dump}.{b}", dtype=np.float64) for b in range(NB)])
     assert got["outer_its"] == ro["outer_its"] and got["norm0"] == ro["norm0"]
     assert [float.fromhex(h) for h in got["hist_hex"]] == list(ro["hist"])
