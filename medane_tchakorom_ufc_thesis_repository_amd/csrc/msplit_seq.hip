@@ -463,8 +463,8 @@ __global__ __launch_bounds__(kT) void k_seqx_prefix(double* __restrict__ a, int6
 
 // One segment's transducers for one sum, from its products the caller has staged in sp (thread t's term i at l + l/16,
 // l = t + 256 i) and g0, the guessed sum at the segment's start: thread t's run of 16 terms, four threads to a
-// sub-segment (sub_out[0..63]), the waves' trees and thread 0's composition to the segment (*seg_out).  Begins and
-// ends with a barrier.  cnt: thread t's terms inside n.
+// sub-segment (sub_out[0..63]), the waves' trees and thread 0's composition to the segment (*seg_out).  Begins
+// with a barrier.  cnt: thread t's terms inside n.
 __device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str, double g0, int cnt,
                                               Tr* __restrict__ sub_out, Tr* __restrict__ seg_out) {
   const int t = threadIdx.x, lane = t & 63, j = t >> 2;
@@ -574,8 +574,9 @@ __device__ __forceinline__ void trans_segment(double* sp, double* ssum, Tr* str,
   }
   if (lane == 0) str[t >> 6] = a;
   __syncthreads();
+  // no barrier after it: every read of sp and ssum is behind the barrier above, and str is next written three
+  // barriers into the next sum, which thread 0 joins after this read
   if (t == 0) *seg_out = tr_comb(tr_comb(str[0], str[1]), tr_comb(str[2], str[3]));
-  __syncthreads();
 }
 
 // Workgroup k: segment k of every sum.  Thread t holds terms 16t..16t+15 of the segment (the products staged
