@@ -367,3 +367,19 @@ def test_bench_smsm_record_checks():
         assert bench.check_configs2_run(args, st, rank) == (False, ["lsqr_its"], 3)
     other = types.SimpleNamespace(**{**vars(args), "smsm_mesh": 256})
     assert bench.check_configs2_run(other, st, 0)[0] is None
+
+
+def test_gpu_steps_runner_stops_after_trouble(tmp_path):
+    """tools/gpu_steps.sh (the one runner of every GPU session): each step's output in its own log, its exit code
+    in status; a failing test run (exit 1) lets the session go on, anything above 1 (a fault, an abort, a time
+    limit) ends it there, and a step that outlives its limit is killed (124)."""
+    import subprocess
+    out = tmp_path / "s"
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "gpu_steps.sh"), str(out), "a|5|echo hello",
+                        "b|5|exit 1", "c|1|sleep 30", "d|5|echo never"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    status = (out / "status").read_text().split("\n")
+    codes = {ln.split()[0]: ln.split()[1] for ln in status if len(ln.split()) == 3 and ln.split()[1] != "start"}
+    assert codes == {"a": "0", "b": "1", "c": "124"}, status
+    assert any(ln.startswith("stopping after c (124)") for ln in status)
+    assert (out / "a.log").read_text() == "hello\n" and not (out / "d.log").exists()
